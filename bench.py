@@ -1,0 +1,235 @@
+"""bench.py -- RWI query hot path throughput on MI355X (BASELINE.json metric).
+
+Workload (a "step"): one batch of the C2 query set -- 1000 two-term AND queries,
+default RankingProfile, top-100 -- over the synthetic C2 index (10M URLs x 10k
+words, 100M postings per GPU), run end to end through libyrwi: join ->
+normalise -> cardinal -> top-k, results back in host memory.
+
+N > 1 GPUs (one process per GPU): the index is YaCy's vertical DHT partition
+by url hash (Distribution.java:153-158); every rank holds a C2-sized shard of an
+N-times larger corpus (weak scaling) and every query runs on all shards, with
+RCCL exchanging the normalisation summaries and the per-shard top-k lists.
+
+value = sum over ranks of the postings of all queries (include + exclude list
+lengths) / max-over-ranks wall time of the K timed steps.
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from yacy_search_server_amd import RWIIndex, RankingProfile, synth  # noqa: E402
+from yacy_search_server_amd._lib import CHit, CQuery, CStats  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def build_queries(idx_hashes, qs, k, now_ms, prof):
+    nq = len(qs)
+    arr = (CQuery * nq)()
+    keep = [prof]
+    for i, (inc, exc) in enumerate(qs):
+        ib = ctypes.create_string_buffer(b"".join(idx_hashes[t] for t in inc), 12 * max(1, len(inc)))
+        eb = ctypes.create_string_buffer(b"".join(idx_hashes[t] for t in exc), 12 * max(1, len(exc)))
+        keep += [ib, eb]
+        arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
+        arr[i].nincl = len(inc)
+        arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
+        arr[i].nexcl = len(exc)
+        arr[i].max_distance = 2147483647
+        arr[i].k = k
+        arr[i].profile = ctypes.pointer(prof.c)
+        arr[i].language = b"en"
+        arr[i].now_ms = now_ms
+    return arr, keep
+
+
+def cpu_baseline(idx, qs, now_ms, k, budget_s):
+    """The oracle (reference algorithm restated in C++, single thread) on a bounded
+    sample of the same query stream."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    d = {}
+    done_post = 0
+    n = 0
+    t0 = time.perf_counter()
+    for inc, exc in qs:
+        for t in inc + exc:
+            if idx.hashes[t] not in d and idx.sizes[t]:
+                d[idx.hashes[t]] = idx.list_rows(t)
+        orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=now_ms, k=k)
+        done_post += int(sum(idx.sizes[t] for t in inc + exc))
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done_post / dt, "unit": "postings/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} of the {len(qs)} C2 queries ({done_post} postings, {dt:.1f}s), "
+                      f"oracle/yrwi_oracle.cpp single thread on this host"}
+
+
+def load_pmc(config):
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--terms", type=int, default=2)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--latency", type=int, default=100, help="single-query latency samples")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+
+    base = synth.preset(args.config)
+    # weak scaling: an N-times larger corpus, URL-hash range partitioned over the N ranks
+    full = synth.SynthConfig(base.seed, base.n_urls * world, base.n_terms, base.n_hosts * world,
+                             base.n_postings * world)
+    cfg = full.shard(rank, world) if world > 1 else full
+    t0 = time.time()
+    idx = synth.build_index(cfg)
+    log(f"rank {rank}: generated {len(idx.rows)} postings in {time.time() - t0:.1f}s")
+
+    if world > 1:
+        import torch
+        from yacy_search_server_amd import unique_id
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        ix = RWIIndex(local, shard=(rank, world, bytes(uid.cpu().numpy())))
+    else:
+        ix = RWIIndex(local)
+    t0 = time.time()
+    for t in range(cfg.n_terms):
+        if idx.sizes[t]:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+    log(f"rank {rank}: index resident in {time.time() - t0:.1f}s, stats {ix.stats()}")
+
+    qs = synth.queries(full, args.nq, args.terms, args.terms, 0)
+    now_ms = 20741 * 86400000
+    prof = RankingProfile()
+    cq, keep = build_queries(idx.hashes, qs, args.k, now_ms, prof)
+    kmax = args.k
+    hits = (CHit * (args.nq * kmax))()
+    nout = (ctypes.c_int32 * args.nq)()
+    st = CStats()
+
+    def step():
+        ix.search_batch_raw(cq, args.nq, kmax, hits, nout, st)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    agg = {"postings_in": 0, "bytes_join": 0, "t_join_ns": 0, "n_join": 0, "bytes_alg": 0, "joined": 0}
+    for _ in range(args.steps):
+        step()
+        agg["postings_in"] += st.postings_in
+        agg["bytes_join"] += st.bytes_join
+        agg["t_join_ns"] += st.t_join_ns
+        agg["n_join"] += st.n_join_launches
+        agg["bytes_alg"] += st.bytes_alg
+        agg["joined"] += st.joined
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        pp = torch.tensor([agg["postings_in"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(pp)
+        total_post = float(pp.item())
+    else:
+        total_post = float(agg["postings_in"])
+    value = total_post / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    # roofline of the dominant kernel (k_join): algorithmic bytes K per launch / mean launch time
+    t_kj = agg["t_join_ns"] / max(1, agg["n_join"]) * 1e-9
+    bytes_per_launch = agg["bytes_join"] / max(1, agg["n_join"])
+    achieved = bytes_per_launch / t_kj / 1e9 if t_kj > 0 else 0.0
+    pmc = load_pmc(args.config)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get("k_join_hbm_bytes_per_launch") if pmc else None,
+            "kernel": "k_join", "bytes_per_launch_alg": int(bytes_per_launch),
+            "mean_launch_us": round(t_kj * 1e6, 2)}
+
+    # single-query latency (host call -> top-k in host memory)
+    lat = []
+    if rank == 0 and world == 1 and args.latency > 0:
+        one = (CHit * kmax)()
+        n1 = (ctypes.c_int32 * 1)()
+        for i in range(min(args.latency, args.nq)):
+            t1 = time.perf_counter()
+            ix.search_batch_raw(ctypes.byref(cq[i]), 1, kmax, one, n1, CStats())
+            lat.append((time.perf_counter() - t1) * 1e3)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": "postings joined+ranked/sec (node)",
+            "value": value, "unit": "postings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int64", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {args.nq} x {args.terms}-term AND queries, default "
+                                   f"RankingProfile, top-{args.k}; {base.n_postings / 1e6:.0f}M postings "
+                                   f"({base.n_urls / 1e6:.0f}M URLs x {base.n_terms} words) per GPU",
+                       "queries_per_step": args.nq, "postings_per_step": total_post / args.steps,
+                       "index_postings_total": int(full.n_postings), "parallelism": f"url-hash shards x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "latency_ms": ({"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                            "n": len(lat)} if lat else None),
+            "joined_per_step": agg["joined"] / args.steps,
+            "bytes_alg_per_step": agg["bytes_alg"] / args.steps,
+        }
+        print(json.dumps(out))
+    ix.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

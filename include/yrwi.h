@@ -1,0 +1,143 @@
+/* yrwi.h -- C ABI of libyrwi, the MI355X-native YaCy RWI query engine.
+ *
+ * Drop-in boundary for YaCy's reverse-word-index query hot path.  Each entry
+ * point names the Java interface it replaces (paths relative to
+ * /root/reference/source/net/yacy).  INTEGRATION.md shows the JNI / Panama
+ * binding a YaCy maintainer would add.
+ *
+ * Conventions:
+ *   - int return codes: 0 = OK, < 0 = error (YRWI_E_*); message via yrwi_last_error();
+ *   - "no result" is an empty result (n = 0), never an error -- as in
+ *     ReferenceContainer.joinExcludeContainers (ReferenceContainer.java:318,322);
+ *   - the caller owns every host buffer; the library owns device memory;
+ *   - a context is bound to one GPU and is not thread-safe: one context per
+ *     host thread, or serialise calls;
+ *   - rows are YaCy's 40-byte WordReferenceRow layout (WordReferenceRow.java:49-72),
+ *     i.e. the bytes of RowSet.chunkcache (RowCollection.java:68).
+ */
+#ifndef YRWI_H
+#define YRWI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YRWI_ROW_BYTES 40
+#define YRWI_HASH_BYTES 12
+#define YRWI_MAX_TERMS 8          /* include or exclude terms per query */
+#define YRWI_MAX_K 3000           /* WeakPriorityBlockingQueue bound, SearchEvent.java:118 */
+#define YRWI_MAX_DISTANCE_ANY 2147483647 /* Integer.MAX_VALUE: unquoted query, yacysearch.java:643 */
+
+enum {
+  YRWI_OK = 0,
+  YRWI_E_ARG = -1,           /* bad argument / capacity too small */
+  YRWI_E_HASH = -2,          /* url or term hash not well-formed Base64 (Base64Order.java:96-106) */
+  YRWI_E_UNSORTED = -3,      /* rows not strictly ascending by url hash (and sorted != 0) */
+  YRWI_E_HIP = -4,           /* HIP runtime error */
+  YRWI_E_NOMEM = -5,         /* device allocation failed (SpaceExceededException) */
+  YRWI_E_RCCL = -6,          /* collective failed */
+  YRWI_E_NULL_LANGUAGE = -7, /* language cell is 0x0000: the reference throws NPE in
+                                ASCII.getBytes(null) (WordReferenceVars.java:315, ReferenceOrder.java:260) */
+  YRWI_E_UNSUPPORTED = -8,
+  YRWI_E_LIMIT = -9          /* list longer than 53,687,091 rows (RowSet.java:90-92) */
+};
+
+typedef struct yrwi_ctx yrwi_ctx;
+
+/* RankingProfile public int coefficients, in the declaration order of
+ * RankingProfile.java:81-88.  Defaults: yrwi_profile_default(). */
+typedef struct yrwi_profile {
+  int32_t coeff_domlength, coeff_date, coeff_wordsintitle, coeff_wordsintext, coeff_phrasesintext,
+      coeff_llocal, coeff_lother, coeff_urllength, coeff_urlcomps, coeff_hitcount,
+      coeff_posintext, coeff_posofphrase, coeff_posinphrase, coeff_authority, coeff_worddistance,
+      coeff_appurl, coeff_app_dc_title, coeff_app_dc_creator, coeff_app_dc_subject,
+      coeff_app_dc_description, coeff_appemph, coeff_catindexof, coeff_cathasimage,
+      coeff_cathasaudio, coeff_cathasvideo, coeff_cathasapp, coeff_urlcompintoplist,
+      coeff_descrcompintoplist, coeff_prefer, coeff_termfrequency, coeff_language, coeff_citation;
+} yrwi_profile;
+
+/* One ranked result: a ReverseElement of SearchEvent.rwiStack
+ * (WeakPriorityBlockingQueue.java:400-426). */
+typedef struct yrwi_hit {
+  uint8_t urlhash[12];
+  int32_t tiebreak; /* ByteArray.hashCode(urlhash) (ByteArray.java:80-84) */
+  int64_t score;    /* ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265) */
+} yrwi_hit;
+
+/* A query: QueryGoal include/exclude word hashes (QueryGoal.java:229-240) plus
+ * QueryParams.maxDistance, the ranking profile and the target language. */
+typedef struct yrwi_query_desc {
+  const uint8_t* incl;        /* nincl * 12 bytes (word hashes) */
+  int32_t nincl;
+  const uint8_t* excl;        /* nexcl * 12 bytes */
+  int32_t nexcl;
+  int32_t max_distance;       /* YRWI_MAX_DISTANCE_ANY or #terms-1 for quoted queries */
+  int32_t k;                  /* results wanted (<= YRWI_MAX_K) */
+  const yrwi_profile* profile;
+  char language[8];           /* ReferenceOrder.language, NUL terminated (any length) */
+  int64_t now_ms;             /* System.currentTimeMillis() of the request; 0 = now */
+} yrwi_query_desc;
+
+typedef struct yrwi_stats {
+  int64_t postings_in;   /* sum of include + exclude list lengths */
+  int64_t joined;        /* rows of the joined container (before exclusion) */
+  int64_t bytes_alg;     /* algorithmic bytes B = sum K + 12 sum n_excl + 23 t m_out */
+  int64_t bytes_join;    /* sum K over the join steps (the k_join launches timed in t_join_ns) */
+  int64_t t_join_ns;     /* device time of the k_join launches (HIP events on the context stream) */
+  int64_t t_norm_ns, t_score_ns, t_total_ns;
+  int32_t n_join_launches, n_enum_steps, n_test_steps, reserved;
+} yrwi_stats;
+
+/* ---- profile helpers (RankingProfile.java) ---- */
+void yrwi_profile_default(yrwi_profile* p);                 /* RankingProfile(TEXT) :90-125 */
+void yrwi_profile_all_zero(yrwi_profile* p);                /* allZero() :200-233 */
+int yrwi_profile_parse(const char* prefix, const char* ext, yrwi_profile* out); /* :127-189 */
+
+/* ---- context ---- */
+int yrwi_open(int device, yrwi_ctx** out);
+/* One shard of a URL-hash-range partitioned index (Distribution.java:153-158):
+ * rank r of `world` (power of two) owns url hashes whose first character index
+ * c satisfies c >> (6 - log2(world)) == r.  `nccl_id` is the 128-byte
+ * ncclUniqueId from yrwi_get_unique_id() on rank 0, broadcast by the caller. */
+int yrwi_open_shard(int device, int rank, int world, const uint8_t nccl_id[128], yrwi_ctx** out);
+int yrwi_get_unique_id(uint8_t nccl_id[128]);
+void yrwi_close(yrwi_ctx* ctx);
+const char* yrwi_last_error(yrwi_ctx* ctx);
+
+/* ---- index (IndexCell.add / RowSet import; the lists are what
+ *      Index.get(termHash) returns, IndexCell.java:353-386) ---- */
+/* Stores (or replaces) the posting list of `term`.  rows40: n rows of 40 bytes.
+ * sorted != 0 promises ascending unique url hashes (validated); sorted == 0
+ * sorts (duplicate url hashes: the first occurrence wins, RowSet.mergeEnum). */
+int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted);
+int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n);
+int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
+
+/* ---- query hot path ---- */
+/* TermSearch + joinExcludeContainers + normalizeWith + cardinal + rwiStack top-k
+ * (SearchEvent.RWIProcess.run :612-631 -> addRWIs :673-836), canonical
+ * deterministic semantics.  out: k hits, best first. */
+int yrwi_query(yrwi_ctx* ctx, const yrwi_query_desc* q, yrwi_hit* out, int32_t* nout, yrwi_stats* st);
+/* nq independent queries in one device pass (throughput mode).
+ * out: nq * kmax hits (row q at out + q*kmax), nout[q] = hits of query q. */
+int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                     yrwi_hit* out, int32_t* nout, yrwi_stats* st);
+
+/* ---- finer-grained drop-ins mirroring the Java split ---- */
+/* == ReferenceContainer.joinExcludeContainers via TermSearch (ReferenceContainer.java:310,
+ *    TermSearch.java:42-70): writes the joined container's rows (sorted) to rows_out. */
+int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nincl, const uint8_t* excl,
+                      int32_t nexcl, int32_t max_distance, int64_t now_ms, uint8_t* rows_out,
+                      int64_t cap_rows, int64_t* m);
+/* == ReferenceOrder.normalizeWith + cardinal (ReferenceOrder.java:70,223) on one
+ *    container (rows sorted by url hash), with settled min/max: score_out[i] =
+ *    cardinal(row i). */
+int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_t m, const yrwi_profile* prof,
+                         const char* language, int64_t now_ms, int64_t* score_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YRWI_H */

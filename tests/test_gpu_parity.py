@@ -1,0 +1,215 @@
+"""GPU parity (MI355X): libyrwi's HIP path vs the oracle, bit-exact.
+
+Every check goes through the C ABI (yacy_search_server_amd.rwi -> libyrwi.so).
+Sizes are ones the C++ oracle finishes in seconds."""
+
+import numpy as np
+import pytest
+
+import java_literal as jl
+import oracle as orc
+from kat_util import kat_index, kat_profile, load_kats, run_kat
+from yacy_search_server_amd import Query, RankingProfile, RWIIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+NOW = 20741 * 86400000 + 4242
+KATS = [k for k in load_kats() if "lists" in k]
+
+
+def _rp(jlprof):
+    rp = RankingProfile()
+    for _, f in jl.PROFILE_FIELDS:
+        setattr(rp, f, getattr(jlprof, f))
+    return rp
+
+
+class GpuEngine:
+    def _ix(self, idx):
+        ix = RWIIndex(0)
+        for h, rows in idx.items():
+            ix.add(h, rows)
+        return ix
+
+    def term_search(self, idx, incl, excl, md, now):
+        ix = self._ix(idx)
+        try:
+            return ix.term_search(incl, excl, md, now)
+        finally:
+            ix.close()
+
+    def search(self, idx, incl, excl, prof, lang, md, now, k):
+        ix = self._ix(idx)
+        try:
+            return [(h.urlhash, h.score) for h in ix.search(incl, excl, _rp(prof), lang, md, now, k)]
+        finally:
+            ix.close()
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_kat_gpu(kat):
+    run_kat(GpuEngine(), kat)
+
+
+@pytest.fixture(scope="module", params=["dense", "tiny", "small"])
+def corpus(request):
+    cfg = synth.preset(request.param)
+    idx = synth.build_index(cfg)
+    ix = RWIIndex(0)
+    for t in range(cfg.n_terms):
+        if idx.sizes[t]:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+    yield cfg, idx, ix
+    ix.close()
+
+
+def _profiles():
+    c5 = jl.RankingProfile.parse("", "date=15,domlength=15,authority=13,tf=10")
+    date = jl.RankingProfile()
+    date.all_zero()
+    date.coeff_date = 15
+    rng = np.random.default_rng(3)
+    rnd = jl.RankingProfile()
+    for _, f in jl.PROFILE_FIELDS:
+        setattr(rnd, f, int(rng.integers(0, 16)))
+    rnd.coeff_urlcomps = 27
+    return [("default", jl.RankingProfile()), ("c5", c5), ("date", date), ("rand", rnd)]
+
+
+def test_join_rows_bit_exact(corpus):
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    for i, (inc, exc) in enumerate(synth.queries(cfg, 25, 1, 4, 1, qseed=11)):
+        ih = [idx.hashes[t] for t in inc]
+        eh = [idx.hashes[t] for t in exc]
+        for md in (2147483647, 60):
+            for now in (NOW, 15500 * 86400000 + 7):
+                exp = orc.term_search(d, ih, eh, md, now)
+                got = ix.term_search(ih, eh, md, now)
+                assert got.shape == exp.shape and np.array_equal(got, exp), (i, md, now)
+
+
+def test_topk_bit_exact(corpus):
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    qs = synth.queries(cfg, 20, 1, 4, 1, qseed=12)
+    for pname, prof in _profiles():
+        for now in (NOW, 15500 * 86400000 + 7):
+            batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=100,
+                           profile=_rp(prof), now_ms=now) for inc, exc in qs]
+            got = ix.search_batch(batch)
+            for qi, (q, g) in enumerate(zip(batch, got)):
+                exp = orc.search(d, q.include, q.exclude, orc.profile_from(prof), "en", now_ms=now, k=100)
+                assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, (pname, now, qi)
+
+
+def test_normalize_score_bit_exact(corpus):
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    for inc, exc in synth.queries(cfg, 8, 1, 3, 0, qseed=13):
+        ih = [idx.hashes[t] for t in inc]
+        rows = orc.term_search(d, ih, [], 2147483647, NOW)
+        if len(rows) == 0:
+            continue
+        for pname, prof in _profiles():
+            exp, _ = orc.normalize_score(rows, orc.profile_from(prof), "en", NOW)
+            got = ix.normalize_score(rows, _rp(prof), "en", NOW)
+            assert np.array_equal(got, exp), pname
+
+
+def test_batch_equals_single_and_k_edges(corpus):
+    cfg, idx, ix = corpus
+    qs = synth.queries(cfg, 10, 1, 3, 1, qseed=14)
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=k, now_ms=NOW)
+             for (inc, exc), k in zip(qs, [1, 5, 100, 3000, 0, 77, 2048, 2049, 10, 100])]
+    got = ix.search_batch(batch)
+    for q, g in zip(batch, got):
+        single = ix.search(q.include, q.exclude, k=q.k, now_ms=NOW)
+        assert [(h.urlhash, h.score) for h in g] == [(h.urlhash, h.score) for h in single]
+        assert len(g) <= q.k
+    d = idx.as_dict()
+    for q, g in zip(batch, got):
+        exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k) if q.k else []
+        assert [(h.urlhash, h.score) for h in g] == [(h, s) for h, s, _ in exp]
+
+
+def test_missing_and_duplicate_terms(corpus):
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    a, b = idx.hashes[0], idx.hashes[1]
+    missing = b"ZZZZZZZZZZZZ"
+    for inc, exc in [([a, missing], []), ([a], [missing]), ([a, a], []), ([a, b, a], [b]), ([], [a])]:
+        got = [(h.urlhash, h.score) for h in ix.search(inc, exc, now_ms=NOW)]
+        exp = [(h, s) for h, s, _ in orc.search(d, inc, exc, now_ms=NOW)]
+        assert got == exp
+
+
+def test_fold_overflow_paths():
+    """Adversarial posintext order (strictly increasing) forces the chunk- and
+    shard-level fold summaries to overflow; the exact fallbacks must agree."""
+    rng = np.random.default_rng(5)
+    for n in (3000, 9000):
+        rows = np.zeros((n, 40), dtype=np.uint8)
+        alpha = np.frombuffer(jl.ALPHA, dtype=np.uint8)
+        for i in range(n):
+            h = jl.key_to_hash((i + 1) << 20 | 7)
+            rows[i, :12] = np.frombuffer(h, dtype=np.uint8)
+        rows[:, 12:14] = np.frombuffer((15000).to_bytes(2, "big"), dtype=np.uint8)
+        rows[:, 17] = 0
+        rows[:, 18] = 50
+        rows[:, 21] = ord("t")
+        rows[:, 22:24] = np.frombuffer(b"en", dtype=np.uint8)
+        p = np.arange(1, n + 1) if n == 3000 else np.maximum.accumulate(rng.integers(1, 60000, n))
+        rows[:, 34] = (p >> 8) & 0xFF
+        rows[:, 35] = p & 0xFF
+        rows[:, 38] = rng.integers(0, 256, n)
+        rows[:, 33] = rng.integers(1, 20, n)
+        ix = RWIIndex(0)
+        for name, prof in _profiles():
+            exp, nm = orc.normalize_score(rows, orc.profile_from(prof), "en", NOW)
+            got = ix.normalize_score(rows, _rp(prof), "en", NOW)
+            assert np.array_equal(got, exp), name
+        ix.add(b"TERMover____", rows)
+        got = [(h.urlhash, h.score) for h in ix.search([b"TERMover____"], now_ms=NOW, k=200)]
+        exp = [(h, s) for h, s, _ in orc.search({b"TERMover____": rows}, [b"TERMover____"], now_ms=NOW, k=200)]
+        assert got == exp
+        ix.close()
+
+
+def test_put_list_validation():
+    ix = RWIIndex(0)
+    good = synth.build_index(synth.preset("dense")).list_rows(0)
+    bad = good.copy()
+    bad[3, 0] = ord("!")
+    with pytest.raises(Exception):
+        ix.add(b"TERMbad_____", bad)
+    unsorted = good[::-1].copy()
+    with pytest.raises(Exception):
+        ix.add(b"TERMuns_____", unsorted, sorted=True)
+    ix.add(b"TERMuns_____", unsorted, sorted=False)
+    assert ix.get_size(b"TERMuns_____") == len(good)
+    nolang = good.copy()
+    nolang[0, 22:24] = 0
+    with pytest.raises(Exception):
+        ix.add(b"TERMnol_____", nolang)
+    ix.close()
+
+
+@pytest.mark.slow
+def test_c1_sample_bit_exact():
+    """C1 (1M URLs x 10k words, 10M postings): 40 queries, full top-100."""
+    cfg = synth.preset("C1")
+    qs = synth.queries(cfg, 40, 2, 3, 1, qseed=21)
+    need = sorted({t for inc, exc in qs for t in inc + exc})
+    idx = synth.build_index(cfg, terms=np.array(need))
+    ix = RWIIndex(0)
+    for t in need:
+        if idx.sizes[t]:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+    d = idx.as_dict()
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW) for inc, exc in qs]
+    got = ix.search_batch(batch)
+    for q, g in zip(batch, got):
+        exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=100)
+        assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp
+    ix.close()

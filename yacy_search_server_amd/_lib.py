@@ -1,0 +1,104 @@
+"""ctypes binding of libyrwi.so (the C ABI in include/yrwi.h).
+
+The library is the only compute path: if it is missing, or no GPU is visible
+when a context is opened, calls fail loudly -- there is no CPU fallback."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyrwi.so")
+
+PROFILE_FIELDS = [
+    "coeff_domlength", "coeff_date", "coeff_wordsintitle", "coeff_wordsintext",
+    "coeff_phrasesintext", "coeff_llocal", "coeff_lother", "coeff_urllength", "coeff_urlcomps",
+    "coeff_hitcount", "coeff_posintext", "coeff_posofphrase", "coeff_posinphrase",
+    "coeff_authority", "coeff_worddistance", "coeff_appurl", "coeff_app_dc_title",
+    "coeff_app_dc_creator", "coeff_app_dc_subject", "coeff_app_dc_description", "coeff_appemph",
+    "coeff_catindexof", "coeff_cathasimage", "coeff_cathasaudio", "coeff_cathasvideo",
+    "coeff_cathasapp", "coeff_urlcompintoplist", "coeff_descrcompintoplist", "coeff_prefer",
+    "coeff_termfrequency", "coeff_language", "coeff_citation",
+]
+
+ERRORS = {
+    -1: "YRWI_E_ARG", -2: "YRWI_E_HASH", -3: "YRWI_E_UNSORTED", -4: "YRWI_E_HIP",
+    -5: "YRWI_E_NOMEM", -6: "YRWI_E_RCCL", -7: "YRWI_E_NULL_LANGUAGE", -8: "YRWI_E_UNSUPPORTED",
+    -9: "YRWI_E_LIMIT",
+}
+
+
+class CProfile(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in PROFILE_FIELDS]
+
+
+class CHit(ctypes.Structure):
+    _fields_ = [("urlhash", ctypes.c_uint8 * 12), ("tiebreak", ctypes.c_int32), ("score", ctypes.c_int64)]
+
+
+class CQuery(ctypes.Structure):
+    _fields_ = [("incl", ctypes.c_void_p), ("nincl", ctypes.c_int32),
+                ("excl", ctypes.c_void_p), ("nexcl", ctypes.c_int32),
+                ("max_distance", ctypes.c_int32), ("k", ctypes.c_int32),
+                ("profile", ctypes.POINTER(CProfile)), ("language", ctypes.c_char * 8),
+                ("now_ms", ctypes.c_int64)]
+
+
+class CStats(ctypes.Structure):
+    _fields_ = [("postings_in", ctypes.c_int64), ("joined", ctypes.c_int64), ("bytes_alg", ctypes.c_int64),
+                ("bytes_join", ctypes.c_int64), ("t_join_ns", ctypes.c_int64), ("t_norm_ns", ctypes.c_int64),
+                ("t_score_ns", ctypes.c_int64), ("t_total_ns", ctypes.c_int64),
+                ("n_join_launches", ctypes.c_int32), ("n_enum_steps", ctypes.c_int32),
+                ("n_test_steps", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+# every symbol include/yrwi.h declares, with its ctypes signature
+_VP = ctypes.c_void_p
+SIGNATURES = {
+    "yrwi_profile_default": (None, [ctypes.POINTER(CProfile)]),
+    "yrwi_profile_all_zero": (None, [ctypes.POINTER(CProfile)]),
+    "yrwi_profile_parse": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(CProfile)]),
+    "yrwi_open": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_VP)]),
+    "yrwi_open_shard": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                       ctypes.POINTER(_VP)]),
+    "yrwi_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "yrwi_close": (None, [_VP]),
+    "yrwi_last_error": (ctypes.c_char_p, [_VP]),
+    "yrwi_put_list": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, ctypes.c_int64, ctypes.c_int]),
+    "yrwi_list_size": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_index_stats": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_query": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.POINTER(CHit),
+                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CStats)]),
+    "yrwi_query_batch": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.POINTER(CHit), ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(CStats)]),
+    "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_normalize_score": (ctypes.c_int, [_VP, _VP, ctypes.c_int64, ctypes.POINTER(CProfile), ctypes.c_char_p,
+                                            ctypes.c_int64, _VP]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class YrwiError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"{ERRORS.get(rc, rc)}: {msg}")
+        self.rc = rc

@@ -279,6 +279,30 @@ int yrwi_synth_fill(const yrwi_synth_cfg* cfg, int32_t t0, int32_t t1, const int
   return 0;
 }
 
+// Fill the rows of an arbitrary term subset: term terms[i] starts at row offsets[i].
+int yrwi_synth_fill_terms(const yrwi_synth_cfg* cfg, const int32_t* terms, int32_t nterms, const int64_t* offsets,
+                          uint8_t* rows, int32_t nthreads) {
+  Gen g(cfg);
+  std::atomic<int32_t> next(0);
+  auto work = [&]() {
+    int32_t i;
+    while ((i = next.fetch_add(1)) < nterms) {
+      const int32_t t = terms[i];
+      uint8_t* out = rows + offsets[i] * 40;
+      for (int64_t ch = g.c.chunk_lo; ch < g.c.chunk_hi; ch++) {
+        g.walk(t, ch, [&](int64_t v) {
+          g.row(t, ch, v, out);
+          out += 40;
+        });
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < std::max(1, nthreads); i++) th.emplace_back(work);
+  for (auto& x : th) x.join();
+  return 0;
+}
+
 // Query stream: terms sampled proportionally to df (query-log-like), distinct
 // within a query.  out_terms[q*(max_incl+max_excl) + j]; -1 pads.  nincl/nexcl
 // per query are returned in out_nincl/out_nexcl.

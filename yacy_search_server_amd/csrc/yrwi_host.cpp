@@ -1,0 +1,919 @@
+// yrwi_host.cpp -- host runtime of libyrwi: index residency, query planning
+// (the Java-side decisions of TermSearch / joinContainers / joinConstructive),
+// batched device execution and the C ABI declared in include/yrwi.h.
+//
+// Planning rules restated here (paths relative to /root/reference/source/net/yacy):
+//   J1  AbstractIndex.searchConjunction :96-128, TermSearch :42-70
+//       (HandleSet: term hashes are a sorted set; a missing include term empties
+//        the result, a missing exclude term disables exclusion)
+//   J2  ReferenceContainer.joinContainers :334-366 (TreeMap key (int)(size*1000+i))
+//   J3  ReferenceContainer.joinConstructive :406-416 (int-wrapping step counts)
+// Everything per posting runs on the GPU (yrwi_kernels.hip).
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "yrwi_internal.h"
+
+using namespace yrwi;
+
+namespace {
+
+constexpr int64_t MAX_LIST = 53687091;  // RowSet.importRowSet: 2^31 bytes of 40-byte rows
+
+int8_t AHP[256];
+struct AhpInit {
+  AhpInit() {
+    const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    for (int i = 0; i < 256; i++) AHP[i] = -1;
+    for (int i = 0; i < 64; i++) AHP[(uint8_t)a[i]] = (int8_t)i;
+  }
+} ahp_init;
+
+struct KeyT {
+  uint64_t hi;
+  uint32_t lo;
+  bool operator<(const KeyT& o) const { return hi < o.hi || (hi == o.hi && lo < o.lo); }
+  bool operator==(const KeyT& o) const { return hi == o.hi && lo == o.lo; }
+};
+
+bool key_of(const uint8_t* h, KeyT* k) {
+  uint64_t x = 0;
+  for (int j = 0; j < 10; j++) {
+    if (AHP[h[j]] < 0) return false;
+    x = (x << 6) | (uint64_t)AHP[h[j]];
+  }
+  if (AHP[h[10]] < 0 || AHP[h[11]] < 0) return false;
+  uint32_t c10 = (uint32_t)AHP[h[10]], c11 = (uint32_t)AHP[h[11]];
+  k->hi = (x << 4) | (c10 >> 2);
+  k->lo = ((c10 & 3u) << 6) | c11;
+  return true;
+}
+
+// Java int arithmetic
+inline int32_t add32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+inline int32_t mul32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+inline int log2j(int32_t x) {
+  int l = 0;
+  while (x > 0) { x >>= 1; l++; }
+  return l;
+}
+
+struct ListRec {
+  uint64_t* khi = nullptr;
+  uint8_t* klo = nullptr;
+  uint8_t* rows = nullptr;
+  int64_t n = 0;
+  DList dl() const { return DList{khi, klo, rows, n}; }
+};
+
+// bump allocator over device chunks
+struct Arena {
+  std::vector<std::pair<uint8_t*, size_t>> chunks;
+  size_t used = 0, cur = 0, total_used = 0, min_chunk;
+  explicit Arena(size_t mc) : min_chunk(mc) {}
+  uint8_t* alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (bytes == 0) bytes = 256;
+    while (cur < chunks.size() && used + bytes > chunks[cur].second) {
+      cur++;
+      used = 0;
+    }
+    if (cur >= chunks.size()) {
+      size_t sz = std::max(bytes, min_chunk);
+      void* p = nullptr;
+      if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
+      chunks.push_back({(uint8_t*)p, sz});
+      cur = chunks.size() - 1;
+      used = 0;
+    }
+    uint8_t* p = chunks[cur].first + used;
+    used += bytes;
+    total_used += bytes;
+    return p;
+  }
+  // only call when no kernel uses arena memory any more
+  void reset() {
+    if (chunks.size() > 1) {
+      size_t need = total_used + (1 << 20);
+      for (auto& c : chunks) hipFree(c.first);
+      chunks.clear();
+      void* p = nullptr;
+      if (hipMalloc(&p, std::max(need, min_chunk)) == hipSuccess)
+        chunks.push_back({(uint8_t*)p, std::max(need, min_chunk)});
+    }
+    used = 0;
+    cur = 0;
+    total_used = 0;
+  }
+  size_t capacity() const {
+    size_t s = 0;
+    for (auto& c : chunks) s += c.second;
+    return s;
+  }
+  void release() {
+    for (auto& c : chunks) hipFree(c.first);
+    chunks.clear();
+  }
+};
+
+struct Plan {
+  bool empty = true;
+  std::vector<const ListRec*> seq;   // fold order
+  std::vector<const ListRec*> excl;  // exclusion lists (empty: no exclusion)
+  int32_t maxd = YRWI_MAX_DISTANCE_ANY, k = 0;
+  yrwi_profile prof{};
+  uint8_t lang[2] = {0, 0};
+  int32_t lang_ok = 0;
+  int64_t now_ms = 0;
+  int64_t postings_in = 0;
+  // runtime container
+  DList cont{nullptr, nullptr, nullptr, 0};
+  uint8_t* removed = nullptr;
+};
+
+}  // namespace
+
+struct yrwi_ctx {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  std::map<KeyT, ListRec> lists;
+  Arena index_mem{(size_t)1 << 30};
+  Arena arena{(size_t)256 << 20};
+  std::string err;
+  int64_t npostings = 0;
+  std::vector<hipEvent_t> evpool;
+  size_t evnext = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  hipEvent_t event() {
+    if (evnext >= evpool.size()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      evpool.push_back(e);
+    }
+    return evpool[evnext++];
+  }
+};
+
+#define HIPCHK(ctx, x)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (x);                                                              \
+    if (_e != hipSuccess) return (ctx)->fail(YRWI_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class T>
+static T* arena_alloc(yrwi_ctx* ctx, int64_t count) {
+  return reinterpret_cast<T*>(ctx->arena.alloc((size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+}
+
+template <class T>
+static int upload(yrwi_ctx* ctx, T* dst, const std::vector<T>& v) {
+  if (v.empty()) return 0;
+  HIPCHK(ctx, hipMemcpyAsync(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  return 0;
+}
+
+// ===================================================================== profile
+extern "C" void yrwi_profile_default(yrwi_profile* p) {
+  std::memset(p, 0, sizeof(*p));
+  p->coeff_appemph = 5; p->coeff_appurl = 12; p->coeff_app_dc_creator = 1;
+  p->coeff_app_dc_description = 10; p->coeff_app_dc_subject = 2; p->coeff_app_dc_title = 14;
+  p->coeff_authority = 5; p->coeff_cathasapp = 0; p->coeff_cathasaudio = 0; p->coeff_cathasimage = 0;
+  p->coeff_cathasvideo = 0; p->coeff_catindexof = 0; p->coeff_date = 9; p->coeff_domlength = 10;
+  p->coeff_hitcount = 1; p->coeff_language = 2; p->coeff_llocal = 0; p->coeff_lother = 7;
+  p->coeff_phrasesintext = 0; p->coeff_posinphrase = 0; p->coeff_posintext = 4; p->coeff_posofphrase = 0;
+  p->coeff_termfrequency = 8; p->coeff_urlcomps = 7; p->coeff_urllength = 6; p->coeff_worddistance = 10;
+  p->coeff_wordsintext = 3; p->coeff_wordsintitle = 2; p->coeff_urlcompintoplist = 2;
+  p->coeff_descrcompintoplist = 2; p->coeff_prefer = 0; p->coeff_citation = 10;
+}
+
+extern "C" void yrwi_profile_all_zero(yrwi_profile* p) { std::memset(p, 0, sizeof(*p)); }
+
+// NumberTools.parseIntDecSubstring (NumberTools.java:91-124); false on NumberFormatException
+static bool parse_int_dec(const std::string& s, size_t start, int32_t* out) {
+  size_t end = s.size();
+  if (end <= start) return false;
+  size_t i = start;
+  while (i < end && s[i] == ' ') i++;
+  if (i >= end) return false;
+  int64_t result = 0;
+  bool neg = false;
+  int64_t limit = -2147483647LL;
+  char first = s[i];
+  if (first < '0') {
+    if (first == '-') { neg = true; limit = -2147483648LL; }
+    else if (first != '+') return false;
+    i++;
+    if (i == end) return false;
+  }
+  int64_t multmin = limit / 10;
+  while (i < end) {
+    char c = s[i++];
+    if (c < '0' || c > '9') break;
+    int d = c - '0';
+    if (result < multmin) return false;
+    result *= 10;
+    if (result < limit + d) return false;
+    result -= d;
+  }
+  *out = (int32_t)(neg ? result : -result);
+  return true;
+}
+
+// RankingProfile(String prefix, String profile) (RankingProfile.java:127-189)
+extern "C" int yrwi_profile_parse(const char* prefix, const char* ext, yrwi_profile* out) {
+  yrwi_profile_default(out);
+  if (!ext || !*ext) return 0;
+  std::string profile(ext);
+  if (profile[0] == '{' && profile.back() == '}') profile = profile.substr(1, profile.size() - 2);
+  auto trim = [](const std::string& x) {
+    size_t a = 0, b = x.size();
+    while (a < b && (unsigned char)x[a] <= ' ') a++;
+    while (b > a && (unsigned char)x[b - 1] <= ' ') b--;
+    return x.substr(a, b - a);
+  };
+  profile = trim(profile);
+  std::vector<std::string> elts;
+  char sep = (profile.find('&') != std::string::npos && profile.find('&') > 0) ? '&' : ',';
+  {
+    // String.split drops trailing empty strings; empty elements are harmless here
+    size_t st = 0;
+    while (true) {
+      size_t p = profile.find(sep, st);
+      elts.push_back(profile.substr(st, p == std::string::npos ? std::string::npos : p - st));
+      if (p == std::string::npos) break;
+      st = p + 1;
+    }
+  }
+  std::string pre = prefix ? prefix : "";
+  std::map<std::string, int32_t> coeff;
+  for (auto& elt : elts) {
+    std::string e = trim(elt);
+    if (pre.empty() || e.compare(0, pre.size(), pre) == 0) {
+      size_t p = e.find('=');
+      if (p != std::string::npos && p > 0 && e.size() > p + 1) {
+        int32_t v;
+        if (parse_int_dec(e, p + 1, &v)) coeff[e.substr(pre.size(), p - pre.size())] = v;
+      }
+    }
+  }
+  struct F { const char* n; int32_t yrwi_profile::*f; };
+  static const F fields[] = {
+      {"domlength", &yrwi_profile::coeff_domlength}, {"date", &yrwi_profile::coeff_date},
+      {"wordsintitle", &yrwi_profile::coeff_wordsintitle}, {"wordsintext", &yrwi_profile::coeff_wordsintext},
+      {"phrasesintext", &yrwi_profile::coeff_phrasesintext}, {"llocal", &yrwi_profile::coeff_llocal},
+      {"lother", &yrwi_profile::coeff_lother}, {"urllength", &yrwi_profile::coeff_urllength},
+      {"urlcomps", &yrwi_profile::coeff_urlcomps}, {"hitcount", &yrwi_profile::coeff_hitcount},
+      {"posintext", &yrwi_profile::coeff_posintext}, {"posofphrase", &yrwi_profile::coeff_posofphrase},
+      {"posinphrase", &yrwi_profile::coeff_posinphrase}, {"authority", &yrwi_profile::coeff_authority},
+      {"worddistance", &yrwi_profile::coeff_worddistance}, {"appurl", &yrwi_profile::coeff_appurl},
+      {"appdescr", &yrwi_profile::coeff_app_dc_title}, {"appauthor", &yrwi_profile::coeff_app_dc_creator},
+      {"apptags", &yrwi_profile::coeff_app_dc_subject}, {"appref", &yrwi_profile::coeff_app_dc_description},
+      {"appemph", &yrwi_profile::coeff_appemph}, {"catindexof", &yrwi_profile::coeff_catindexof},
+      {"cathasimage", &yrwi_profile::coeff_cathasimage}, {"cathasaudio", &yrwi_profile::coeff_cathasaudio},
+      {"cathasvideo", &yrwi_profile::coeff_cathasvideo}, {"cathasapp", &yrwi_profile::coeff_cathasapp},
+      {"tf", &yrwi_profile::coeff_termfrequency}, {"urlcompintoplist", &yrwi_profile::coeff_urlcompintoplist},
+      {"descrcompintoplist", &yrwi_profile::coeff_descrcompintoplist}, {"prefer", &yrwi_profile::coeff_prefer},
+      {"language", &yrwi_profile::coeff_language}, {"citation", &yrwi_profile::coeff_citation}};
+  for (auto& f : fields) {
+    auto it = coeff.find(f.n);
+    if (it != coeff.end()) out->*(f.f) = it->second;
+  }
+  return 0;
+}
+
+// ===================================================================== context
+extern "C" int yrwi_get_unique_id(uint8_t id[128]) {
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return YRWI_E_RCCL;
+  static_assert(sizeof(u) == 128, "ncclUniqueId size");
+  std::memcpy(id, &u, 128);
+  return 0;
+}
+
+static int open_common(int device, yrwi_ctx** out) {
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return YRWI_E_HIP;
+  yrwi_ctx* ctx = new yrwi_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return YRWI_E_HIP;
+  }
+  *out = ctx;
+  return 0;
+}
+
+extern "C" int yrwi_open(int device, yrwi_ctx** out) { return open_common(device, out); }
+
+extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nccl_id[128], yrwi_ctx** out) {
+  if (world < 1 || (world & (world - 1)) || world > 64 || rank < 0 || rank >= world) return YRWI_E_ARG;
+  int rc = open_common(device, out);
+  if (rc) return rc;
+  (*out)->rank = rank;
+  (*out)->world = world;
+  if (world > 1) {
+    ncclUniqueId u;
+    std::memcpy(&u, nccl_id, 128);
+    if (ncclCommInitRank(&(*out)->comm, world, u, rank) != ncclSuccess) {
+      yrwi_close(*out);
+      *out = nullptr;
+      return YRWI_E_RCCL;
+    }
+  }
+  return 0;
+}
+
+extern "C" void yrwi_close(yrwi_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  ctx->arena.release();
+  ctx->index_mem.release();
+  for (auto e : ctx->evpool) hipEventDestroy(e);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" const char* yrwi_last_error(yrwi_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+// ======================================================================= index
+extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted) {
+  if (!ctx || !term || n < 0 || (n > 0 && !rows40)) return YRWI_E_ARG;
+  KeyT tk;
+  if (!key_of(term, &tk)) return ctx->fail(YRWI_E_HASH, "term hash is not well-formed Base64");
+  if (n > MAX_LIST) return ctx->fail(YRWI_E_LIMIT, "list longer than 53,687,091 rows (RowSet.importRowSet)");
+  hipSetDevice(ctx->device);
+  if (n == 0) {
+    auto it = ctx->lists.find(tk);
+    if (it != ctx->lists.end()) { ctx->npostings -= it->second.n; ctx->lists.erase(it); }
+    return 0;
+  }
+  std::vector<uint8_t> tmp;
+  const uint8_t* src = rows40;
+  if (!sorted) {
+    // RowSet sort; on duplicate url hashes the first occurrence wins (RowSet.mergeEnum)
+    std::vector<std::pair<KeyT, int64_t>> ks((size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+      if (!key_of(rows40 + i * 40, &ks[(size_t)i].first)) return ctx->fail(YRWI_E_HASH, "malformed url hash");
+      ks[(size_t)i].second = i;
+    }
+    std::stable_sort(ks.begin(), ks.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    tmp.reserve((size_t)n * 40);
+    for (size_t i = 0; i < ks.size(); i++) {
+      if (i > 0 && ks[i].first == ks[i - 1].first) continue;
+      tmp.insert(tmp.end(), rows40 + ks[i].second * 40, rows40 + ks[i].second * 40 + 40);
+    }
+    src = tmp.data();
+    n = (int64_t)(tmp.size() / 40);
+  }
+  ListRec L;
+  L.n = n;
+  L.rows = ctx->index_mem.alloc((size_t)n * 40);
+  L.khi = reinterpret_cast<uint64_t*>(ctx->index_mem.alloc((size_t)n * 8));
+  L.klo = ctx->index_mem.alloc((size_t)n);
+  int32_t* derr = reinterpret_cast<int32_t*>(ctx->index_mem.alloc(4));
+  if (!L.rows || !L.khi || !L.klo || !derr) return ctx->fail(YRWI_E_NOMEM, "device index allocation failed");
+  HIPCHK(ctx, hipMemcpyAsync(L.rows, src, (size_t)n * 40, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(derr, 0, 4, ctx->stream));
+  if (launch_validate_rows(L.rows, n, L.khi, L.klo, derr, ctx->stream)) return ctx->fail(YRWI_E_HIP, "validate launch");
+  int32_t herr = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (herr & 1) return ctx->fail(YRWI_E_HASH, "url hash is not well-formed Base64");
+  if (herr & 2) return ctx->fail(YRWI_E_NULL_LANGUAGE, "row with empty language cell (reference NPE)");
+  if (herr & 4) return ctx->fail(YRWI_E_UNSORTED, "rows are not strictly ascending by url hash");
+  auto it = ctx->lists.find(tk);
+  if (it != ctx->lists.end()) ctx->npostings -= it->second.n;
+  ctx->lists[tk] = L;
+  ctx->npostings += n;
+  return 0;
+}
+
+extern "C" int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n) {
+  KeyT tk;
+  if (!ctx || !n) return YRWI_E_ARG;
+  if (!key_of(term, &tk)) return ctx->fail(YRWI_E_HASH, "term hash is not well-formed Base64");
+  auto it = ctx->lists.find(tk);
+  *n = it == ctx->lists.end() ? 0 : it->second.n;
+  return 0;
+}
+
+extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes) {
+  if (!ctx) return YRWI_E_ARG;
+  if (nterms) *nterms = (int64_t)ctx->lists.size();
+  if (npostings) *npostings = ctx->npostings;
+  if (device_bytes) *device_bytes = (int64_t)(ctx->index_mem.capacity() + ctx->arena.capacity());
+  return 0;
+}
+
+// ================================================================== planning
+static int plan_query(yrwi_ctx* ctx, const yrwi_query_desc& d, Plan* P) {
+  P->maxd = d.max_distance;
+  P->k = std::min<int32_t>(std::max<int32_t>(d.k, 0), YRWI_MAX_K);
+  if (d.profile) P->prof = *d.profile; else yrwi_profile_default(&P->prof);
+  size_t ll = strnlen(d.language, sizeof(d.language));
+  P->lang_ok = ll == 2;
+  P->lang[0] = ll > 0 ? (uint8_t)d.language[0] : 0;
+  P->lang[1] = ll > 1 ? (uint8_t)d.language[1] : 0;
+  if (d.now_ms != 0) {
+    P->now_ms = d.now_ms;
+  } else {
+    P->now_ms = (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                    std::chrono::system_clock::now().time_since_epoch()).count();
+  }
+  if (d.nincl < 0 || d.nexcl < 0 || d.nincl > YRWI_MAX_TERMS || d.nexcl > YRWI_MAX_TERMS)
+    return ctx->fail(YRWI_E_ARG, "too many terms");
+  // HandleSet: sorted (Base64Order) set of term hashes
+  std::map<KeyT, int> inc, exc;
+  for (int i = 0; i < d.nincl; i++) {
+    KeyT k;
+    if (!key_of(d.incl + 12 * i, &k)) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
+    inc.emplace(k, i);
+  }
+  for (int i = 0; i < d.nexcl; i++) {
+    KeyT k;
+    if (!key_of(d.excl + 12 * i, &k)) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
+    exc.emplace(k, i);
+  }
+  P->empty = true;
+  P->postings_in = 0;
+  if (inc.empty()) return 0;
+  std::vector<const ListRec*> incl;
+  for (auto& kv : inc) {
+    auto it = ctx->lists.find(kv.first);
+    if (it == ctx->lists.end() || it->second.n == 0) return 0;  // conjunction: any missing term -> empty
+    incl.push_back(&it->second);
+  }
+  bool use_excl = !exc.empty();
+  std::vector<const ListRec*> excl;
+  for (auto& kv : exc) {
+    auto it = ctx->lists.find(kv.first);
+    if (it == ctx->lists.end() || it->second.n == 0) { use_excl = false; break; }
+    excl.push_back(&it->second);
+  }
+  // joinContainers: TreeMap<Long>((int)(size*1000 + count)); put overwrites equal keys
+  std::map<int64_t, const ListRec*> tm;
+  for (size_t c = 0; c < incl.size(); c++) tm[(int64_t)add32(mul32((int32_t)incl[c]->n, 1000), (int32_t)c)] = incl[c];
+  for (auto& kv : tm) P->seq.push_back(kv.second);
+  if (use_excl) P->excl = excl;
+  for (auto* l : incl) P->postings_in += l->n;
+  for (auto* l : P->excl) P->postings_in += l->n;
+  P->empty = false;
+  return 0;
+}
+
+// joinConstructive dispatch (ReferenceContainer.java:406-416); returns JoinMode
+static int32_t dispatch_mode(int64_t n1, int64_t n2) {
+  int32_t s1 = (int32_t)n1, s2 = (int32_t)n2;
+  int32_t high = s1 > s2 ? s1 : s2, low = s1 > s2 ? s2 : s1;
+  int32_t steps_enum = mul32(10, add32(add32(high, low), -1));
+  int32_t steps_test = mul32(mul32(12, log2j(high)), low);
+  if (steps_enum > steps_test) return s1 < s2 ? JM_TEST_LARGE_B : JM_TEST_LARGE_A;
+  return JM_ENUM;
+}
+
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// algorithmic bytes of one join step
+static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
+  if (mode == JM_ENUM) return 12 * (na + nb);
+  int64_t ns = std::min(na, nb), nl = std::max(na, nb);
+  int64_t lg = 0;
+  while ((ns << lg) < nl) lg++;  // ceil(log2(nl/ns))
+  return 12 * (ns + std::min(nl, ns * (lg + 1)));
+}
+
+struct Timing {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> kjoin;
+  hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
+};
+
+// Run the join/exclusion phase of all plans; leaves each plan's container in P.cont.
+static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
+  for (auto& P : plans) {
+    if (P.empty) { P.cont = DList{nullptr, nullptr, nullptr, 0}; continue; }
+    P.cont = P.seq[0]->dl();
+  }
+  size_t maxsteps = 0;
+  for (auto& P : plans) if (!P.empty) maxsteps = std::max(maxsteps, P.seq.size() - 1);
+  std::vector<int64_t> mh;
+  for (size_t s = 0; s < maxsteps; s++) {
+    std::vector<JoinQ> jobs;
+    std::vector<int> owner;
+    std::vector<int64_t> tile_base;
+    int64_t tiles = 0;
+    for (size_t qi = 0; qi < plans.size(); qi++) {
+      Plan& P = plans[qi];
+      if (P.empty || P.seq.size() <= s + 1 || P.cont.n == 0) continue;
+      JoinQ J{};
+      J.A = P.cont;
+      J.B = P.seq[s + 1]->dl();
+      J.mode = dispatch_mode(J.A.n, J.B.n);
+      J.maxd = P.maxd;
+      J.now_ms = P.now_ms;
+      int64_t cap = std::min(J.A.n, J.B.n);
+      J.out_rows = arena_alloc<uint8_t>(ctx, cap * 40);
+      J.out_khi = arena_alloc<uint64_t>(ctx, cap);
+      J.out_klo = arena_alloc<uint8_t>(ctx, cap);
+      J.ntiles = ceil_div(J.A.n + J.B.n, JOIN_TILE);
+      J.tile_base = tiles;
+      if (!J.out_rows || !J.out_khi || !J.out_klo) return ctx->fail(YRWI_E_NOMEM, "arena");
+      tile_base.push_back(tiles);
+      tiles += J.ntiles;
+      if (st) {
+        { int64_t kb = step_bytes(J.mode, J.A.n, J.B.n); st->bytes_alg += kb; st->bytes_join += kb; }
+        if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
+      }
+      jobs.push_back(J);
+      owner.push_back((int)qi);
+    }
+    if (jobs.empty()) break;
+    const int nj = (int)jobs.size();
+    int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
+    for (int j = 0; j < nj; j++) jobs[j].m_out = d_mout + j;
+    JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
+    int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
+    int64_t* d_split = arena_alloc<int64_t>(ctx, tiles);
+    uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
+    int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
+    int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
+    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+    hipEvent_t e0 = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
+    if (launch_join_step(d_jobs, d_tb, nj, tiles, d_split, d_pairs, d_cnt, d_off, false, ctx->stream, e0, e1))
+      return ctx->fail(YRWI_E_HIP, "join launch");
+    if (tm) tm->kjoin.push_back({e0, e1});
+    if (st) st->n_join_launches++;
+    mh.assign((size_t)nj, 0);
+    HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int j = 0; j < nj; j++) {
+      Plan& P = plans[(size_t)owner[(size_t)j]];
+      P.cont = DList{jobs[(size_t)j].out_khi, jobs[(size_t)j].out_klo, jobs[(size_t)j].out_rows, mh[(size_t)j]};
+    }
+  }
+  // exclusion (excludeContainers :373-388): mark container rows present in an exclude list
+  {
+    std::vector<JoinQ> jobs;
+    std::vector<int64_t> tile_base;
+    int64_t tiles = 0;
+    for (auto& P : plans) {
+      P.removed = nullptr;
+      if (P.empty || P.cont.n == 0 || P.excl.empty()) continue;
+      P.removed = arena_alloc<uint8_t>(ctx, P.cont.n);
+      if (!P.removed) return ctx->fail(YRWI_E_NOMEM, "arena");
+      HIPCHK(ctx, hipMemsetAsync(P.removed, 0, (size_t)P.cont.n, ctx->stream));
+      for (auto* E : P.excl) {
+        JoinQ J{};
+        J.A = P.cont;
+        J.B = E->dl();
+        J.mode = JM_MARK;
+        J.maxd = YRWI_MAX_DISTANCE_ANY;
+        J.removed = P.removed;
+        J.ntiles = ceil_div(J.A.n + J.B.n, JOIN_TILE);
+        J.tile_base = tiles;
+        tile_base.push_back(tiles);
+        tiles += J.ntiles;
+        if (st) st->bytes_alg += 12 * E->n;
+        jobs.push_back(J);
+      }
+    }
+    if (!jobs.empty()) {
+      const int nj = (int)jobs.size();
+      JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
+      int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
+      int64_t* d_split = arena_alloc<int64_t>(ctx, tiles);
+      if (!d_jobs || !d_tb || !d_split) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+      if (launch_join_step(d_jobs, d_tb, nj, tiles, d_split, nullptr, nullptr, nullptr, true, ctx->stream, nullptr,
+                           nullptr))
+        return ctx->fail(YRWI_E_HIP, "exclude launch");
+    }
+  }
+  return 0;
+}
+
+// Normalise (+ cross-shard exchange), then either score+top-k (hits) or all scores.
+static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax, yrwi_hit* h_hits,
+                          int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
+  const int nq = (int)plans.size();
+  const int W = exchange ? ctx->world : 1;
+  std::vector<RankQ> rq((size_t)nq);
+  std::vector<int64_t> chunk_base((size_t)nq);
+  int64_t chunks = 0;
+  bool any_auth = false;
+  for (int qi = 0; qi < nq; qi++) {
+    Plan& P = plans[(size_t)qi];
+    RankQ& R = rq[(size_t)qi];
+    std::memset(&R, 0, sizeof(R));
+    R.rows = P.cont.rows;
+    R.removed = P.removed;
+    R.n = P.empty ? 0 : P.cont.n;
+    R.nchunks = ceil_div(R.n, CHUNK);
+    R.chunk_base = chunks;
+    chunk_base[(size_t)qi] = chunks;
+    chunks += R.nchunks;
+    R.prof = P.prof;
+    R.lang[0] = P.lang[0];
+    R.lang[1] = P.lang[1];
+    R.lang_ok = P.lang_ok;
+    R.now_ms = P.now_ms;
+    R.k = P.k;
+    R.want_authority = P.prof.coeff_authority > 12 && R.n > 0;
+    R.idx_tag = W > 1 ? (uint32_t)ctx->rank << 28 : 0u;
+    if (R.want_authority) {
+      if (W > 1) return ctx->fail(YRWI_E_UNSUPPORTED, "authority ranking across shards is not implemented");
+      uint64_t cap = 1;
+      while (cap < (uint64_t)(2 * R.n)) cap <<= 1;
+      R.hkeys = arena_alloc<uint64_t>(ctx, (int64_t)cap);
+      R.hcnt = arena_alloc<uint32_t>(ctx, (int64_t)cap);
+      if (!R.hkeys || !R.hcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+      R.hmask = cap - 1;
+      HIPCHK(ctx, hipMemsetAsync(R.hkeys, 0, cap * 8, ctx->stream));
+      HIPCHK(ctx, hipMemsetAsync(R.hcnt, 0, cap * 4, ctx->stream));
+      any_auth = true;
+    }
+    if (st) {
+      st->joined += R.n;
+      st->bytes_alg += 23 * (int64_t)P.seq.size() * R.n;  // ranking feature bytes per surviving posting and term
+    }
+  }
+  (void)any_auth;
+  RankQ* d_q = arena_alloc<RankQ>(ctx, nq);
+  int64_t* d_cb = arena_alloc<int64_t>(ctx, nq);
+  ChunkSum* d_cs = arena_alloc<ChunkSum>(ctx, chunks);
+  ShardSum* d_ss = arena_alloc<ShardSum>(ctx, nq);
+  ShardSum* d_all = W > 1 ? arena_alloc<ShardSum>(ctx, (int64_t)nq * W) : d_ss;
+  NormState* d_norm = arena_alloc<NormState>(ctx, nq);
+  if (!d_q || !d_cb || !d_cs || !d_ss || !d_all || !d_norm) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base)) return YRWI_E_HIP;
+  HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
+  if (launch_reduce(d_q, d_cb, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (W > 1) {
+    if (ncclAllGather(d_ss, d_all, sizeof(ShardSum) * nq, ncclChar, ctx->comm, ctx->stream) != ncclSuccess)
+      return ctx->fail(YRWI_E_RCCL, "allgather of shard summaries");
+  }
+  if (launch_combine(d_q, nq, d_all, W, d_norm, ctx->stream)) return ctx->fail(YRWI_E_HIP, "combine launch");
+  if (tm) { tm->tn = ctx->event(); hipEventRecord(tm->tn, ctx->stream); }
+
+  if (h_scores_all) {  // yrwi_normalize_score
+    int64_t* d_sc = arena_alloc<int64_t>(ctx, rq[0].n);
+    if (!d_sc) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (launch_score_all(d_q, d_cb, nq, chunks, d_norm, d_sc, ctx->stream)) return ctx->fail(YRWI_E_HIP, "score launch");
+    HIPCHK(ctx, hipMemcpyAsync(h_scores_all, d_sc, sizeof(int64_t) * rq[0].n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    NormState nsh;
+    HIPCHK(ctx, hipMemcpy(&nsh, d_norm, sizeof(nsh), hipMemcpyDeviceToHost));
+    if (nsh.D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
+    return 0;
+  }
+
+  // ---- score + per-chunk top-k
+  int32_t keff = 1;
+  for (auto& R : rq) keff = std::max(keff, R.k);
+  const int32_t kc = std::min<int32_t>(keff, CHUNK);  // per-chunk candidate list stride
+  Cand* d_cand = arena_alloc<Cand>(ctx, std::max<int64_t>(chunks, 1) * kc);
+  int32_t* d_ccnt = arena_alloc<int32_t>(ctx, std::max<int64_t>(chunks, 1));
+  if (!d_cand || !d_ccnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (launch_score(d_q, d_cb, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "score launch");
+  // ---- merge passes until one list per query
+  const int sort_n = keff <= 1024 ? 2048 : 8192;
+  const int64_t G = std::max<int64_t>(2, std::min<int64_t>(64, sort_n / keff));
+  int32_t in_stride = kc;
+  std::vector<int64_t> lists((size_t)nq), lbase((size_t)nq);
+  for (int qi = 0; qi < nq; qi++) { lists[(size_t)qi] = rq[(size_t)qi].nchunks; lbase[(size_t)qi] = chunk_base[(size_t)qi]; }
+  const Cand* cur = d_cand;
+  const int32_t* curc = d_ccnt;
+  bool first = true;
+  while (true) {
+    bool more = false;
+    for (auto L : lists) more |= L > 1;
+    if (!more && !first) break;
+    first = false;
+    std::vector<int64_t> gb, gn;
+    std::vector<int64_t> nl((size_t)nq), nb((size_t)nq);
+    for (int qi = 0; qi < nq; qi++) {
+      int64_t L = lists[(size_t)qi];
+      int64_t ng = std::max<int64_t>(1, ceil_div(L, G));
+      nb[(size_t)qi] = (int64_t)gb.size();
+      nl[(size_t)qi] = ng;
+      for (int64_t g = 0; g < ng; g++) {
+        gb.push_back(lbase[(size_t)qi] + g * G);
+        gn.push_back(std::max<int64_t>(0, std::min<int64_t>(G, L - g * G)));
+      }
+    }
+    const int64_t ngr = (int64_t)gb.size();
+    int64_t* d_gb = arena_alloc<int64_t>(ctx, ngr);
+    int64_t* d_gn = arena_alloc<int64_t>(ctx, ngr);
+    Cand* d_out = arena_alloc<Cand>(ctx, ngr * keff);
+    int32_t* d_oc = arena_alloc<int32_t>(ctx, ngr);
+    if (!d_gb || !d_gn || !d_out || !d_oc) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn)) return YRWI_E_HIP;
+    if (launch_merge(cur, curc, in_stride, d_gb, d_gn, ngr, keff, d_out, d_oc, keff, sort_n, ctx->stream))
+      return ctx->fail(YRWI_E_HIP, "merge launch");
+    in_stride = keff;
+    cur = d_out;
+    curc = d_oc;
+    lists = nl;
+    lbase = nb;
+  }
+  // after the loop every query owns exactly one list, at index qi
+  yrwi_hit* d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);
+  int32_t* d_nout = arena_alloc<int32_t>(ctx, nq);
+  if (!d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (launch_emit(d_q, nq, cur, curc, keff, kmax, d_hits, d_nout, ctx->stream)) return ctx->fail(YRWI_E_HIP, "emit launch");
+  if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
+  if (W == 1) {
+    HIPCHK(ctx, hipMemcpyAsync(h_hits, d_hits, sizeof(yrwi_hit) * nq * kmax, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(h_nout, d_nout, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+  }
+  // ---- multi-GPU: gather every shard's top-k, merge in shard (= url hash) order
+  yrwi_hit* d_allh = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax * W);
+  int32_t* d_alln = arena_alloc<int32_t>(ctx, (int64_t)nq * W);
+  if (!d_allh || !d_alln) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (ncclGroupStart() != ncclSuccess ||
+      ncclAllGather(d_hits, d_allh, sizeof(yrwi_hit) * nq * kmax, ncclChar, ctx->comm, ctx->stream) != ncclSuccess ||
+      ncclAllGather(d_nout, d_alln, sizeof(int32_t) * nq, ncclChar, ctx->comm, ctx->stream) != ncclSuccess ||
+      ncclGroupEnd() != ncclSuccess)
+    return ctx->fail(YRWI_E_RCCL, "allgather of top-k lists");
+  std::vector<yrwi_hit> allh((size_t)nq * kmax * W);
+  std::vector<int32_t> alln((size_t)nq * W);
+  HIPCHK(ctx, hipMemcpyAsync(allh.data(), d_allh, allh.size() * sizeof(yrwi_hit), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(alln.data(), d_alln, alln.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<NormState> nsh((size_t)nq);
+  HIPCHK(ctx, hipMemcpyAsync(nsh.data(), d_norm, nq * sizeof(NormState), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  for (int qi = 0; qi < nq; qi++) {
+    if (nsh[(size_t)qi].D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
+    std::vector<yrwi_hit> v;
+    for (int s = 0; s < W; s++) {
+      int32_t n = alln[(size_t)s * nq + qi];
+      const yrwi_hit* src = &allh[((size_t)s * nq + qi) * kmax];
+      v.insert(v.end(), src, src + n);
+    }
+    // stable: among equal (score, hashCode) the lower shard (smaller url hash) stays first
+    std::stable_sort(v.begin(), v.end(), [](const yrwi_hit& a, const yrwi_hit& b) {
+      if (a.score != b.score) return a.score > b.score;
+      return a.tiebreak > b.tiebreak;
+    });
+    int32_t n = 0;
+    const int32_t kq = std::min(plans[(size_t)qi].k, kmax);
+    for (size_t i = 0; i < v.size() && n < kq; i++) {
+      if (n > 0 && v[i].score == h_hits[(size_t)qi * kmax + n - 1].score &&
+          v[i].tiebreak == h_hits[(size_t)qi * kmax + n - 1].tiebreak)
+        continue;
+      h_hits[(size_t)qi * kmax + n] = v[i];
+      n++;
+    }
+    h_nout[qi] = n;
+  }
+  return 0;
+}
+
+static int64_t now_ns() {
+  return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax, yrwi_hit* out,
+                                int32_t* nout, yrwi_stats* st) {
+  if (!ctx || (nq > 0 && (!q || !out || !nout)) || nq < 0 || kmax < 1 || kmax > YRWI_MAX_K) return YRWI_E_ARG;
+  if (nq == 0) return 0;
+  hipSetDevice(ctx->device);
+  const int64_t t0 = now_ns();
+  if (st) std::memset(st, 0, sizeof(*st));
+  std::vector<Plan> plans((size_t)nq);
+  for (int i = 0; i < nq; i++) {
+    int rc = plan_query(ctx, q[i], &plans[(size_t)i]);
+    if (rc) return rc;
+    if (st) st->postings_in += plans[(size_t)i].postings_in;
+  }
+  ctx->arena.reset();
+  ctx->evnext = 0;
+  Timing tm;
+  tm.t0 = ctx->event();
+  hipEventRecord(tm.t0, ctx->stream);
+  int rc = run_join_phase(ctx, plans, st, &tm);
+  if (rc) return rc;
+  tm.tj = ctx->event();
+  hipEventRecord(tm.tj, ctx->stream);
+  rc = run_rank_phase(ctx, plans, kmax, out, nout, nullptr, st, &tm);
+  if (rc) return rc;
+  if (st) {
+    float ms = 0;
+    int64_t kj = 0;
+    for (auto& pr : tm.kjoin)
+      if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) kj += (int64_t)(ms * 1e6);
+    st->t_join_ns = kj;
+    if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns = (int64_t)(ms * 1e6);
+    if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns = (int64_t)(ms * 1e6);
+    st->t_total_ns = now_ns() - t0;
+  }
+  return 0;
+}
+
+extern "C" int yrwi_query(yrwi_ctx* ctx, const yrwi_query_desc* q, yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
+  if (!q) return YRWI_E_ARG;
+  int32_t kmax = std::max<int32_t>(1, std::min<int32_t>(q->k, YRWI_MAX_K));
+  return yrwi_query_batch(ctx, q, 1, kmax, out, nout, st);
+}
+
+extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nincl, const uint8_t* excl,
+                                 int32_t nexcl, int32_t max_distance, int64_t now_ms, uint8_t* rows_out,
+                                 int64_t cap_rows, int64_t* m) {
+  if (!ctx || !m) return YRWI_E_ARG;
+  *m = 0;
+  hipSetDevice(ctx->device);
+  yrwi_query_desc d{};
+  d.incl = incl;
+  d.nincl = nincl;
+  d.excl = excl;
+  d.nexcl = nexcl;
+  d.max_distance = max_distance;
+  d.k = 1;
+  d.now_ms = now_ms;
+  std::vector<Plan> plans(1);
+  int rc = plan_query(ctx, d, &plans[0]);
+  if (rc) return rc;
+  ctx->arena.reset();
+  rc = run_join_phase(ctx, plans, nullptr, nullptr);
+  if (rc) return rc;
+  const Plan& P = plans[0];
+  if (P.empty || P.cont.n == 0) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+  }
+  std::vector<uint8_t> rows((size_t)P.cont.n * 40), rem;
+  HIPCHK(ctx, hipMemcpyAsync(rows.data(), P.cont.rows, rows.size(), hipMemcpyDeviceToHost, ctx->stream));
+  if (P.removed) {
+    rem.resize((size_t)P.cont.n);
+    HIPCHK(ctx, hipMemcpyAsync(rem.data(), P.removed, rem.size(), hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  int64_t k = 0;
+  for (int64_t i = 0; i < P.cont.n; i++) {
+    if (!rem.empty() && rem[(size_t)i]) continue;
+    if (k >= cap_rows) return ctx->fail(YRWI_E_ARG, "rows_out capacity too small");
+    std::memcpy(rows_out + k * 40, rows.data() + i * 40, 40);
+    k++;
+  }
+  *m = k;
+  return 0;
+}
+
+extern "C" int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_t m, const yrwi_profile* prof,
+                                    const char* language, int64_t now_ms, int64_t* score_out) {
+  if (!ctx || (m > 0 && (!rows40 || !score_out))) return YRWI_E_ARG;
+  if (m <= 0) return 0;
+  if (m > MAX_LIST) return ctx->fail(YRWI_E_LIMIT, "container longer than 53,687,091 rows");
+  hipSetDevice(ctx->device);
+  ctx->arena.reset();
+  uint8_t* rows = arena_alloc<uint8_t>(ctx, m * 40);
+  uint64_t* khi = arena_alloc<uint64_t>(ctx, m);
+  uint8_t* klo = arena_alloc<uint8_t>(ctx, m);
+  int32_t* derr = arena_alloc<int32_t>(ctx, 1);
+  if (!rows || !khi || !klo || !derr) return ctx->fail(YRWI_E_NOMEM, "arena");
+  HIPCHK(ctx, hipMemcpyAsync(rows, rows40, (size_t)m * 40, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(derr, 0, 4, ctx->stream));
+  if (launch_validate_rows(rows, m, khi, klo, derr, ctx->stream)) return ctx->fail(YRWI_E_HIP, "validate launch");
+  int32_t herr = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (herr & 1) return ctx->fail(YRWI_E_HASH, "url hash is not well-formed Base64");
+  if (herr & 2) return ctx->fail(YRWI_E_NULL_LANGUAGE, "row with empty language cell (reference NPE)");
+  if (herr & 4) return ctx->fail(YRWI_E_UNSORTED, "container rows are not strictly ascending by url hash");
+  std::vector<Plan> plans(1);
+  Plan& P = plans[0];
+  P.empty = false;
+  P.cont = DList{khi, klo, rows, m};
+  P.removed = nullptr;
+  if (prof) P.prof = *prof; else yrwi_profile_default(&P.prof);
+  size_t ll = language ? strnlen(language, 8) : 0;
+  P.lang_ok = ll == 2;
+  P.lang[0] = ll > 0 ? (uint8_t)language[0] : 0;
+  P.lang[1] = ll > 1 ? (uint8_t)language[1] : 0;
+  P.now_ms = now_ms != 0 ? now_ms
+                         : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::system_clock::now().time_since_epoch()).count();
+  P.k = 1;
+  return run_rank_phase(ctx, plans, 1, nullptr, nullptr, score_out, nullptr, nullptr, false);
+}

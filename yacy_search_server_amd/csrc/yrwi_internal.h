@@ -1,0 +1,149 @@
+// yrwi_internal.h -- structures shared by the host runtime (yrwi_host.cpp) and
+// the gfx950 kernels (yrwi_kernels.hip).  Plain PODs only.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/yrwi.h"
+
+namespace yrwi {
+
+// ---------------------------------------------------------------- geometry
+constexpr int JOIN_TILE = 2048;      // merge-path items per join workgroup
+constexpr int JOIN_THREADS = 256;
+constexpr int JOIN_IPT = JOIN_TILE / JOIN_THREADS;
+constexpr int JOIN_MAXM = JOIN_TILE / 2 + 1;  // matches per tile <= min(#A, #B + 1)
+
+constexpr int CHUNK = 2048;          // container elements per rank/score workgroup
+constexpr int CHUNK_THREADS = 256;
+constexpr int CHUNK_IPT = CHUNK / CHUNK_THREADS;
+constexpr int SEGC = 16;             // fold segments kept per chunk summary
+constexpr int SSEG = 128;            // fold segments kept per shard summary
+constexpr int NF = 11;               // min/max int fields (virtualAge handled apart)
+
+constexpr int64_t DAY_MS = 86400000LL;
+
+// 72-bit url-hash key (Base64Order.enhancedCoder order == unsigned integer order):
+// hi = key >> 8 (chars 0..9 and the top 4 bits of char 10), lo = key & 0xFF.
+
+// A sorted posting list / container on the device (SoA keys + AoS rows).
+struct DList {
+  const uint64_t* khi;
+  const uint8_t* klo;
+  const uint8_t* rows;  // 40-byte WordReferenceRow
+  int64_t n;
+};
+
+// Feature rule of a join step (ReferenceContainer.joinConstructive :406-416).
+enum JoinMode : int32_t {
+  JM_ENUM = 0,        // joinConstructiveByEnumeration: join(Vars(A), B)
+  JM_TEST_LARGE_B = 1,// joinConstructiveByTest, small = A (acc), large = B: self-join of B
+  JM_TEST_LARGE_A = 2,// joinConstructiveByTest, small = B, large = A: self-join of A
+  JM_MARK = 3         // excludeDestructive: mark A rows present in B
+};
+
+struct JoinQ {
+  DList A, B;
+  int64_t tile_base;   // first global tile of this job
+  int64_t ntiles;
+  int32_t mode;
+  int32_t maxd;
+  uint8_t* removed;    // JM_MARK target (indexed like A)
+  uint64_t* out_khi;   // compacted output container (capacity min(nA, nB))
+  uint8_t* out_klo;
+  uint8_t* out_rows;
+  int64_t now_ms;
+  int64_t* m_out;      // number of output rows (written by the scan kernel)
+};
+
+// Per-chunk normalisation summary (ReferenceOrder.NormalizeWorker :163-210,
+// restated as an order-preserving reduction).
+struct ChunkSum {
+  int32_t nvalid;
+  int32_t first;        // container index of the first valid element, -1 if none
+  int32_t p_first, od_first, a_first;
+  int32_t pmax;         // max posintext over valid elements
+  int32_t M_rest, L_rest;  // max / last positive stored distance over the rest
+  int32_t mn[NF], mx[NF];  // over all valid elements
+  int32_t va_mn_rest, va_mx_rest;  // raw lastModified days over the rest
+  int32_t nseg, overflow;
+  double tf_mn, tf_mx;
+  uint32_t seg[SEGC];   // (P << 16) | (M << 8) | L, in order, P strictly increasing
+};
+
+struct ShardSum {
+  int32_t nvalid;
+  int32_t has_first;
+  int32_t p_first, od_first, a_first;
+  int32_t mn[NF], mx[NF];
+  int32_t va_mn_rest, va_mx_rest;
+  int32_t nseg, overflow;
+  double tf_mn, tf_mx;
+  int32_t maxdom;       // max host count (authority), -1 if not computed
+  int32_t pad;
+  uint32_t seg[SSEG];
+};
+
+struct NormState {
+  int32_t mn[NF], mx[NF];
+  int32_t va_mn, va_mx;
+  int32_t D;            // max.distance() after the fold; min.distance() == 0
+  int32_t maxdom;
+  int64_t nvalid;
+  double tf_mn, tf_mx;
+};
+
+// Field indices inside mn/mx.
+enum : int {
+  F_HITCOUNT = 0, F_LLOCAL, F_LOTHER, F_WORDSINTEXT, F_PHRASESINTEXT, F_POSINTEXT,
+  F_POSINPHRASE, F_POSOFPHRASE, F_URLLENGTH, F_URLCOMPS, F_WORDSINTITLE
+};
+
+struct RankQ {
+  const uint8_t* rows;     // container rows (sorted by url hash)
+  const uint8_t* removed;  // exclusion marks or nullptr
+  int64_t n;
+  int64_t chunk_base;
+  int64_t nchunks;
+  yrwi_profile prof;
+  uint8_t lang[2];
+  int32_t lang_ok;         // target language has exactly 2 chars
+  int64_t now_ms;
+  int32_t k;
+  int32_t want_authority;  // coeff_authority > 12
+  uint64_t* hkeys;         // authority host table (open addressing), nullptr if unused
+  uint32_t* hcnt;
+  uint64_t hmask;
+  uint32_t idx_tag;        // shard << 28, OR-ed into candidate indices
+  int32_t pad;
+};
+
+struct Cand {  // top-k candidate: sort descending on (k1, k2)
+  uint64_t k1;  // score ^ 2^63
+  uint64_t k2;  // ((hashCode ^ 2^31) << 32) | ~index
+};
+
+// ---------------------------------------------------------------- launchers
+// (defined in yrwi_kernels.hip; all asynchronous on `stream`)
+int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err,
+                         void* stream);
+int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
+                     int64_t* d_split, uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off,
+                     bool mark, void* stream, void* ev_begin, void* ev_end);
+int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
+int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
+int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
+                   NormState* d_norm, void* stream);
+int launch_score(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                 const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* stream);
+int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, const int64_t* d_grp_in_base,
+                 const int64_t* d_grp_in_n, int64_t ngroups, int32_t k, Cand* d_out, int32_t* d_out_cnt,
+                 int32_t out_stride, int sort_n, void* stream);
+int launch_emit(const RankQ* d_q, int32_t nq, const Cand* d_final, const int32_t* d_final_cnt,
+                int32_t stride, int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
+int launch_score_all(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                     const NormState* d_norm, int64_t* d_scores, void* stream);
+
+}  // namespace yrwi

@@ -1,0 +1,1260 @@
+// yrwi_kernels.hip -- gfx950 kernels of the YaCy RWI query hot path.
+//
+//   k_validate   put_list: url-hash keys (Base64Order) + row checks
+//   k_partition  merge-path split points of every join tile
+//   k_join       sorted-list intersection of ReferenceContainers by url hash
+//                (ReferenceContainer.joinConstructive :397-489) or exclusion
+//                marking (excludeDestructive :491-571)
+//   k_scan_tiles per-job exclusive scan of tile match counts (order preserving)
+//   k_compact    joined 40-byte rows (WordReferenceVars.join :465-499 and
+//                toRowEntry :301-322 -> WordReferenceRow ctor :116-161)
+//   k_reduce     per-chunk normalisation summary (ReferenceOrder.NormalizeWorker
+//                :163-210; WordReferenceVars.min/max :383-455)
+//   k_shard_fin  per-query, per-shard summary (ordered fold of chunk summaries)
+//   k_combine    settled min/max + max-distance fold over shards
+//   k_score      ReferenceOrder.cardinal :223-265 + per-chunk top-k in the
+//                WeakPriorityBlockingQueue order (:119-134, :414-425)
+//   k_merge      top-k merge of candidate lists
+//   k_emit       yrwi_hit records
+//
+// Java int/long semantics are reproduced with explicit uint32_t/uint64_t
+// arithmetic (wrap-around, shift counts masked with 31).  Built with
+// -ffp-contract=off so the one fp64 term (tf) rounds exactly like Java.
+
+#include <hip/hip_runtime.h>
+
+#include "yrwi_internal.h"
+
+namespace yrwi {
+
+// ------------------------------------------------------------- helpers
+__device__ __forceinline__ int ahpla(uint32_t c) {
+  if (c >= 'A' && c <= 'Z') return (int)c - 'A';
+  if (c >= 'a' && c <= 'z') return (int)c - 'a' + 26;
+  if (c >= '0' && c <= '9') return (int)c - '0' + 52;
+  if (c == '-') return 62;
+  if (c == '_') return 63;
+  return -1;
+}
+
+__device__ __forceinline__ int32_t add32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int32_t sub32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+__device__ __forceinline__ int32_t mul32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+__device__ __forceinline__ int32_t shl32(int32_t a, int32_t n) { return (int32_t)((uint32_t)a << (n & 31)); }
+__device__ __forceinline__ int32_t div32(int32_t a, int32_t b) {
+  if (b == -1) return (int32_t)(0u - (uint32_t)a);
+  return a / b;
+}
+__device__ __forceinline__ int64_t add64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__device__ __forceinline__ int32_t d2i(double d) {  // Java (int) cast
+  if (d != d) return 0;
+  if (d >= 2147483647.0) return 2147483647;
+  if (d <= -2147483648.0) return (int32_t)0x80000000u;
+  return (int32_t)d;
+}
+
+__device__ __forceinline__ int32_t micro_date_days(int64_t ms) { return (int32_t)((ms / DAY_MS) % 262144LL); }
+// microDateDays(reverseMicroDateDays(days)) (MicroDate.java:37-55)
+__device__ __forceinline__ int32_t clamp_days(int32_t days, int64_t now_ms) {
+  int64_t v = (int64_t)((uint64_t)(int64_t)days * (uint64_t)DAY_MS);
+  return micro_date_days(v < now_ms ? v : now_ms);
+}
+
+struct Row {
+  uint64_t w[5];
+  __device__ __forceinline__ uint32_t b(int i) const { return (uint32_t)(w[i >> 3] >> (8 * (i & 7))) & 0xFFu; }
+  __device__ __forceinline__ uint32_t u16(int i) const { return (b(i) << 8) | b(i + 1); }
+  __device__ __forceinline__ void set(int i, uint32_t v) {
+    const int s = 8 * (i & 7);
+    w[i >> 3] = (w[i >> 3] & ~(0xFFull << s)) | ((uint64_t)(v & 0xFFu) << s);
+  }
+};
+
+__device__ __forceinline__ Row load_row(const uint8_t* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  Row r;
+#pragma unroll
+  for (int i = 0; i < 5; i++) r.w[i] = q[i];
+  return r;
+}
+__device__ __forceinline__ void store_row(uint8_t* p, const Row& r) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 5; i++) q[i] = r.w[i];
+}
+
+// row byte offsets (WordReferenceRow.java:49-72)
+enum : int {
+  O_A = 12, O_S = 14, O_U = 16, O_W = 17, O_P = 19, O_D = 21, O_L = 22, O_X = 24, O_Y = 25,
+  O_M = 26, O_N = 27, O_G = 28, O_Z = 29, O_C = 33, O_T = 34, O_R = 36, O_O = 37, O_I = 38, O_K = 39
+};
+
+__device__ __forceinline__ bool key_le(uint64_t ah, uint32_t al, uint64_t bh, uint32_t bl) {
+  return ah < bh || (ah == bh && al <= bl);
+}
+
+template <class T>
+__device__ __forceinline__ int find_job(const int64_t* base, int n, T b) {
+  int lo = 0, hi = n - 1;  // largest j with base[j] <= b
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (base[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// wave (64-lane) inclusive scan / reductions
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v = max(v, t);
+  }
+  return v;
+}
+
+// block exclusive scan (sum) for 256 threads; returns exclusive prefix, total in *tot
+__device__ __forceinline__ int32_t block_excl_sum256(int32_t v, int32_t* sh /*4*/, int32_t* tot) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t inc = wave_incl_sum(v);
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  int32_t off = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i < wv) off += sh[i];
+    all += sh[i];
+  }
+  __syncthreads();
+  *tot = all;
+  return off + inc - v;
+}
+__device__ __forceinline__ int32_t block_excl_max256(int32_t v, int32_t* sh /*4*/) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t inc = wave_incl_max(v);
+  int32_t prev = __shfl_up(inc, 1, 64);
+  if (lane == 0) prev = -1;
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  int32_t off = -1;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (i < wv) off = max(off, sh[i]);
+  __syncthreads();
+  return max(off, prev);
+}
+
+// ====================================================== put_list validation
+// err bits: 1 = malformed hash, 2 = empty language cell, 4 = not strictly ascending
+__global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t* __restrict__ khi,
+                           uint8_t* __restrict__ klo, int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* r = rows + i * YRWI_ROW_BYTES;
+  int bad = 0;
+  auto keyof = [&](const uint8_t* h, uint64_t& hi, uint32_t& lo) {
+    uint64_t x = 0;
+    for (int j = 0; j < 10; j++) {
+      int c = ahpla(h[j]);
+      bad |= (c < 0);
+      x = (x << 6) | (uint64_t)(c & 63);
+    }
+    int c10 = ahpla(h[10]), c11 = ahpla(h[11]);
+    bad |= (c10 < 0) | (c11 < 0);
+    hi = (x << 4) | (uint64_t)((c10 & 63) >> 2);
+    lo = (uint32_t)(((c10 & 3) << 6) | (c11 & 63));
+  };
+  uint64_t hi;
+  uint32_t lo;
+  keyof(r, hi, lo);
+  int e = bad ? 1 : 0;
+  if (r[O_L] == 0 && r[O_L + 1] == 0) e |= 2;
+  if (i > 0) {
+    uint64_t ph;
+    uint32_t pl;
+    keyof(r - YRWI_ROW_BYTES, ph, pl);
+    if (!(ph < hi || (ph == hi && pl < lo))) e |= 4;
+  }
+  khi[i] = hi;
+  klo[i] = (uint8_t)lo;
+  if (e) atomicOr(err, e);
+}
+
+// =========================================================== join: partition
+__global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
+                            int64_t total_tiles, int64_t* __restrict__ split) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= total_tiles) return;
+  const int j = find_job(tile_base, njobs, b);
+  const JoinQ& J = jobs[j];
+  const int64_t nA = J.A.n, nB = J.B.n;
+  const int64_t d = (b - tile_base[j]) * JOIN_TILE;
+  int64_t lo = d - nB > 0 ? d - nB : 0, hi = d < nA ? d : nA;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    int64_t bj = d - 1 - mid;
+    uint64_t ah = J.A.khi[mid], bh = J.B.khi[bj];
+    bool le = ah < bh || (ah == bh && J.A.klo[mid] <= J.B.klo[bj]);
+    if (le) lo = mid + 1; else hi = mid;
+  }
+  split[b] = lo;
+}
+
+// joined worddistance (WordReferenceVars.distance :287-294 after join :465-499)
+__device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint8_t* rb, int mode) {
+  if (mode == JM_TEST_LARGE_B) return rb[O_I];
+  if (mode == JM_TEST_LARGE_A) return ra[O_I];
+  int pa = ((int)ra[O_T] << 8) | ra[O_T + 1], pb = ((int)rb[O_T] << 8) | rb[O_T + 1];
+  if (pa > 0 && pb > 0) {
+    int d = pa > pb ? pa - pb : pb - pa;
+    if (d != 0) return d;
+  }
+  return ra[O_I];
+}
+
+// ============================================================ join: tiles
+__global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
+                                                      const int64_t* __restrict__ tile_base, int njobs,
+                                                      const int64_t* __restrict__ split, uint2* __restrict__ pairs,
+                                                      int32_t* __restrict__ tile_cnt, int mark) {
+  __shared__ uint64_t sAh[JOIN_TILE];
+  __shared__ uint64_t sBh[JOIN_TILE + 1];
+  __shared__ uint8_t sAl[JOIN_TILE];
+  __shared__ uint8_t sBl[JOIN_TILE + 1];
+  __shared__ int32_t sScan[4];
+
+  const int64_t b = blockIdx.x;
+  const int j = find_job(tile_base, njobs, b);
+  const JoinQ& J = jobs[j];
+  const int64_t nA = J.A.n, nB = J.B.n;
+  const int64_t t = b - tile_base[j];
+  const int64_t d0 = t * JOIN_TILE;
+  const int64_t d1 = d0 + JOIN_TILE < nA + nB ? d0 + JOIN_TILE : nA + nB;
+  const int64_t a0 = split[b];
+  const int64_t a1 = (t + 1 < J.ntiles) ? split[b + 1] : nA;
+  const int64_t b0 = d0 - a0, b1 = d1 - a1;
+  const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
+  const int nbl = nb + (b1 < nB ? 1 : 0);  // + lookahead element B[b1]
+
+  for (int i = threadIdx.x; i < na; i += JOIN_THREADS) {
+    sAh[i] = J.A.khi[a0 + i];
+    sAl[i] = J.A.klo[a0 + i];
+  }
+  for (int i = threadIdx.x; i < nbl; i += JOIN_THREADS) {
+    sBh[i] = J.B.khi[b0 + i];
+    sBl[i] = J.B.klo[b0 + i];
+  }
+  __syncthreads();
+
+  const int dd0 = threadIdx.x * JOIN_IPT;
+  const int dtot = na + nb;
+  int ia = 0, ib = 0;
+  if (dd0 < dtot) {
+    int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      int bj = dd0 - 1 - mid;
+      if (key_le(sAh[mid], sAl[mid], sBh[bj], sBl[bj])) lo = mid + 1; else hi = mid;
+    }
+    ia = lo;
+    ib = dd0 - lo;
+  }
+  int32_t ma[JOIN_IPT], mb[JOIN_IPT];
+  uint32_t mbits = 0;
+#pragma unroll
+  for (int s = 0; s < JOIN_IPT; s++) {
+    ma[s] = 0;
+    mb[s] = 0;
+    if (dd0 + s < dtot) {
+      bool takeA;
+      if (ia >= na) takeA = false;
+      else if (ib >= nb) takeA = true;
+      else takeA = key_le(sAh[ia], sAl[ia], sBh[ib], sBl[ib]);
+      if (takeA) {
+        if (ib < nbl && sAh[ia] == sBh[ib] && sAl[ia] == sBl[ib]) {
+          ma[s] = ia;
+          mb[s] = ib;
+          mbits |= 1u << s;
+        }
+        ia++;
+      } else {
+        ib++;
+      }
+    }
+  }
+  // maxDistance filter (ReferenceContainer.java:442,482); distance <= 65535 always
+  if (mbits && !mark && J.maxd < 65535) {
+#pragma unroll
+    for (int s = 0; s < JOIN_IPT; s++) {
+      if (mbits & (1u << s)) {
+        const uint8_t* ra = J.A.rows + (a0 + ma[s]) * YRWI_ROW_BYTES;
+        const uint8_t* rb = J.B.rows + (b0 + mb[s]) * YRWI_ROW_BYTES;
+        if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << s);
+      }
+    }
+  }
+  if (mark) {
+#pragma unroll
+    for (int s = 0; s < JOIN_IPT; s++)
+      if (mbits & (1u << s)) J.removed[a0 + ma[s]] = 1;
+    return;
+  }
+  const int32_t cnt = __popc(mbits);
+  int32_t tot;
+  int32_t off = block_excl_sum256(cnt, sScan, &tot);
+  uint2* out = pairs + b * (int64_t)JOIN_MAXM;
+#pragma unroll
+  for (int s = 0; s < JOIN_IPT; s++) {
+    if (mbits & (1u << s)) {
+      out[off] = make_uint2((uint32_t)(a0 + ma[s]), (uint32_t)(b0 + mb[s]));
+      off++;
+    }
+  }
+  if (threadIdx.x == 0) tile_cnt[b] = tot;
+}
+
+// ============================================================ join: scan
+__global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jobs,
+                                                    const int64_t* __restrict__ tile_base,
+                                                    const int32_t* __restrict__ tile_cnt,
+                                                    int64_t* __restrict__ tile_off) {
+  __shared__ int32_t sScan[4];
+  const JoinQ& J = jobs[blockIdx.x];
+  const int64_t base = tile_base[blockIdx.x];
+  int64_t running = 0;
+  for (int64_t t0 = 0; t0 < J.ntiles; t0 += 256) {
+    int64_t t = t0 + threadIdx.x;
+    int32_t c = t < J.ntiles ? tile_cnt[base + t] : 0;
+    int32_t tot;
+    int32_t ex = block_excl_sum256(c, sScan, &tot);
+    if (t < J.ntiles) tile_off[base + t] = running + ex;
+    running += tot;
+  }
+  if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
+}
+
+// ============================================================ join: compact
+// Joined row: J5 (WordReferenceVars.join :465-499) + J6 (toRowEntry :301-322 ->
+// WordReferenceRow ctor :116-161).
+__device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, int mode, int64_t now_ms) {
+  Row o;
+  if (mode == JM_ENUM) {
+    o = load_row(ra);
+    const Row B = load_row(rb);
+    int pa = (int)o.u16(O_T), pb = (int)B.u16(O_T);
+    int pos = 0, post = pa;
+    bool has = false;
+    if (pa > 0 && pb > 0) {
+      if (pa > pb) { pos = pa; post = pb; } else { pos = pb; }
+      has = true;
+    } else if (pa == 0) {
+      post = pb;
+    }
+    int oa = (int)o.b(O_O), ob = (int)B.b(O_O), r = (int)o.b(O_R), op = oa;
+    if (oa == ob) r = min(r, (int)B.b(O_R));
+    else if (oa > ob) { op = ob; r = (int)B.b(O_R); }
+    int w = max((int)o.u16(O_W), (int)B.u16(O_W));
+    int u = max((int)o.b(O_U), (int)B.b(O_U));
+    int p = max((int)o.u16(O_P), (int)B.u16(O_P));
+    int c = max((int)o.b(O_C), (int)B.b(O_C));
+    int dist = 0;
+    if (has && post > 0) dist = post > pos ? post - pos : pos - post;
+    if (dist == 0) dist = (int)o.b(O_I);
+    o.set(O_T, (uint32_t)post >> 8); o.set(O_T + 1, (uint32_t)post);
+    o.set(O_O, (uint32_t)op); o.set(O_R, (uint32_t)r);
+    o.set(O_W, (uint32_t)w >> 8); o.set(O_W + 1, (uint32_t)w);
+    o.set(O_U, (uint32_t)u);
+    o.set(O_P, (uint32_t)p >> 8); o.set(O_P + 1, (uint32_t)p);
+    o.set(O_C, (uint32_t)c);
+    o.set(O_I, (uint32_t)dist);
+  } else {
+    // by test: the large row joined with itself -> its own features, stored distance
+    o = load_row(mode == JM_TEST_LARGE_B ? rb : ra);
+  }
+  const int32_t mddlm = clamp_days((int32_t)o.u16(O_A), now_ms);
+  const int32_t mddct = micro_date_days(now_ms);
+  int32_t fresh = add32(mddlm, mul32(sub32(mddct, mddlm), 2));
+  if (fresh < 0) fresh = 0;
+  o.set(O_A, (uint32_t)mddlm >> 8); o.set(O_A + 1, (uint32_t)mddlm);
+  o.set(O_S, (uint32_t)fresh >> 8); o.set(O_S + 1, (uint32_t)fresh);
+  o.set(O_G, 0);
+  o.set(O_K, 0);
+  return o;
+}
+
+__global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
+                                                 int njobs, const uint2* __restrict__ pairs,
+                                                 const int32_t* __restrict__ tile_cnt,
+                                                 const int64_t* __restrict__ tile_off) {
+  const int64_t b = blockIdx.x;
+  const int32_t cnt = tile_cnt[b];
+  if (cnt == 0) return;
+  const int j = find_job(tile_base, njobs, b);
+  const JoinQ& J = jobs[j];
+  const int64_t off = tile_off[b];
+  const uint2* in = pairs + b * (int64_t)JOIN_MAXM;
+  for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const uint2 pr = in[i];
+    const uint8_t* ra = J.A.rows + (int64_t)pr.x * YRWI_ROW_BYTES;
+    const uint8_t* rb = J.B.rows + (int64_t)pr.y * YRWI_ROW_BYTES;
+    Row o = joined_row(ra, rb, J.mode, J.now_ms);
+    store_row(J.out_rows + (off + i) * YRWI_ROW_BYTES, o);
+    J.out_khi[off + i] = J.A.khi[pr.x];
+    J.out_klo[off + i] = J.A.klo[pr.x];
+  }
+}
+
+// ================================================================ ranking
+struct Feat {  // decoded WordReferenceVars fields of one row
+  int32_t f[NF];
+  int32_t a, p, od;
+  double tf;
+};
+
+__device__ __forceinline__ Feat decode(const Row& r) {
+  Feat x;
+  x.f[F_HITCOUNT] = (int32_t)r.b(O_C);
+  x.f[F_LLOCAL] = (int32_t)r.b(O_X);
+  x.f[F_LOTHER] = (int32_t)r.b(O_Y);
+  x.f[F_WORDSINTEXT] = (int32_t)r.u16(O_W);
+  x.f[F_PHRASESINTEXT] = (int32_t)r.u16(O_P);
+  x.f[F_POSINTEXT] = (int32_t)r.u16(O_T);
+  x.f[F_POSINPHRASE] = (int32_t)r.b(O_R);
+  x.f[F_POSOFPHRASE] = (int32_t)r.b(O_O);
+  x.f[F_URLLENGTH] = (int32_t)r.b(O_M);
+  x.f[F_URLCOMPS] = (int32_t)r.b(O_N);
+  x.f[F_WORDSINTITLE] = (int32_t)r.b(O_U);
+  x.a = (int32_t)r.u16(O_A);
+  x.p = x.f[F_POSINTEXT];
+  x.od = (int32_t)r.b(O_I);
+  // WordReferenceRow.termFrequency (WordReferenceRow.java:355-357)
+  x.tf = (double)x.f[F_HITCOUNT] / (double)(x.f[F_WORDSINTEXT] + x.f[F_WORDSINTITLE] + 1);
+  return x;
+}
+
+__device__ __forceinline__ uint64_t host36(const Row& r) {
+  uint64_t h = 0;
+#pragma unroll
+  for (int j = 6; j < 12; j++) h = (h << 6) | (uint64_t)(ahpla(r.b(j)) & 63);
+  return h;
+}
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int32_t wave_max_i(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int32_t wave_min_i(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int32_t wave_sum_i(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+constexpr int32_t BIG = 0x7FFFFFFF;
+
+__global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
+                                                         const int64_t* __restrict__ chunk_base, int nq,
+                                                         ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
+  __shared__ int32_t sI[4 * (2 * NF + 8)];
+  __shared__ double sD[8];
+  __shared__ int32_t sScan[4];
+  __shared__ int32_t sFirst[4];
+  __shared__ uint32_t sSegP[CHUNK_THREADS * CHUNK_IPT];
+  __shared__ uint32_t sSegM[CHUNK_THREADS * CHUNK_IPT];
+  __shared__ uint32_t sSegL[CHUNK_THREADS * CHUNK_IPT];
+
+  const int64_t b = blockIdx.x;
+  const int qi = find_job(chunk_base, nq, b);
+  const RankQ& Q = qs[qi];
+  const int64_t c = b - chunk_base[qi];
+  const int64_t e0 = c * CHUNK + (int64_t)threadIdx.x * CHUNK_IPT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+
+  bool valid[CHUNK_IPT];
+  Feat F[CHUNK_IPT];
+  int myfirst = BIG;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int64_t e = e0 + s;
+    valid[s] = e < Q.n && !(Q.removed && Q.removed[e]);
+    if (valid[s]) {
+      Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+      F[s] = decode(r);
+      if (myfirst == BIG) myfirst = s;
+      if (Q.want_authority) {
+        uint64_t key = host36(r) + 1;
+        uint64_t slot = mix64(key) & Q.hmask;
+        while (true) {
+          unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
+          if (prev == 0ull || prev == key) {
+            uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
+            atomicMax(&shard[qi].maxdom, (int32_t)cnt);
+            break;
+          }
+          slot = (slot + 1) & Q.hmask;
+        }
+      }
+    } else {
+      F[s] = Feat{};
+    }
+  }
+  // first valid element of the chunk
+  int32_t firstIdx = myfirst == BIG ? BIG : (int32_t)threadIdx.x * CHUNK_IPT + myfirst;
+  {
+    int32_t v = wave_min_i(firstIdx);
+    if (lane == 0) sFirst[wv] = v;
+    __syncthreads();
+    v = min(min(sFirst[0], sFirst[1]), min(sFirst[2], sFirst[3]));
+    __syncthreads();
+    firstIdx = v;
+  }
+  const int32_t firstT = firstIdx == BIG ? -1 : firstIdx / CHUNK_IPT;
+  const int32_t firstS = firstIdx == BIG ? -1 : firstIdx % CHUNK_IPT;
+
+  // rest = valid elements after the chunk's first one
+  bool rest[CHUNK_IPT];
+  int32_t nval = 0, pmax_rest = -1;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    rest[s] = valid[s] && !((int)threadIdx.x == firstT && s == firstS);
+    nval += valid[s] ? 1 : 0;
+    if (rest[s]) pmax_rest = max(pmax_rest, F[s].p);
+  }
+  // local fold segments (records of the prefix max of posintext over the rest)
+  const int32_t lpin = block_excl_max256(pmax_rest, sScan);
+  bool isrec[CHUNK_IPT];
+  int32_t LP = lpin, nrec = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    isrec[s] = rest[s] && F[s].p > LP;
+    if (isrec[s]) { LP = F[s].p; nrec++; }
+  }
+  // backward pass: per record, max od and the last positive od (keyed by element
+  // position so that a max over keys selects the latest one)
+  int32_t recM[CHUNK_IPT];
+  uint32_t recL[CHUNK_IPT];
+  int32_t accM = 0;
+  uint32_t accL = 0;
+#pragma unroll
+  for (int s = CHUNK_IPT - 1; s >= 0; s--) {
+    recM[s] = 0;
+    recL[s] = 0;
+    if (rest[s]) {
+      accM = max(accM, F[s].od);
+      if (accL == 0 && F[s].od > 0)
+        accL = (((uint32_t)threadIdx.x * CHUNK_IPT + (uint32_t)s + 1u) << 8) | (uint32_t)F[s].od;
+    }
+    if (isrec[s]) {
+      recM[s] = accM;
+      recL[s] = accL;
+      accM = 0;
+      accL = 0;
+    }
+  }
+  int32_t nsegTot;
+  int32_t segOff = block_excl_sum256(nrec, sScan, &nsegTot);
+  // assemble segments in LDS (capacity CHUNK: every element could be a record)
+  {
+    int32_t o = segOff;
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++) {
+      if (isrec[s]) {
+        sSegP[o] = (uint32_t)F[s].p;
+        sSegM[o] = (uint32_t)recM[s];
+        sSegL[o] = recL[s];
+        o++;
+      }
+    }
+  }
+  __syncthreads();
+  // the continuation piece (elements before this thread's first record) belongs to segment segOff-1
+  if (segOff > 0 && (accM > 0 || accL > 0)) {
+    atomicMax(&sSegM[segOff - 1], (uint32_t)accM);
+    if (accL > 0) atomicMax(&sSegL[segOff - 1], accL);
+  }
+  __syncthreads();
+
+  // block reductions of the min/max fields
+  int32_t mn[NF], mx[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
+  int32_t vamn = BIG, vamx = -1, pmax = -1;
+  double tfmn = 1e300, tfmx = -1e300;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    if (valid[s]) {
+#pragma unroll
+      for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], F[s].f[f]); mx[f] = max(mx[f], F[s].f[f]); }
+      tfmn = fmin(tfmn, F[s].tf);
+      tfmx = fmax(tfmx, F[s].tf);
+      pmax = max(pmax, F[s].p);
+    }
+    if (rest[s]) { vamn = min(vamn, F[s].a); vamx = max(vamx, F[s].a); }
+  }
+  const int NI = 2 * NF + 4;
+  int32_t vals[2 * NF + 4];
+#pragma unroll
+  for (int f = 0; f < NF; f++) { vals[f] = wave_min_i(mn[f]); vals[NF + f] = wave_max_i(mx[f]); }
+  vals[2 * NF + 0] = wave_min_i(vamn);
+  vals[2 * NF + 1] = wave_max_i(vamx);
+  vals[2 * NF + 2] = wave_max_i(pmax);
+  vals[2 * NF + 3] = wave_sum_i(nval);
+  tfmn = wave_min_d(tfmn);
+  tfmx = wave_max_d(tfmx);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NI; i++) sI[wv * NI + i] = vals[i];
+    sD[wv] = tfmn;
+    sD[4 + wv] = tfmx;
+  }
+  // first element info, owned by thread firstT
+  __shared__ int32_t sFirstInfo[3];
+  if ((int)threadIdx.x == firstT) {
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++)
+      if (s == firstS) { sFirstInfo[0] = F[s].p; sFirstInfo[1] = F[s].od; sFirstInfo[2] = F[s].a; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ChunkSum& S = out[b];
+    for (int f = 0; f < NF; f++) {
+      int32_t a = BIG, z = -1;
+      for (int w = 0; w < 4; w++) { a = min(a, sI[w * NI + f]); z = max(z, sI[w * NI + NF + f]); }
+      S.mn[f] = a;
+      S.mx[f] = z;
+    }
+    int32_t a = BIG, z = -1, pm = -1, nv = 0;
+    for (int w = 0; w < 4; w++) {
+      a = min(a, sI[w * NI + 2 * NF]);
+      z = max(z, sI[w * NI + 2 * NF + 1]);
+      pm = max(pm, sI[w * NI + 2 * NF + 2]);
+      nv += sI[w * NI + 2 * NF + 3];
+    }
+    S.va_mn_rest = a;
+    S.va_mx_rest = z;
+    S.pmax = pm;
+    S.nvalid = nv;
+    S.tf_mn = fmin(fmin(sD[0], sD[1]), fmin(sD[2], sD[3]));
+    S.tf_mx = fmax(fmax(sD[4], sD[5]), fmax(sD[6], sD[7]));
+    if (firstIdx != BIG) {
+      S.first = (int32_t)(c * CHUNK + firstIdx);
+      S.p_first = sFirstInfo[0];
+      S.od_first = sFirstInfo[1];
+      S.a_first = sFirstInfo[2];
+    } else {
+      S.first = -1;
+      S.p_first = S.od_first = S.a_first = 0;
+    }
+    int32_t Mr = 0;
+    uint32_t Lkey = 0;
+    for (int i = 0; i < nsegTot; i++) { Mr = max(Mr, (int32_t)sSegM[i]); Lkey = max(Lkey, sSegL[i]); }
+    S.M_rest = Mr;
+    S.L_rest = (int32_t)(Lkey & 0xFFu);
+    S.nseg = nsegTot;
+    S.overflow = nsegTot > SEGC ? 1 : 0;
+    if (nsegTot <= SEGC)
+      for (int i = 0; i < nsegTot; i++)
+        S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
+  }
+}
+
+// ------------------------------------------------- fold piece bookkeeping
+struct SegList {
+  uint32_t* seg;
+  int32_t cap;
+  int32_t n;
+  int32_t overflow;
+  int32_t prun;  // running prefix max of the rest (-1: none yet)
+  __device__ void add(int32_t P, int32_t M, int32_t L) {
+    if (P > prun) {
+      if (n < cap) seg[n] = ((uint32_t)P << 16) | ((uint32_t)M << 8) | (uint32_t)L;
+      else overflow = 1;
+      n++;
+      prun = P;
+    } else if (n > 0 && n <= cap) {
+      uint32_t s = seg[n - 1];
+      uint32_t m = max((s >> 8) & 0xFFu, (uint32_t)M);
+      uint32_t l = L > 0 ? (uint32_t)L : (s & 0xFFu);
+      seg[n - 1] = (s & 0xFFFF0000u) | (m << 8) | l;
+    }
+  }
+};
+
+// walk every valid element of chunk c after its first one as a single-element piece
+__device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& L) {
+  const int64_t e0 = c * CHUNK, e1 = min((int64_t)(c + 1) * CHUNK, Q.n);
+  for (int64_t e = e0; e < e1; e++) {
+    if (e <= first) continue;
+    if (Q.removed && Q.removed[e]) continue;
+    const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
+    int32_t p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
+    int32_t od = r[O_I];
+    L.add(p, od, od);
+  }
+}
+
+// one wave per query: ordered combination of the chunk summaries of this shard
+__global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, const int64_t* __restrict__ chunk_base,
+                                                  const ChunkSum* __restrict__ cs, ShardSum* __restrict__ out) {
+  __shared__ uint32_t sSeg[SSEG];
+  const int qi = blockIdx.x;
+  const RankQ& Q = qs[qi];
+  const int lane = threadIdx.x;
+  const ChunkSum* C = cs + chunk_base[qi];
+  const int64_t nc = Q.nchunks;
+  ShardSum& S = out[qi];
+
+  // ---- min / max / counts / first chunk
+  int32_t mn[NF], mx[NF];
+  for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
+  double tfmn = 1e300, tfmx = -1e300;
+  int32_t nv = 0;
+  int64_t firstc = INT64_MAX;
+  for (int64_t c = lane; c < nc; c += 64) {
+    const ChunkSum& X = C[c];
+    if (X.nvalid == 0) continue;
+    nv += X.nvalid;
+    firstc = min(firstc, c);
+    for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], X.mn[f]); mx[f] = max(mx[f], X.mx[f]); }
+    tfmn = fmin(tfmn, X.tf_mn);
+    tfmx = fmax(tfmx, X.tf_mx);
+  }
+  for (int f = 0; f < NF; f++) { mn[f] = wave_min_i(mn[f]); mx[f] = wave_max_i(mx[f]); }
+  tfmn = wave_min_d(tfmn);
+  tfmx = wave_max_d(tfmx);
+  nv = wave_sum_i(nv);
+  {
+    int32_t lo = (int32_t)(firstc == INT64_MAX ? BIG : firstc);
+    firstc = wave_min_i(lo);
+  }
+  // virtualAge over the shard's rest: chunk rests + first elements of later chunks
+  int32_t vamn = BIG, vamx = -1;
+  for (int64_t c = lane; c < nc; c += 64) {
+    const ChunkSum& X = C[c];
+    if (X.nvalid == 0) continue;
+    vamn = min(vamn, X.va_mn_rest);
+    vamx = max(vamx, X.va_mx_rest);
+    if (c != firstc) { vamn = min(vamn, X.a_first); vamx = max(vamx, X.a_first); }
+  }
+  vamn = wave_min_i(vamn);
+  vamx = wave_max_i(vamx);
+
+  // ---- ordered fold pieces
+  SegList L{sSeg, SSEG, 0, 0, -1};
+  if (lane == 0 && nv > 0) {
+    const ChunkSum& X = C[firstc];
+    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L);
+    else for (int i = 0; i < X.nseg; i++) L.add((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
+  }
+  L.n = __shfl(L.n, 0, 64);
+  L.prun = __shfl(L.prun, 0, 64);
+  L.overflow = __shfl(L.overflow, 0, 64);
+  int32_t nseg = L.n, prun = L.prun;
+  for (int64_t c0 = (nv > 0 ? firstc + 1 : nc); c0 < nc; c0 += 64) {
+    const int64_t c = c0 + lane;
+    int32_t nvc = 0, pm = -1, Mall = 0, Lall = 0;
+    if (c < nc) {
+      const ChunkSum& X = C[c];
+      nvc = X.nvalid;
+      pm = X.pmax;
+      Mall = max(X.od_first, X.M_rest);
+      Lall = X.L_rest > 0 ? X.L_rest : (X.od_first > 0 ? X.od_first : 0);
+    }
+    const bool fast = __all(nvc == 0 || pm <= prun);
+    if (fast) {
+      int32_t m = wave_max_i(nvc ? Mall : 0);
+      // last positive L in lane order
+      int32_t key = (nvc && Lall > 0) ? ((lane + 1) << 8) | Lall : 0;
+      key = wave_max_i(key);
+      if (lane == 0 && (m > 0 || key > 0)) L.add(-1, m, key & 0xFF);  // P=-1 <= prun: merge
+    } else if (lane == 0) {
+      for (int i = 0; i < 64 && c0 + i < nc; i++) {
+        const ChunkSum& X = C[c0 + i];
+        if (X.nvalid == 0) continue;
+        L.add(X.p_first, X.od_first, X.od_first);
+        if (X.overflow) rewalk_chunk(Q, c0 + i, X.first, L);
+        else for (int s = 0; s < X.nseg; s++) L.add((int32_t)(X.seg[s] >> 16), (int32_t)((X.seg[s] >> 8) & 0xFF), (int32_t)(X.seg[s] & 0xFF));
+      }
+    }
+    // broadcast lane 0's list state
+    L.n = __shfl(L.n, 0, 64);
+    L.prun = __shfl(L.prun, 0, 64);
+    L.overflow = __shfl(L.overflow, 0, 64);
+    prun = L.prun;
+    nseg = L.n;
+  }
+  (void)nseg;
+  __syncthreads();
+  if (lane == 0) {
+    S.nvalid = nv;
+    S.has_first = nv > 0;
+    if (nv > 0) {
+      S.p_first = C[firstc].p_first;
+      S.od_first = C[firstc].od_first;
+      S.a_first = C[firstc].a_first;
+    } else {
+      S.p_first = S.od_first = S.a_first = 0;
+    }
+    for (int f = 0; f < NF; f++) { S.mn[f] = mn[f]; S.mx[f] = mx[f]; }
+    S.va_mn_rest = vamn;
+    S.va_mx_rest = vamx;
+    S.tf_mn = tfmn;
+    S.tf_mx = tfmx;
+    S.nseg = L.n > SSEG ? SSEG : L.n;
+    S.overflow = L.overflow;
+  }
+  for (int i = lane; i < SSEG && i < L.n; i += 64) S.seg[i] = sSeg[i];
+}
+
+// fold state transition for one piece (WordReferenceVars.max :431-445)
+struct Fold {
+  int32_t P, A;
+  bool hasA;
+  __device__ void piece(int32_t Pj, int32_t M, int32_t Lp) {
+    int32_t Pe = max(P, Pj);
+    if (Pe > 0) {
+      int32_t d0 = hasA ? abs(Pe - A) : 0;
+      if (M > d0) { A = Pe + M; hasA = true; }
+    } else if (Lp > 0) {
+      A = Lp;
+      hasA = true;
+    }
+    P = Pe;
+  }
+  __device__ int32_t D() const { return (hasA && P > 0) ? abs(P - A) : 0; }
+};
+
+// one thread per query: combine `world` shard summaries in shard (= url-hash) order
+__global__ void k_combine(const RankQ* __restrict__ qs, int nq, const ShardSum* __restrict__ sh, int world,
+                          NormState* __restrict__ norm) {
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= nq) return;
+  const RankQ& Q = qs[qi];
+  NormState N;
+  for (int f = 0; f < NF; f++) { N.mn[f] = BIG; N.mx[f] = -1; }
+  N.tf_mn = 1e300;
+  N.tf_mx = -1e300;
+  N.va_mn = BIG;
+  N.va_mx = -1;
+  N.nvalid = 0;
+  N.maxdom = 0;
+  int gf = -1, ovf = 0;
+  for (int s = 0; s < world; s++) {
+    const ShardSum& X = sh[(int64_t)s * nq + qi];
+    if (X.nvalid == 0) continue;
+    if (gf < 0) gf = s;
+    N.nvalid += X.nvalid;
+    for (int f = 0; f < NF; f++) { N.mn[f] = min(N.mn[f], X.mn[f]); N.mx[f] = max(N.mx[f], X.mx[f]); }
+    N.tf_mn = fmin(N.tf_mn, X.tf_mn);
+    N.tf_mx = fmax(N.tf_mx, X.tf_mx);
+    // the very first element is min/max's clone: its virtualAge is clamped (:357-361)
+    int32_t af = (s == gf) ? clamp_days(X.a_first, Q.now_ms) : X.a_first;
+    N.va_mn = min(N.va_mn, min(af, X.va_mn_rest));
+    N.va_mx = max(N.va_mx, max(af, X.va_mx_rest));
+    N.maxdom = max(N.maxdom, X.maxdom);
+    ovf |= X.overflow;
+  }
+  Fold fd{0, 0, false};
+  if (gf >= 0) {
+    if (ovf && world == 1) {
+      // exact sequential fold over the whole container
+      bool first = true;
+      for (int64_t e = 0; e < Q.n; e++) {
+        if (Q.removed && Q.removed[e]) continue;
+        const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
+        int32_t p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
+        int32_t od = r[O_I];
+        if (first) { fd.P = p; first = false; }
+        else fd.piece(p, od, od);
+      }
+    } else {
+      for (int s = gf; s < world; s++) {
+        const ShardSum& X = sh[(int64_t)s * nq + qi];
+        if (X.nvalid == 0) continue;
+        if (s == gf) fd.P = X.p_first;
+        else fd.piece(X.p_first, X.od_first, X.od_first);
+        for (int i = 0; i < X.nseg; i++)
+          fd.piece((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
+      }
+    }
+  }
+  N.D = (ovf && world > 1) ? -1 : fd.D();
+  if (N.nvalid == 0) {
+    for (int f = 0; f < NF; f++) { N.mn[f] = 0; N.mx[f] = 0; }
+    N.va_mn = N.va_mx = 0;
+    N.tf_mn = N.tf_mx = 0.0;
+  }
+  norm[qi] = N;
+}
+
+// ------------------------------------------------------------------ scoring
+// ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265), settled min/max.
+__device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const NormState& N, const RankQ& Q,
+                                            int32_t hcount) {
+  const yrwi_profile& rk = Q.prof;
+  int32_t tfterm = 0;
+  if (!(N.tf_mx == N.tf_mn))
+    tfterm = shl32(d2i(((t.tf - N.tf_mn) * 256.0) / (N.tf_mx - N.tf_mn)), rk.coeff_termfrequency);
+  auto inv = [](int32_t tv, int32_t lo, int32_t hi, int32_t c) -> int32_t {
+    if (hi == lo) return 0;
+    return shl32(sub32(256, div32(shl32(sub32(tv, lo), 8), sub32(hi, lo))), c);
+  };
+  auto fwd = [](int32_t tv, int32_t lo, int32_t hi, int32_t c) -> int32_t {
+    if (hi == lo) return 0;
+    return shl32(div32(shl32(sub32(tv, lo), 8), sub32(hi, lo)), c);
+  };
+  const int dl = ahpla(r.b(11)) & 3;  // DigestURL.domLengthEstimation; << (8/20) == << 0
+  const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
+  int32_t s = shl32(256 - dln, rk.coeff_domlength);
+  s = add32(s, inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], rk.coeff_urlcomps));
+  s = add32(s, inv(t.f[F_URLLENGTH], N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], rk.coeff_urllength));
+  s = add32(s, inv(t.f[F_POSINTEXT], N.mn[F_POSINTEXT], N.mx[F_POSINTEXT], rk.coeff_posintext));
+  s = add32(s, inv(t.f[F_POSOFPHRASE], N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], rk.coeff_posofphrase));
+  s = add32(s, inv(t.f[F_POSINPHRASE], N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], rk.coeff_posinphrase));
+  s = add32(s, inv(t.od, 0, N.D, rk.coeff_worddistance));
+  s = add32(s, fwd(t.a, N.va_mn, N.va_mx, rk.coeff_date));
+  s = add32(s, fwd(t.f[F_WORDSINTITLE], N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], rk.coeff_wordsintitle));
+  s = add32(s, fwd(t.f[F_WORDSINTEXT], N.mn[F_WORDSINTEXT], N.mx[F_WORDSINTEXT], rk.coeff_wordsintext));
+  s = add32(s, fwd(t.f[F_PHRASESINTEXT], N.mn[F_PHRASESINTEXT], N.mx[F_PHRASESINTEXT], rk.coeff_phrasesintext));
+  s = add32(s, fwd(t.f[F_LLOCAL], N.mn[F_LLOCAL], N.mx[F_LLOCAL], rk.coeff_llocal));
+  s = add32(s, fwd(t.f[F_LOTHER], N.mn[F_LOTHER], N.mx[F_LOTHER], rk.coeff_lother));
+  s = add32(s, fwd(t.f[F_HITCOUNT], N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], rk.coeff_hitcount));
+  int64_t R = add64((int64_t)s, (int64_t)tfterm);  // + tf turns the sum into a long
+  if (rk.coeff_authority > 12) {
+    int32_t auth = div32(shl32(hcount, 8), add32(1, N.maxdom));  // ReferenceOrder.authority :213-216
+    R = add64(R, (int64_t)shl32(auth, rk.coeff_authority));
+  }
+  const uint32_t z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24);
+  const int32_t c255 = 255;
+  if (z & (1u << 28)) R = add64(R, shl32(c255, rk.coeff_appurl));
+  if (z & (1u << 25)) R = add64(R, shl32(c255, rk.coeff_app_dc_title));
+  if (z & (1u << 26)) R = add64(R, shl32(c255, rk.coeff_app_dc_creator));
+  if (z & (1u << 27)) R = add64(R, shl32(c255, rk.coeff_app_dc_subject));
+  if (z & (1u << 24)) R = add64(R, shl32(c255, rk.coeff_app_dc_description));
+  if (z & (1u << 29)) R = add64(R, shl32(c255, rk.coeff_appemph));
+  if (z & (1u << 0)) R = add64(R, shl32(c255, rk.coeff_catindexof));
+  if (z & (1u << 20)) R = add64(R, shl32(c255, rk.coeff_cathasimage));
+  if (z & (1u << 21)) R = add64(R, shl32(c255, rk.coeff_cathasaudio));
+  if (z & (1u << 22)) R = add64(R, shl32(c255, rk.coeff_cathasvideo));
+  if (z & (1u << 23)) R = add64(R, shl32(c255, rk.coeff_cathasapp));
+  if (Q.lang_ok && r.b(O_L) == Q.lang[0] && r.b(O_L + 1) == Q.lang[1]) R = add64(R, shl32(c255, rk.coeff_language));
+  return R;
+}
+
+__device__ __forceinline__ int32_t url_hashcode(const Row& r) {
+  int32_t h = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) h = add32(mul32(31, h), (int32_t)r.b(j));
+  return h;
+}
+
+__device__ __forceinline__ int32_t host_count(const RankQ& Q, const Row& r) {
+  uint64_t key = host36(r) + 1;
+  uint64_t slot = mix64(key) & Q.hmask;
+  while (true) {
+    uint64_t k = Q.hkeys[slot];
+    if (k == key) return (int32_t)Q.hcnt[slot];
+    if (k == 0) return 0;
+    slot = (slot + 1) & Q.hmask;
+  }
+}
+
+// bitonic sort, descending on (k1, k2), N entries in LDS, all threads participate
+template <int N, int NT>
+__device__ __forceinline__ void bitonic_desc(uint64_t* k1, uint64_t* k2) {
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < N / 2; i += NT) {
+        const int pos = 2 * i - (i & (stride - 1));
+        const int par = pos + stride;
+        const bool desc = (pos & size) == 0;
+        uint64_t a1 = k1[pos], a2 = k2[pos], b1 = k1[par], b2 = k2[par];
+        const bool a_lt_b = a1 < b1 || (a1 == b1 && a2 < b2);
+        if (a_lt_b == desc) {
+          k1[pos] = b1; k2[pos] = b2;
+          k1[par] = a1; k2[par] = a2;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// dedupe (equal score and hashCode: the TreeSet keeps the first arrival) and
+// compact the first `k` survivors of a sorted LDS list into out; returns count
+template <int N, int NT>
+__device__ __forceinline__ int32_t dedupe_take(const uint64_t* k1, const uint64_t* k2, int32_t k, Cand* out,
+                                               int32_t* sScan) {
+  constexpr int IPT = N / NT;
+  const int i0 = threadIdx.x * IPT;
+  int32_t keep = 0;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int s = 0; s < IPT; s++) {
+    const int i = i0 + s;
+    bool v = k2[i] != 0;
+    if (v && i > 0 && k1[i] == k1[i - 1] && (k2[i] >> 32) == (k2[i - 1] >> 32)) v = false;
+    if (v) { bits |= 1u << s; keep++; }
+  }
+  int32_t tot;
+  int32_t off;
+  if (NT == 256) {
+    off = block_excl_sum256(keep, sScan, &tot);
+  } else {
+    // generic NT (multiple of 64, <= 1024)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t inc = wave_incl_sum(keep);
+    if (lane == 63) sScan[wv] = inc;
+    __syncthreads();
+    int32_t o = 0, all = 0;
+    for (int w = 0; w < NT / 64; w++) { if (w < wv) o += sScan[w]; all += sScan[w]; }
+    __syncthreads();
+    off = o + inc - keep;
+    tot = all;
+  }
+#pragma unroll
+  for (int s = 0; s < IPT; s++) {
+    if (bits & (1u << s)) {
+      if (off < k) { out[off].k1 = k1[i0 + s]; out[off].k2 = k2[i0 + s]; }
+      off++;
+    }
+  }
+  return tot < k ? tot : k;
+}
+
+__global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
+                                                        const int64_t* __restrict__ chunk_base, int nq,
+                                                        const NormState* __restrict__ norm, Cand* __restrict__ cand,
+                                                        int32_t* __restrict__ cand_cnt, int32_t kc) {
+  __shared__ uint64_t s1[CHUNK];
+  __shared__ uint64_t s2[CHUNK];
+  __shared__ int32_t sScan[4];
+  __shared__ NormState sN;
+  const int64_t b = blockIdx.x;
+  const int qi = find_job(chunk_base, nq, b);
+  const RankQ& Q = qs[qi];
+  if (threadIdx.x == 0) sN = norm[qi];
+  __syncthreads();
+  const int64_t c = b - chunk_base[qi];
+  const int64_t e0 = c * CHUNK + (int64_t)threadIdx.x * CHUNK_IPT;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int64_t e = e0 + s;
+    const int li = threadIdx.x * CHUNK_IPT + s;
+    uint64_t a = 0, z = 0;
+    if (e < Q.n && !(Q.removed && Q.removed[e])) {
+      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+      const Feat t = decode(r);
+      const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
+      const int64_t score = cardinal(r, t, sN, Q, hc);
+      const int32_t h = url_hashcode(r);
+      a = (uint64_t)score ^ 0x8000000000000000ull;
+      z = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+    }
+    s1[li] = a;
+    s2[li] = z;
+  }
+  __syncthreads();
+  bitonic_desc<CHUNK, CHUNK_THREADS>(s1, s2);
+  const int32_t kq = Q.k < kc ? Q.k : kc;
+  int32_t n = dedupe_take<CHUNK, CHUNK_THREADS>(s1, s2, kq, cand + b * (int64_t)kc, sScan);
+  if (threadIdx.x == 0) cand_cnt[b] = n;
+}
+
+// merge: group g gathers lists [in_base[g], in_base[g]+in_n[g]) (each <= k valid
+// entries at stride in_stride) and writes its top-k list
+template <int SORTN>
+__global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, const int32_t* __restrict__ in_cnt,
+                                               int32_t in_stride, const int64_t* __restrict__ grp_base,
+                                               const int64_t* __restrict__ grp_n, int32_t k, Cand* __restrict__ out,
+                                               int32_t* __restrict__ out_cnt, int32_t out_stride) {
+  extern __shared__ uint64_t smem[];
+  uint64_t* s1 = smem;
+  uint64_t* s2 = smem + SORTN;
+  __shared__ int32_t sScan[16];
+  __shared__ int32_t sOff[65];
+  const int64_t g = blockIdx.x;
+  const int64_t base = grp_base[g], nl = grp_n[g];
+  // offsets of each list inside the LDS image
+  if (threadIdx.x == 0) {
+    int32_t o = 0;
+    for (int64_t l = 0; l < nl && l < 64; l++) { sOff[l] = o; o += in_cnt[base + l]; }
+    sOff[nl < 64 ? nl : 64] = o;
+  }
+  __syncthreads();
+  const int32_t total = sOff[nl < 64 ? nl : 64];
+  for (int i = threadIdx.x; i < SORTN; i += 1024) { s1[i] = 0; s2[i] = 0; }
+  __syncthreads();
+  for (int64_t l = 0; l < nl; l++) {
+    const int32_t c = in_cnt[base + l], o = sOff[l];
+    const Cand* src = in + (base + l) * (int64_t)in_stride;
+    for (int i = threadIdx.x; i < c; i += 1024) {
+      s1[o + i] = src[i].k1;
+      s2[o + i] = src[i].k2;
+    }
+  }
+  (void)total;
+  __syncthreads();
+  bitonic_desc<SORTN, 1024>(s1, s2);
+  int32_t n = dedupe_take<SORTN, 1024>(s1, s2, k, out + g * (int64_t)out_stride, sScan);
+  if (threadIdx.x == 0) out_cnt[g] = n;
+}
+
+__global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* __restrict__ fin,
+                       const int32_t* __restrict__ fin_cnt, int32_t stride, int32_t kmax,
+                       yrwi_hit* __restrict__ hits, int32_t* __restrict__ nout) {
+  const int qi = blockIdx.x;
+  const RankQ& Q = qs[qi];
+  const int32_t n = min(fin_cnt[qi], min(Q.k, kmax));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const Cand cd = fin[(int64_t)qi * stride + i];
+    const uint32_t idx = ~(uint32_t)cd.k2 & 0x0FFFFFFFu;
+    const uint8_t* r = Q.rows + (int64_t)idx * YRWI_ROW_BYTES;
+    yrwi_hit h;
+    for (int j = 0; j < 12; j++) h.urlhash[j] = r[j];
+    h.tiebreak = (int32_t)((uint32_t)(cd.k2 >> 32) ^ 0x80000000u);
+    h.score = (int64_t)(cd.k1 ^ 0x8000000000000000ull);
+    hits[(int64_t)qi * kmax + i] = h;
+  }
+  if (threadIdx.x == 0) nout[qi] = n;
+}
+
+// all scores of a container (yrwi_normalize_score)
+__global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
+                                                   const int64_t* __restrict__ chunk_base, int nq,
+                                                   const NormState* __restrict__ norm, int64_t* __restrict__ out) {
+  const int64_t b = blockIdx.x;
+  const int qi = find_job(chunk_base, nq, b);
+  const RankQ& Q = qs[qi];
+  const NormState N = norm[qi];
+  const int64_t c = b - chunk_base[qi];
+  for (int s = threadIdx.x; s < CHUNK; s += blockDim.x) {
+    const int64_t e = c * CHUNK + s;
+    if (e >= Q.n) break;
+    const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+    const Feat t = decode(r);
+    const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
+    out[e] = cardinal(r, t, N, Q, hc);
+  }
+}
+
+// ================================================================ launchers
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int rc(hipError_t e) { return e == hipSuccess ? 0 : YRWI_E_HIP; }
+
+int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_validate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), rows, n, khi, klo, err);
+  return rc(hipGetLastError());
+}
+
+int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
+                     int64_t* d_split, uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark,
+                     void* st, void* ev0, void* ev1) {
+  if (total_tiles <= 0) return 0;
+  hipLaunchKernelGGL(k_partition, dim3((unsigned)((total_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                     d_tile_base, njobs, total_tiles, d_split);
+  if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
+  hipLaunchKernelGGL(k_join, dim3((unsigned)total_tiles), dim3(JOIN_THREADS), 0, S(st), d_jobs, d_tile_base, njobs,
+                     d_split, d_pairs, d_tile_cnt, mark ? 1 : 0);
+  if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
+  if (!mark) {
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
+                       d_tile_off);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
+                       d_pairs, d_tile_cnt, d_tile_off);
+  }
+  return rc(hipGetLastError());
+}
+
+int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st) {
+  if (total_chunks > 0)
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_base, nq,
+                       d_chunks, d_shard);
+  hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
+  return rc(hipGetLastError());
+}
+
+int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world, NormState* d_norm,
+                   void* st) {
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, S(st), d_q, nq, d_shards, world, d_norm);
+  return rc(hipGetLastError());
+}
+
+int launch_score(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                 const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* st) {
+  if (total_chunks <= 0) return 0;
+  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_base, nq,
+                     d_norm, d_cand, d_cand_cnt, kc);
+  return rc(hipGetLastError());
+}
+
+int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, const int64_t* d_grp_in_base,
+                 const int64_t* d_grp_in_n, int64_t ngroups, int32_t k, Cand* d_out, int32_t* d_out_cnt,
+                 int32_t out_stride, int sort_n, void* st) {
+  if (ngroups <= 0) return 0;
+  if (sort_n == 2048) {
+    hipLaunchKernelGGL(k_merge<2048>, dim3((unsigned)ngroups), dim3(1024), 2 * 2048 * sizeof(uint64_t), S(st), d_in,
+                       d_in_cnt, in_stride, d_grp_in_base, d_grp_in_n, k, d_out, d_out_cnt, out_stride);
+  } else if (sort_n == 8192) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge<8192>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          2 * 8192 * sizeof(uint64_t));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_merge<8192>, dim3((unsigned)ngroups), dim3(1024), 2 * 8192 * sizeof(uint64_t), S(st), d_in,
+                       d_in_cnt, in_stride, d_grp_in_base, d_grp_in_n, k, d_out, d_out_cnt, out_stride);
+  } else {
+    return YRWI_E_ARG;
+  }
+  return rc(hipGetLastError());
+}
+
+int launch_emit(const RankQ* d_q, int32_t nq, const Cand* d_final, const int32_t* d_final_cnt, int32_t stride,
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
+  hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, stride, kmax,
+                     d_hits, d_nout);
+  return rc(hipGetLastError());
+}
+
+int launch_score_all(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+                     const NormState* d_norm, int64_t* d_scores, void* st) {
+  if (total_chunks <= 0) return 0;
+  hipLaunchKernelGGL(k_score_all, dim3((unsigned)total_chunks), dim3(256), 0, S(st), d_q, d_chunk_base, nq, d_norm,
+                     d_scores);
+  return rc(hipGetLastError());
+}
+
+}  // namespace yrwi

@@ -1,0 +1,245 @@
+"""Host-side mirror of YaCy's RWI query API over libyrwi (MI355X).
+
+Mirrors the reference interface of the hot path so a caller written against
+YaCy's classes finds the same names, argument meanings and "empty means no
+result" behaviour (paths relative to /root/reference/source/net/yacy):
+
+  RankingProfile           search/ranking/RankingProfile.java (defaults, external
+                           string form, allZero)
+  RWIIndex.add / get_size  kelondro/rwi/IndexCell.add (:289) / count
+  RWIIndex.term_search     kelondro/rwi/TermSearch (:42-70) ->
+                           ReferenceContainer.joinExcludeContainers (:310-326)
+  ReferenceOrder           search/ranking/ReferenceOrder.normalizeWith (:70) +
+                           cardinal (:223); settled (deterministic) min/max
+  RWIIndex.search          SearchEvent.RWIProcess.run (:601-631) -> addRWIs
+                           (:673-836) -> rwiStack top-k
+
+All posting work runs in libyrwi's HIP kernels; this module only marshals.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import CHit, CProfile, CQuery, CStats, YrwiError
+
+INTEGER_MAX = 2147483647
+MAX_RESULTS_RWI = 3000  # SearchEvent.java:118
+
+# external attribute names (RankingProfile.java:42-75) -> coefficient field
+_EXTERNAL = {
+    "domlength": "coeff_domlength", "date": "coeff_date", "wordsintitle": "coeff_wordsintitle",
+    "wordsintext": "coeff_wordsintext", "phrasesintext": "coeff_phrasesintext", "llocal": "coeff_llocal",
+    "lother": "coeff_lother", "urllength": "coeff_urllength", "urlcomps": "coeff_urlcomps",
+    "hitcount": "coeff_hitcount", "posintext": "coeff_posintext", "posofphrase": "coeff_posofphrase",
+    "posinphrase": "coeff_posinphrase", "authority": "coeff_authority", "worddistance": "coeff_worddistance",
+    "appurl": "coeff_appurl", "appdescr": "coeff_app_dc_title", "appauthor": "coeff_app_dc_creator",
+    "apptags": "coeff_app_dc_subject", "appref": "coeff_app_dc_description", "appemph": "coeff_appemph",
+    "catindexof": "coeff_catindexof", "cathasimage": "coeff_cathasimage", "cathasaudio": "coeff_cathasaudio",
+    "cathasvideo": "coeff_cathasvideo", "cathasapp": "coeff_cathasapp", "tf": "coeff_termfrequency",
+    "urlcompintoplist": "coeff_urlcompintoplist", "descrcompintoplist": "coeff_descrcompintoplist",
+    "prefer": "coeff_prefer", "language": "coeff_language", "citation": "coeff_citation",
+}
+
+
+class RankingProfile:
+    """search/ranking/RankingProfile.java.  Default = RankingProfile(ContentDomain.TEXT)."""
+
+    COEFF_MIN = 0
+    COEFF_MAX = 15
+
+    def __init__(self, prefix: Optional[str] = None, profile: Optional[str] = None):
+        self._c = CProfile()
+        if profile:
+            _lib.lib().yrwi_profile_parse((prefix or "").encode(), profile.encode(), ctypes.byref(self._c))
+        else:
+            _lib.lib().yrwi_profile_default(ctypes.byref(self._c))
+
+    def __getattr__(self, name):
+        if name.startswith("coeff_"):
+            return getattr(self._c, name)
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name.startswith("coeff_"):
+            setattr(self._c, name, int(value))
+        else:
+            object.__setattr__(self, name, value)
+
+    def all_zero(self) -> "RankingProfile":  # allZero() :200-233
+        _lib.lib().yrwi_profile_all_zero(ctypes.byref(self._c))
+        return self
+
+    @classmethod
+    def date(cls) -> "RankingProfile":  # "/date" modifier, htroot/yacysearch.java:495-499
+        p = cls().all_zero()
+        p.coeff_date = cls.COEFF_MAX
+        return p
+
+    @classmethod
+    def near(cls) -> "RankingProfile":  # "/near" modifier, htroot/yacysearch.java:489-494
+        p = cls().all_zero()
+        p.coeff_worddistance = cls.COEFF_MAX
+        return p
+
+    def to_external_map(self) -> dict:
+        return {k: getattr(self._c, v) for k, v in _EXTERNAL.items()}
+
+    @property
+    def c(self) -> CProfile:
+        return self._c
+
+
+@dataclass
+class Hit:
+    urlhash: bytes
+    score: int      # ReferenceOrder.cardinal
+    tiebreak: int   # ByteArray.hashCode(urlhash)
+
+
+@dataclass
+class Query:
+    include: Sequence[bytes]
+    exclude: Sequence[bytes] = ()
+    max_distance: int = INTEGER_MAX
+    k: int = 100
+    profile: Optional[RankingProfile] = None
+    language: str = "en"
+    now_ms: int = 0
+
+
+def _check(ctx, rc: int):
+    if rc != 0:
+        msg = _lib.lib().yrwi_last_error(ctx) if ctx else b""
+        raise YrwiError(rc, (msg or b"").decode(errors="replace"))
+
+
+def _hashes(hs: Sequence[bytes]) -> bytes:
+    out = b"".join(bytes(h) for h in hs)
+    if len(out) != 12 * len(hs):
+        raise ValueError("term hashes must be 12 bytes")
+    return out
+
+
+class RWIIndex:
+    """A device-resident reverse word index (one GPU, or one URL-hash shard).
+
+    rows: numpy uint8 arrays of shape (n, 40) -- WordReferenceRow rows, i.e. the
+    bytes of a RowSet chunkcache (RowCollection.java:68)."""
+
+    def __init__(self, device: int = 0, shard: Optional[Tuple[int, int, bytes]] = None):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        if shard is None:
+            _check(None, L.yrwi_open(device, ctypes.byref(h)))
+        else:
+            rank, world, uid = shard
+            _check(None, L.yrwi_open_shard(device, rank, world, uid, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if self._h:
+            _lib.lib().yrwi_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- index maintenance (IndexCell) ----
+    def add(self, term: bytes, rows: np.ndarray, sorted: bool = True) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, 40)
+        _check(self._h, _lib.lib().yrwi_put_list(self._h, bytes(term), rows.ctypes.data, len(rows), 1 if sorted else 0))
+
+    def get_size(self, term: bytes) -> int:
+        n = ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_list_size(self._h, bytes(term), ctypes.byref(n)))
+        return n.value
+
+    def stats(self) -> Tuple[int, int, int]:
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_index_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    # ---- TermSearch / joinExcludeContainers ----
+    def term_search(self, include: Sequence[bytes], exclude: Sequence[bytes] = (),
+                    max_distance: int = INTEGER_MAX, now_ms: int = 0) -> np.ndarray:
+        """The joined (and excluded) ReferenceContainer as (m, 40) uint8 rows."""
+        cap = 0
+        for t in include:
+            cap = max(cap, self.get_size(t))
+        out = np.zeros((max(cap, 1), 40), dtype=np.uint8)
+        m = ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_join_exclude(self._h, _hashes(include), len(include), _hashes(exclude),
+                                                     len(exclude), max_distance, now_ms, out.ctypes.data, cap,
+                                                     ctypes.byref(m)))
+        return out[:m.value].copy()
+
+    # ---- ReferenceOrder.normalizeWith + cardinal ----
+    def normalize_score(self, rows: np.ndarray, profile: Optional[RankingProfile] = None, language: str = "en",
+                        now_ms: int = 0) -> np.ndarray:
+        rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, 40)
+        out = np.zeros(len(rows), dtype=np.int64)
+        prof = profile or RankingProfile()
+        _check(self._h, _lib.lib().yrwi_normalize_score(self._h, rows.ctypes.data, len(rows), ctypes.byref(prof.c),
+                                                        language.encode(), now_ms, out.ctypes.data))
+        return out
+
+    # ---- full query: TermSearch -> normalise -> cardinal -> top-k ----
+    def search(self, include: Sequence[bytes], exclude: Sequence[bytes] = (), profile: Optional[RankingProfile] = None,
+               language: str = "en", max_distance: int = INTEGER_MAX, now_ms: int = 0, k: int = 100,
+               stats: Optional[CStats] = None) -> List[Hit]:
+        return self.search_batch([Query(include, exclude, max_distance, k, profile, language, now_ms)],
+                                 stats=stats)[0]
+
+    def search_batch(self, queries: Sequence[Query], stats: Optional[CStats] = None,
+                     kmax: Optional[int] = None) -> List[List[Hit]]:
+        nq = len(queries)
+        if nq == 0:
+            return []
+        kmax = kmax or max(1, min(MAX_RESULTS_RWI, max(q.k for q in queries)))
+        arr = (CQuery * nq)()
+        keep = []
+        for i, q in enumerate(queries):
+            inc = _hashes(q.include)
+            exc = _hashes(q.exclude)
+            ib = ctypes.create_string_buffer(inc, max(1, len(inc)))
+            eb = ctypes.create_string_buffer(exc, max(1, len(exc)))
+            prof = q.profile or RankingProfile()
+            keep += [ib, eb, prof]
+            arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
+            arr[i].nincl = len(q.include)
+            arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
+            arr[i].nexcl = len(q.exclude)
+            arr[i].max_distance = q.max_distance
+            arr[i].k = q.k
+            arr[i].profile = ctypes.pointer(prof.c)
+            arr[i].language = q.language.encode()[:7]
+            arr[i].now_ms = q.now_ms
+        hits = (CHit * (nq * kmax))()
+        nout = (ctypes.c_int32 * nq)()
+        st = stats if stats is not None else CStats()
+        _check(self._h, _lib.lib().yrwi_query_batch(self._h, arr, nq, kmax, hits, nout, ctypes.byref(st)))
+        res = []
+        for i in range(nq):
+            res.append([Hit(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score, hits[i * kmax + j].tiebreak)
+                        for j in range(nout[i])])
+        return res
+
+    def search_batch_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> None:
+        """Zero-marshalling batch call for benchmarks (pre-built ctypes arrays)."""
+        _check(self._h, _lib.lib().yrwi_query_batch(self._h, cq, nq, kmax, hits, nout, ctypes.byref(st)))
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(None, _lib.lib().yrwi_get_unique_id(buf))
+    return buf.raw

@@ -47,7 +47,9 @@ def _load():
         lib.yrwi_synth_counts.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int32, ctypes.c_void_p]
         lib.yrwi_synth_fill.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
-        lib.yrwi_synth_queries.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_uint64, ctypes.c_int32,
+        lib.yrwi_synth_fill_terms.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_void_p, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+        lib.yrwi_synth_queries.argtypes =[ctypes.POINTER(_Cfg), ctypes.c_uint64, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib = lib
@@ -158,16 +160,13 @@ def build_index(cfg: SynthConfig, terms: Optional[np.ndarray] = None, nthreads: 
     total = int(sizes.sum())
     rows = np.zeros((max(total, 1), 40), dtype=np.uint8)
     c = cfg._c()
-    if terms is None or len(terms) == cfg.n_terms:
+    if len(terms) == cfg.n_terms:
         lib.yrwi_synth_fill(ctypes.byref(c), 0, cfg.n_terms, offsets.ctypes.data, rows.ctypes.data, nthreads)
     else:
-        for t in terms:
-            t = int(t)
-            off = np.array([0], dtype=np.int64)
-            sub = rows[offsets[t]:offsets[t] + sizes[t]]
-            if sizes[t]:
-                lib.yrwi_synth_fill(ctypes.byref(c), t, t + 1, off.ctypes.data,
-                                    sub.ctypes.data, 1)
+        tl = np.ascontiguousarray(terms, dtype=np.int32)
+        offs = np.ascontiguousarray(offsets[tl], dtype=np.int64)
+        lib.yrwi_synth_fill_terms(ctypes.byref(c), tl.ctypes.data, len(tl), offs.ctypes.data,
+                                  rows.ctypes.data, nthreads)
     hashes = [term_hash(cfg, t) for t in range(cfg.n_terms)]
     return Index(cfg, rows[:total], offsets, sizes, hashes)
 
