@@ -1,0 +1,105 @@
+/* yrwi_jni.c -- JNI glue between net.yacy.kelondro.rwi.GpuRWI and libyrwi.
+ * UNVERIFIED (no JDK / jni.h in this image); see INTEGRATION.md.
+ * Build on a JDK host:
+ *   cc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
+ *      yrwi_jni.c -L../../yacy_search_server_amd -lyrwi -o libyrwi_jni.so */
+#include <jni.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "yrwi.h"
+
+static void to_profile(JNIEnv* env, jintArray a, yrwi_profile* p) {
+  if (a == NULL) { yrwi_profile_default(p); return; }
+  (*env)->GetIntArrayRegion(env, a, 0, 32, (jint*)p);
+}
+
+JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_open(JNIEnv* env, jclass c, jint dev) {
+  yrwi_ctx* ctx = NULL;
+  return yrwi_open(dev, &ctx) == 0 ? (jlong)(intptr_t)ctx : 0;
+}
+
+JNIEXPORT void JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_close(JNIEnv* env, jclass c, jlong ctx) {
+  yrwi_close((yrwi_ctx*)(intptr_t)ctx);
+}
+
+JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_putList(JNIEnv* env, jclass c, jlong ctx, jbyteArray term,
+                                                                jbyteArray rows, jint n, jint sorted) {
+  jbyte t[12];
+  (*env)->GetByteArrayRegion(env, term, 0, 12, t);
+  /* RowSet.chunkcache is pinned only for the H2D copy */
+  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
+  int rc = yrwi_put_list((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)t, (const uint8_t*)p, n, sorted);
+  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  return rc;
+}
+
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_joinExclude(JNIEnv* env, jclass c, jlong ctx,
+                                                                          jbyteArray incl, jint nincl, jbyteArray excl,
+                                                                          jint nexcl, jint maxd, jlong now) {
+  yrwi_ctx* x = (yrwi_ctx*)(intptr_t)ctx;
+  jbyte* ib = (*env)->GetByteArrayElements(env, incl, NULL);
+  jbyte* eb = (*env)->GetByteArrayElements(env, excl, NULL);
+  int64_t cap = 0, n;
+  for (int i = 0; i < nincl; i++) {
+    if (yrwi_list_size(x, (const uint8_t*)ib + 12 * i, &n) == 0 && n > cap) cap = n;
+  }
+  uint8_t* out = (uint8_t*)malloc((size_t)(cap > 0 ? cap : 1) * 40);
+  int64_t m = 0;
+  int rc = yrwi_join_exclude(x, (const uint8_t*)ib, nincl, (const uint8_t*)eb, nexcl, maxd, now, out, cap, &m);
+  (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
+  (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewByteArray(env, (jsize)(m * 40));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(m * 40), (const jbyte*)out);
+  }
+  free(out);
+  return res;  /* null on error (caller: yrwi_last_error) */
+}
+
+JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_normalizeScore(JNIEnv* env, jclass c, jlong ctx,
+                                                                             jbyteArray rows, jint m, jintArray prof,
+                                                                             jstring lang, jlong now) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  jlongArray res = (*env)->NewLongArray(env, m);
+  jlong* sc = (*env)->GetLongArrayElements(env, res, NULL);
+  void* r = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
+  int rc = yrwi_normalize_score((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)r, m, &p, l, now, (int64_t*)sc);
+  (*env)->ReleasePrimitiveArrayCritical(env, rows, r, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, res, sc, 0);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  return rc == 0 ? res : NULL;
+}
+
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_query(JNIEnv* env, jclass c, jlong ctx,
+                                                                    jbyteArray incl, jint nincl, jbyteArray excl,
+                                                                    jint nexcl, jint maxd, jint k, jintArray prof,
+                                                                    jstring lang, jlong now) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  yrwi_query_desc q;
+  memset(&q, 0, sizeof(q));
+  jbyte* ib = (*env)->GetByteArrayElements(env, incl, NULL);
+  jbyte* eb = (*env)->GetByteArrayElements(env, excl, NULL);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  q.incl = (const uint8_t*)ib; q.nincl = nincl;
+  q.excl = (const uint8_t*)eb; q.nexcl = nexcl;
+  q.max_distance = maxd; q.k = k; q.profile = &p; q.now_ms = now;
+  strncpy(q.language, l, sizeof(q.language) - 1);
+  yrwi_hit* hits = (yrwi_hit*)malloc(sizeof(yrwi_hit) * (size_t)(k > 0 ? k : 1));
+  int32_t n = 0;
+  int rc = yrwi_query((yrwi_ctx*)(intptr_t)ctx, &q, hits, &n, NULL);
+  (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
+  (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewByteArray(env, (jsize)(n * (jint)sizeof(yrwi_hit)));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * (jint)sizeof(yrwi_hit)), (const jbyte*)hits);
+  }
+  free(hits);
+  return res;
+}

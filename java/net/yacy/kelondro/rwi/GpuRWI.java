@@ -1,0 +1,87 @@
+// GpuRWI.java -- JNI binding of libyrwi (include/yrwi.h) for YaCy.
+//
+// UNVERIFIED: this image has no JDK (no javac, no jni.h), so this file and
+// java/jni/yrwi_jni.c are shipped as the binding a YaCy maintainer would add;
+// they have not been compiled here.  See INTEGRATION.md.
+//
+// Drop-in points (paths relative to source/net/yacy):
+//   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.joinExclude(...)
+//   kelondro/rwi/ReferenceContainer.java:310   -> GpuRWI.joinExclude(...)
+//   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.normalizeScore(...)
+//   search/query/SearchEvent.java:612-631      -> GpuRWI.query(...) (whole local RWI path)
+package net.yacy.kelondro.rwi;
+
+public final class GpuRWI implements AutoCloseable {
+
+    static { System.loadLibrary("yrwi_jni"); }  // links libyrwi.so
+
+    private long ctx;  // yrwi_ctx*
+
+    public GpuRWI(final int device) {
+        this.ctx = open(device);
+        if (this.ctx == 0) throw new IllegalStateException("yrwi_open failed");
+    }
+
+    /** IndexCell.add for a whole container: the RowSet chunkcache bytes (n * 40, sorted). */
+    public void putList(final byte[] termHash, final byte[] chunkcache, final int n) {
+        check(putList(this.ctx, termHash, chunkcache, n, 1));
+    }
+
+    /** TermSearch + joinExcludeContainers: returns the joined container's rows (m * 40 bytes). */
+    public byte[] joinExclude(final byte[][] include, final byte[][] exclude, final int maxDistance,
+                              final long nowMillis) {
+        return joinExclude(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
+                           maxDistance, nowMillis);
+    }
+
+    /** ReferenceOrder.normalizeWith + cardinal with settled min/max: one score per row. */
+    public long[] normalizeScore(final byte[] rows, final int m, final int[] profile32, final String language,
+                                 final long nowMillis) {
+        return normalizeScore(this.ctx, rows, m, profile32, language, nowMillis);
+    }
+
+    /** SearchEvent local RWI path: top-k (urlhash, cardinal) of one query. Output: k * 24 bytes
+     *  (12-byte url hash, int32 ByteArray.hashCode, int64 score), little endian. */
+    public byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+                        final int[] profile32, final String language, final long nowMillis) {
+        return query(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length, maxDistance, k,
+                     profile32, language, nowMillis);
+    }
+
+    @Override
+    public void close() {
+        if (this.ctx != 0) { close(this.ctx); this.ctx = 0; }
+    }
+
+    /** RankingProfile public coefficients in declaration order (RankingProfile.java:81-88). */
+    public static int[] profile32(final net.yacy.search.ranking.RankingProfile p) {
+        return new int[] {
+            p.coeff_domlength, p.coeff_date, p.coeff_wordsintitle, p.coeff_wordsintext, p.coeff_phrasesintext,
+            p.coeff_llocal, p.coeff_lother, p.coeff_urllength, p.coeff_urlcomps, p.coeff_hitcount,
+            p.coeff_posintext, p.coeff_posofphrase, p.coeff_posinphrase, p.coeff_authority, p.coeff_worddistance,
+            p.coeff_appurl, p.coeff_app_dc_title, p.coeff_app_dc_creator, p.coeff_app_dc_subject,
+            p.coeff_app_dc_description, p.coeff_appemph, p.coeff_catindexof, p.coeff_cathasimage,
+            p.coeff_cathasaudio, p.coeff_cathasvideo, p.coeff_cathasapp, p.coeff_urlcompintoplist,
+            p.coeff_descrcompintoplist, p.coeff_prefer, p.coeff_termfrequency, p.coeff_language, p.coeff_citation};
+    }
+
+    private static byte[] flatten(final byte[][] hashes) {
+        final byte[] b = new byte[12 * hashes.length];
+        for (int i = 0; i < hashes.length; i++) System.arraycopy(hashes[i], 0, b, 12 * i, 12);
+        return b;
+    }
+
+    private static void check(final int rc) {
+        if (rc != 0) throw new IllegalStateException("libyrwi error " + rc);
+    }
+
+    private static native long open(int device);
+    private static native void close(long ctx);
+    private static native int putList(long ctx, byte[] term, byte[] rows, int n, int sorted);
+    private static native byte[] joinExclude(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl,
+                                             int maxDistance, long nowMillis);
+    private static native long[] normalizeScore(long ctx, byte[] rows, int m, int[] profile32, String language,
+                                                long nowMillis);
+    private static native byte[] query(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl, int maxDistance,
+                                       int k, int[] profile32, String language, long nowMillis);
+}

@@ -1,0 +1,98 @@
+"""World-size-2 (and 4) CPU tests of the URL-hash-range sharded path over gloo.
+
+Each rank holds one vertical DHT partition of the synthetic index
+(Distribution.java:153-158), computes its part of the joined container, its
+normalisation summary and its local top-k; the summaries and lists are
+exchanged with all_gather (RCCL on the GPUs, gloo here) and combined in shard
+order.  The result must equal the single-container oracle bit for bit."""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, preset, out_q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as orc
+        import shard_fold as sf
+        from yacy_search_server_amd import synth
+        full = synth.preset(preset)
+        part = synth.build_index(full.shard(rank, world))
+        whole = synth.build_index(full)
+        now = 20741 * 86400000 + 99
+        prof = orc.default_profile()
+        fails = []
+        for qi, (inc, exc) in enumerate(synth.queries(full, 12, 1, 3, 1, qseed=5)):
+            ih = [whole.hashes[t] for t in inc]
+            eh = [whole.hashes[t] for t in exc]
+            mine = orc.term_search(part.as_dict(), ih, eh, 2147483647, now)
+            # every url of my part maps to my shard
+            for r in mine:
+                assert sf.shard_of(bytes(r[:12]), world) == rank
+            summ = sf.shard_summary([bytes(r) for r in mine])
+            allsum = [None] * world
+            dist.all_gather_object(allsum, summ)
+            mn, mx, tf, vmn, vmx, D = sf.combine(allsum, now)
+            ref_rows = orc.term_search(whole.as_dict(), ih, eh, 2147483647, now)
+            if len(ref_rows) == 0:
+                assert all(s["n"] == 0 for s in allsum)
+                continue
+            ref_scores, nm = orc.normalize_score(ref_rows, prof, "en", now)
+            order = ["hitcount", "llocal", "lother", None, "wordsintext", "phrasesintext", "posintext",
+                     "posinphrase", "posofphrase", "urllength", "urlcomps", "wordsintitle"]
+            for i, f in enumerate(order):
+                if f is None:
+                    if (vmn, vmx) != (nm.min_f[3], nm.max_f[3]):
+                        fails.append((qi, "va", vmn, vmx, nm.min_f[3], nm.max_f[3]))
+                    continue
+                if (mn[f], mx[f]) != (nm.min_f[i], nm.max_f[i]):
+                    fails.append((qi, f))
+            if D != nm.max_distance_D or tf != (nm.min_tf, nm.max_tf):
+                fails.append((qi, "D/tf", D, nm.max_distance_D))
+            # local top-k with the settled (global) scores, then the ordered merge
+            keys = {bytes(r[:12]): i for i, r in enumerate(ref_rows)}
+            my_idx = np.array([keys[bytes(r[:12])] for r in mine], dtype=np.int64)
+            local = orc.topk(ref_rows[my_idx], ref_scores[my_idx], 100) if len(my_idx) else []
+            lists = [None] * world
+            dist.all_gather_object(lists, local)
+            merged = []
+            for shard_list in lists:
+                merged += shard_list
+            merged.sort(key=lambda h: (-h[1], -h[2]))  # stable: lower shard first on ties
+            out = []
+            for h in merged:
+                if out and out[-1][1] == h[1] and out[-1][2] == h[2]:
+                    continue
+                out.append(h)
+            exp = orc.topk(ref_rows, ref_scores, 100)
+            if out[:100] != exp:
+                fails.append((qi, "topk"))
+        out_q.put((rank, fails))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_normalisation_and_topk_merge(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + world * 7 + os.getpid() % 500
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "dense", q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, fails in res:
+        assert fails == [], (rank, fails[:5])
