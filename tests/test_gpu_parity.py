@@ -213,3 +213,18 @@ def test_c1_sample_bit_exact():
         exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=100)
         assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp
     ix.close()
+
+
+@pytest.mark.parametrize("ratio", ["1", "1000000000"])
+def test_forced_join_algorithm(corpus, ratio, monkeypatch):
+    """Every join/exclusion step through the probe kernel (ratio 1) or through
+    merge-path tiles (huge ratio): results identical to the oracle either way."""
+    monkeypatch.setenv("YRWI_PROBE_RATIO", ratio)
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    for inc, exc in synth.queries(cfg, 12, 1, 4, 1, qseed=31):
+        ih = [idx.hashes[t] for t in inc]
+        eh = [idx.hashes[t] for t in exc]
+        assert np.array_equal(ix.term_search(ih, eh, 2147483647, NOW), orc.term_search(d, ih, eh, 2147483647, NOW))
+        got = [(h.urlhash, h.score) for h in ix.search(ih, eh, now_ms=NOW)]
+        assert got == [(h, s) for h, s, _ in orc.search(d, ih, eh, now_ms=NOW)]

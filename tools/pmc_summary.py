@@ -1,0 +1,81 @@
+"""Summarise rocprofv3 CSV output of tools/profile_gpu.sh into profiles/.
+
+profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
+profiles/pmc_<config>.json        per-kernel mean duration and HBM bytes per launch
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch: FETCH_SIZE on gfx950
+reports half of a wide coalesced stream (MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def find(pattern):
+    return sorted(glob.glob(pattern, recursive=True))
+
+
+def short(name):
+    for k in ("k_join", "k_partition", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
+              "k_score_all", "k_score", "k_merge", "k_emit", "k_validate"):
+        if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
+            return k
+    return name[:40]
+
+
+def counters(path):
+    per = defaultdict(lambda: defaultdict(float))
+    n = defaultdict(set)
+    for f in find(os.path.join(path, "**", "*counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            k = short(row.get("Kernel_Name", ""))
+            did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            per[k][row.get("Counter_Name")] += float(row.get("Counter_Value", 0))
+            n[k].add(did)
+    return per, {k: len(v) for k, v in n.items()}
+
+
+def main(tag, config):
+    base = os.path.join(ROOT, "gpurun_out", "prof", tag)
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    stats = find(os.path.join(base, "kt", "**", "*kernel_stats.csv"))
+    out = {"tag": tag, "config": config, "kernels": {}}
+    if stats:
+        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+        for row in csv.DictReader(open(stats[0])):
+            k = short(row["Name"])
+            out["kernels"].setdefault(k, {})
+            out["kernels"][k]["calls"] = int(row["Calls"])
+            out["kernels"][k]["avg_ns"] = float(row["AverageNs"])
+            out["kernels"][k]["pct"] = float(row.get("Percentage", 0))
+    fetch, nf = counters(os.path.join(base, "fetch"))
+    write, nw = counters(os.path.join(base, "write"))
+    for k in set(fetch) | set(write):
+        d = out["kernels"].setdefault(k, {})
+        if k in fetch and nf.get(k):
+            d["fetch_kb_per_launch_raw"] = fetch[k]["FETCH_SIZE"] / nf[k]
+        if k in write and nw.get(k):
+            d["write_kb_per_launch"] = write[k]["WRITE_SIZE"] / nw[k]
+        if "fetch_kb_per_launch_raw" in d and "write_kb_per_launch" in d:
+            d["hbm_bytes_per_launch"] = (2 * d["fetch_kb_per_launch_raw"] + d["write_kb_per_launch"]) * 1024
+    kj = out["kernels"].get("k_join", {})
+    out["k_join_hbm_bytes_per_launch"] = kj.get("hbm_bytes_per_launch")
+    out["k_join_avg_ns"] = kj.get("avg_ns")
+    for log in ("kt.log", "fetch.log", "write.log"):
+        p = os.path.join(base, log)
+        if os.path.exists(p):
+            for line in open(p):
+                if line.startswith("{") and '"metric"' in line:
+                    out.setdefault("bench_lines", {})[log] = json.loads(line)
+    with open(os.path.join(ROOT, "profiles", f"pmc_{config}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "bench_lines"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "C2")

@@ -504,6 +504,45 @@ struct Timing {
   hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
 };
 
+// Intersection algorithm: probe the large list when sizes are skewed.
+static int64_t probe_ratio() {
+  const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either algorithm with it
+  return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
+}
+
+// Give every job its algorithm and tile count, put merge jobs first and lay out
+// the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
+static void layout_jobs(std::vector<JoinQ>& jobs, std::vector<int>& owner, std::vector<int64_t>& tile_base,
+                        int* nmerge, int64_t* merge_tiles, int64_t* tiles) {
+  std::vector<size_t> order(jobs.size());
+  for (size_t i = 0; i < jobs.size(); i++) {
+    JoinQ& J = jobs[i];
+    const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
+    J.algo = (nl > probe_ratio() * ns) ? JA_PROBE : JA_MERGE;
+    J.small_is_A = J.A.n <= J.B.n;
+    J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, PROBE_TILE);
+    order[i] = i;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return jobs[a].algo < jobs[b].algo; });
+  std::vector<JoinQ> js;
+  std::vector<int> ow;
+  tile_base.clear();
+  *nmerge = 0;
+  *merge_tiles = 0;
+  *tiles = 0;
+  for (size_t i : order) {
+    JoinQ J = jobs[i];
+    J.tile_base = *tiles;
+    tile_base.push_back(*tiles);
+    *tiles += J.ntiles;
+    if (J.algo == JA_MERGE) { (*nmerge)++; *merge_tiles = *tiles; }
+    js.push_back(J);
+    if (!owner.empty()) ow.push_back(owner[i]);
+  }
+  jobs.swap(js);
+  if (!owner.empty()) owner.swap(ow);
+}
+
 // Run the join/exclusion phase of all plans; leaves each plan's container in P.cont.
 static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   for (auto& P : plans) {
@@ -517,7 +556,6 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     std::vector<JoinQ> jobs;
     std::vector<int> owner;
     std::vector<int64_t> tile_base;
-    int64_t tiles = 0;
     for (size_t qi = 0; qi < plans.size(); qi++) {
       Plan& P = plans[qi];
       if (P.empty || P.seq.size() <= s + 1 || P.cont.n == 0) continue;
@@ -531,32 +569,34 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
       J.out_rows = arena_alloc<uint8_t>(ctx, cap * 40);
       J.out_khi = arena_alloc<uint64_t>(ctx, cap);
       J.out_klo = arena_alloc<uint8_t>(ctx, cap);
-      J.ntiles = ceil_div(J.A.n + J.B.n, JOIN_TILE);
-      J.tile_base = tiles;
       if (!J.out_rows || !J.out_khi || !J.out_klo) return ctx->fail(YRWI_E_NOMEM, "arena");
-      tile_base.push_back(tiles);
-      tiles += J.ntiles;
       if (st) {
-        { int64_t kb = step_bytes(J.mode, J.A.n, J.B.n); st->bytes_alg += kb; st->bytes_join += kb; }
+        int64_t kb = step_bytes(J.mode, J.A.n, J.B.n);
+        st->bytes_alg += kb;
+        st->bytes_join += kb;
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
       }
       jobs.push_back(J);
       owner.push_back((int)qi);
     }
     if (jobs.empty()) break;
+    int nmerge;
+    int64_t merge_tiles, tiles;
+    layout_jobs(jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
     const int nj = (int)jobs.size();
     int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
-    for (int j = 0; j < nj; j++) jobs[j].m_out = d_mout + j;
+    for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
     JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
     int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-    int64_t* d_split = arena_alloc<int64_t>(ctx, tiles);
+    int64_t* d_split = arena_alloc<int64_t>(ctx, merge_tiles);
     uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
     int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
     int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
     if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
     hipEvent_t e0 = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
-    if (launch_join_step(d_jobs, d_tb, nj, tiles, d_split, d_pairs, d_cnt, d_off, false, ctx->stream, e0, e1))
+    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pairs, d_cnt, d_off, false,
+                         ctx->stream, e0, e1))
       return ctx->fail(YRWI_E_HIP, "join launch");
     if (tm) tm->kjoin.push_back({e0, e1});
     if (st) st->n_join_launches++;
@@ -571,8 +611,8 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
   // exclusion (excludeContainers :373-388): mark container rows present in an exclude list
   {
     std::vector<JoinQ> jobs;
+    std::vector<int> owner;
     std::vector<int64_t> tile_base;
-    int64_t tiles = 0;
     for (auto& P : plans) {
       P.removed = nullptr;
       if (P.empty || P.cont.n == 0 || P.excl.empty()) continue;
@@ -586,23 +626,22 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
         J.mode = JM_MARK;
         J.maxd = YRWI_MAX_DISTANCE_ANY;
         J.removed = P.removed;
-        J.ntiles = ceil_div(J.A.n + J.B.n, JOIN_TILE);
-        J.tile_base = tiles;
-        tile_base.push_back(tiles);
-        tiles += J.ntiles;
         if (st) st->bytes_alg += 12 * E->n;
         jobs.push_back(J);
       }
     }
     if (!jobs.empty()) {
+      int nmerge;
+      int64_t merge_tiles, tiles;
+      layout_jobs(jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
       const int nj = (int)jobs.size();
       JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
       int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-      int64_t* d_split = arena_alloc<int64_t>(ctx, tiles);
+      int64_t* d_split = arena_alloc<int64_t>(ctx, merge_tiles);
       if (!d_jobs || !d_tb || !d_split) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-      if (launch_join_step(d_jobs, d_tb, nj, tiles, d_split, nullptr, nullptr, nullptr, true, ctx->stream, nullptr,
-                           nullptr))
+      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, nullptr, nullptr, nullptr, true,
+                           ctx->stream, nullptr, nullptr))
         return ctx->fail(YRWI_E_HIP, "exclude launch");
     }
   }

@@ -42,12 +42,20 @@ enum JoinMode : int32_t {
   JM_MARK = 3         // excludeDestructive: mark A rows present in B
 };
 
+// Intersection algorithm of a job (independent of the reference's feature rule):
+// merge-path tiles for comparable sizes, per-element probing of the large list
+// for skewed ones (the galloping bound of BASELINE.md §4).
+enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1 };
+constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
+
 struct JoinQ {
   DList A, B;
   int64_t tile_base;   // first global tile of this job
   int64_t ntiles;
   int32_t mode;
   int32_t maxd;
+  int32_t algo;        // JoinAlgo
+  int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint64_t* out_khi;   // compacted output container (capacity min(nA, nB))
   uint8_t* out_klo;
@@ -127,9 +135,11 @@ struct Cand {  // top-k candidate: sort descending on (k1, k2)
 // (defined in yrwi_kernels.hip; all asynchronous on `stream`)
 int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err,
                          void* stream);
-int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
-                     int64_t* d_split, uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off,
-                     bool mark, void* stream, void* ev_begin, void* ev_end);
+// jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
+int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
+                     int64_t merge_tiles, int64_t total_tiles, int64_t* d_split, uint2* d_pairs,
+                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
+                     void* ev_end);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

@@ -323,6 +323,65 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
   if (threadIdx.x == 0) tile_cnt[b] = tot;
 }
 
+// ============================================================ join: probe
+// Skewed sizes: each thread looks one small-list key up in the large list,
+// inside the large-list range spanned by the workgroup's 256 small keys (the
+// by-test access pattern of joinConstructiveByTest :419-446, RowSet.binarySearch
+// RowSet.java:319-335).  Output and mark semantics are those of k_join.
+__device__ __forceinline__ int64_t lower_bound_key(const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
+                                                   int64_t lo, int64_t hi, uint64_t h, uint32_t l) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const uint64_t mh = kh[mid];
+    const bool less = mh < h || (mh == h && (uint32_t)kl[mid] < l);
+    if (less) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
+                                                     const int64_t* __restrict__ tile_base, int njobs,
+                                                     int64_t tile0, uint2* __restrict__ pairs,
+                                                     int32_t* __restrict__ tile_cnt, int mark) {
+  __shared__ int64_t sRange[2];
+  __shared__ int32_t sScan[4];
+  const int64_t b = tile0 + blockIdx.x;
+  const int j = find_job(tile_base, njobs, b);
+  const JoinQ& J = jobs[j];
+  const DList& Sm = J.small_is_A ? J.A : J.B;
+  const DList& Lg = J.small_is_A ? J.B : J.A;
+  const int64_t s0 = (b - tile_base[j]) * PROBE_TILE;
+  const int64_t s1 = s0 + PROBE_TILE < Sm.n ? s0 + PROBE_TILE : Sm.n;
+  if (threadIdx.x < 2) {
+    const int64_t e = threadIdx.x == 0 ? s0 : s1 - 1;
+    int64_t p = lower_bound_key(Lg.khi, Lg.klo, 0, Lg.n, Sm.khi[e], Sm.klo[e]);
+    if (threadIdx.x == 1 && p < Lg.n) p++;  // range end (exclusive) covers an equal key
+    sRange[threadIdx.x] = p;
+  }
+  __syncthreads();
+  const int64_t i = s0 + threadIdx.x;
+  bool hit = false;
+  int64_t jl = 0;
+  if (i < s1) {
+    const uint64_t h = Sm.khi[i];
+    const uint32_t l = Sm.klo[i];
+    jl = lower_bound_key(Lg.khi, Lg.klo, sRange[0], sRange[1], h, l);
+    hit = jl < Lg.n && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
+  }
+  const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
+  if (hit && !mark && J.maxd < 65535) {
+    if (joined_distance(J.A.rows + ia * YRWI_ROW_BYTES, J.B.rows + ib * YRWI_ROW_BYTES, J.mode) > J.maxd) hit = false;
+  }
+  if (mark) {
+    if (hit) J.removed[ia] = 1;
+    return;
+  }
+  int32_t tot;
+  const int32_t off = block_excl_sum256(hit ? 1 : 0, sScan, &tot);
+  if (hit) pairs[b * (int64_t)JOIN_MAXM + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
+  if (threadIdx.x == 0) tile_cnt[b] = tot;
+}
+
 // ============================================================ join: scan
 __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jobs,
                                                     const int64_t* __restrict__ tile_base,
@@ -1178,15 +1237,21 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
   return rc(hipGetLastError());
 }
 
-int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
-                     int64_t* d_split, uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark,
-                     void* st, void* ev0, void* ev1) {
+int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
+                     int64_t merge_tiles, int64_t total_tiles, int64_t* d_split, uint2* d_pairs,
+                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0, void* ev1) {
   if (total_tiles <= 0) return 0;
-  hipLaunchKernelGGL(k_partition, dim3((unsigned)((total_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                     d_tile_base, njobs, total_tiles, d_split);
+  if (merge_tiles > 0)
+    hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                       d_tile_base, nmerge, merge_tiles, d_split);
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
-  hipLaunchKernelGGL(k_join, dim3((unsigned)total_tiles), dim3(JOIN_THREADS), 0, S(st), d_jobs, d_tile_base, njobs,
-                     d_split, d_pairs, d_tile_cnt, mark ? 1 : 0);
+  if (merge_tiles > 0)
+    hipLaunchKernelGGL(k_join, dim3((unsigned)merge_tiles), dim3(JOIN_THREADS), 0, S(st), d_jobs, d_tile_base, nmerge,
+                       d_split, d_pairs, d_tile_cnt, mark ? 1 : 0);
+  if (total_tiles > merge_tiles)
+    hipLaunchKernelGGL(k_probe, dim3((unsigned)(total_tiles - merge_tiles)), dim3(PROBE_TILE), 0, S(st),
+                       d_jobs + nmerge, d_tile_base + nmerge, njobs - nmerge, merge_tiles, d_pairs, d_tile_cnt,
+                       mark ? 1 : 0);
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
