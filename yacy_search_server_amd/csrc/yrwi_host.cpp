@@ -648,14 +648,89 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
   return 0;
 }
 
+// Global host counts for authority (ReferenceOrder.java:176-216) across url-hash
+// shards: (query, host, count) messages to the host's owner rank, summed there,
+// totals sent back; the per-query max count is all-reduced.  Collective.
+static int exchange_host_counts(yrwi_ctx* ctx, int nq, int64_t nslots, const std::vector<int64_t>& slot_base,
+                                uint64_t* d_hkeys, uint32_t* d_hcnt, ShardSum* d_ss) {
+  const int W = ctx->world, me = ctx->rank;
+  uint32_t* d_ocnt = arena_alloc<uint32_t>(ctx, W);
+  uint32_t* d_M = arena_alloc<uint32_t>(ctx, (int64_t)W * W);
+  int64_t* d_sb = arena_alloc<int64_t>(ctx, nq + 1);
+  int32_t* d_gmax = arena_alloc<int32_t>(ctx, nq);
+  if (!d_ocnt || !d_M || !d_sb || !d_gmax) return ctx->fail(YRWI_E_NOMEM, "arena");
+  HIPCHK(ctx, hipMemsetAsync(d_ocnt, 0, W * 4, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(d_gmax, 0, nq * 4, ctx->stream));
+  if (upload(ctx, d_sb, slot_base)) return YRWI_E_HIP;
+  if (launch_host_count(d_hkeys, nslots, W, d_ocnt, ctx->stream)) return ctx->fail(YRWI_E_HIP, "host count");
+  if (ncclAllGather(d_ocnt, d_M, W, ncclUint32, ctx->comm, ctx->stream) != ncclSuccess)
+    return ctx->fail(YRWI_E_RCCL, "allgather of host message counts");
+  std::vector<uint32_t> M((size_t)W * W);
+  HIPCHK(ctx, hipMemcpyAsync(M.data(), d_M, M.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  // row s of M = what rank s sends to each owner
+  std::vector<int64_t> soff((size_t)W + 1, 0), roff((size_t)W + 1, 0);
+  for (int p = 0; p < W; p++) {
+    soff[(size_t)p + 1] = soff[(size_t)p] + M[(size_t)me * W + p];
+    roff[(size_t)p + 1] = roff[(size_t)p] + M[(size_t)p * W + me];
+  }
+  const int64_t nsend = soff[(size_t)W], nrecv = roff[(size_t)W];
+  std::vector<uint32_t> cur((size_t)W);
+  for (int p = 0; p < W; p++) cur[(size_t)p] = (uint32_t)soff[(size_t)p];
+  uint32_t* d_cur = arena_alloc<uint32_t>(ctx, W);
+  HostMsg* d_send = arena_alloc<HostMsg>(ctx, nsend);
+  uint64_t* d_sslot = arena_alloc<uint64_t>(ctx, nsend);
+  HostMsg* d_recv = arena_alloc<HostMsg>(ctx, nrecv);
+  uint32_t* d_reply = arena_alloc<uint32_t>(ctx, nrecv);
+  uint32_t* d_back = arena_alloc<uint32_t>(ctx, nsend);
+  uint64_t ocap = 1;
+  while (ocap < (uint64_t)(2 * std::max<int64_t>(nrecv, 1))) ocap <<= 1;
+  uint64_t* d_okeys = arena_alloc<uint64_t>(ctx, (int64_t)ocap);
+  uint32_t* d_ovals = arena_alloc<uint32_t>(ctx, (int64_t)ocap);
+  if (!d_cur || !d_send || !d_sslot || !d_recv || !d_reply || !d_back || !d_okeys || !d_ovals)
+    return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_cur, cur)) return YRWI_E_HIP;
+  HIPCHK(ctx, hipMemsetAsync(d_okeys, 0, ocap * 8, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(d_ovals, 0, ocap * 4, ctx->stream));
+  if (launch_host_pack(d_hkeys, d_hcnt, d_sb, nq, nslots, W, d_cur, d_send, d_sslot, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "host pack");
+  if (ncclGroupStart() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group");
+  for (int p = 0; p < W; p++) {
+    size_t sn = (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * sizeof(HostMsg);
+    size_t rn = (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * sizeof(HostMsg);
+    if (sn && ncclSend(d_send + soff[(size_t)p], sn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
+      return ctx->fail(YRWI_E_RCCL, "send host messages");
+    if (rn && ncclRecv(d_recv + roff[(size_t)p], rn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
+      return ctx->fail(YRWI_E_RCCL, "recv host messages");
+  }
+  if (ncclGroupEnd() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group end");
+  if (launch_host_owner(d_recv, nrecv, d_okeys, d_ovals, ocap - 1, d_gmax, d_reply, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "host owner");
+  if (ncclAllReduce(d_gmax, d_gmax, nq, ncclInt32, ncclMax, ctx->comm, ctx->stream) != ncclSuccess)
+    return ctx->fail(YRWI_E_RCCL, "allreduce max host count");
+  if (ncclGroupStart() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group");
+  for (int p = 0; p < W; p++) {
+    size_t rn = (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * 4;  // replies to what p sent me
+    size_t sn = (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * 4;  // totals for what I sent p
+    if (rn && ncclSend(d_reply + roff[(size_t)p], rn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
+      return ctx->fail(YRWI_E_RCCL, "send host totals");
+    if (sn && ncclRecv(d_back + soff[(size_t)p], sn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
+      return ctx->fail(YRWI_E_RCCL, "recv host totals");
+  }
+  if (ncclGroupEnd() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group end");
+  if (launch_host_apply(d_back, d_sslot, nsend, d_hcnt, d_ss, d_gmax, nq, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "host apply");
+  return 0;
+}
+
 // Normalise (+ cross-shard exchange), then either score+top-k (hits) or all scores.
 static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax, yrwi_hit* h_hits,
                           int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
   const int nq = (int)plans.size();
   const int W = exchange ? ctx->world : 1;
   std::vector<RankQ> rq((size_t)nq);
-  std::vector<int64_t> chunk_base((size_t)nq);
-  int64_t chunks = 0;
+  std::vector<int64_t> chunk_base((size_t)nq), slot_base((size_t)nq + 1);
+  int64_t chunks = 0, nslots = 0;
   bool any_auth = false;
   for (int qi = 0; qi < nq; qi++) {
     Plan& P = plans[(size_t)qi];
@@ -676,24 +751,39 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
     R.k = P.k;
     R.want_authority = P.prof.coeff_authority > 12 && R.n > 0;
     R.idx_tag = W > 1 ? (uint32_t)ctx->rank << 28 : 0u;
+    // identical on every rank (same queries): decides the collective host-count exchange
+    if (P.prof.coeff_authority > 12) any_auth = true;
     if (R.want_authority) {
-      if (W > 1) return ctx->fail(YRWI_E_UNSUPPORTED, "authority ranking across shards is not implemented");
       uint64_t cap = 1;
       while (cap < (uint64_t)(2 * R.n)) cap <<= 1;
-      R.hkeys = arena_alloc<uint64_t>(ctx, (int64_t)cap);
-      R.hcnt = arena_alloc<uint32_t>(ctx, (int64_t)cap);
-      if (!R.hkeys || !R.hcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
       R.hmask = cap - 1;
-      HIPCHK(ctx, hipMemsetAsync(R.hkeys, 0, cap * 8, ctx->stream));
-      HIPCHK(ctx, hipMemsetAsync(R.hcnt, 0, cap * 4, ctx->stream));
-      any_auth = true;
+      slot_base[(size_t)qi] = nslots;
+      nslots += (int64_t)cap;
+    } else {
+      slot_base[(size_t)qi] = nslots;
     }
     if (st) {
       st->joined += R.n;
       st->bytes_alg += 23 * (int64_t)P.seq.size() * R.n;  // ranking feature bytes per surviving posting and term
     }
   }
-  (void)any_auth;
+  slot_base[(size_t)nq] = nslots;
+  // authority host tables of all queries, one allocation
+  uint64_t* d_hkeys = nullptr;
+  uint32_t* d_hcnt = nullptr;
+  if (nslots > 0) {
+    d_hkeys = arena_alloc<uint64_t>(ctx, nslots);
+    d_hcnt = arena_alloc<uint32_t>(ctx, nslots);
+    if (!d_hkeys || !d_hcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+    HIPCHK(ctx, hipMemsetAsync(d_hkeys, 0, (size_t)nslots * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(d_hcnt, 0, (size_t)nslots * 4, ctx->stream));
+    for (int qi = 0; qi < nq; qi++) {
+      RankQ& R = rq[(size_t)qi];
+      if (!R.want_authority) continue;
+      R.hkeys = d_hkeys + slot_base[(size_t)qi];
+      R.hcnt = d_hcnt + slot_base[(size_t)qi];
+    }
+  }
   RankQ* d_q = arena_alloc<RankQ>(ctx, nq);
   int64_t* d_cb = arena_alloc<int64_t>(ctx, nq);
   ChunkSum* d_cs = arena_alloc<ChunkSum>(ctx, chunks);
@@ -704,6 +794,10 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   if (launch_reduce(d_q, d_cb, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (W > 1 && any_auth) {
+    int rc2 = exchange_host_counts(ctx, nq, nslots, slot_base, d_hkeys, d_hcnt, d_ss);
+    if (rc2) return rc2;
+  }
   if (W > 1) {
     if (ncclAllGather(d_ss, d_all, sizeof(ShardSum) * nq, ncclChar, ctx->comm, ctx->stream) != ncclSuccess)
       return ctx->fail(YRWI_E_RCCL, "allgather of shard summaries");

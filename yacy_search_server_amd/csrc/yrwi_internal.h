@@ -131,7 +131,21 @@ struct Cand {  // top-k candidate: sort descending on (k1, k2)
   uint64_t k2;  // ((hashCode ^ 2^31) << 32) | ~index
 };
 
+// host-count exchange between url-hash shards (authority, ReferenceOrder.java:176-216)
+struct HostMsg {
+  uint64_t key;  // host hash (url-hash chars 6..11, 36 bits) + 1
+  uint32_t q;    // query index in the batch
+  uint32_t cnt;  // count of that host in the sender's part of the joined container
+};
+
 // ---------------------------------------------------------------- launchers
+int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* stream);
+int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
+                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* stream);
+int launch_host_owner(const HostMsg* recv, int64_t nrecv, uint64_t* okeys, uint32_t* ocnt, uint64_t omask,
+                      int32_t* gmax, uint32_t* reply, void* stream);
+int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n, uint32_t* hcnt_all,
+                      ShardSum* ss, const int32_t* gmax, int nq, void* stream);
 // (defined in yrwi_kernels.hip; all asynchronous on `stream`)
 int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err,
                          void* stream);

@@ -1227,6 +1227,84 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
   }
 }
 
+// ======================================================= host-count exchange
+// Global host counts for ReferenceOrder.authority (:176-216) when the joined
+// container is spread over url-hash shards: every (query, host, local count) is
+// sent to the host's owner rank, summed there and the totals are sent back.
+__device__ __forceinline__ uint32_t owner_of(uint64_t key, int world) {
+  return (uint32_t)((mix64(key ^ 0x5BD1E995ull) >> 32) % (uint64_t)world);
+}
+
+__global__ void k_host_count(const uint64_t* __restrict__ hkeys, int64_t nslots, int world,
+                             uint32_t* __restrict__ owner_cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  const uint64_t k = hkeys[i];
+  if (k) atomicAdd(&owner_cnt[owner_of(k, world)], 1u);
+}
+
+__global__ void k_host_pack(const uint64_t* __restrict__ hkeys, const uint32_t* __restrict__ hcnt,
+                            const int64_t* __restrict__ slot_base, int nq, int64_t nslots, int world,
+                            uint32_t* __restrict__ cursor, HostMsg* __restrict__ send,
+                            uint64_t* __restrict__ send_slot) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  const uint64_t k = hkeys[i];
+  if (!k) return;
+  const int q = find_job(slot_base, nq, i);
+  const uint32_t pos = atomicAdd(&cursor[owner_of(k, world)], 1u);
+  send[pos] = HostMsg{k, (uint32_t)q, hcnt[i]};
+  send_slot[pos] = (uint64_t)i;
+}
+
+__device__ __forceinline__ uint64_t owner_key(const HostMsg& m) { return ((uint64_t)m.q << 37) | m.key; }
+
+__global__ void k_host_insert(const HostMsg* __restrict__ recv, int64_t n, uint64_t* __restrict__ okeys,
+                              uint32_t* __restrict__ ocnt, uint64_t omask) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const HostMsg m = recv[i];
+  const uint64_t ck = owner_key(m);
+  uint64_t slot = mix64(ck) & omask;
+  while (true) {
+    unsigned long long prev = atomicCAS((unsigned long long*)&okeys[slot], 0ull, (unsigned long long)ck);
+    if (prev == 0ull || prev == ck) {
+      atomicAdd(&ocnt[slot], m.cnt);
+      return;
+    }
+    slot = (slot + 1) & omask;
+  }
+}
+
+__global__ void k_host_max(const uint64_t* __restrict__ okeys, const uint32_t* __restrict__ ocnt, int64_t ocap,
+                           int32_t* __restrict__ gmax) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ocap) return;
+  const uint64_t ck = okeys[i];
+  if (ck) atomicMax(&gmax[ck >> 37], (int32_t)ocnt[i]);
+}
+
+__global__ void k_host_reply(const HostMsg* __restrict__ recv, int64_t n, const uint64_t* __restrict__ okeys,
+                             const uint32_t* __restrict__ ocnt, uint64_t omask, uint32_t* __restrict__ reply) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ck = owner_key(recv[i]);
+  uint64_t slot = mix64(ck) & omask;
+  while (okeys[slot] != ck) slot = (slot + 1) & omask;  // present: inserted above
+  reply[i] = ocnt[slot];
+}
+
+__global__ void k_host_apply(const uint32_t* __restrict__ back, const uint64_t* __restrict__ send_slot, int64_t n,
+                             uint32_t* __restrict__ hcnt_all) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hcnt_all[send_slot[i]] = back[i];
+}
+
+__global__ void k_set_maxdom(ShardSum* __restrict__ ss, const int32_t* __restrict__ gmax, int nq) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq) ss[q].maxdom = gmax[q];
+}
+
 // ================================================================ launchers
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int rc(hipError_t e) { return e == hipSuccess ? 0 : YRWI_E_HIP; }
@@ -1259,6 +1337,39 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     hipLaunchKernelGGL(k_compact, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
                        d_pairs, d_tile_cnt, d_tile_off);
   }
+  return rc(hipGetLastError());
+}
+
+static inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* st) {
+  if (nslots > 0) hipLaunchKernelGGL(k_host_count, dim3(nblk(nslots)), dim3(256), 0, S(st), hkeys, nslots, world, owner_cnt);
+  return rc(hipGetLastError());
+}
+
+int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
+                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* st) {
+  if (nslots > 0)
+    hipLaunchKernelGGL(k_host_pack, dim3(nblk(nslots)), dim3(256), 0, S(st), hkeys, hcnt, slot_base, nq, nslots, world,
+                       cursor, send, send_slot);
+  return rc(hipGetLastError());
+}
+
+int launch_host_owner(const HostMsg* recv, int64_t nrecv, uint64_t* okeys, uint32_t* ocnt, uint64_t omask,
+                      int32_t* gmax, uint32_t* reply, void* st) {
+  if (nrecv > 0) {
+    hipLaunchKernelGGL(k_host_insert, dim3(nblk(nrecv)), dim3(256), 0, S(st), recv, nrecv, okeys, ocnt, omask);
+    hipLaunchKernelGGL(k_host_max, dim3(nblk((int64_t)omask + 1)), dim3(256), 0, S(st), okeys, ocnt,
+                       (int64_t)omask + 1, gmax);
+    hipLaunchKernelGGL(k_host_reply, dim3(nblk(nrecv)), dim3(256), 0, S(st), recv, nrecv, okeys, ocnt, omask, reply);
+  }
+  return rc(hipGetLastError());
+}
+
+int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n, uint32_t* hcnt_all, ShardSum* ss,
+                      const int32_t* gmax, int nq, void* st) {
+  if (n > 0) hipLaunchKernelGGL(k_host_apply, dim3(nblk(n)), dim3(256), 0, S(st), back, send_slot, n, hcnt_all);
+  hipLaunchKernelGGL(k_set_maxdom, dim3(nblk(nq)), dim3(256), 0, S(st), ss, gmax, nq);
   return rc(hipGetLastError());
 }
 
