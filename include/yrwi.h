@@ -84,10 +84,12 @@ typedef struct yrwi_stats {
   int64_t postings_in;   /* sum of include + exclude list lengths */
   int64_t joined;        /* rows of the joined container (before exclusion) */
   int64_t bytes_alg;     /* algorithmic bytes B = sum K + 12 sum n_excl + 23 t m_out */
-  int64_t bytes_join;    /* sum K over the join steps (the k_join launches timed in t_join_ns) */
+  int64_t bytes_join;    /* sum K over the merge-path join jobs (the k_join launches timed in t_join_ns) */
   int64_t t_join_ns;     /* device time of the k_join launches (HIP events on the context stream) */
   int64_t t_norm_ns, t_score_ns, t_total_ns;
   int32_t n_join_launches, n_enum_steps, n_test_steps, reserved;
+  int64_t bytes_probe;   /* sum K over the skewed (probe) join jobs, timed in t_probe_ns */
+  int64_t t_probe_ns;    /* device time of the k_probe launches */
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

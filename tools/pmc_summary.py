@@ -21,7 +21,7 @@ def find(pattern):
 
 
 def short(name):
-    for k in ("k_join", "k_partition", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
+    for k in ("k_join", "k_probe", "k_partition", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
               "k_score_all", "k_score", "k_merge", "k_emit", "k_validate"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
             return k
@@ -66,6 +66,9 @@ def main(tag, config):
     kj = out["kernels"].get("k_join", {})
     out["k_join_hbm_bytes_per_launch"] = kj.get("hbm_bytes_per_launch")
     out["k_join_avg_ns"] = kj.get("avg_ns")
+    kp = out["kernels"].get("k_probe", {})
+    out["k_probe_hbm_bytes_per_launch"] = kp.get("hbm_bytes_per_launch")
+    out["k_probe_avg_ns"] = kp.get("avg_ns")
     for log in ("kt.log", "fetch.log", "write.log"):
         p = os.path.join(base, log)
         if os.path.exists(p):

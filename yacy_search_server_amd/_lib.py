@@ -50,7 +50,8 @@ class CStats(ctypes.Structure):
                 ("bytes_join", ctypes.c_int64), ("t_join_ns", ctypes.c_int64), ("t_norm_ns", ctypes.c_int64),
                 ("t_score_ns", ctypes.c_int64), ("t_total_ns", ctypes.c_int64),
                 ("n_join_launches", ctypes.c_int32), ("n_enum_steps", ctypes.c_int32),
-                ("n_test_steps", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("n_test_steps", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64)]
 
 
 # every symbol include/yrwi.h declares, with its ctypes signature

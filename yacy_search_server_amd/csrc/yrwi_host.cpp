@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -500,7 +501,8 @@ static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
 }
 
 struct Timing {
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> kjoin;
+  // per join step: before k_join, between k_join and k_probe, after k_probe
+  std::vector<std::array<hipEvent_t, 3>> kjoin;
   hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
 };
 
@@ -571,9 +573,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
       J.out_klo = arena_alloc<uint8_t>(ctx, cap);
       if (!J.out_rows || !J.out_khi || !J.out_klo) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (st) {
-        int64_t kb = step_bytes(J.mode, J.A.n, J.B.n);
-        st->bytes_alg += kb;
-        st->bytes_join += kb;
+        st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
       }
       jobs.push_back(J);
@@ -584,6 +584,8 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     int64_t merge_tiles, tiles;
     layout_jobs(jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
     const int nj = (int)jobs.size();
+    if (st)
+      for (const JoinQ& J : jobs) (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) += step_bytes(J.mode, J.A.n, J.B.n);
     int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
     for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
     JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
@@ -594,11 +596,11 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
     if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-    hipEvent_t e0 = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
+    hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
     if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pairs, d_cnt, d_off, false,
-                         ctx->stream, e0, e1))
+                         ctx->stream, e0, em, e1))
       return ctx->fail(YRWI_E_HIP, "join launch");
-    if (tm) tm->kjoin.push_back({e0, e1});
+    if (tm) tm->kjoin.push_back({e0, em, e1});
     if (st) st->n_join_launches++;
     mh.assign((size_t)nj, 0);
     HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -641,7 +643,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
       if (!d_jobs || !d_tb || !d_split) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
       if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, nullptr, nullptr, nullptr, true,
-                           ctx->stream, nullptr, nullptr))
+                           ctx->stream, nullptr, nullptr, nullptr))
         return ctx->fail(YRWI_E_HIP, "exclude launch");
     }
   }
@@ -953,10 +955,13 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   if (rc) return rc;
   if (st) {
     float ms = 0;
-    int64_t kj = 0;
-    for (auto& pr : tm.kjoin)
-      if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) kj += (int64_t)(ms * 1e6);
+    int64_t kj = 0, kp = 0;
+    for (auto& ev : tm.kjoin) {
+      if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) kj += (int64_t)(ms * 1e6);
+      if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) kp += (int64_t)(ms * 1e6);
+    }
     st->t_join_ns = kj;
+    st->t_probe_ns = kp;
     if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns = (int64_t)(ms * 1e6);
     if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns = (int64_t)(ms * 1e6);
     st->t_total_ns = now_ns() - t0;

@@ -769,16 +769,44 @@ struct SegList {
   }
 };
 
-// walk every valid element of chunk c after its first one as a single-element piece
-__device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& L) {
+// broadcast lane 0's list state to the wave (only lane 0 mutates L)
+__device__ __forceinline__ void seg_bcast(SegList& L) {
+  L.n = __shfl(L.n, 0, 64);
+  L.prun = __shfl(L.prun, 0, 64);
+  L.overflow = __shfl(L.overflow, 0, 64);
+}
+
+// Walk every valid element of chunk c after its first one as a single-element
+// piece (exact fallback for a chunk whose summary overflowed).  Whole wave: 64
+// elements per step are loaded in parallel; a step without a new prefix-max
+// record merges with two wave reductions, otherwise lane 0 walks it from LDS.
+// L must be wave-uniform on entry and is wave-uniform on exit.
+__device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& L, int32_t* sP, int32_t* sO) {
+  const int lane = threadIdx.x;
   const int64_t e0 = c * CHUNK, e1 = min((int64_t)(c + 1) * CHUNK, Q.n);
-  for (int64_t e = e0; e < e1; e++) {
-    if (e <= first) continue;
-    if (Q.removed && Q.removed[e]) continue;
-    const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
-    int32_t p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
-    int32_t od = r[O_I];
-    L.add(p, od, od);
+  for (int64_t b = e0; b < e1; b += 64) {
+    const int64_t e = b + lane;
+    bool ok = e < e1 && e > first && !(Q.removed && Q.removed[e]);
+    int32_t p = -1, od = 0;
+    if (ok) {
+      const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
+      p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
+      od = r[O_I];
+    }
+    if (__all(!ok || p <= L.prun)) {
+      const int32_t m = wave_max_i(ok ? od : 0);
+      const int32_t key = wave_max_i((ok && od > 0) ? ((lane + 1) << 8) | od : 0);
+      if (lane == 0 && (m > 0 || key > 0)) L.add(-1, m, key & 0xFF);
+    } else {
+      sP[lane] = ok ? p : -2;
+      sO[lane] = od;
+      __syncthreads();
+      if (lane == 0)
+        for (int i = 0; i < 64; i++)
+          if (sP[i] != -2) L.add(sP[i], sO[i], sO[i]);
+      __syncthreads();
+    }
+    seg_bcast(L);
   }
 }
 
@@ -786,6 +814,9 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
 __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, const int64_t* __restrict__ chunk_base,
                                                   const ChunkSum* __restrict__ cs, ShardSum* __restrict__ out) {
   __shared__ uint32_t sSeg[SSEG];
+  __shared__ int32_t sNv[64], sPm[64], sMall[64], sLall[64], sPf[64], sOf[64], sNs[64], sFirst[64];
+  __shared__ uint32_t sSg[64 * SEGC];
+  __shared__ int32_t sRw[128];
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
   const int lane = threadIdx.x;
@@ -830,14 +861,13 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
 
   // ---- ordered fold pieces
   SegList L{sSeg, SSEG, 0, 0, -1};
-  if (lane == 0 && nv > 0) {
+  if (nv > 0) {
     const ChunkSum& X = C[firstc];
-    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L);
-    else for (int i = 0; i < X.nseg; i++) L.add((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
+    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L, sNv, sPm);
+    else if (lane == 0)
+      for (int i = 0; i < X.nseg; i++) L.add((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
   }
-  L.n = __shfl(L.n, 0, 64);
-  L.prun = __shfl(L.prun, 0, 64);
-  L.overflow = __shfl(L.overflow, 0, 64);
+  seg_bcast(L);
   int32_t nseg = L.n, prun = L.prun;
   for (int64_t c0 = (nv > 0 ? firstc + 1 : nc); c0 < nc; c0 += 64) {
     const int64_t c = c0 + lane;
@@ -856,19 +886,46 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
       int32_t key = (nvc && Lall > 0) ? ((lane + 1) << 8) | Lall : 0;
       key = wave_max_i(key);
       if (lane == 0 && (m > 0 || key > 0)) L.add(-1, m, key & 0xFF);  // P=-1 <= prun: merge
-    } else if (lane == 0) {
-      for (int i = 0; i < 64 && c0 + i < nc; i++) {
-        const ChunkSum& X = C[c0 + i];
-        if (X.nvalid == 0) continue;
-        L.add(X.p_first, X.od_first, X.od_first);
-        if (X.overflow) rewalk_chunk(Q, c0 + i, X.first, L);
-        else for (int s = 0; s < X.nseg; s++) L.add((int32_t)(X.seg[s] >> 16), (int32_t)((X.seg[s] >> 8) & 0xFF), (int32_t)(X.seg[s] & 0xFF));
+    } else {
+      // stage this batch's summaries in LDS (all lanes, parallel loads), then lane 0
+      // walks them: chunks without a new prefix-max record merge in O(1)
+      if (c < nc) {
+        const ChunkSum& X = C[c];
+        sNv[lane] = nvc;
+        sPm[lane] = pm;
+        sMall[lane] = Mall;
+        sLall[lane] = Lall;
+        sPf[lane] = X.p_first;
+        sOf[lane] = X.od_first;
+        sNs[lane] = X.overflow ? -1 : X.nseg;
+        sFirst[lane] = X.first;
+        for (int s = 0; s < SEGC && s < X.nseg && !X.overflow; s++) sSg[lane * SEGC + s] = X.seg[s];
+      } else {
+        sNv[lane] = 0;
       }
+      __syncthreads();
+      // loop and branch conditions are wave-uniform (LDS + broadcast state); only
+      // lane 0 mutates L except inside the cooperative rewalk
+      for (int i = 0; i < 64 && c0 + i < nc; i++) {
+        if (sNv[i] == 0) continue;
+        if (sPm[i] <= L.prun) {
+          if (lane == 0 && (sMall[i] > 0 || sLall[i] > 0)) L.add(-1, sMall[i], sLall[i]);
+          continue;
+        }
+        if (lane == 0) L.add(sPf[i], sOf[i], sOf[i]);
+        if (sNs[i] < 0) {
+          seg_bcast(L);
+          rewalk_chunk(Q, c0 + i, sFirst[i], L, sRw, sRw + 64);
+        } else if (lane == 0) {
+          for (int s = 0; s < sNs[i]; s++)
+            L.add((int32_t)(sSg[i * SEGC + s] >> 16), (int32_t)((sSg[i * SEGC + s] >> 8) & 0xFF),
+                  (int32_t)(sSg[i * SEGC + s] & 0xFF));
+        }
+        seg_bcast(L);
+      }
+      __syncthreads();
     }
-    // broadcast lane 0's list state
-    L.n = __shfl(L.n, 0, 64);
-    L.prun = __shfl(L.prun, 0, 64);
-    L.overflow = __shfl(L.overflow, 0, 64);
+    seg_bcast(L);
     prun = L.prun;
     nseg = L.n;
   }
@@ -1317,7 +1374,8 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, int64_t* d_split, uint2* d_pairs,
-                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0, void* ev1) {
+                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0, void* evm,
+                     void* ev1) {
   if (total_tiles <= 0) return 0;
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
@@ -1326,6 +1384,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)merge_tiles), dim3(JOIN_THREADS), 0, S(st), d_jobs, d_tile_base, nmerge,
                        d_split, d_pairs, d_tile_cnt, mark ? 1 : 0);
+  if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (total_tiles > merge_tiles)
     hipLaunchKernelGGL(k_probe, dim3((unsigned)(total_tiles - merge_tiles)), dim3(PROBE_TILE), 0, S(st),
                        d_jobs + nmerge, d_tile_base + nmerge, njobs - nmerge, merge_tiles, d_pairs, d_tile_cnt,
