@@ -590,7 +590,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
     JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
     int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-    int64_t* d_split = arena_alloc<int64_t>(ctx, merge_tiles);
+    TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
     uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
     int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
     int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
@@ -639,7 +639,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
       const int nj = (int)jobs.size();
       JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
       int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-      int64_t* d_split = arena_alloc<int64_t>(ctx, merge_tiles);
+      TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
       if (!d_jobs || !d_tb || !d_split) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
       if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, nullptr, nullptr, nullptr, true,

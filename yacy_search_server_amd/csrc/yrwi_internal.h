@@ -64,6 +64,18 @@ struct JoinQ {
   int64_t* m_out;      // number of output rows (written by the scan kernel)
 };
 
+// One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
+// range [a0, a0+na) and B range [b0, b0+nb) plus one lookahead B key (nbl = nb+1
+// unless B is exhausted), with direct key pointers so k_join needs no job lookup.
+struct TileDesc {
+  const uint64_t* ah;
+  const uint8_t* al;
+  const uint64_t* bh;
+  const uint8_t* bl;
+  int64_t a0, b0;
+  int32_t na, nb, nbl, job;
+};
+
 // Per-chunk normalisation summary (ReferenceOrder.NormalizeWorker :163-210,
 // restated as an order-preserving reduction).
 struct ChunkSum {
@@ -151,7 +163,7 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
                          void* stream);
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
-                     int64_t merge_tiles, int64_t total_tiles, int64_t* d_split, uint2* d_pairs,
+                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, uint2* d_pairs,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
                      void* ev_mid, void* ev_end);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

@@ -191,23 +191,46 @@ __global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t
 }
 
 // =========================================================== join: partition
+// One thread per merge tile: the merge-path split of the tile's first and last
+// diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
+__device__ __forceinline__ bool key_le_at(const DList& A, int64_t i, const DList& B, int64_t j) {
+  const uint64_t ah = A.khi[i], bh = B.khi[j];
+  return ah < bh || (ah == bh && A.klo[i] <= B.klo[j]);
+}
+
 __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                            int64_t total_tiles, int64_t* __restrict__ split) {
+                            int64_t total_tiles, TileDesc* __restrict__ desc) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total_tiles) return;
   const int j = find_job(tile_base, njobs, b);
   const JoinQ& J = jobs[j];
   const int64_t nA = J.A.n, nB = J.B.n;
-  const int64_t d = (b - tile_base[j]) * JOIN_TILE;
-  int64_t lo = d - nB > 0 ? d - nB : 0, hi = d < nA ? d : nA;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    int64_t bj = d - 1 - mid;
-    uint64_t ah = J.A.khi[mid], bh = J.B.khi[bj];
-    bool le = ah < bh || (ah == bh && J.A.klo[mid] <= J.B.klo[bj]);
-    if (le) lo = mid + 1; else hi = mid;
+  const int64_t d0 = (b - tile_base[j]) * JOIN_TILE;
+  const int64_t d1 = d0 + JOIN_TILE < nA + nB ? d0 + JOIN_TILE : nA + nB;
+  int64_t lo0 = d0 - nB > 0 ? d0 - nB : 0, hi0 = d0 < nA ? d0 : nA;
+  int64_t lo1 = d1 - nB > 0 ? d1 - nB : 0, hi1 = d1 < nA ? d1 : nA;
+  while (lo0 < hi0 || lo1 < hi1) {
+    if (lo0 < hi0) {
+      const int64_t mid = (lo0 + hi0) >> 1;
+      if (key_le_at(J.A, mid, J.B, d0 - 1 - mid)) lo0 = mid + 1; else hi0 = mid;
+    }
+    if (lo1 < hi1) {
+      const int64_t mid = (lo1 + hi1) >> 1;
+      if (key_le_at(J.A, mid, J.B, d1 - 1 - mid)) lo1 = mid + 1; else hi1 = mid;
+    }
   }
-  split[b] = lo;
+  TileDesc D;
+  D.ah = J.A.khi;
+  D.al = J.A.klo;
+  D.bh = J.B.khi;
+  D.bl = J.B.klo;
+  D.a0 = lo0;
+  D.b0 = d0 - lo0;
+  D.na = (int32_t)(lo1 - lo0);
+  D.nb = (int32_t)((d1 - lo1) - (d0 - lo0));
+  D.nbl = D.nb + ((d1 - lo1) < nB ? 1 : 0);  // + lookahead element B[b1]
+  D.job = j;
+  desc[b] = D;
 }
 
 // joined worddistance (WordReferenceVars.distance :287-294 after join :465-499)
@@ -223,104 +246,162 @@ __device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint
 }
 
 // ============================================================ join: tiles
-__global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
-                                                      const int64_t* __restrict__ tile_base, int njobs,
-                                                      const int64_t* __restrict__ split, uint2* __restrict__ pairs,
-                                                      int32_t* __restrict__ tile_cnt, int mark) {
-  __shared__ uint64_t sAh[JOIN_TILE];
-  __shared__ uint64_t sBh[JOIN_TILE + 1];
-  __shared__ uint8_t sAl[JOIN_TILE];
-  __shared__ uint8_t sBl[JOIN_TILE + 1];
-  __shared__ int32_t sScan[4];
+// Persistent workgroups walk the merge tiles t = blockIdx.x + k*gridDim.x.  The
+// keys of the next tile are loaded into registers while the current tile is
+// merged out of LDS (and its descriptor two tiles ahead), so every workgroup
+// keeps one tile of key loads in flight for the whole kernel.
+constexpr int JOIN_SLOTS = (JOIN_TILE + 1 + JOIN_THREADS - 1) / JOIN_THREADS;  // 2049 items max per tile
 
-  const int64_t b = blockIdx.x;
-  const int j = find_job(tile_base, njobs, b);
-  const JoinQ& J = jobs[j];
-  const int64_t nA = J.A.n, nB = J.B.n;
-  const int64_t t = b - tile_base[j];
-  const int64_t d0 = t * JOIN_TILE;
-  const int64_t d1 = d0 + JOIN_TILE < nA + nB ? d0 + JOIN_TILE : nA + nB;
-  const int64_t a0 = split[b];
-  const int64_t a1 = (t + 1 < J.ntiles) ? split[b + 1] : nA;
-  const int64_t b0 = d0 - a0, b1 = d1 - a1;
-  const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
-  const int nbl = nb + (b1 < nB ? 1 : 0);  // + lookahead element B[b1]
+struct TileKeys {
+  uint64_t h[JOIN_SLOTS];
+  uint32_t l[JOIN_SLOTS];
+};
 
-  for (int i = threadIdx.x; i < na; i += JOIN_THREADS) {
-    sAh[i] = J.A.khi[a0 + i];
-    sAl[i] = J.A.klo[a0 + i];
-  }
-  for (int i = threadIdx.x; i < nbl; i += JOIN_THREADS) {
-    sBh[i] = J.B.khi[b0 + i];
-    sBl[i] = J.B.klo[b0 + i];
-  }
-  __syncthreads();
+__device__ uint64_t g_pad_h[1];
+__device__ uint8_t g_pad_l[1];
 
-  const int dd0 = threadIdx.x * JOIN_IPT;
-  const int dtot = na + nb;
-  int ia = 0, ib = 0;
-  if (dd0 < dtot) {
-    int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      int bj = dd0 - 1 - mid;
-      if (key_le(sAh[mid], sAl[mid], sBh[bj], sBl[bj])) lo = mid + 1; else hi = mid;
-    }
-    ia = lo;
-    ib = dd0 - lo;
-  }
-  int32_t ma[JOIN_IPT], mb[JOIN_IPT];
-  uint32_t mbits = 0;
+// global (address space 1) pointers: flat loads would also count in lgkmcnt and
+// every LDS wait of the merge would then wait for the prefetch as well
+typedef __attribute__((address_space(1))) const uint64_t gu64c;
+typedef __attribute__((address_space(1))) const uint32_t gu32c;
+
+// Branch-free address select: one load per slot, so no wait is forced before the
+// merge.  klo bytes are read as the aligned dword that holds them (key arrays are
+// 256-byte aligned allocations rounded up to 256 bytes, so the dword is in bounds):
+// a full-width loaded register is carried to the next iteration without a
+// narrowing instruction that would wait for the load.
+__device__ __forceinline__ void tile_load(const TileDesc& D, TileKeys& K) {
 #pragma unroll
-  for (int s = 0; s < JOIN_IPT; s++) {
-    ma[s] = 0;
-    mb[s] = 0;
-    if (dd0 + s < dtot) {
-      bool takeA;
-      if (ia >= na) takeA = false;
-      else if (ib >= nb) takeA = true;
-      else takeA = key_le(sAh[ia], sAl[ia], sBh[ib], sBl[ib]);
-      if (takeA) {
-        if (ib < nbl && sAh[ia] == sBh[ib] && sAl[ia] == sBl[ib]) {
-          ma[s] = ia;
-          mb[s] = ib;
-          mbits |= 1u << s;
-        }
-        ia++;
-      } else {
-        ib++;
-      }
+  for (int s = 0; s < JOIN_SLOTS; s++) {
+    const int x = threadIdx.x + s * JOIN_THREADS;
+    const uint64_t* ph = g_pad_h;
+    const uint8_t* pl = g_pad_l;
+    if (x < D.na) {
+      ph = D.ah + D.a0 + x;
+      pl = D.al + D.a0 + x;
+    } else if (x < D.na + D.nbl) {
+      ph = D.bh + D.b0 + (x - D.na);
+      pl = D.bl + D.b0 + (x - D.na);
     }
+    K.h[s] = *(gu64c*)ph;
+    K.l[s] = *(gu32c*)((uintptr_t)pl & ~(uintptr_t)3);
   }
-  // maxDistance filter (ReferenceContainer.java:442,482); distance <= 65535 always
-  if (mbits && !mark && J.maxd < 65535) {
+}
+
+__global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
+                                                      const TileDesc* __restrict__ desc, int64_t ntiles,
+                                                      uint2* __restrict__ pairs, int32_t* __restrict__ tile_cnt,
+                                                      int mark) {
+  // A keys at [0, na), B keys (+ lookahead) at [JOIN_TILE, JOIN_TILE + nbl), one pad slot
+  __shared__ uint64_t sH[2 * JOIN_TILE + 2];
+  __shared__ uint8_t sL[2 * JOIN_TILE + 2];
+  __shared__ int32_t sScan[4];
+  const uint64_t* sAh = sH;
+  const uint64_t* sBh = sH + JOIN_TILE;
+  const uint8_t* sAl = sL;
+  const uint8_t* sBl = sL + JOIN_TILE;
+
+  const int64_t G = gridDim.x;
+  int64_t b = blockIdx.x;
+  if (b >= ntiles) return;
+  TileDesc Dc = desc[b];
+  TileDesc Dn;
+  if (b + G < ntiles) Dn = desc[b + G];
+  TileKeys K;
+  tile_load(Dc, K);
+  for (; b < ntiles; b += G) {
+    const int na = Dc.na, nb = Dc.nb, nbl = Dc.nbl;
+    // branch-free LDS fill (a branchy one would leave the prefetch registers "maybe
+    // pending" on skipped paths and force waits in the middle of the next prefetch)
+#pragma unroll
+    for (int s = 0; s < JOIN_SLOTS; s++) {
+      const int x = threadIdx.x + s * JOIN_THREADS;
+      const int64_t gi = x < na ? Dc.a0 + x : Dc.b0 + (x - na);
+      const int slot = x < na ? x : (x < na + nbl ? JOIN_TILE + (x - na) : 2 * JOIN_TILE + 1);
+      sH[slot] = K.h[s];
+      sL[slot] = (uint8_t)(K.l[s] >> (8 * (gi & 3)));
+    }
+    __syncthreads();
+    // prefetch: keys of the next tile, descriptor of the one after
+    const int64_t a0 = Dc.a0, b0 = Dc.b0;
+    const int jc = Dc.job;
+    if (b + G < ntiles) {
+      Dc = Dn;
+      if (b + 2 * G < ntiles) Dn = desc[b + 2 * G];
+      tile_load(Dc, K);
+    }
+
+    const int dd0 = threadIdx.x * JOIN_IPT;
+    const int dtot = na + nb;
+    int ia = 0, ib = 0;
+    if (dd0 < dtot) {
+      int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        int bj = dd0 - 1 - mid;
+        if (key_le(sAh[mid], sAl[mid], sBh[bj], sBl[bj])) lo = mid + 1; else hi = mid;
+      }
+      ia = lo;
+      ib = dd0 - lo;
+    }
+    int32_t ma[JOIN_IPT], mb[JOIN_IPT];
+    uint32_t mbits = 0;
 #pragma unroll
     for (int s = 0; s < JOIN_IPT; s++) {
-      if (mbits & (1u << s)) {
-        const uint8_t* ra = J.A.rows + (a0 + ma[s]) * YRWI_ROW_BYTES;
-        const uint8_t* rb = J.B.rows + (b0 + mb[s]) * YRWI_ROW_BYTES;
-        if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << s);
+      ma[s] = 0;
+      mb[s] = 0;
+      if (dd0 + s < dtot) {
+        bool takeA;
+        if (ia >= na) takeA = false;
+        else if (ib >= nb) takeA = true;
+        else takeA = key_le(sAh[ia], sAl[ia], sBh[ib], sBl[ib]);
+        if (takeA) {
+          if (ib < nbl && sAh[ia] == sBh[ib] && sAl[ia] == sBl[ib]) {
+            ma[s] = ia;
+            mb[s] = ib;
+            mbits |= 1u << s;
+          }
+          ia++;
+        } else {
+          ib++;
+        }
       }
     }
-  }
-  if (mark) {
+    if (__syncthreads_or(mbits != 0)) {
+      const JoinQ& J = jobs[jc];
+      // maxDistance filter (ReferenceContainer.java:442,482); distance <= 65535 always
+      if (mbits && !mark && J.maxd < 65535) {
 #pragma unroll
-    for (int s = 0; s < JOIN_IPT; s++)
-      if (mbits & (1u << s)) J.removed[a0 + ma[s]] = 1;
-    return;
-  }
-  const int32_t cnt = __popc(mbits);
-  int32_t tot;
-  int32_t off = block_excl_sum256(cnt, sScan, &tot);
-  uint2* out = pairs + b * (int64_t)JOIN_MAXM;
+        for (int s = 0; s < JOIN_IPT; s++) {
+          if (mbits & (1u << s)) {
+            const uint8_t* ra = J.A.rows + (a0 + ma[s]) * YRWI_ROW_BYTES;
+            const uint8_t* rb = J.B.rows + (b0 + mb[s]) * YRWI_ROW_BYTES;
+            if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << s);
+          }
+        }
+      }
+      if (mark) {
 #pragma unroll
-  for (int s = 0; s < JOIN_IPT; s++) {
-    if (mbits & (1u << s)) {
-      out[off] = make_uint2((uint32_t)(a0 + ma[s]), (uint32_t)(b0 + mb[s]));
-      off++;
+        for (int s = 0; s < JOIN_IPT; s++)
+          if (mbits & (1u << s)) J.removed[a0 + ma[s]] = 1;
+      }
     }
+    if (!mark) {
+      const int32_t cnt = __popc(mbits);
+      int32_t tot;
+      int32_t off = block_excl_sum256(cnt, sScan, &tot);
+      uint2* out = pairs + b * (int64_t)JOIN_MAXM;
+#pragma unroll
+      for (int s = 0; s < JOIN_IPT; s++) {
+        if (mbits & (1u << s)) {
+          out[off] = make_uint2((uint32_t)(a0 + ma[s]), (uint32_t)(b0 + mb[s]));
+          off++;
+        }
+      }
+      if (threadIdx.x == 0) tile_cnt[b] = tot;
+    }
+    __syncthreads();  // LDS is rewritten for the next tile
   }
-  if (threadIdx.x == 0) tile_cnt[b] = tot;
 }
 
 // ============================================================ join: probe
@@ -451,25 +532,50 @@ __device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, 
   return o;
 }
 
+// One workgroup per 64 consecutive tiles: the tiles' matches are concatenated
+// (LDS prefix of their counts) and spread over all 256 threads.
+constexpr int COMPACT_TILES = 64;
+
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
-                                                 int njobs, const uint2* __restrict__ pairs,
+                                                 int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off) {
-  const int64_t b = blockIdx.x;
-  const int32_t cnt = tile_cnt[b];
-  if (cnt == 0) return;
-  const int j = find_job(tile_base, njobs, b);
-  const JoinQ& J = jobs[j];
-  const int64_t off = tile_off[b];
-  const uint2* in = pairs + b * (int64_t)JOIN_MAXM;
-  for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const uint2 pr = in[i];
+  __shared__ int32_t sPre[COMPACT_TILES + 1];
+  __shared__ int32_t sJob[COMPACT_TILES];
+  __shared__ int64_t sOff[COMPACT_TILES];
+  const int64_t t0 = (int64_t)blockIdx.x * COMPACT_TILES;
+  if (threadIdx.x < 64) {
+    const int64_t t = t0 + threadIdx.x;
+    int32_t c = 0;
+    if (t < ntiles) {
+      c = tile_cnt[t];
+      if (c) {
+        sJob[threadIdx.x] = find_job(tile_base, njobs, t);
+        sOff[threadIdx.x] = tile_off[t];
+      }
+    }
+    const int32_t inc = wave_incl_sum(c);
+    sPre[threadIdx.x + 1] = inc;
+    if (threadIdx.x == 0) sPre[0] = 0;
+  }
+  __syncthreads();
+  const int32_t total = sPre[COMPACT_TILES];
+  for (int m = threadIdx.x; m < total; m += blockDim.x) {
+    int lo = 0, hi = COMPACT_TILES - 1;  // largest lt with sPre[lt] <= m
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sPre[mid] <= m) lo = mid; else hi = mid - 1;
+    }
+    const int i = m - sPre[lo];
+    const JoinQ& J = jobs[sJob[lo]];
+    const uint2 pr = pairs[(t0 + lo) * (int64_t)JOIN_MAXM + i];
+    const int64_t o = sOff[lo] + i;
     const uint8_t* ra = J.A.rows + (int64_t)pr.x * YRWI_ROW_BYTES;
     const uint8_t* rb = J.B.rows + (int64_t)pr.y * YRWI_ROW_BYTES;
-    Row o = joined_row(ra, rb, J.mode, J.now_ms);
-    store_row(J.out_rows + (off + i) * YRWI_ROW_BYTES, o);
-    J.out_khi[off + i] = J.A.khi[pr.x];
-    J.out_klo[off + i] = J.A.klo[pr.x];
+    const Row r = joined_row(ra, rb, J.mode, J.now_ms);
+    store_row(J.out_rows + o * YRWI_ROW_BYTES, r);
+    J.out_khi[o] = J.A.khi[pr.x];
+    J.out_klo[o] = J.A.klo[pr.x];
   }
 }
 
@@ -1105,9 +1211,9 @@ __device__ __forceinline__ int32_t host_count(const RankQ& Q, const Row& r) {
   }
 }
 
-// bitonic sort, descending on (k1, k2), N entries in LDS, all threads participate
-template <int N, int NT>
-__device__ __forceinline__ void bitonic_desc(uint64_t* k1, uint64_t* k2) {
+// bitonic sort, descending on (k1, k2), N (power of two) entries in LDS, all NT threads participate
+template <int NT>
+__device__ __forceinline__ void bitonic_desc(uint64_t* k1, uint64_t* k2, int N) {
   for (int size = 2; size <= N; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = threadIdx.x; i < N / 2; i += NT) {
@@ -1126,48 +1232,72 @@ __device__ __forceinline__ void bitonic_desc(uint64_t* k1, uint64_t* k2) {
   }
 }
 
+__device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 2;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// block exclusive scan (sum) for NT threads (multiple of 64, <= 1024); sh >= NT/64 ints
+template <int NT>
+__device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t* sh, int32_t* tot) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t inc = wave_incl_sum(v);
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  int32_t o = 0, all = 0;
+  for (int w = 0; w < NT / 64; w++) { if (w < wv) o += sh[w]; all += sh[w]; }
+  __syncthreads();
+  *tot = all;
+  return o + inc - v;
+}
+
 // dedupe (equal score and hashCode: the TreeSet keeps the first arrival) and
-// compact the first `k` survivors of a sorted LDS list into out; returns count
-template <int N, int NT>
-__device__ __forceinline__ int32_t dedupe_take(const uint64_t* k1, const uint64_t* k2, int32_t k, Cand* out,
-                                               int32_t* sScan) {
-  constexpr int IPT = N / NT;
-  const int i0 = threadIdx.x * IPT;
+// compact the first `k` survivors of a sorted LDS list of N entries into out;
+// returns the number written, *distinct = survivors before the cut at k
+template <int NT>
+__device__ __forceinline__ int32_t dedupe_take(const uint64_t* k1, const uint64_t* k2, int N, int32_t k, Cand* out,
+                                               int32_t* sScan, int32_t* distinct) {
+  const int ipt = (N + NT - 1) / NT;  // <= 32
+  const int i0 = threadIdx.x * ipt;
   int32_t keep = 0;
   uint32_t bits = 0;
-#pragma unroll
-  for (int s = 0; s < IPT; s++) {
+  for (int s = 0; s < ipt; s++) {
     const int i = i0 + s;
+    if (i >= N) break;
     bool v = k2[i] != 0;
     if (v && i > 0 && k1[i] == k1[i - 1] && (k2[i] >> 32) == (k2[i - 1] >> 32)) v = false;
     if (v) { bits |= 1u << s; keep++; }
   }
   int32_t tot;
-  int32_t off;
-  if (NT == 256) {
-    off = block_excl_sum256(keep, sScan, &tot);
-  } else {
-    // generic NT (multiple of 64, <= 1024)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int32_t inc = wave_incl_sum(keep);
-    if (lane == 63) sScan[wv] = inc;
-    __syncthreads();
-    int32_t o = 0, all = 0;
-    for (int w = 0; w < NT / 64; w++) { if (w < wv) o += sScan[w]; all += sScan[w]; }
-    __syncthreads();
-    off = o + inc - keep;
-    tot = all;
-  }
-#pragma unroll
-  for (int s = 0; s < IPT; s++) {
+  int32_t off = block_excl_sum<NT>(keep, sScan, &tot);
+  for (int s = 0; s < ipt; s++) {
     if (bits & (1u << s)) {
       if (off < k) { out[off].k1 = k1[i0 + s]; out[off].k2 = k2[i0 + s]; }
       off++;
     }
   }
+  if (distinct) *distinct = tot;
   return tot < k ? tot : k;
 }
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const uint64_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const uint64_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+  return v;
+}
+
+// Per chunk: cardinal of every live posting, then the chunk's first kq distinct
+// (score, hashCode) classes in TreeSet order.  The kq-th largest score key T is
+// found by an MSB-first radix select (8-bit digits over the bits where the
+// chunk's keys differ, LDS histograms); only keys >= T -- a prefix of the sorted
+// chunk -- are sorted.  If the TreeSet dedupe leaves fewer than kq classes in
+// that prefix, the whole chunk is sorted instead (exact either way).
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
                                                         const int64_t* __restrict__ chunk_base, int nq,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
@@ -1175,36 +1305,117 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ uint64_t s1[CHUNK];
   __shared__ uint64_t s2[CHUNK];
   __shared__ int32_t sScan[4];
+  __shared__ int32_t sHist[256];
+  __shared__ int32_t sSel[2];
+  __shared__ uint64_t sRed[8];
   __shared__ NormState sN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t b = blockIdx.x;
   const int qi = find_job(chunk_base, nq, b);
   const RankQ& Q = qs[qi];
-  if (threadIdx.x == 0) sN = norm[qi];
+  if (tid == 0) sN = norm[qi];
   __syncthreads();
   const int64_t c = b - chunk_base[qi];
-  const int64_t e0 = c * CHUNK + (int64_t)threadIdx.x * CHUNK_IPT;
+  const int64_t e0 = c * CHUNK + (int64_t)tid * CHUNK_IPT;
+  uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
+  int32_t nvl = 0;
+  uint64_t mx = 0, mn = ~0ull;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int64_t e = e0 + s;
-    const int li = threadIdx.x * CHUNK_IPT + s;
-    uint64_t a = 0, z = 0;
+    a[s] = 0;
+    z[s] = 0;
     if (e < Q.n && !(Q.removed && Q.removed[e])) {
       const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
       const Feat t = decode(r);
       const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
       const int64_t score = cardinal(r, t, sN, Q, hc);
       const int32_t h = url_hashcode(r);
-      a = (uint64_t)score ^ 0x8000000000000000ull;
-      z = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+      a[s] = (uint64_t)score ^ 0x8000000000000000ull;
+      z[s] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+      nvl++;
+      mx = a[s] > mx ? a[s] : mx;
+      mn = a[s] < mn ? a[s] : mn;
     }
-    s1[li] = a;
-    s2[li] = z;
   }
-  __syncthreads();
-  bitonic_desc<CHUNK, CHUNK_THREADS>(s1, s2);
   const int32_t kq = Q.k < kc ? Q.k : kc;
-  int32_t n = dedupe_take<CHUNK, CHUNK_THREADS>(s1, s2, kq, cand + b * (int64_t)kc, sScan);
-  if (threadIdx.x == 0) cand_cnt[b] = n;
+  int32_t nv;
+  (void)block_excl_sum<CHUNK_THREADS>(nvl, sScan, &nv);
+  if (kq <= 0 || nv == 0) {
+    if (tid == 0) cand_cnt[b] = 0;
+    return;
+  }
+  Cand* out = cand + b * (int64_t)kc;
+  uint64_t T = 0;  // select live keys >= T
+  if (nv > kq) {
+    mx = wave_max_u64(mx);
+    mn = wave_min_u64(mn);
+    if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
+    __syncthreads();
+    uint64_t gmx = sRed[0], gmn = sRed[4];
+    for (int w = 1; w < 4; w++) { gmx = sRed[w] > gmx ? sRed[w] : gmx; gmn = sRed[4 + w] < gmn ? sRed[4 + w] : gmn; }
+    const uint64_t diff = gmx ^ gmn;
+    if (diff == 0) {
+      T = gmx;
+    } else {
+      int hi = 64 - __clzll((long long)diff);  // keys differ only in bits [0, hi)
+      uint64_t prefix = hi == 64 ? 0 : (gmx >> hi) << hi;
+      int32_t rem = kq;
+      while (hi > 0) {
+        const int lo = hi > 8 ? hi - 8 : 0;
+        const uint32_t wmask = (1u << (hi - lo)) - 1u;
+        sHist[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < CHUNK_IPT; s++)
+          if (z[s] && (hi == 64 || (a[s] >> hi) == (prefix >> hi)))
+            atomicAdd(&sHist[(uint32_t)(a[s] >> lo) & wmask], 1);
+        __syncthreads();
+        if (tid < 64) {
+          int32_t h4[4];
+          int32_t sum = 0;
+          for (int j = 0; j < 4; j++) { h4[j] = sHist[4 * lane + j]; sum += h4[j]; }
+          const int32_t inc = wave_incl_sum(sum);
+          const int32_t all = __shfl(inc, 63, 64);
+          int32_t cum = all - inc;  // keys in higher bins than this lane's
+          for (int j = 3; j >= 0; j--) {
+            if (cum < rem && cum + h4[j] >= rem) { sSel[0] = 4 * lane + j; sSel[1] = rem - cum; }
+            cum += h4[j];
+          }
+        }
+        __syncthreads();
+        prefix |= (uint64_t)sSel[0] << lo;
+        rem = sSel[1];
+        hi = lo;
+      }
+      T = prefix;
+    }
+  }
+  // compact the selected prefix into LDS and sort it
+  int32_t mine = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) mine += (z[s] && a[s] >= T) ? 1 : 0;
+  int32_t nsel;
+  int32_t off = block_excl_sum<CHUNK_THREADS>(mine, sScan, &nsel);
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++)
+    if (z[s] && a[s] >= T) { s1[off] = a[s]; s2[off] = z[s]; off++; }
+  const int P = pow2_at_least(nsel);
+  for (int i = nsel + tid; i < P; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
+  __syncthreads();
+  bitonic_desc<CHUNK_THREADS>(s1, s2, P);
+  int32_t distinct;
+  int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, P, kq, out, sScan, &distinct);
+  if (distinct < kq && nsel < nv) {
+    // the TreeSet dedupe consumed part of the prefix: sort the whole chunk
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++) { s1[tid * CHUNK_IPT + s] = a[s]; s2[tid * CHUNK_IPT + s] = z[s]; }
+    __syncthreads();
+    bitonic_desc<CHUNK_THREADS>(s1, s2, CHUNK);
+    n = dedupe_take<CHUNK_THREADS>(s1, s2, CHUNK, kq, out, sScan, nullptr);
+  }
+  if (tid == 0) cand_cnt[b] = n;
 }
 
 // merge: group g gathers lists [in_base[g], in_base[g]+in_n[g]) (each <= k valid
@@ -1221,6 +1432,13 @@ __global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, con
   __shared__ int32_t sOff[65];
   const int64_t g = blockIdx.x;
   const int64_t base = grp_base[g], nl = grp_n[g];
+  if (nl <= 1) {  // one list: already sorted and deduplicated
+    const int32_t c = nl == 1 ? min(in_cnt[base], k) : 0;
+    const Cand* src = in + base * (int64_t)in_stride;
+    for (int i = threadIdx.x; i < c; i += 1024) out[g * (int64_t)out_stride + i] = src[i];
+    if (threadIdx.x == 0) out_cnt[g] = c;
+    return;
+  }
   // offsets of each list inside the LDS image
   if (threadIdx.x == 0) {
     int32_t o = 0;
@@ -1229,9 +1447,8 @@ __global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, con
   }
   __syncthreads();
   const int32_t total = sOff[nl < 64 ? nl : 64];
-  for (int i = threadIdx.x; i < SORTN; i += 1024) { s1[i] = 0; s2[i] = 0; }
-  __syncthreads();
-  for (int64_t l = 0; l < nl; l++) {
+  const int P = pow2_at_least(total);
+  for (int l = 0; l < nl; l++) {
     const int32_t c = in_cnt[base + l], o = sOff[l];
     const Cand* src = in + (base + l) * (int64_t)in_stride;
     for (int i = threadIdx.x; i < c; i += 1024) {
@@ -1239,10 +1456,10 @@ __global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, con
       s2[o + i] = src[i].k2;
     }
   }
-  (void)total;
+  for (int i = total + threadIdx.x; i < P; i += 1024) { s1[i] = 0; s2[i] = 0; }
   __syncthreads();
-  bitonic_desc<SORTN, 1024>(s1, s2);
-  int32_t n = dedupe_take<SORTN, 1024>(s1, s2, k, out + g * (int64_t)out_stride, sScan);
+  bitonic_desc<1024>(s1, s2, P);
+  int32_t n = dedupe_take<1024>(s1, s2, P, k, out + g * (int64_t)out_stride, sScan, nullptr);
   if (threadIdx.x == 0) out_cnt[g] = n;
 }
 
@@ -1373,17 +1590,27 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
 }
 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
-                     int64_t merge_tiles, int64_t total_tiles, int64_t* d_split, uint2* d_pairs,
+                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, uint2* d_pairs,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0, void* evm,
                      void* ev1) {
   if (total_tiles <= 0) return 0;
+  static int join_grid = 0;  // resident k_join workgroups on the whole device
+  if (!join_grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_join), JOIN_THREADS,
+                                                     0) != hipSuccess)
+      return YRWI_E_HIP;
+    join_grid = std::max(1, cus * std::max(1, per_cu));
+  }
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, nmerge, merge_tiles, d_split);
+                       d_tile_base, nmerge, merge_tiles, d_desc);
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
-    hipLaunchKernelGGL(k_join, dim3((unsigned)merge_tiles), dim3(JOIN_THREADS), 0, S(st), d_jobs, d_tile_base, nmerge,
-                       d_split, d_pairs, d_tile_cnt, mark ? 1 : 0);
+    hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
+                       S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (total_tiles > merge_tiles)
     hipLaunchKernelGGL(k_probe, dim3((unsigned)(total_tiles - merge_tiles)), dim3(PROBE_TILE), 0, S(st),
@@ -1393,8 +1620,8 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
-                       d_pairs, d_tile_cnt, d_tile_off);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
+                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_tile_cnt, d_tile_off);
   }
   return rc(hipGetLastError());
 }
