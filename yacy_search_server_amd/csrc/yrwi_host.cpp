@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -144,11 +145,23 @@ struct Plan {
 
 }  // namespace
 
+struct KeyHash {
+  size_t operator()(const KeyT& k) const { return (size_t)(k.hi * 0x9E3779B97F4A7C15ull) ^ k.lo; }
+};
+
+// pinned host staging for the per-batch uploads (pageable copies would block)
+struct Stage {
+  uint8_t* p = nullptr;
+  size_t cap = 0, used = 0;
+};
+
 struct yrwi_ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
-  std::map<KeyT, ListRec> lists;
+  std::unordered_map<KeyT, ListRec, KeyHash> lists;
+  Stage stage;
+  int64_t probe_ratio = 16;  // YRWI_PROBE_RATIO, read once per call
   Arena index_mem{(size_t)1 << 30};
   Arena arena{(size_t)256 << 20};
   std::string err;
@@ -184,7 +197,32 @@ static T* arena_alloc(yrwi_ctx* ctx, int64_t count) {
 template <class T>
 static int upload(yrwi_ctx* ctx, T* dst, const std::vector<T>& v) {
   if (v.empty()) return 0;
-  HIPCHK(ctx, hipMemcpyAsync(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  const size_t bytes = v.size() * sizeof(T);
+  Stage& S = ctx->stage;
+  size_t off = (S.used + 255) & ~(size_t)255;
+  if (off + bytes > S.cap) {
+    // copies still read the old buffer: drain them, then grow
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (S.p) HIPCHK(ctx, hipHostFree(S.p));
+    S.p = nullptr;
+    S.cap = std::max<size_t>(std::max<size_t>(2 * S.cap, bytes + 256), (size_t)4 << 20);
+    HIPCHK(ctx, hipHostMalloc(reinterpret_cast<void**>(&S.p), S.cap, hipHostMallocDefault));
+    off = 0;
+  }
+  std::memcpy(S.p + off, v.data(), bytes);
+  HIPCHK(ctx, hipMemcpyAsync(dst, S.p + off, bytes, hipMemcpyHostToDevice, ctx->stream));
+  S.used = off + bytes;
+  return 0;
+}
+
+// start of a device pass: nothing is in flight any more, scratch can be reused
+static int begin_pass(yrwi_ctx* ctx) {
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->arena.reset();
+  ctx->stage.used = 0;
+  ctx->evnext = 0;
+  const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
+  ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
   return 0;
 }
 
@@ -347,6 +385,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   ctx->arena.release();
   ctx->index_mem.release();
   for (auto e : ctx->evpool) hipEventDestroy(e);
+  if (ctx->stage.p) hipHostFree(ctx->stage.p);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -441,39 +480,45 @@ static int plan_query(yrwi_ctx* ctx, const yrwi_query_desc& d, Plan* P) {
   if (d.nincl < 0 || d.nexcl < 0 || d.nincl > YRWI_MAX_TERMS || d.nexcl > YRWI_MAX_TERMS)
     return ctx->fail(YRWI_E_ARG, "too many terms");
   // HandleSet: sorted (Base64Order) set of term hashes
-  std::map<KeyT, int> inc, exc;
-  for (int i = 0; i < d.nincl; i++) {
-    KeyT k;
-    if (!key_of(d.incl + 12 * i, &k)) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
-    inc.emplace(k, i);
-  }
-  for (int i = 0; i < d.nexcl; i++) {
-    KeyT k;
-    if (!key_of(d.excl + 12 * i, &k)) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
-    exc.emplace(k, i);
-  }
+  KeyT inc[YRWI_MAX_TERMS], exc[YRWI_MAX_TERMS];
+  int ninc = 0, nexc = 0;
+  for (int i = 0; i < d.nincl; i++)
+    if (!key_of(d.incl + 12 * i, &inc[ninc++])) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
+  for (int i = 0; i < d.nexcl; i++)
+    if (!key_of(d.excl + 12 * i, &exc[nexc++])) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
+  std::sort(inc, inc + ninc);
+  ninc = (int)(std::unique(inc, inc + ninc) - inc);
+  std::sort(exc, exc + nexc);
+  nexc = (int)(std::unique(exc, exc + nexc) - exc);
   P->empty = true;
   P->postings_in = 0;
-  if (inc.empty()) return 0;
-  std::vector<const ListRec*> incl;
-  for (auto& kv : inc) {
-    auto it = ctx->lists.find(kv.first);
+  if (ninc == 0) return 0;
+  const ListRec* incl[YRWI_MAX_TERMS];
+  for (int i = 0; i < ninc; i++) {
+    auto it = ctx->lists.find(inc[i]);
     if (it == ctx->lists.end() || it->second.n == 0) return 0;  // conjunction: any missing term -> empty
-    incl.push_back(&it->second);
+    incl[i] = &it->second;
   }
-  bool use_excl = !exc.empty();
-  std::vector<const ListRec*> excl;
-  for (auto& kv : exc) {
-    auto it = ctx->lists.find(kv.first);
-    if (it == ctx->lists.end() || it->second.n == 0) { use_excl = false; break; }
-    excl.push_back(&it->second);
+  bool use_excl = nexc > 0;
+  P->excl.clear();
+  for (int i = 0; i < nexc && use_excl; i++) {
+    auto it = ctx->lists.find(exc[i]);
+    if (it == ctx->lists.end() || it->second.n == 0) use_excl = false;
+    else P->excl.push_back(&it->second);
   }
+  if (!use_excl) P->excl.clear();
   // joinContainers: TreeMap<Long>((int)(size*1000 + count)); put overwrites equal keys
-  std::map<int64_t, const ListRec*> tm;
-  for (size_t c = 0; c < incl.size(); c++) tm[(int64_t)add32(mul32((int32_t)incl[c]->n, 1000), (int32_t)c)] = incl[c];
-  for (auto& kv : tm) P->seq.push_back(kv.second);
-  if (use_excl) P->excl = excl;
-  for (auto* l : incl) P->postings_in += l->n;
+  std::pair<int32_t, int> tm[YRWI_MAX_TERMS];
+  for (int c = 0; c < ninc; c++) tm[c] = {add32(mul32((int32_t)incl[c]->n, 1000), c), c};
+  std::stable_sort(tm, tm + ninc, [](const std::pair<int32_t, int>& a, const std::pair<int32_t, int>& b) {
+    return a.first < b.first;
+  });
+  P->seq.clear();
+  for (int i = 0; i < ninc; i++) {
+    if (i + 1 < ninc && tm[i + 1].first == tm[i].first) continue;  // the later put wins
+    P->seq.push_back(incl[tm[i].second]);
+  }
+  for (int i = 0; i < ninc; i++) P->postings_in += incl[i]->n;
   for (auto* l : P->excl) P->postings_in += l->n;
   P->empty = false;
   return 0;
@@ -506,21 +551,15 @@ struct Timing {
   hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
 };
 
-// Intersection algorithm: probe the large list when sizes are skewed.
-static int64_t probe_ratio() {
-  const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either algorithm with it
-  return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
-}
-
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
-static void layout_jobs(std::vector<JoinQ>& jobs, std::vector<int>& owner, std::vector<int64_t>& tile_base,
+static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vector<int>& owner, std::vector<int64_t>& tile_base,
                         int* nmerge, int64_t* merge_tiles, int64_t* tiles) {
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
     JoinQ& J = jobs[i];
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
-    J.algo = (nl > probe_ratio() * ns) ? JA_PROBE : JA_MERGE;
+    J.algo = (nl > probe_ratio * ns) ? JA_PROBE : JA_MERGE;  // skewed sizes: probe the large list
     J.small_is_A = J.A.n <= J.B.n;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, PROBE_TILE);
     order[i] = i;
@@ -582,7 +621,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     if (jobs.empty()) break;
     int nmerge;
     int64_t merge_tiles, tiles;
-    layout_jobs(jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+    layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
     const int nj = (int)jobs.size();
     if (st)
       for (const JoinQ& J : jobs) (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) += step_bytes(J.mode, J.A.n, J.B.n);
@@ -635,7 +674,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     if (!jobs.empty()) {
       int nmerge;
       int64_t merge_tiles, tiles;
-      layout_jobs(jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+      layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
       const int nj = (int)jobs.size();
       JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
       int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
@@ -793,9 +832,14 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   ShardSum* d_all = W > 1 ? arena_alloc<ShardSum>(ctx, (int64_t)nq * W) : d_ss;
   NormState* d_norm = arena_alloc<NormState>(ctx, nq);
   if (!d_q || !d_cb || !d_cs || !d_ss || !d_all || !d_norm) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base)) return YRWI_E_HIP;
+  std::vector<int32_t> chunk_q((size_t)chunks);
+  for (int qi = 0; qi < nq; qi++)
+    for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++) chunk_q[(size_t)(chunk_base[(size_t)qi] + c)] = qi;
+  int32_t* d_cq = arena_alloc<int32_t>(ctx, chunks);
+  if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base) || upload(ctx, d_cq, chunk_q)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
-  if (launch_reduce(d_q, d_cb, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
   if (W > 1 && any_auth) {
     int rc2 = exchange_host_counts(ctx, nq, nslots, slot_base, d_hkeys, d_hcnt, d_ss);
     if (rc2) return rc2;
@@ -810,7 +854,7 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   if (h_scores_all) {  // yrwi_normalize_score
     int64_t* d_sc = arena_alloc<int64_t>(ctx, rq[0].n);
     if (!d_sc) return ctx->fail(YRWI_E_NOMEM, "arena");
-    if (launch_score_all(d_q, d_cb, nq, chunks, d_norm, d_sc, ctx->stream)) return ctx->fail(YRWI_E_HIP, "score launch");
+    if (launch_score_all(d_q, d_cq, nq, chunks, d_norm, d_sc, ctx->stream)) return ctx->fail(YRWI_E_HIP, "score launch");
     HIPCHK(ctx, hipMemcpyAsync(h_scores_all, d_sc, sizeof(int64_t) * rq[0].n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     NormState nsh;
@@ -826,34 +870,44 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   Cand* d_cand = arena_alloc<Cand>(ctx, std::max<int64_t>(chunks, 1) * kc);
   int32_t* d_ccnt = arena_alloc<int32_t>(ctx, std::max<int64_t>(chunks, 1));
   if (!d_cand || !d_ccnt) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (launch_score(d_q, d_cb, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
+  if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
-  // ---- merge passes until one list per query
+  // ---- merge passes until one list per query; a query with a single list (one
+  // chunk) is final as it stands and takes no part in any pass
   const int sort_n = keff <= 1024 ? 2048 : 8192;
   const int64_t G = std::max<int64_t>(2, std::min<int64_t>(64, sort_n / keff));
-  int32_t in_stride = kc;
+  int32_t* d_zero = arena_alloc<int32_t>(ctx, 1);
+  if (!d_zero) return ctx->fail(YRWI_E_NOMEM, "arena");
+  HIPCHK(ctx, hipMemsetAsync(d_zero, 0, sizeof(int32_t), ctx->stream));
+  std::vector<const Cand*> fptr((size_t)nq);
+  std::vector<const int32_t*> fcnt((size_t)nq);
   std::vector<int64_t> lists((size_t)nq), lbase((size_t)nq);
-  for (int qi = 0; qi < nq; qi++) { lists[(size_t)qi] = rq[(size_t)qi].nchunks; lbase[(size_t)qi] = chunk_base[(size_t)qi]; }
+  for (int qi = 0; qi < nq; qi++) {
+    lists[(size_t)qi] = rq[(size_t)qi].nchunks;
+    lbase[(size_t)qi] = chunk_base[(size_t)qi];
+    fptr[(size_t)qi] = d_cand + chunk_base[(size_t)qi] * kc;
+    fcnt[(size_t)qi] = lists[(size_t)qi] ? d_ccnt + chunk_base[(size_t)qi] : d_zero;
+  }
   const Cand* cur = d_cand;
   const int32_t* curc = d_ccnt;
-  bool first = true;
+  int32_t in_stride = kc;
   while (true) {
-    bool more = false;
-    for (auto L : lists) more |= L > 1;
-    if (!more && !first) break;
-    first = false;
     std::vector<int64_t> gb, gn;
-    std::vector<int64_t> nl((size_t)nq), nb((size_t)nq);
+    std::vector<int> part;
     for (int qi = 0; qi < nq; qi++) {
-      int64_t L = lists[(size_t)qi];
-      int64_t ng = std::max<int64_t>(1, ceil_div(L, G));
-      nb[(size_t)qi] = (int64_t)gb.size();
-      nl[(size_t)qi] = ng;
+      const int64_t L = lists[(size_t)qi];
+      if (L <= 1) continue;
+      const int64_t ng = ceil_div(L, G);
+      const int64_t first = (int64_t)gb.size();
       for (int64_t g = 0; g < ng; g++) {
         gb.push_back(lbase[(size_t)qi] + g * G);
-        gn.push_back(std::max<int64_t>(0, std::min<int64_t>(G, L - g * G)));
+        gn.push_back(std::min<int64_t>(G, L - g * G));
       }
+      lists[(size_t)qi] = ng;
+      lbase[(size_t)qi] = first;
+      part.push_back(qi);
     }
+    if (gb.empty()) break;
     const int64_t ngr = (int64_t)gb.size();
     int64_t* d_gb = arena_alloc<int64_t>(ctx, ngr);
     int64_t* d_gn = arena_alloc<int64_t>(ctx, ngr);
@@ -863,17 +917,21 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
     if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn)) return YRWI_E_HIP;
     if (launch_merge(cur, curc, in_stride, d_gb, d_gn, ngr, keff, d_out, d_oc, keff, sort_n, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "merge launch");
+    for (int qi : part) {
+      fptr[(size_t)qi] = d_out + lbase[(size_t)qi] * keff;
+      fcnt[(size_t)qi] = d_oc + lbase[(size_t)qi];
+    }
     in_stride = keff;
     cur = d_out;
     curc = d_oc;
-    lists = nl;
-    lbase = nb;
   }
-  // after the loop every query owns exactly one list, at index qi
+  const Cand** d_fptr = arena_alloc<const Cand*>(ctx, nq);
+  const int32_t** d_fcnt = arena_alloc<const int32_t*>(ctx, nq);
   yrwi_hit* d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);
   int32_t* d_nout = arena_alloc<int32_t>(ctx, nq);
-  if (!d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (launch_emit(d_q, nq, cur, curc, keff, kmax, d_hits, d_nout, ctx->stream)) return ctx->fail(YRWI_E_HIP, "emit launch");
+  if (!d_fptr || !d_fcnt || !d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
+  if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, ctx->stream)) return ctx->fail(YRWI_E_HIP, "emit launch");
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
   if (W == 1) {
     HIPCHK(ctx, hipMemcpyAsync(h_hits, d_hits, sizeof(yrwi_hit) * nq * kmax, hipMemcpyDeviceToHost, ctx->stream));
@@ -942,8 +1000,7 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
     if (rc) return rc;
     if (st) st->postings_in += plans[(size_t)i].postings_in;
   }
-  ctx->arena.reset();
-  ctx->evnext = 0;
+  if (begin_pass(ctx)) return YRWI_E_HIP;
   Timing tm;
   tm.t0 = ctx->event();
   hipEventRecord(tm.t0, ctx->stream);
@@ -992,7 +1049,7 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
   std::vector<Plan> plans(1);
   int rc = plan_query(ctx, d, &plans[0]);
   if (rc) return rc;
-  ctx->arena.reset();
+  if (begin_pass(ctx)) return YRWI_E_HIP;
   rc = run_join_phase(ctx, plans, nullptr, nullptr);
   if (rc) return rc;
   const Plan& P = plans[0];
@@ -1024,7 +1081,7 @@ extern "C" int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_
   if (m <= 0) return 0;
   if (m > MAX_LIST) return ctx->fail(YRWI_E_LIMIT, "container longer than 53,687,091 rows");
   hipSetDevice(ctx->device);
-  ctx->arena.reset();
+  if (begin_pass(ctx)) return YRWI_E_HIP;
   uint8_t* rows = arena_alloc<uint8_t>(ctx, m * 40);
   uint64_t* khi = arena_alloc<uint64_t>(ctx, m);
   uint8_t* klo = arena_alloc<uint8_t>(ctx, m);

@@ -168,18 +168,19 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_mid, void* ev_end);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
-int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
+                  int64_t total_chunks,
                   ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
-int launch_score(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                  const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* stream);
 int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, const int64_t* d_grp_in_base,
                  const int64_t* d_grp_in_n, int64_t ngroups, int32_t k, Cand* d_out, int32_t* d_out_cnt,
                  int32_t out_stride, int sort_n, void* stream);
-int launch_emit(const RankQ* d_q, int32_t nq, const Cand* d_final, const int32_t* d_final_cnt,
-                int32_t stride, int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
-int launch_score_all(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
+int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* stream);
 
 }  // namespace yrwi

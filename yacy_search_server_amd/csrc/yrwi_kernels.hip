@@ -532,9 +532,20 @@ __device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, 
   return o;
 }
 
-// One workgroup per 64 consecutive tiles: the tiles' matches are concatenated
-// (LDS prefix of their counts) and spread over all 256 threads.
-constexpr int COMPACT_TILES = 64;
+// url-hash key of a row (bytes 0..11), as k_validate computes it for the index
+__device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 10; j++) x = (x << 6) | (uint64_t)(ahpla(r.b(j)) & 63);
+  const uint32_t c10 = (uint32_t)ahpla(r.b(10)) & 63, c11 = (uint32_t)ahpla(r.b(11)) & 63;
+  hi = (x << 4) | (c10 >> 2);
+  lo = ((c10 & 3u) << 6) | c11;
+}
+
+// One workgroup per COMPACT_TILES consecutive tiles: the tiles' matches are
+// concatenated (LDS prefix of their counts) and spread over all 256 threads.
+// The output key is recomputed from the gathered row (no key gathers).
+constexpr int COMPACT_TILES = 16;
 
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
@@ -547,7 +558,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
   if (threadIdx.x < 64) {
     const int64_t t = t0 + threadIdx.x;
     int32_t c = 0;
-    if (t < ntiles) {
+    if (threadIdx.x < COMPACT_TILES && t < ntiles) {
       c = tile_cnt[t];
       if (c) {
         sJob[threadIdx.x] = find_job(tile_base, njobs, t);
@@ -555,7 +566,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       }
     }
     const int32_t inc = wave_incl_sum(c);
-    sPre[threadIdx.x + 1] = inc;
+    if (threadIdx.x < COMPACT_TILES) sPre[threadIdx.x + 1] = inc;
     if (threadIdx.x == 0) sPre[0] = 0;
   }
   __syncthreads();
@@ -573,9 +584,12 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     const uint8_t* ra = J.A.rows + (int64_t)pr.x * YRWI_ROW_BYTES;
     const uint8_t* rb = J.B.rows + (int64_t)pr.y * YRWI_ROW_BYTES;
     const Row r = joined_row(ra, rb, J.mode, J.now_ms);
+    uint64_t kh;
+    uint32_t kl;
+    row_key(r, kh, kl);
     store_row(J.out_rows + o * YRWI_ROW_BYTES, r);
-    J.out_khi[o] = J.A.khi[pr.x];
-    J.out_klo[o] = J.A.klo[pr.x];
+    J.out_khi[o] = kh;
+    J.out_klo[o] = (uint8_t)kl;
   }
 }
 
@@ -648,7 +662,7 @@ __device__ __forceinline__ double wave_min_d(double v) {
 constexpr int32_t BIG = 0x7FFFFFFF;
 
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
-                                                         const int64_t* __restrict__ chunk_base, int nq,
+                                                         const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
   __shared__ int32_t sI[4 * (2 * NF + 8)];
   __shared__ double sD[8];
@@ -659,9 +673,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ uint32_t sSegL[CHUNK_THREADS * CHUNK_IPT];
 
   const int64_t b = blockIdx.x;
-  const int qi = find_job(chunk_base, nq, b);
+  const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
-  const int64_t c = b - chunk_base[qi];
+  const int64_t c = b - Q.chunk_base;
   const int64_t e0 = c * CHUNK + (int64_t)threadIdx.x * CHUNK_IPT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 
@@ -1299,7 +1313,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // chunk -- are sorted.  If the TreeSet dedupe leaves fewer than kq classes in
 // that prefix, the whole chunk is sorted instead (exact either way).
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
-                                                        const int64_t* __restrict__ chunk_base, int nq,
+                                                        const int32_t* __restrict__ chunk_q,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
                                                         int32_t* __restrict__ cand_cnt, int32_t kc) {
   __shared__ uint64_t s1[CHUNK];
@@ -1311,18 +1325,20 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ NormState sN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t b = blockIdx.x;
-  const int qi = find_job(chunk_base, nq, b);
+  const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   if (tid == 0) sN = norm[qi];
   __syncthreads();
-  const int64_t c = b - chunk_base[qi];
-  const int64_t e0 = c * CHUNK + (int64_t)tid * CHUNK_IPT;
+  const int64_t c = b - Q.chunk_base;
+  // strided element map (neighbouring lanes read neighbouring rows); order is
+  // irrelevant here, the candidate key carries the container index
+  const int64_t e0 = c * CHUNK + tid;
   uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
   int32_t nvl = 0;
   uint64_t mx = 0, mn = ~0ull;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    const int64_t e = e0 + s;
+    const int64_t e = e0 + s * CHUNK_THREADS;
     a[s] = 0;
     z[s] = 0;
     if (e < Q.n && !(Q.removed && Q.removed[e])) {
@@ -1463,14 +1479,15 @@ __global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, con
   if (threadIdx.x == 0) out_cnt[g] = n;
 }
 
-__global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* __restrict__ fin,
-                       const int32_t* __restrict__ fin_cnt, int32_t stride, int32_t kmax,
-                       yrwi_hit* __restrict__ hits, int32_t* __restrict__ nout) {
+__global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* __restrict__ fin,
+                       const int32_t* const* __restrict__ fin_cnt, int32_t kmax, yrwi_hit* __restrict__ hits,
+                       int32_t* __restrict__ nout) {
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
-  const int32_t n = min(fin_cnt[qi], min(Q.k, kmax));
+  const int32_t n = min(*fin_cnt[qi], min(Q.k, kmax));
+  const Cand* f = fin[qi];
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const Cand cd = fin[(int64_t)qi * stride + i];
+    const Cand cd = f[i];
     const uint32_t idx = ~(uint32_t)cd.k2 & 0x0FFFFFFFu;
     const uint8_t* r = Q.rows + (int64_t)idx * YRWI_ROW_BYTES;
     yrwi_hit h;
@@ -1484,13 +1501,13 @@ __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* __restr
 
 // all scores of a container (yrwi_normalize_score)
 __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
-                                                   const int64_t* __restrict__ chunk_base, int nq,
+                                                   const int32_t* __restrict__ chunk_q,
                                                    const NormState* __restrict__ norm, int64_t* __restrict__ out) {
   const int64_t b = blockIdx.x;
-  const int qi = find_job(chunk_base, nq, b);
+  const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   const NormState N = norm[qi];
-  const int64_t c = b - chunk_base[qi];
+  const int64_t c = b - Q.chunk_base;
   for (int s = threadIdx.x; s < CHUNK; s += blockDim.x) {
     const int64_t e = c * CHUNK + s;
     if (e >= Q.n) break;
@@ -1659,10 +1676,11 @@ int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n
   return rc(hipGetLastError());
 }
 
-int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
+                  int64_t total_chunks,
                   ChunkSum* d_chunks, ShardSum* d_shard, void* st) {
   if (total_chunks > 0)
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_base, nq,
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
@@ -1674,10 +1692,10 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
   return rc(hipGetLastError());
 }
 
-int launch_score(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                  const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* st) {
   if (total_chunks <= 0) return 0;
-  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_base, nq,
+  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                      d_norm, d_cand, d_cand_cnt, kc);
   return rc(hipGetLastError());
 }
@@ -1704,17 +1722,17 @@ int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, c
   return rc(hipGetLastError());
 }
 
-int launch_emit(const RankQ* d_q, int32_t nq, const Cand* d_final, const int32_t* d_final_cnt, int32_t stride,
+int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
                 int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
-  hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, stride, kmax,
+  hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, kmax,
                      d_hits, d_nout);
   return rc(hipGetLastError());
 }
 
-int launch_score_all(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
+int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* st) {
   if (total_chunks <= 0) return 0;
-  hipLaunchKernelGGL(k_score_all, dim3((unsigned)total_chunks), dim3(256), 0, S(st), d_q, d_chunk_base, nq, d_norm,
+  hipLaunchKernelGGL(k_score_all, dim3((unsigned)total_chunks), dim3(256), 0, S(st), d_q, d_chunk_q, d_norm,
                      d_scores);
   return rc(hipGetLastError());
 }
