@@ -228,3 +228,63 @@ def test_forced_join_algorithm(corpus, ratio, monkeypatch):
         assert np.array_equal(ix.term_search(ih, eh, 2147483647, NOW), orc.term_search(d, ih, eh, 2147483647, NOW))
         got = [(h.urlhash, h.score) for h in ix.search(ih, eh, now_ms=NOW)]
         assert got == [(h, s) for h, s, _ in orc.search(d, ih, eh, now_ms=NOW)]
+
+
+def _collision_family(base, n_blocks=6):
+    """64 url hashes with one Java hashCode: 6 two-char blocks, each either
+    (x, y) or (x + 1, y - 31) -- equal 31 * x + y."""
+    out = []
+    for m in range(1 << n_blocks):
+        h = bytearray(base[:12 - 2 * n_blocks])
+        for j in range(n_blocks):
+            x, y = base[12 - 2 * n_blocks + 2 * j], base[12 - 2 * n_blocks + 2 * j + 1]
+            h += bytes([x + 1, y - 31]) if (m >> j) & 1 else bytes([x, y])
+        out.append(bytes(h))
+    return out
+
+
+def test_treeset_dedupe_across_chunks():
+    """Many postings tying in (score, ByteArray.hashCode) spread over several
+    2048-posting chunks: the TreeSet keeps the first arrival of each class, so
+    chunk lists lose entries to the dedupe and the per-query top-k must go on
+    below its first selection.  k from 10 to 3000."""
+    rng = np.random.default_rng(17)
+    fam = []
+    for f in range(120):
+        # x in A..Y, y in g..x: (x + 1, y - 31) is again a pair of valid url-hash characters
+        base = bytes(rng.choice(np.frombuffer(jl.ALPHA[:26], dtype=np.uint8), 2)) + b"".join(
+            bytes([int(rng.integers(65, 90)), int(rng.integers(97 + 6, 97 + 25))]) for _ in range(5))
+        fam.append((f, _collision_family(base, 5)))
+    hashes = {}
+    for f, hs in fam:
+        assert len({jl.bytearray_hashcode(h) for h in hs}) == 1
+        for h in hs:
+            hashes.setdefault(h, f)
+    filler = set()
+    while len(filler) < 5000:
+        h = bytes(rng.choice(np.frombuffer(jl.ALPHA, dtype=np.uint8), 12))
+        if h not in hashes:
+            filler.add(h)
+    allh = sorted(list(hashes) + list(filler), key=jl.key72)
+    n = len(allh)
+    rows = np.zeros((n, 40), dtype=np.uint8)
+    for i, h in enumerate(allh):
+        rows[i, :12] = np.frombuffer(h, dtype=np.uint8)
+        f = hashes.get(h)
+        day = 20000 + f if f is not None else 15000 + int(rng.integers(0, 300))  # families rank first
+        rows[i, 12:14] = np.frombuffer(day.to_bytes(2, "big"), dtype=np.uint8)
+        rows[i, 17:19] = np.frombuffer((40 + (f or 0) % 7).to_bytes(2, "big"), dtype=np.uint8)
+        rows[i, 21] = ord("t")
+        rows[i, 22:24] = np.frombuffer(b"en", dtype=np.uint8)
+        rows[i, 33] = 9 if f is not None else int(rng.integers(1, 9))
+        p = 3 if f is not None else int(rng.integers(1, 400))
+        rows[i, 34], rows[i, 35] = p >> 8, p & 0xFF
+    term = b"TERMdedupe__"
+    ix = RWIIndex(0)
+    ix.add(term, rows)
+    d = {term: rows}
+    for k in (10, 100, 1000, 3000):
+        got = [(h.urlhash, h.score, h.tiebreak) for h in ix.search([term], now_ms=NOW, k=k)]
+        exp = orc.search(d, [term], [], now_ms=NOW, k=k)
+        assert got == exp, k
+    ix.close()

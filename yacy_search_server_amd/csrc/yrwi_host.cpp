@@ -872,10 +872,9 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   if (!d_cand || !d_ccnt) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
-  // ---- merge passes until one list per query; a query with a single list (one
-  // chunk) is final as it stands and takes no part in any pass
-  const int sort_n = keff <= 1024 ? 2048 : 8192;
-  const int64_t G = std::max<int64_t>(2, std::min<int64_t>(64, sort_n / keff));
+  // ---- top-k passes over groups of <= 64 candidate lists until one list per
+  // query; a query with a single list (one chunk) is final as it stands
+  constexpr int64_t G = 64;
   int32_t* d_zero = arena_alloc<int32_t>(ctx, 1);
   if (!d_zero) return ctx->fail(YRWI_E_NOMEM, "arena");
   HIPCHK(ctx, hipMemsetAsync(d_zero, 0, sizeof(int32_t), ctx->stream));
@@ -892,7 +891,8 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   const int32_t* curc = d_ccnt;
   int32_t in_stride = kc;
   while (true) {
-    std::vector<int64_t> gb, gn;
+    std::vector<int64_t> gb;
+    std::vector<int32_t> gn, gk;
     std::vector<int> part;
     for (int qi = 0; qi < nq; qi++) {
       const int64_t L = lists[(size_t)qi];
@@ -901,7 +901,8 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
       const int64_t first = (int64_t)gb.size();
       for (int64_t g = 0; g < ng; g++) {
         gb.push_back(lbase[(size_t)qi] + g * G);
-        gn.push_back(std::min<int64_t>(G, L - g * G));
+        gn.push_back((int32_t)std::min<int64_t>(G, L - g * G));
+        gk.push_back(rq[(size_t)qi].k);
       }
       lists[(size_t)qi] = ng;
       lbase[(size_t)qi] = first;
@@ -910,13 +911,14 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
     if (gb.empty()) break;
     const int64_t ngr = (int64_t)gb.size();
     int64_t* d_gb = arena_alloc<int64_t>(ctx, ngr);
-    int64_t* d_gn = arena_alloc<int64_t>(ctx, ngr);
+    int32_t* d_gn = arena_alloc<int32_t>(ctx, ngr);
+    int32_t* d_gk = arena_alloc<int32_t>(ctx, ngr);
     Cand* d_out = arena_alloc<Cand>(ctx, ngr * keff);
     int32_t* d_oc = arena_alloc<int32_t>(ctx, ngr);
-    if (!d_gb || !d_gn || !d_out || !d_oc) return ctx->fail(YRWI_E_NOMEM, "arena");
-    if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn)) return YRWI_E_HIP;
-    if (launch_merge(cur, curc, in_stride, d_gb, d_gn, ngr, keff, d_out, d_oc, keff, sort_n, ctx->stream))
-      return ctx->fail(YRWI_E_HIP, "merge launch");
+    if (!d_gb || !d_gn || !d_gk || !d_out || !d_oc) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn) || upload(ctx, d_gk, gk)) return YRWI_E_HIP;
+    if (launch_topq(d_gb, d_gn, d_gk, ngr, cur, curc, in_stride, keff, d_out, d_oc, ctx->stream))
+      return ctx->fail(YRWI_E_HIP, "top-k launch");
     for (int qi : part) {
       fptr[(size_t)qi] = d_out + lbase[(size_t)qi] * keff;
       fcnt[(size_t)qi] = d_oc + lbase[(size_t)qi];

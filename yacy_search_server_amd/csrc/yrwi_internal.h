@@ -175,9 +175,10 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
                    NormState* d_norm, void* stream);
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                  const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* stream);
-int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, const int64_t* d_grp_in_base,
-                 const int64_t* d_grp_in_n, int64_t ngroups, int32_t k, Cand* d_out, int32_t* d_out_cnt,
-                 int32_t out_stride, int sort_n, void* stream);
+// top-k of candidate-list groups: group g = lists [gbase[g], gbase[g]+gn[g]) of d_in (stride
+// in_stride, counts d_in_cnt), k = gk[g]; output list g at d_out + g*keff, count d_out_cnt[g]
+int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
+                const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* stream);
 int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
                 int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
 int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,

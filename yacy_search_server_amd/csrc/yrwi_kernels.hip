@@ -14,7 +14,7 @@
 //   k_combine    settled min/max + max-distance fold over shards
 //   k_score      ReferenceOrder.cardinal :223-265 + per-chunk top-k in the
 //                WeakPriorityBlockingQueue order (:119-134, :414-425)
-//   k_merge      top-k merge of candidate lists
+//   k_topq       per-query top-k over the chunk candidate lists
 //   k_emit       yrwi_hit records
 //
 // Java int/long semantics are reproduced with explicit uint32_t/uint64_t
@@ -1306,6 +1306,23 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   return v;
 }
 
+// Radix-select digit search by one wave over a 256-bin histogram (descending
+// digits): the bin holding the rem-th largest key -> sSel[0] = digit, sSel[1] =
+// rank inside that bin, sSel[2] = keys in that bin.
+__device__ __forceinline__ void radix_pick(const int32_t* sHist, int32_t rem, int32_t* sSel) {
+  const int lane = threadIdx.x & 63;
+  int32_t h4[4];
+  int32_t sum = 0;
+  for (int j = 0; j < 4; j++) { h4[j] = sHist[4 * lane + j]; sum += h4[j]; }
+  const int32_t inc = wave_incl_sum(sum);
+  const int32_t all = __shfl(inc, 63, 64);
+  int32_t cum = all - inc;  // keys in higher bins than this lane's
+  for (int j = 3; j >= 0; j--) {
+    if (cum < rem && cum + h4[j] >= rem) { sSel[0] = 4 * lane + j; sSel[1] = rem - cum; sSel[2] = h4[j]; }
+    cum += h4[j];
+  }
+}
+
 // Per chunk: cardinal of every live posting, then the chunk's first kq distinct
 // (score, hashCode) classes in TreeSet order.  The kq-th largest score key T is
 // found by an MSB-first radix select (8-bit digits over the bits where the
@@ -1320,7 +1337,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ uint64_t s2[CHUNK];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sHist[256];
-  __shared__ int32_t sSel[2];
+  __shared__ int32_t sSel[3];
   __shared__ uint64_t sRed[8];
   __shared__ NormState sN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1387,18 +1404,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
           if (z[s] && (hi == 64 || (a[s] >> hi) == (prefix >> hi)))
             atomicAdd(&sHist[(uint32_t)(a[s] >> lo) & wmask], 1);
         __syncthreads();
-        if (tid < 64) {
-          int32_t h4[4];
-          int32_t sum = 0;
-          for (int j = 0; j < 4; j++) { h4[j] = sHist[4 * lane + j]; sum += h4[j]; }
-          const int32_t inc = wave_incl_sum(sum);
-          const int32_t all = __shfl(inc, 63, 64);
-          int32_t cum = all - inc;  // keys in higher bins than this lane's
-          for (int j = 3; j >= 0; j--) {
-            if (cum < rem && cum + h4[j] >= rem) { sSel[0] = 4 * lane + j; sSel[1] = rem - cum; }
-            cum += h4[j];
-          }
-        }
+        if (tid < 64) radix_pick(sHist, rem, sSel);
         __syncthreads();
         prefix |= (uint64_t)sSel[0] << lo;
         rem = sSel[1];
@@ -1434,49 +1440,178 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   if (tid == 0) cand_cnt[b] = n;
 }
 
-// merge: group g gathers lists [in_base[g], in_base[g]+in_n[g]) (each <= k valid
-// entries at stride in_stride) and writes its top-k list
+// Top-k of a group of candidate lists (gn[g] lists from list gbase[g]; each list
+// sorted, deduped, <= k entries at stride kc; k = gk[g]), in rounds.  A round takes the r = k - emitted
+// largest remaining candidates by the full 128-bit key (k1, k2) -- exact, keys
+// are unique -- found by MSB-first radix select (k1 digits over the bits where
+// the candidates differ, then k2 digits only if the cut falls inside a run of
+// equal k1), sorts them in LDS and applies the TreeSet dedupe against the
+// predecessor (the previous round's last key at the boundary).  A second round
+// is needed only when the dedupe dropped candidates.
+constexpr int TOPQ_THREADS = 256;
+
+struct TopqSrc {
+  const Cand* base;
+  const int32_t* cnt;
+  int32_t kc;
+  int64_t nslots;
+  __device__ __forceinline__ bool get(int64_t s, Cand& c) const {
+    const int64_t ch = s / kc;
+    const int32_t i = (int32_t)(s - ch * kc);
+    if (i >= cnt[ch]) return false;
+    c = base[s];
+    return true;
+  }
+};
+
+// radix select of the r-th largest 64-bit key among members (F: slot -> member?, key)
+template <class F>
+__device__ uint64_t topq_select(F key_of_slot, int64_t nslots, int32_t r, uint64_t mx, uint64_t mn, int32_t nmem,
+                                int32_t* grp, int32_t* rank, int32_t* sHist, int32_t* sSel) {
+  const uint64_t diff = mx ^ mn;
+  if (diff == 0) { *grp = nmem; *rank = r; return mx; }
+  int hi = 64 - __clzll((long long)diff);
+  uint64_t prefix = hi == 64 ? 0 : (mx >> hi) << hi;
+  int32_t rem = r, g = nmem;
+  while (hi > 0) {
+    const int lo = hi > 8 ? hi - 8 : 0;
+    const uint32_t wmask = (1u << (hi - lo)) - 1u;
+    sHist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t s = threadIdx.x; s < nslots; s += TOPQ_THREADS) {
+      uint64_t key;
+      if (key_of_slot(s, key) && (hi == 64 || (key >> hi) == (prefix >> hi)))
+        atomicAdd(&sHist[(uint32_t)(key >> lo) & wmask], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) radix_pick(sHist, rem, sSel);
+    __syncthreads();
+    prefix |= (uint64_t)sSel[0] << lo;
+    rem = sSel[1];
+    g = sSel[2];
+    hi = lo;
+    __syncthreads();
+  }
+  *grp = g;
+  *rank = rem;
+  return prefix;
+}
+
 template <int SORTN>
-__global__ __launch_bounds__(1024) void k_merge(const Cand* __restrict__ in, const int32_t* __restrict__ in_cnt,
-                                               int32_t in_stride, const int64_t* __restrict__ grp_base,
-                                               const int64_t* __restrict__ grp_n, int32_t k, Cand* __restrict__ out,
-                                               int32_t* __restrict__ out_cnt, int32_t out_stride) {
+__global__ __launch_bounds__(TOPQ_THREADS) void k_topq(const int64_t* __restrict__ gbase, const int32_t* __restrict__ gn,
+                                                      const int32_t* __restrict__ gk, const Cand* __restrict__ cand,
+                                                      const int32_t* __restrict__ ccnt, int32_t kc, int32_t keff,
+                                                      Cand* __restrict__ out, int32_t* __restrict__ out_cnt) {
   extern __shared__ uint64_t smem[];
   uint64_t* s1 = smem;
   uint64_t* s2 = smem + SORTN;
-  __shared__ int32_t sScan[16];
-  __shared__ int32_t sOff[65];
+  __shared__ int32_t sHist[256];
+  __shared__ int32_t sSel[3];
+  __shared__ int32_t sScan[4];
+  __shared__ int32_t sN;
+  __shared__ uint64_t sRed[12];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t g = blockIdx.x;
-  const int64_t base = grp_base[g], nl = grp_n[g];
-  if (nl <= 1) {  // one list: already sorted and deduplicated
-    const int32_t c = nl == 1 ? min(in_cnt[base], k) : 0;
-    const Cand* src = in + base * (int64_t)in_stride;
-    for (int i = threadIdx.x; i < c; i += 1024) out[g * (int64_t)out_stride + i] = src[i];
-    if (threadIdx.x == 0) out_cnt[g] = c;
-    return;
-  }
-  // offsets of each list inside the LDS image
-  if (threadIdx.x == 0) {
-    int32_t o = 0;
-    for (int64_t l = 0; l < nl && l < 64; l++) { sOff[l] = o; o += in_cnt[base + l]; }
-    sOff[nl < 64 ? nl : 64] = o;
-  }
-  __syncthreads();
-  const int32_t total = sOff[nl < 64 ? nl : 64];
-  const int P = pow2_at_least(total);
-  for (int l = 0; l < nl; l++) {
-    const int32_t c = in_cnt[base + l], o = sOff[l];
-    const Cand* src = in + (base + l) * (int64_t)in_stride;
-    for (int i = threadIdx.x; i < c; i += 1024) {
-      s1[o + i] = src[i].k1;
-      s2[o + i] = src[i].k2;
+  const int32_t k = min(gk[g], keff);
+  const TopqSrc src{cand + gbase[g] * kc, ccnt + gbase[g], kc, (int64_t)gn[g] * kc};
+  Cand* dst = out + g * keff;
+  bool first = true;
+  uint64_t U1 = 0, U2 = 0;  // exclusive upper bound (previous round's smallest key)
+  int32_t emitted = 0;
+  while (emitted < k) {
+    auto inC = [&](const Cand& c) { return first || c.k1 < U1 || (c.k1 == U1 && c.k2 < U2); };
+    // members, k1 range
+    int32_t n = 0;
+    uint64_t mx = 0, mn = ~0ull;
+    for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
+      Cand c;
+      if (src.get(s, c) && inC(c)) { n++; mx = c.k1 > mx ? c.k1 : mx; mn = c.k1 < mn ? c.k1 : mn; }
     }
+    int32_t nmem;
+    (void)block_excl_sum<TOPQ_THREADS>(n, sScan, &nmem);
+    if (nmem == 0) break;
+    mx = wave_max_u64(mx);
+    mn = wave_min_u64(mn);
+    if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
+    __syncthreads();
+    mx = sRed[0];
+    mn = sRed[4];
+    for (int w = 1; w < TOPQ_THREADS / 64; w++) { mx = sRed[w] > mx ? sRed[w] : mx; mn = sRed[4 + w] < mn ? sRed[4 + w] : mn; }
+    __syncthreads();
+    const int32_t r = min(k - emitted, nmem);
+    int32_t grp, rank;
+    const uint64_t T1 = topq_select([&](int64_t s, uint64_t& key) {
+      Cand c;
+      if (!src.get(s, c) || !inC(c)) return false;
+      key = c.k1;
+      return true;
+    }, src.nslots, r, mx, mn, nmem, &grp, &rank, sHist, sSel);
+    uint64_t T2 = 0;
+    if (rank < grp) {  // the cut falls inside the run k1 == T1: select on k2 there
+      uint64_t zx = 0, zn = ~0ull;
+      for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
+        Cand c;
+        if (src.get(s, c) && inC(c) && c.k1 == T1) { zx = c.k2 > zx ? c.k2 : zx; zn = c.k2 < zn ? c.k2 : zn; }
+      }
+      zx = wave_max_u64(zx);
+      zn = wave_min_u64(zn);
+      if (lane == 0) { sRed[wv] = zx; sRed[4 + wv] = zn; }
+      __syncthreads();
+      zx = sRed[0];
+      zn = sRed[4];
+      for (int w = 1; w < TOPQ_THREADS / 64; w++) { zx = sRed[w] > zx ? sRed[w] : zx; zn = sRed[4 + w] < zn ? sRed[4 + w] : zn; }
+      __syncthreads();
+      int32_t g2, r2;
+      T2 = topq_select([&](int64_t s, uint64_t& key) {
+        Cand c;
+        if (!src.get(s, c) || !inC(c) || c.k1 != T1) return false;
+        key = c.k2;
+        return true;
+      }, src.nslots, rank, zx, zn, grp, &g2, &r2, sHist, sSel);
+    }
+    // gather the r selected keys (exactly r: keys are unique), sort, dedupe
+    if (tid == 0) sN = 0;
+    __syncthreads();
+    for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
+      Cand c;
+      if (src.get(s, c) && inC(c) && (c.k1 > T1 || (c.k1 == T1 && c.k2 >= T2))) {
+        const int pos = atomicAdd(&sN, 1);
+        if (pos < SORTN) { s1[pos] = c.k1; s2[pos] = c.k2; }
+      }
+    }
+    __syncthreads();
+    const int nsel = min(sN, SORTN);
+    const int P = pow2_at_least(nsel);
+    for (int i = nsel + tid; i < P; i += TOPQ_THREADS) { s1[i] = 0; s2[i] = 0; }
+    __syncthreads();
+    bitonic_desc<TOPQ_THREADS>(s1, s2, P);
+    // dedupe: drop a key equal in (score, hashCode) to its predecessor
+    const int ipt = (nsel + TOPQ_THREADS - 1) / TOPQ_THREADS;
+    const int i0 = tid * ipt;
+    int32_t keep = 0;
+    uint32_t bits = 0;
+    for (int t = 0; t < ipt; t++) {
+      const int i = i0 + t;
+      if (i >= nsel) break;
+      const uint64_t p1 = i > 0 ? s1[i - 1] : U1, p2 = i > 0 ? s2[i - 1] : U2;
+      const bool dup = (i > 0 || !first) && s1[i] == p1 && (s2[i] >> 32) == (p2 >> 32);
+      if (!dup) { bits |= 1u << t; keep++; }
+    }
+    int32_t kept;
+    int32_t off = block_excl_sum<TOPQ_THREADS>(keep, sScan, &kept);
+    for (int t = 0; t < ipt; t++) {
+      if (bits & (1u << t)) {
+        if (emitted + off < k) { dst[emitted + off].k1 = s1[i0 + t]; dst[emitted + off].k2 = s2[i0 + t]; }
+        off++;
+      }
+    }
+    emitted = min(k, emitted + kept);
+    U1 = s1[nsel - 1];
+    U2 = s2[nsel - 1];
+    first = false;
+    __syncthreads();
   }
-  for (int i = total + threadIdx.x; i < P; i += 1024) { s1[i] = 0; s2[i] = 0; }
-  __syncthreads();
-  bitonic_desc<1024>(s1, s2, P);
-  int32_t n = dedupe_take<1024>(s1, s2, P, k, out + g * (int64_t)out_stride, sScan, nullptr);
-  if (threadIdx.x == 0) out_cnt[g] = n;
+  if (tid == 0) out_cnt[g] = emitted;
 }
 
 __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* __restrict__ fin,
@@ -1700,24 +1835,22 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t
   return rc(hipGetLastError());
 }
 
-int launch_merge(const Cand* d_in, const int32_t* d_in_cnt, int32_t in_stride, const int64_t* d_grp_in_base,
-                 const int64_t* d_grp_in_n, int64_t ngroups, int32_t k, Cand* d_out, int32_t* d_out_cnt,
-                 int32_t out_stride, int sort_n, void* st) {
+int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
+                const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* st) {
   if (ngroups <= 0) return 0;
-  if (sort_n == 2048) {
-    hipLaunchKernelGGL(k_merge<2048>, dim3((unsigned)ngroups), dim3(1024), 2 * 2048 * sizeof(uint64_t), S(st), d_in,
-                       d_in_cnt, in_stride, d_grp_in_base, d_grp_in_n, k, d_out, d_out_cnt, out_stride);
-  } else if (sort_n == 8192) {
+  if (keff <= 2048) {
+    hipLaunchKernelGGL(k_topq<2048>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 2048 * sizeof(uint64_t), S(st),
+                       d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);
+  } else {
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge<8192>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          2 * 8192 * sizeof(uint64_t));
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_topq<4096>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 4096 * sizeof(uint64_t)) != hipSuccess)
+        return YRWI_E_HIP;
       attr = true;
     }
-    hipLaunchKernelGGL(k_merge<8192>, dim3((unsigned)ngroups), dim3(1024), 2 * 8192 * sizeof(uint64_t), S(st), d_in,
-                       d_in_cnt, in_stride, d_grp_in_base, d_grp_in_n, k, d_out, d_out_cnt, out_stride);
-  } else {
-    return YRWI_E_ARG;
+    hipLaunchKernelGGL(k_topq<4096>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 4096 * sizeof(uint64_t), S(st),
+                       d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);
   }
   return rc(hipGetLastError());
 }
