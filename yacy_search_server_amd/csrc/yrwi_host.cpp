@@ -872,9 +872,8 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   if (!d_cand || !d_ccnt) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
-  // ---- top-k passes over groups of <= 64 candidate lists until one list per
-  // query; a query with a single list (one chunk) is final as it stands
-  constexpr int64_t G = 64;
+  // ---- top-k passes over groups of candidate lists until one list per query;
+  // a query with a single list (one chunk) is final as it stands
   int32_t* d_zero = arena_alloc<int32_t>(ctx, 1);
   if (!d_zero) return ctx->fail(YRWI_E_NOMEM, "arena");
   HIPCHK(ctx, hipMemsetAsync(d_zero, 0, sizeof(int32_t), ctx->stream));
@@ -891,6 +890,7 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   const int32_t* curc = d_ccnt;
   int32_t in_stride = kc;
   while (true) {
+    const int64_t G = std::max<int64_t>(2, std::min<int64_t>(64, topq_capacity(keff) / in_stride));
     std::vector<int64_t> gb;
     std::vector<int32_t> gn, gk;
     std::vector<int> part;

@@ -175,6 +175,8 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
                    NormState* d_norm, void* stream);
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                  const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* stream);
+// candidates one k_topq group may hold (lists per group = min(64, capacity / list stride))
+int topq_capacity(int32_t keff);
 // top-k of candidate-list groups: group g = lists [gbase[g], gbase[g]+gn[g]) of d_in (stride
 // in_stride, counts d_in_cnt), k = gk[g]; output list g at d_out + g*keff, count d_out_cnt[g]
 int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,

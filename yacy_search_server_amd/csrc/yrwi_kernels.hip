@@ -1440,33 +1440,22 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   if (tid == 0) cand_cnt[b] = n;
 }
 
-// Top-k of a group of candidate lists (gn[g] lists from list gbase[g]; each list
-// sorted, deduped, <= k entries at stride kc; k = gk[g]), in rounds.  A round takes the r = k - emitted
-// largest remaining candidates by the full 128-bit key (k1, k2) -- exact, keys
-// are unique -- found by MSB-first radix select (k1 digits over the bits where
-// the candidates differ, then k2 digits only if the cut falls inside a run of
-// equal k1), sorts them in LDS and applies the TreeSet dedupe against the
-// predecessor (the previous round's last key at the boundary).  A second round
-// is needed only when the dedupe dropped candidates.
+// Top-k of a group of candidate lists (gn[g] <= 64 lists from list gbase[g];
+// each list sorted, deduped, <= its stride kc entries; k = gk[g]; the host sizes
+// groups to <= CAP candidates), in rounds.  The group's candidates are staged in
+// LDS; a round takes the r = k - emitted largest remaining candidates by the full
+// 128-bit key (k1, k2) -- exact, keys are unique -- found by MSB-first radix
+// select (k1 digits over the bits where the candidates differ, then k2 digits
+// only if the cut falls inside a run of equal k1), moves them to the front,
+// sorts them and applies the TreeSet dedupe against the predecessor (the previous
+// round's last key at the boundary).  A further round (after re-staging) is
+// needed only when the dedupe dropped candidates.
 constexpr int TOPQ_THREADS = 256;
 
-struct TopqSrc {
-  const Cand* base;
-  const int32_t* cnt;
-  int32_t kc;
-  int64_t nslots;
-  __device__ __forceinline__ bool get(int64_t s, Cand& c) const {
-    const int64_t ch = s / kc;
-    const int32_t i = (int32_t)(s - ch * kc);
-    if (i >= cnt[ch]) return false;
-    c = base[s];
-    return true;
-  }
-};
-
-// radix select of the r-th largest 64-bit key among members (F: slot -> member?, key)
+// radix select of the r-th largest 64-bit key among the members of the staged
+// candidates; F(f, key&) -> member?
 template <class F>
-__device__ uint64_t topq_select(F key_of_slot, int64_t nslots, int32_t r, uint64_t mx, uint64_t mn, int32_t nmem,
+__device__ uint64_t topq_select(F key_at, int32_t total, int32_t r, uint64_t mx, uint64_t mn, int32_t nmem,
                                 int32_t* grp, int32_t* rank, int32_t* sHist, int32_t* sSel) {
   const uint64_t diff = mx ^ mn;
   if (diff == 0) { *grp = nmem; *rank = r; return mx; }
@@ -1478,9 +1467,9 @@ __device__ uint64_t topq_select(F key_of_slot, int64_t nslots, int32_t r, uint64
     const uint32_t wmask = (1u << (hi - lo)) - 1u;
     sHist[threadIdx.x] = 0;
     __syncthreads();
-    for (int64_t s = threadIdx.x; s < nslots; s += TOPQ_THREADS) {
+    for (int f = threadIdx.x; f < total; f += TOPQ_THREADS) {
       uint64_t key;
-      if (key_of_slot(s, key) && (hi == 64 || (key >> hi) == (prefix >> hi)))
+      if (key_at(f, key) && (hi == 64 || (key >> hi) == (prefix >> hi)))
         atomicAdd(&sHist[(uint32_t)(key >> lo) & wmask], 1);
     }
     __syncthreads();
@@ -1497,95 +1486,116 @@ __device__ uint64_t topq_select(F key_of_slot, int64_t nslots, int32_t r, uint64
   return prefix;
 }
 
-template <int SORTN>
+__device__ __forceinline__ void block_minmax_u64(uint64_t& mx, uint64_t& mn, uint64_t* sRed) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  mx = wave_max_u64(mx);
+  mn = wave_min_u64(mn);
+  if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
+  __syncthreads();
+  mx = sRed[0];
+  mn = sRed[4];
+  for (int w = 1; w < TOPQ_THREADS / 64; w++) { mx = sRed[w] > mx ? sRed[w] : mx; mn = sRed[4 + w] < mn ? sRed[4 + w] : mn; }
+  __syncthreads();
+}
+
+template <int CAP>
 __global__ __launch_bounds__(TOPQ_THREADS) void k_topq(const int64_t* __restrict__ gbase, const int32_t* __restrict__ gn,
                                                       const int32_t* __restrict__ gk, const Cand* __restrict__ cand,
                                                       const int32_t* __restrict__ ccnt, int32_t kc, int32_t keff,
                                                       Cand* __restrict__ out, int32_t* __restrict__ out_cnt) {
+  constexpr int EPT = CAP / TOPQ_THREADS;
   extern __shared__ uint64_t smem[];
-  uint64_t* s1 = smem;
-  uint64_t* s2 = smem + SORTN;
+  uint64_t* c1 = smem;
+  uint64_t* c2 = smem + CAP;
   __shared__ int32_t sHist[256];
   __shared__ int32_t sSel[3];
   __shared__ int32_t sScan[4];
-  __shared__ int32_t sN;
-  __shared__ uint64_t sRed[12];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ int32_t sOff[65];
+  __shared__ uint64_t sRed[8];
+  const int tid = threadIdx.x;
   const int64_t g = blockIdx.x;
   const int32_t k = min(gk[g], keff);
-  const TopqSrc src{cand + gbase[g] * kc, ccnt + gbase[g], kc, (int64_t)gn[g] * kc};
+  const int32_t nl = gn[g];
+  const Cand* lists = cand + gbase[g] * kc;
+  if (tid < 64) {
+    const int32_t c = tid < nl ? ccnt[gbase[g] + tid] : 0;
+    sOff[tid + 1] = wave_incl_sum(c);
+    if (tid == 0) sOff[0] = 0;
+  }
+  __syncthreads();
+  const int32_t total = sOff[nl];
+  auto stage = [&]() {  // flatten the group's lists into c1/c2[0, total)
+    for (int f = tid; f < total; f += TOPQ_THREADS) {
+      int lo = 0, hi = nl - 1;  // largest l with sOff[l] <= f
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sOff[mid] <= f) lo = mid; else hi = mid - 1;
+      }
+      const Cand c = lists[(int64_t)lo * kc + (f - sOff[lo])];
+      c1[f] = c.k1;
+      c2[f] = c.k2;
+    }
+    __syncthreads();
+  };
+  stage();
   Cand* dst = out + g * keff;
   bool first = true;
-  uint64_t U1 = 0, U2 = 0;  // exclusive upper bound (previous round's smallest key)
+  uint64_t U1 = 0, U2 = 0;  // exclusive upper bound: the previous round's smallest key
   int32_t emitted = 0;
   while (emitted < k) {
-    auto inC = [&](const Cand& c) { return first || c.k1 < U1 || (c.k1 == U1 && c.k2 < U2); };
-    // members, k1 range
+    auto inC = [&](uint64_t a, uint64_t z) { return first || a < U1 || (a == U1 && z < U2); };
     int32_t n = 0;
     uint64_t mx = 0, mn = ~0ull;
-    for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
-      Cand c;
-      if (src.get(s, c) && inC(c)) { n++; mx = c.k1 > mx ? c.k1 : mx; mn = c.k1 < mn ? c.k1 : mn; }
-    }
+    for (int f = tid; f < total; f += TOPQ_THREADS)
+      if (inC(c1[f], c2[f])) { n++; mx = c1[f] > mx ? c1[f] : mx; mn = c1[f] < mn ? c1[f] : mn; }
     int32_t nmem;
     (void)block_excl_sum<TOPQ_THREADS>(n, sScan, &nmem);
     if (nmem == 0) break;
-    mx = wave_max_u64(mx);
-    mn = wave_min_u64(mn);
-    if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
-    __syncthreads();
-    mx = sRed[0];
-    mn = sRed[4];
-    for (int w = 1; w < TOPQ_THREADS / 64; w++) { mx = sRed[w] > mx ? sRed[w] : mx; mn = sRed[4 + w] < mn ? sRed[4 + w] : mn; }
-    __syncthreads();
+    block_minmax_u64(mx, mn, sRed);
     const int32_t r = min(k - emitted, nmem);
     int32_t grp, rank;
-    const uint64_t T1 = topq_select([&](int64_t s, uint64_t& key) {
-      Cand c;
-      if (!src.get(s, c) || !inC(c)) return false;
-      key = c.k1;
+    const uint64_t T1 = topq_select([&](int f, uint64_t& key) {
+      if (!inC(c1[f], c2[f])) return false;
+      key = c1[f];
       return true;
-    }, src.nslots, r, mx, mn, nmem, &grp, &rank, sHist, sSel);
+    }, total, r, mx, mn, nmem, &grp, &rank, sHist, sSel);
     uint64_t T2 = 0;
     if (rank < grp) {  // the cut falls inside the run k1 == T1: select on k2 there
       uint64_t zx = 0, zn = ~0ull;
-      for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
-        Cand c;
-        if (src.get(s, c) && inC(c) && c.k1 == T1) { zx = c.k2 > zx ? c.k2 : zx; zn = c.k2 < zn ? c.k2 : zn; }
-      }
-      zx = wave_max_u64(zx);
-      zn = wave_min_u64(zn);
-      if (lane == 0) { sRed[wv] = zx; sRed[4 + wv] = zn; }
-      __syncthreads();
-      zx = sRed[0];
-      zn = sRed[4];
-      for (int w = 1; w < TOPQ_THREADS / 64; w++) { zx = sRed[w] > zx ? sRed[w] : zx; zn = sRed[4 + w] < zn ? sRed[4 + w] : zn; }
-      __syncthreads();
+      for (int f = tid; f < total; f += TOPQ_THREADS)
+        if (c1[f] == T1 && inC(c1[f], c2[f])) { zx = c2[f] > zx ? c2[f] : zx; zn = c2[f] < zn ? c2[f] : zn; }
+      block_minmax_u64(zx, zn, sRed);
       int32_t g2, r2;
-      T2 = topq_select([&](int64_t s, uint64_t& key) {
-        Cand c;
-        if (!src.get(s, c) || !inC(c) || c.k1 != T1) return false;
-        key = c.k2;
+      T2 = topq_select([&](int f, uint64_t& key) {
+        if (c1[f] != T1 || !inC(c1[f], c2[f])) return false;
+        key = c2[f];
         return true;
-      }, src.nslots, rank, zx, zn, grp, &g2, &r2, sHist, sSel);
+      }, total, rank, zx, zn, grp, &g2, &r2, sHist, sSel);
     }
-    // gather the r selected keys (exactly r: keys are unique), sort, dedupe
-    if (tid == 0) sN = 0;
-    __syncthreads();
-    for (int64_t s = tid; s < src.nslots; s += TOPQ_THREADS) {
-      Cand c;
-      if (src.get(s, c) && inC(c) && (c.k1 > T1 || (c.k1 == T1 && c.k2 >= T2))) {
-        const int pos = atomicAdd(&sN, 1);
-        if (pos < SORTN) { s1[pos] = c.k1; s2[pos] = c.k2; }
+    // move the r selected keys (exactly r: keys are unique) to the front, sort, dedupe
+    uint64_t v1[EPT], v2[EPT];
+    uint32_t selb = 0;
+    int32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+      const int f = j * TOPQ_THREADS + tid;
+      v1[j] = 0;
+      v2[j] = 0;
+      if (f < total) {
+        v1[j] = c1[f];
+        v2[j] = c2[f];
+        if (inC(v1[j], v2[j]) && (v1[j] > T1 || (v1[j] == T1 && v2[j] >= T2))) { selb |= 1u << j; mine++; }
       }
     }
-    __syncthreads();
-    const int nsel = min(sN, SORTN);
+    int32_t nsel;
+    int32_t off = block_excl_sum<TOPQ_THREADS>(mine, sScan, &nsel);  // (its barriers order the reads above)
+#pragma unroll
+    for (int j = 0; j < EPT; j++)
+      if (selb & (1u << j)) { c1[off] = v1[j]; c2[off] = v2[j]; off++; }
     const int P = pow2_at_least(nsel);
-    for (int i = nsel + tid; i < P; i += TOPQ_THREADS) { s1[i] = 0; s2[i] = 0; }
+    for (int i = nsel + tid; i < P; i += TOPQ_THREADS) { c1[i] = 0; c2[i] = 0; }
     __syncthreads();
-    bitonic_desc<TOPQ_THREADS>(s1, s2, P);
-    // dedupe: drop a key equal in (score, hashCode) to its predecessor
+    bitonic_desc<TOPQ_THREADS>(c1, c2, P);
     const int ipt = (nsel + TOPQ_THREADS - 1) / TOPQ_THREADS;
     const int i0 = tid * ipt;
     int32_t keep = 0;
@@ -1593,23 +1603,24 @@ __global__ __launch_bounds__(TOPQ_THREADS) void k_topq(const int64_t* __restrict
     for (int t = 0; t < ipt; t++) {
       const int i = i0 + t;
       if (i >= nsel) break;
-      const uint64_t p1 = i > 0 ? s1[i - 1] : U1, p2 = i > 0 ? s2[i - 1] : U2;
-      const bool dup = (i > 0 || !first) && s1[i] == p1 && (s2[i] >> 32) == (p2 >> 32);
+      const uint64_t p1 = i > 0 ? c1[i - 1] : U1, p2 = i > 0 ? c2[i - 1] : U2;
+      const bool dup = (i > 0 || !first) && c1[i] == p1 && (c2[i] >> 32) == (p2 >> 32);
       if (!dup) { bits |= 1u << t; keep++; }
     }
     int32_t kept;
-    int32_t off = block_excl_sum<TOPQ_THREADS>(keep, sScan, &kept);
+    off = block_excl_sum<TOPQ_THREADS>(keep, sScan, &kept);
     for (int t = 0; t < ipt; t++) {
       if (bits & (1u << t)) {
-        if (emitted + off < k) { dst[emitted + off].k1 = s1[i0 + t]; dst[emitted + off].k2 = s2[i0 + t]; }
+        if (emitted + off < k) { dst[emitted + off].k1 = c1[i0 + t]; dst[emitted + off].k2 = c2[i0 + t]; }
         off++;
       }
     }
     emitted = min(k, emitted + kept);
-    U1 = s1[nsel - 1];
-    U2 = s2[nsel - 1];
+    U1 = c1[nsel - 1];
+    U2 = c2[nsel - 1];
     first = false;
     __syncthreads();
+    if (emitted < k) stage();  // the front of the image was overwritten
   }
   if (tid == 0) out_cnt[g] = emitted;
 }
@@ -1835,23 +1846,26 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t
   return rc(hipGetLastError());
 }
 
+int topq_capacity(int32_t keff) { return keff <= 2048 ? 4096 : 8192; }
+
 int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
                 const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* st) {
   if (ngroups <= 0) return 0;
-  if (keff <= 2048) {
-    hipLaunchKernelGGL(k_topq<2048>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 2048 * sizeof(uint64_t), S(st),
-                       d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);
-  } else {
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_topq<4096>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 4096 * sizeof(uint64_t)) != hipSuccess)
-        return YRWI_E_HIP;
-      attr = true;
-    }
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_topq<4096>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * 4096 * sizeof(uint64_t)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_topq<8192>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * 8192 * sizeof(uint64_t)) != hipSuccess)
+      return YRWI_E_HIP;
+    attr = true;
+  }
+  if (topq_capacity(keff) == 4096)
     hipLaunchKernelGGL(k_topq<4096>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 4096 * sizeof(uint64_t), S(st),
                        d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);
-  }
+  else
+    hipLaunchKernelGGL(k_topq<8192>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 8192 * sizeof(uint64_t), S(st),
+                       d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);
   return rc(hipGetLastError());
 }
 
