@@ -630,13 +630,14 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
     int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
     TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
+    ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
     uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
     int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
     int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
-    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
     hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
-    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pairs, d_cnt, d_off, false,
+    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_cnt, d_off, false,
                          ctx->stream, e0, em, e1))
       return ctx->fail(YRWI_E_HIP, "join launch");
     if (tm) tm->kjoin.push_back({e0, em, e1});
@@ -679,9 +680,10 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
       JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
       int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
       TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
-      if (!d_jobs || !d_tb || !d_split) return ctx->fail(YRWI_E_NOMEM, "arena");
+      ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
+      if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, nullptr, nullptr, nullptr, true,
+      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, true,
                            ctx->stream, nullptr, nullptr, nullptr))
         return ctx->fail(YRWI_E_HIP, "exclude launch");
     }

@@ -74,6 +74,15 @@ struct TileDesc {
   const uint8_t* bl;
   int64_t a0, b0;
   int32_t na, nb, nbl, job;
+  int32_t maxd, pad;
+};
+constexpr int TILEDESC_DWORDS = (int)(sizeof(TileDesc) / 4);
+
+// One tile of a JA_PROBE job (written by k_probe_part): the large-list range
+// [lo, hi) that holds every key of the tile's PROBE_TILE small-list keys.
+struct ProbeDesc {
+  int64_t lo, hi;
+  int32_t job, pad;
 };
 
 // Per-chunk normalisation summary (ReferenceOrder.NormalizeWorker :163-210,
@@ -163,7 +172,8 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
                          void* stream);
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
-                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, uint2* d_pairs,
+                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
+                     uint2* d_pairs,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
                      void* ev_mid, void* ev_end);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

@@ -230,6 +230,8 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   D.nb = (int32_t)((d1 - lo1) - (d0 - lo0));
   D.nbl = D.nb + ((d1 - lo1) < nB ? 1 : 0);  // + lookahead element B[b1]
   D.job = j;
+  D.maxd = J.maxd;
+  D.pad = 0;
   desc[b] = D;
 }
 
@@ -301,12 +303,25 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
   const uint8_t* sAl = sL;
   const uint8_t* sBl = sL + JOIN_TILE;
 
+  // Tile descriptors travel through VGPRs (lane i holds dword i, read with
+  // v_readlane when due): a scalar load would share lgkmcnt with LDS traffic and
+  // every LDS wait of the merge would also wait for the next descriptor.
+  const int lane = threadIdx.x & 63;
+  auto desc_fetch = [&](int64_t t) -> uint32_t {
+    return (t < ntiles && lane < TILEDESC_DWORDS) ? ((const gu32c*)(desc + t))[lane] : 0u;
+  };
+  auto desc_get = [&](uint32_t v) -> TileDesc {
+    TileDesc D;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&D);
+#pragma unroll
+    for (int i = 0; i < TILEDESC_DWORDS; i++) w[i] = __builtin_amdgcn_readlane(v, i);
+    return D;
+  };
   const int64_t G = gridDim.x;
   int64_t b = blockIdx.x;
   if (b >= ntiles) return;
-  TileDesc Dc = desc[b];
-  TileDesc Dn;
-  if (b + G < ntiles) Dn = desc[b + G];
+  TileDesc Dc = desc_get(desc_fetch(b));
+  uint32_t dnext = desc_fetch(b + G);
   TileKeys K;
   tile_load(Dc, K);
   for (; b < ntiles; b += G) {
@@ -324,10 +339,10 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
     __syncthreads();
     // prefetch: keys of the next tile, descriptor of the one after
     const int64_t a0 = Dc.a0, b0 = Dc.b0;
-    const int jc = Dc.job;
+    const int jc = Dc.job, maxd = Dc.maxd;
     if (b + G < ntiles) {
-      Dc = Dn;
-      if (b + 2 * G < ntiles) Dn = desc[b + 2 * G];
+      Dc = desc_get(dnext);
+      dnext = desc_fetch(b + 2 * G);
       tile_load(Dc, K);
     }
 
@@ -367,10 +382,11 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
         }
       }
     }
-    if (__syncthreads_or(mbits != 0)) {
+    // maxDistance filter (ReferenceContainer.java:442,482; distance <= 65535 always)
+    // and exclusion marks need the job's rows; plain joins never touch the job
+    if ((mark || maxd < 65535) && __syncthreads_or(mbits != 0)) {
       const JoinQ& J = jobs[jc];
-      // maxDistance filter (ReferenceContainer.java:442,482); distance <= 65535 always
-      if (mbits && !mark && J.maxd < 65535) {
+      if (mbits && !mark) {
 #pragma unroll
         for (int s = 0; s < JOIN_IPT; s++) {
           if (mbits & (1u << s)) {
@@ -405,10 +421,16 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 }
 
 // ============================================================ join: probe
-// Skewed sizes: each thread looks one small-list key up in the large list,
-// inside the large-list range spanned by the workgroup's 256 small keys (the
-// by-test access pattern of joinConstructiveByTest :419-446, RowSet.binarySearch
-// RowSet.java:319-335).  Output and mark semantics are those of k_join.
+// Skewed sizes (the by-test access pattern of joinConstructiveByTest :419-446,
+// RowSet.binarySearch RowSet.java:319-335): every small-list key is looked up in
+// the large list.  k_probe_part finds, per tile of PROBE_TILE small keys, the
+// large-list range that can hold them (two interleaved binary searches per
+// thread, all tiles in parallel).  k_probe then samples 256 evenly spaced keys
+// of that range into LDS, narrows each lookup to one sample interval in LDS and
+// finishes with a short binary search inside that interval (ranges of at most
+// PROBE_STAGE keys are staged whole).  Output and mark semantics are k_join's.
+constexpr int PROBE_STAGE = 2048;
+
 __device__ __forceinline__ int64_t lower_bound_key(const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
                                                    int64_t lo, int64_t hi, uint64_t h, uint32_t l) {
   while (lo < hi) {
@@ -420,34 +442,92 @@ __device__ __forceinline__ int64_t lower_bound_key(const uint64_t* __restrict__ 
   return lo;
 }
 
-__global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
-                                                     const int64_t* __restrict__ tile_base, int njobs,
-                                                     int64_t tile0, uint2* __restrict__ pairs,
-                                                     int32_t* __restrict__ tile_cnt, int mark) {
-  __shared__ int64_t sRange[2];
-  __shared__ int32_t sScan[4];
-  const int64_t b = tile0 + blockIdx.x;
-  const int j = find_job(tile_base, njobs, b);
+__global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
+                             int64_t tile0, int64_t ntiles, ProbeDesc* __restrict__ pdesc) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const int j = find_job(tile_base, njobs, tile0 + t);
   const JoinQ& J = jobs[j];
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
-  const int64_t s0 = (b - tile_base[j]) * PROBE_TILE;
+  const int64_t s0 = (tile0 + t - tile_base[j]) * PROBE_TILE;
   const int64_t s1 = s0 + PROBE_TILE < Sm.n ? s0 + PROBE_TILE : Sm.n;
-  if (threadIdx.x < 2) {
-    const int64_t e = threadIdx.x == 0 ? s0 : s1 - 1;
-    int64_t p = lower_bound_key(Lg.khi, Lg.klo, 0, Lg.n, Sm.khi[e], Sm.klo[e]);
-    if (threadIdx.x == 1 && p < Lg.n) p++;  // range end (exclusive) covers an equal key
-    sRange[threadIdx.x] = p;
+  const uint64_t h0 = Sm.khi[s0], h1 = Sm.khi[s1 - 1];
+  const uint32_t l0 = Sm.klo[s0], l1 = Sm.klo[s1 - 1];
+  // lower bound of the first key, upper bound (lower bound of key + 1) of the last
+  int64_t lo0 = 0, hi0 = Lg.n, lo1 = 0, hi1 = Lg.n;
+  while (lo0 < hi0 || lo1 < hi1) {
+    if (lo0 < hi0) {
+      const int64_t mid = (lo0 + hi0) >> 1;
+      const uint64_t mh = Lg.khi[mid];
+      if (mh < h0 || (mh == h0 && (uint32_t)Lg.klo[mid] < l0)) lo0 = mid + 1; else hi0 = mid;
+    }
+    if (lo1 < hi1) {
+      const int64_t mid = (lo1 + hi1) >> 1;
+      const uint64_t mh = Lg.khi[mid];
+      if (mh < h1 || (mh == h1 && (uint32_t)Lg.klo[mid] <= l1)) lo1 = mid + 1; else hi1 = mid;
+    }
+  }
+  ProbeDesc D;
+  D.lo = lo0;
+  D.hi = lo1;
+  D.job = j;
+  D.pad = 0;
+  pdesc[t] = D;
+}
+
+__global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
+                                                     const int64_t* __restrict__ tile_base,
+                                                     const ProbeDesc* __restrict__ pdesc, int64_t tile0,
+                                                     uint2* __restrict__ pairs, int32_t* __restrict__ tile_cnt,
+                                                     int mark) {
+  __shared__ uint64_t sH[PROBE_STAGE];
+  __shared__ uint8_t sL[PROBE_STAGE];
+  __shared__ int32_t sScan[4];
+  const int64_t t = blockIdx.x;
+  const int64_t b = tile0 + t;
+  const ProbeDesc D = pdesc[t];
+  const JoinQ& J = jobs[D.job];
+  const DList& Sm = J.small_is_A ? J.A : J.B;
+  const DList& Lg = J.small_is_A ? J.B : J.A;
+  const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
+  const int64_t i = s0 + threadIdx.x;
+  const bool live = i < Sm.n;
+  uint64_t h = 0;
+  uint32_t l = 0;
+  if (live) { h = Sm.khi[i]; l = Sm.klo[i]; }
+  const int64_t n = D.hi - D.lo;
+  const bool staged = n <= PROBE_STAGE;
+  // stride between samples (staged: every key)
+  const int64_t S = staged ? 1 : (n + PROBE_TILE - 1) / PROBE_TILE;
+  const int ns = staged ? (int)n : (int)((n + S - 1) / S);
+  for (int x = threadIdx.x; x < ns; x += PROBE_TILE) {
+    const int64_t g = D.lo + (int64_t)x * S;
+    sH[x] = Lg.khi[g];
+    sL[x] = Lg.klo[g];
   }
   __syncthreads();
-  const int64_t i = s0 + threadIdx.x;
   bool hit = false;
   int64_t jl = 0;
-  if (i < s1) {
-    const uint64_t h = Sm.khi[i];
-    const uint32_t l = Sm.klo[i];
-    jl = lower_bound_key(Lg.khi, Lg.klo, sRange[0], sRange[1], h, l);
-    hit = jl < Lg.n && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
+  if (live && ns > 0) {
+    // largest sample index c with sample[c] <= key (or -1)
+    int lo = 0, hi = ns;  // first sample > key
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sH[mid] < h || (sH[mid] == h && (uint32_t)sL[mid] <= l)) lo = mid + 1; else hi = mid;
+    }
+    const int c = lo - 1;
+    if (c >= 0) {
+      if (sH[c] == h && (uint32_t)sL[c] == l) {
+        hit = true;
+        jl = D.lo + (int64_t)c * S;
+      } else if (!staged) {
+        const int64_t w0 = D.lo + (int64_t)c * S + 1;
+        const int64_t w1 = min(D.lo + (int64_t)(c + 1) * S, D.hi);
+        jl = lower_bound_key(Lg.khi, Lg.klo, w0, w1, h, l);
+        hit = jl < w1 && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
+      }
+    }
   }
   const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
   if (hit && !mark && J.maxd < 65535) {
@@ -1753,9 +1833,9 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
 }
 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
-                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, uint2* d_pairs,
-                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0, void* evm,
-                     void* ev1) {
+                     int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
+                     uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0,
+                     void* evm, void* ev1) {
   if (total_tiles <= 0) return 0;
   static int join_grid = 0;  // resident k_join workgroups on the whole device
   if (!join_grid) {
@@ -1767,18 +1847,21 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
       return YRWI_E_HIP;
     join_grid = std::max(1, cus * std::max(1, per_cu));
   }
+  const int64_t probe_tiles = total_tiles - merge_tiles;
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, nmerge, merge_tiles, d_desc);
+  if (probe_tiles > 0)
+    hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                       d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc);
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
-  if (total_tiles > merge_tiles)
-    hipLaunchKernelGGL(k_probe, dim3((unsigned)(total_tiles - merge_tiles)), dim3(PROBE_TILE), 0, S(st),
-                       d_jobs + nmerge, d_tile_base + nmerge, njobs - nmerge, merge_tiles, d_pairs, d_tile_cnt,
-                       mark ? 1 : 0);
+  if (probe_tiles > 0)
+    hipLaunchKernelGGL(k_probe, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
+                       merge_tiles, d_pairs, d_tile_cnt, mark ? 1 : 0);
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
