@@ -425,11 +425,8 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 // RowSet.binarySearch RowSet.java:319-335): every small-list key is looked up in
 // the large list.  k_probe_part finds, per tile of PROBE_TILE small keys, the
 // large-list range that can hold them (two interleaved binary searches per
-// thread, all tiles in parallel).  k_probe then samples 256 evenly spaced keys
-// of that range into LDS, narrows each lookup to one sample interval in LDS and
-// finishes with a short binary search inside that interval (ranges of at most
-// PROBE_STAGE keys are staged whole).  Output and mark semantics are k_join's.
-constexpr int PROBE_STAGE = 2048;
+// thread, all tiles in parallel); k_probe binary-searches each key inside its
+// tile's range.  Output and mark semantics are k_join's.
 
 __device__ __forceinline__ int64_t lower_bound_key(const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
                                                    int64_t lo, int64_t hi, uint64_t h, uint32_t l) {
@@ -481,8 +478,6 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, int32_t* __restrict__ tile_cnt,
                                                      int mark) {
-  __shared__ uint64_t sH[PROBE_STAGE];
-  __shared__ uint8_t sL[PROBE_STAGE];
   __shared__ int32_t sScan[4];
   const int64_t t = blockIdx.x;
   const int64_t b = tile0 + t;
@@ -492,42 +487,14 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
   const int64_t i = s0 + threadIdx.x;
-  const bool live = i < Sm.n;
-  uint64_t h = 0;
-  uint32_t l = 0;
-  if (live) { h = Sm.khi[i]; l = Sm.klo[i]; }
-  const int64_t n = D.hi - D.lo;
-  const bool staged = n <= PROBE_STAGE;
-  // stride between samples (staged: every key)
-  const int64_t S = staged ? 1 : (n + PROBE_TILE - 1) / PROBE_TILE;
-  const int ns = staged ? (int)n : (int)((n + S - 1) / S);
-  for (int x = threadIdx.x; x < ns; x += PROBE_TILE) {
-    const int64_t g = D.lo + (int64_t)x * S;
-    sH[x] = Lg.khi[g];
-    sL[x] = Lg.klo[g];
-  }
-  __syncthreads();
   bool hit = false;
   int64_t jl = 0;
-  if (live && ns > 0) {
-    // largest sample index c with sample[c] <= key (or -1)
-    int lo = 0, hi = ns;  // first sample > key
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (sH[mid] < h || (sH[mid] == h && (uint32_t)sL[mid] <= l)) lo = mid + 1; else hi = mid;
-    }
-    const int c = lo - 1;
-    if (c >= 0) {
-      if (sH[c] == h && (uint32_t)sL[c] == l) {
-        hit = true;
-        jl = D.lo + (int64_t)c * S;
-      } else if (!staged) {
-        const int64_t w0 = D.lo + (int64_t)c * S + 1;
-        const int64_t w1 = min(D.lo + (int64_t)(c + 1) * S, D.hi);
-        jl = lower_bound_key(Lg.khi, Lg.klo, w0, w1, h, l);
-        hit = jl < w1 && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
-      }
-    }
+  if (i < Sm.n) {
+    // the upper levels of the 256 searches share lines of the range (L2 hits)
+    const uint64_t h = Sm.khi[i];
+    const uint32_t l = Sm.klo[i];
+    jl = lower_bound_key(Lg.khi, Lg.klo, D.lo, D.hi, h, l);
+    hit = jl < D.hi && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
   }
   const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
   if (hit && !mark && J.maxd < 65535) {
