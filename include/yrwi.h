@@ -18,6 +18,7 @@
 #ifndef YRWI_H
 #define YRWI_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -126,6 +127,22 @@ int yrwi_query(yrwi_ctx* ctx, const yrwi_query_desc* q, yrwi_hit* out, int32_t* 
  * out: nq * kmax hits (row q at out + q*kmax), nout[q] = hits of query q. */
 int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                      yrwi_hit* out, int32_t* nout, yrwi_stats* st);
+
+/* Asynchronous batches (throughput mode: SearchEvent runs many RWIProcess
+ * feeders concurrently, SearchEvent.java:612-631).  submit returns at once with
+ * a ticket; the batch runs on one of the context's lanes (own HIP stream and
+ * host thread) while the caller prepares the next one.  q, the profiles it
+ * points to, out, nout and st must stay valid until yrwi_query_batch_wait(ticket)
+ * returns; every ticket must be waited for exactly once.  Lists must not be
+ * changed while batches are in flight (put_list waits for them). */
+int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                            yrwi_hit* out, int32_t* nout, yrwi_stats* st, int64_t* ticket);
+int yrwi_query_batch_wait(yrwi_ctx* ctx, int64_t ticket);
+
+/* Pinned host memory for result buffers: hits written into such a buffer come
+ * straight from the GPU (no staging copy).  Free with yrwi_host_free. */
+int yrwi_host_alloc(yrwi_ctx* ctx, size_t bytes, void** p);
+int yrwi_host_free(yrwi_ctx* ctx, void* p);
 
 /* ---- finer-grained drop-ins mirroring the Java split ---- */
 /* == ReferenceContainer.joinExcludeContainers via TermSearch (ReferenceContainer.java:310,

@@ -288,3 +288,61 @@ def test_treeset_dedupe_across_chunks():
         exp = orc.search(d, [term], [], now_ms=NOW, k=k)
         assert got == exp, k
     ix.close()
+
+
+def _cqueries(batch):
+    from yacy_search_server_amd._lib import CQuery
+    import ctypes
+    arr = (CQuery * len(batch))()
+    keep = []
+    for i, q in enumerate(batch):
+        ib = ctypes.create_string_buffer(b"".join(q.include), max(1, 12 * len(q.include)))
+        eb = ctypes.create_string_buffer(b"".join(q.exclude), max(1, 12 * len(q.exclude)))
+        prof = RankingProfile()
+        keep += [ib, eb, prof]
+        arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
+        arr[i].nincl = len(q.include)
+        arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
+        arr[i].nexcl = len(q.exclude)
+        arr[i].max_distance = q.max_distance
+        arr[i].k = q.k
+        arr[i].profile = ctypes.pointer(prof.c)
+        arr[i].language = b"en"
+        arr[i].now_ms = q.now_ms
+    return arr, keep
+
+
+def test_async_batches_pinned_and_pageable(corpus):
+    """yrwi_query_batch_submit/_wait: several batches in flight on the lanes, results
+    in pinned (yrwi_host_alloc, written by the GPU directly) and in pageable buffers,
+    equal to the synchronous batch call and to the oracle."""
+    import ctypes
+    from yacy_search_server_amd._lib import CHit, CStats
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    batches = []
+    for s in range(4):
+        qs = synth.queries(cfg, 9 + s, 1, 3, s % 2, qseed=40 + s)
+        batches.append([Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=50, now_ms=NOW)
+                        for inc, exc in qs])
+    kmax = 50
+    tickets = []
+    for s, b in enumerate(batches):
+        arr, keep = _cqueries(b)
+        if s % 2:
+            hits, nout = ix.host_array(CHit, len(b) * kmax), ix.host_array(ctypes.c_int32, len(b))
+        else:
+            hits, nout = (CHit * (len(b) * kmax))(), (ctypes.c_int32 * len(b))()
+        st = CStats()
+        tickets.append((ix.submit_raw(arr, len(b), kmax, hits, nout, st), b, hits, nout, st, keep, arr))
+    for t, b, hits, nout, st, keep, arr in tickets:
+        ix.wait(t)
+        assert st.postings_in > 0
+        sync = ix.search_batch(b, kmax=kmax)
+        for i, q in enumerate(b):
+            got = [(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score) for j in range(nout[i])]
+            assert got == [(h.urlhash, h.score) for h in sync[i]]
+            exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)
+            assert got == [(h, s) for h, s, _ in exp]
+    with pytest.raises(Exception):
+        ix.wait(tickets[0][0])  # a ticket is collected once

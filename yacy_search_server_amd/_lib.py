@@ -75,6 +75,12 @@ SIGNATURES = {
     "yrwi_query_batch": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.c_int32, ctypes.c_int32,
                                         ctypes.POINTER(CHit), ctypes.POINTER(ctypes.c_int32),
                                         ctypes.POINTER(CStats)]),
+    "yrwi_query_batch_submit": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.POINTER(CHit), ctypes.POINTER(ctypes.c_int32),
+                                               ctypes.POINTER(CStats), ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_query_batch_wait": (ctypes.c_int, [_VP, ctypes.c_int64]),
+    "yrwi_host_alloc": (ctypes.c_int, [_VP, ctypes.c_size_t, ctypes.POINTER(_VP)]),
+    "yrwi_host_free": (ctypes.c_int, [_VP, _VP]),
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),

@@ -16,6 +16,10 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -155,19 +159,47 @@ struct Stage {
   size_t cap = 0, used = 0;
 };
 
-struct yrwi_ctx {
+// Pinned host buffers handed out by yrwi_host_alloc: results whose destination
+// lies inside one are written there by the GPU directly (no staging copy).
+struct HostRegistry {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, size_t>> bufs;
+  bool contains(const void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    const uint8_t* q = static_cast<const uint8_t*>(p);
+    for (auto& b : bufs)
+      if (q >= b.first && q + bytes <= b.first + b.second) return true;
+    return false;
+  }
+};
+
+// One execution lane: a HIP stream with its own scratch arena, pinned staging,
+// events and (sharded) communicator.  A batch is split over the lanes and each
+// lane runs its part from its own host thread, so one lane's host planning and
+// synchronisation overlap the other lane's kernels (and latency-bound kernels
+// of the two lanes share the device).
+struct Lane {
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
-  std::unordered_map<KeyT, ListRec, KeyHash> lists;
   Stage stage;
+  Stage out_stage;           // pinned landing buffer for results
   int64_t probe_ratio = 16;  // YRWI_PROBE_RATIO, read once per call
-  Arena index_mem{(size_t)1 << 30};
   Arena arena{(size_t)256 << 20};
   std::string err;
-  int64_t npostings = 0;
   std::vector<hipEvent_t> evpool;
   size_t evnext = 0;
+  HostRegistry* hostreg = nullptr;
+  hipEvent_t sync_ev = nullptr;
+  bool own_stream = true;
+  // persistent worker thread; `done` = last finished async ticket
+  int64_t done = -1;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool busy = false, quit = false;
+  int rc = 0;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -181,7 +213,68 @@ struct yrwi_ctx {
     }
     return evpool[evnext++];
   }
+  void start_worker() {
+    th = std::thread([this] {
+      hipSetDevice(device);
+      std::unique_lock<std::mutex> lk(mu);
+      while (true) {
+        cv.wait(lk, [this] { return busy || quit; });
+        if (quit) return;
+        lk.unlock();
+        job();
+        lk.lock();
+        busy = false;
+        cv.notify_all();
+      }
+    });
+  }
+  void submit(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu);
+    job = std::move(f);
+    busy = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !busy; });
+  }
+  void stop() {
+    if (!th.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+      cv.notify_all();
+    }
+    th.join();
+  }
 };
+
+struct yrwi_ctx {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;  // == lanes[0]->stream (index uploads)
+  std::vector<Lane*> lanes;
+  HostRegistry hostreg;
+  // asynchronous batches: ticket t runs on lane t % lanes; finished status by ticket
+  int64_t next_ticket = 0;
+  std::mutex st_mu;
+  std::unordered_map<int64_t, std::pair<int, std::string>> status;
+  std::unordered_map<KeyT, ListRec, KeyHash> lists;
+  Arena index_mem{(size_t)1 << 30};
+  std::string err;
+  int64_t npostings = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  // a lane's error becomes the context's
+  int take(Lane* l, int rc) {
+    if (rc) err = l->err;
+    return rc;
+  }
+};
+
+static void drain(yrwi_ctx* ctx);
 
 #define HIPCHK(ctx, x)                                                                 \
   do {                                                                                \
@@ -190,19 +283,44 @@ struct yrwi_ctx {
   } while (0)
 
 template <class T>
-static T* arena_alloc(yrwi_ctx* ctx, int64_t count) {
+static T* arena_alloc(Lane* ctx, int64_t count) {
   return reinterpret_cast<T*>(ctx->arena.alloc((size_t)std::max<int64_t>(count, 1) * sizeof(T)));
 }
 
+// Wait for this lane's work so far: an event, not a stream sync, so lanes that
+// share one stream do not wait for work the other lane enqueues later.
+static hipError_t lane_sync(Lane* L) {
+  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
+    return hipErrorOutOfMemory;
+  hipError_t e = hipEventRecord(L->sync_ev, L->stream);
+  return e != hipSuccess ? e : hipEventSynchronize(L->sync_ev);
+}
+
+// pinned buffer of at least `bytes` (contents dropped on growth); nullptr on failure
+static uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
+  if (bytes > S->cap) {
+    if (drain && lane_sync(ctx) != hipSuccess) return nullptr;
+    if (S->p) hipHostFree(S->p);
+    S->p = nullptr;
+    S->cap = std::max<size_t>(std::max<size_t>(2 * S->cap, bytes), (size_t)4 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&S->p), S->cap, hipHostMallocDefault) != hipSuccess) {
+      S->cap = 0;
+      ctx->fail(YRWI_E_HIP, "pinned host allocation failed");
+      return nullptr;
+    }
+  }
+  return S->p;
+}
+
 template <class T>
-static int upload(yrwi_ctx* ctx, T* dst, const std::vector<T>& v) {
+static int upload(Lane* ctx, T* dst, const std::vector<T>& v) {
   if (v.empty()) return 0;
   const size_t bytes = v.size() * sizeof(T);
   Stage& S = ctx->stage;
   size_t off = (S.used + 255) & ~(size_t)255;
   if (off + bytes > S.cap) {
     // copies still read the old buffer: drain them, then grow
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, lane_sync(ctx));
     if (S.p) HIPCHK(ctx, hipHostFree(S.p));
     S.p = nullptr;
     S.cap = std::max<size_t>(std::max<size_t>(2 * S.cap, bytes + 256), (size_t)4 << 20);
@@ -216,8 +334,8 @@ static int upload(yrwi_ctx* ctx, T* dst, const std::vector<T>& v) {
 }
 
 // start of a device pass: nothing is in flight any more, scratch can be reused
-static int begin_pass(yrwi_ctx* ctx) {
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+static int begin_pass(Lane* ctx) {
+  HIPCHK(ctx, lane_sync(ctx));
   ctx->arena.reset();
   ctx->stage.used = 0;
   ctx->evnext = 0;
@@ -344,32 +462,78 @@ extern "C" int yrwi_get_unique_id(uint8_t id[128]) {
   return 0;
 }
 
-static int open_common(int device, yrwi_ctx** out) {
+static void close_lanes(yrwi_ctx* ctx) {
+  for (Lane* L : ctx->lanes) L->wait();
+  for (Lane* L : ctx->lanes) {
+    L->stop();
+    if (L->stream) hipStreamSynchronize(L->stream);
+    if (L->comm && L->comm != ctx->lanes[0]->comm) ncclCommDestroy(L->comm);
+  }
+  if (!ctx->lanes.empty() && ctx->lanes[0]->comm) ncclCommDestroy(ctx->lanes[0]->comm);
+  for (Lane* L : ctx->lanes) {
+    L->arena.release();
+    for (auto e : L->evpool) hipEventDestroy(e);
+    if (L->stage.p) hipHostFree(L->stage.p);
+    if (L->out_stage.p) hipHostFree(L->out_stage.p);
+    if (L->sync_ev) hipEventDestroy(L->sync_ev);
+    if (L->stream && L->own_stream) hipStreamDestroy(L->stream);
+    delete L;
+  }
+  ctx->lanes.clear();
+}
+
+static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   *out = nullptr;
   if (hipSetDevice(device) != hipSuccess) return YRWI_E_HIP;
   yrwi_ctx* ctx = new yrwi_ctx();
   ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return YRWI_E_HIP;
+  ctx->rank = rank;
+  ctx->world = world;
+  // Sharded contexts default to one lane: collectives of concurrently running
+  // communicators on the same GPUs are not ordered against each other.
+  const char* e = getenv("YRWI_LANES");
+  const int nl = e ? std::max(1, std::min(8, atoi(e))) : (world > 1 ? 1 : 2);
+  for (int l = 0; l < nl; l++) {
+    Lane* L = new Lane();
+    L->device = device;
+    L->rank = rank;
+    L->world = world;
+    ctx->lanes.push_back(L);
+    const char* sh = getenv("YRWI_SHARED_STREAM");
+    if (l > 0 && sh && atoi(sh)) {
+      L->stream = ctx->lanes[0]->stream;  // lanes overlap host work only; the device runs one queue
+      L->own_stream = false;
+    } else if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
+      close_lanes(ctx);
+      delete ctx;
+      return YRWI_E_HIP;
+    }
+    L->hostreg = &ctx->hostreg;
+    L->start_worker();
   }
+  ctx->stream = ctx->lanes[0]->stream;
   *out = ctx;
   return 0;
 }
 
-extern "C" int yrwi_open(int device, yrwi_ctx** out) { return open_common(device, out); }
+extern "C" int yrwi_open(int device, yrwi_ctx** out) { return open_common(device, 0, 1, out); }
 
 extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nccl_id[128], yrwi_ctx** out) {
   if (world < 1 || (world & (world - 1)) || world > 64 || rank < 0 || rank >= world) return YRWI_E_ARG;
-  int rc = open_common(device, out);
+  int rc = open_common(device, rank, world, out);
   if (rc) return rc;
-  (*out)->rank = rank;
-  (*out)->world = world;
+  yrwi_ctx* ctx = *out;
   if (world > 1) {
     ncclUniqueId u;
     std::memcpy(&u, nccl_id, 128);
-    if (ncclCommInitRank(&(*out)->comm, world, u, rank) != ncclSuccess) {
-      yrwi_close(*out);
+    ncclComm_t c0 = nullptr;
+    bool ok = ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
+    if (ok) ctx->lanes[0]->comm = c0;
+    // one communicator per lane: lanes issue their collectives independently
+    for (size_t l = 1; ok && l < ctx->lanes.size(); l++)
+      ok = ncclCommSplit(c0, 0, rank, &ctx->lanes[l]->comm, nullptr) == ncclSuccess;
+    if (!ok) {
+      yrwi_close(ctx);
       *out = nullptr;
       return YRWI_E_RCCL;
     }
@@ -380,13 +544,8 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
 extern "C" void yrwi_close(yrwi_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  if (ctx->comm) ncclCommDestroy(ctx->comm);
-  ctx->arena.release();
+  close_lanes(ctx);
   ctx->index_mem.release();
-  for (auto e : ctx->evpool) hipEventDestroy(e);
-  if (ctx->stage.p) hipHostFree(ctx->stage.p);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
@@ -399,6 +558,7 @@ extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_
   if (!key_of(term, &tk)) return ctx->fail(YRWI_E_HASH, "term hash is not well-formed Base64");
   if (n > MAX_LIST) return ctx->fail(YRWI_E_LIMIT, "list longer than 53,687,091 rows (RowSet.importRowSet)");
   hipSetDevice(ctx->device);
+  drain(ctx);  // in-flight batches read the list table
   if (n == 0) {
     auto it = ctx->lists.find(tk);
     if (it != ctx->lists.end()) { ctx->npostings -= it->second.n; ctx->lists.erase(it); }
@@ -458,12 +618,16 @@ extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostin
   if (!ctx) return YRWI_E_ARG;
   if (nterms) *nterms = (int64_t)ctx->lists.size();
   if (npostings) *npostings = ctx->npostings;
-  if (device_bytes) *device_bytes = (int64_t)(ctx->index_mem.capacity() + ctx->arena.capacity());
+  if (device_bytes) {
+    size_t b = ctx->index_mem.capacity();
+    for (Lane* L : ctx->lanes) b += L->arena.capacity();
+    *device_bytes = (int64_t)b;
+  }
   return 0;
 }
 
 // ================================================================== planning
-static int plan_query(yrwi_ctx* ctx, const yrwi_query_desc& d, Plan* P) {
+static int plan_query(const yrwi_ctx* ix, Lane* ctx, const yrwi_query_desc& d, Plan* P) {
   P->maxd = d.max_distance;
   P->k = std::min<int32_t>(std::max<int32_t>(d.k, 0), YRWI_MAX_K);
   if (d.profile) P->prof = *d.profile; else yrwi_profile_default(&P->prof);
@@ -495,15 +659,15 @@ static int plan_query(yrwi_ctx* ctx, const yrwi_query_desc& d, Plan* P) {
   if (ninc == 0) return 0;
   const ListRec* incl[YRWI_MAX_TERMS];
   for (int i = 0; i < ninc; i++) {
-    auto it = ctx->lists.find(inc[i]);
-    if (it == ctx->lists.end() || it->second.n == 0) return 0;  // conjunction: any missing term -> empty
+    auto it = ix->lists.find(inc[i]);
+    if (it == ix->lists.end() || it->second.n == 0) return 0;  // conjunction: any missing term -> empty
     incl[i] = &it->second;
   }
   bool use_excl = nexc > 0;
   P->excl.clear();
   for (int i = 0; i < nexc && use_excl; i++) {
-    auto it = ctx->lists.find(exc[i]);
-    if (it == ctx->lists.end() || it->second.n == 0) use_excl = false;
+    auto it = ix->lists.find(exc[i]);
+    if (it == ix->lists.end() || it->second.n == 0) use_excl = false;
     else P->excl.push_back(&it->second);
   }
   if (!use_excl) P->excl.clear();
@@ -585,7 +749,7 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
 }
 
 // Run the join/exclusion phase of all plans; leaves each plan's container in P.cont.
-static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
+static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   for (auto& P : plans) {
     if (P.empty) { P.cont = DList{nullptr, nullptr, nullptr, 0}; continue; }
     P.cont = P.seq[0]->dl();
@@ -644,7 +808,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
     if (st) st->n_join_launches++;
     mh.assign((size_t)nj, 0);
     HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, lane_sync(ctx));
     for (int j = 0; j < nj; j++) {
       Plan& P = plans[(size_t)owner[(size_t)j]];
       P.cont = DList{jobs[(size_t)j].out_khi, jobs[(size_t)j].out_klo, jobs[(size_t)j].out_rows, mh[(size_t)j]};
@@ -694,7 +858,7 @@ static int run_join_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, yrwi_stats* s
 // Global host counts for authority (ReferenceOrder.java:176-216) across url-hash
 // shards: (query, host, count) messages to the host's owner rank, summed there,
 // totals sent back; the per-query max count is all-reduced.  Collective.
-static int exchange_host_counts(yrwi_ctx* ctx, int nq, int64_t nslots, const std::vector<int64_t>& slot_base,
+static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::vector<int64_t>& slot_base,
                                 uint64_t* d_hkeys, uint32_t* d_hcnt, ShardSum* d_ss) {
   const int W = ctx->world, me = ctx->rank;
   uint32_t* d_ocnt = arena_alloc<uint32_t>(ctx, W);
@@ -710,7 +874,7 @@ static int exchange_host_counts(yrwi_ctx* ctx, int nq, int64_t nslots, const std
     return ctx->fail(YRWI_E_RCCL, "allgather of host message counts");
   std::vector<uint32_t> M((size_t)W * W);
   HIPCHK(ctx, hipMemcpyAsync(M.data(), d_M, M.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, lane_sync(ctx));
   // row s of M = what rank s sends to each owner
   std::vector<int64_t> soff((size_t)W + 1, 0), roff((size_t)W + 1, 0);
   for (int p = 0; p < W; p++) {
@@ -767,7 +931,7 @@ static int exchange_host_counts(yrwi_ctx* ctx, int nq, int64_t nslots, const std
 }
 
 // Normalise (+ cross-shard exchange), then either score+top-k (hits) or all scores.
-static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax, yrwi_hit* h_hits,
+static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrwi_hit* h_hits,
                           int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
   const int nq = (int)plans.size();
   const int W = exchange ? ctx->world : 1;
@@ -858,7 +1022,7 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
     if (!d_sc) return ctx->fail(YRWI_E_NOMEM, "arena");
     if (launch_score_all(d_q, d_cq, nq, chunks, d_norm, d_sc, ctx->stream)) return ctx->fail(YRWI_E_HIP, "score launch");
     HIPCHK(ctx, hipMemcpyAsync(h_scores_all, d_sc, sizeof(int64_t) * rq[0].n, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, lane_sync(ctx));
     NormState nsh;
     HIPCHK(ctx, hipMemcpy(&nsh, d_norm, sizeof(nsh), hipMemcpyDeviceToHost));
     if (nsh.D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
@@ -931,16 +1095,43 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   }
   const Cand** d_fptr = arena_alloc<const Cand*>(ctx, nq);
   const int32_t** d_fcnt = arena_alloc<const int32_t*>(ctx, nq);
-  yrwi_hit* d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);
-  int32_t* d_nout = arena_alloc<int32_t>(ctx, nq);
+  // one GPU: k_emit writes the results straight into pinned host memory -- the
+  // caller's buffer when it came from yrwi_host_alloc, else this lane's landing
+  // buffer (then copied out per query)
+  const size_t hb = sizeof(yrwi_hit) * (size_t)nq * kmax, hb_al = (hb + 255) & ~(size_t)255;
+  const size_t nb = sizeof(int32_t) * (size_t)nq;
+  yrwi_hit* d_hits = nullptr;
+  int32_t* d_nout = nullptr;
+  uint8_t* land = nullptr;
+  bool direct = false;
+  if (W == 1) {
+    direct = ctx->hostreg && ctx->hostreg->contains(h_hits, hb) && ctx->hostreg->contains(h_nout, nb);
+    void* hp = h_hits;
+    void* np = h_nout;
+    if (!direct) {
+      land = stage_reserve(ctx, &ctx->out_stage, hb_al + nb, true);
+      if (!land) return YRWI_E_HIP;
+      hp = land;
+      np = land + hb_al;
+    }
+    HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hits), hp, 0));
+    HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));
+  } else {
+    d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);
+    d_nout = arena_alloc<int32_t>(ctx, nq);
+  }
   if (!d_fptr || !d_fcnt || !d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
   if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, ctx->stream)) return ctx->fail(YRWI_E_HIP, "emit launch");
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
   if (W == 1) {
-    HIPCHK(ctx, hipMemcpyAsync(h_hits, d_hits, sizeof(yrwi_hit) * nq * kmax, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(h_nout, d_nout, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, lane_sync(ctx));
+    if (!direct) {
+      std::memcpy(h_nout, land + hb_al, nb);
+      for (int qi = 0; qi < nq; qi++)
+        std::memcpy(h_hits + (size_t)qi * kmax, land + sizeof(yrwi_hit) * (size_t)qi * kmax,
+                    sizeof(yrwi_hit) * (size_t)std::max(0, std::min(h_nout[qi], kmax)));
+    }
     return 0;
   }
   // ---- multi-GPU: gather every shard's top-k, merge in shard (= url hash) order
@@ -958,7 +1149,7 @@ static int run_rank_phase(yrwi_ctx* ctx, std::vector<Plan>& plans, int32_t kmax,
   HIPCHK(ctx, hipMemcpyAsync(alln.data(), d_alln, alln.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   std::vector<NormState> nsh((size_t)nq);
   HIPCHK(ctx, hipMemcpyAsync(nsh.data(), d_norm, nq * sizeof(NormState), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, lane_sync(ctx));
   for (int qi = 0; qi < nq; qi++) {
     if (nsh[(size_t)qi].D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
     std::vector<yrwi_hit> v;
@@ -991,43 +1182,160 @@ static int64_t now_ns() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax, yrwi_hit* out,
-                                int32_t* nout, yrwi_stats* st) {
-  if (!ctx || (nq > 0 && (!q || !out || !nout)) || nq < 0 || kmax < 1 || kmax > YRWI_MAX_K) return YRWI_E_ARG;
-  if (nq == 0) return 0;
-  hipSetDevice(ctx->device);
+// Plan and run queries q[0, nq) on lane L; results at out (row stride kmax).
+// Every field of *st is this part's own (the caller sums parts).
+static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                          yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
-  if (st) std::memset(st, 0, sizeof(*st));
   std::vector<Plan> plans((size_t)nq);
   for (int i = 0; i < nq; i++) {
-    int rc = plan_query(ctx, q[i], &plans[(size_t)i]);
+    int rc = plan_query(ix, L, q[i], &plans[(size_t)i]);
     if (rc) return rc;
     if (st) st->postings_in += plans[(size_t)i].postings_in;
   }
-  if (begin_pass(ctx)) return YRWI_E_HIP;
+  if (begin_pass(L)) return YRWI_E_HIP;
   Timing tm;
-  tm.t0 = ctx->event();
-  hipEventRecord(tm.t0, ctx->stream);
-  int rc = run_join_phase(ctx, plans, st, &tm);
+  tm.t0 = L->event();
+  hipEventRecord(tm.t0, L->stream);
+  int rc = run_join_phase(L, plans, st, &tm);
   if (rc) return rc;
-  tm.tj = ctx->event();
-  hipEventRecord(tm.tj, ctx->stream);
-  rc = run_rank_phase(ctx, plans, kmax, out, nout, nullptr, st, &tm);
+  tm.tj = L->event();
+  hipEventRecord(tm.tj, L->stream);
+  rc = run_rank_phase(L, plans, kmax, out, nout, nullptr, st, &tm);
   if (rc) return rc;
   if (st) {
     float ms = 0;
-    int64_t kj = 0, kp = 0;
     for (auto& ev : tm.kjoin) {
-      if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) kj += (int64_t)(ms * 1e6);
-      if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) kp += (int64_t)(ms * 1e6);
+      if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_join_ns += (int64_t)(ms * 1e6);
+      if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) st->t_probe_ns += (int64_t)(ms * 1e6);
     }
-    st->t_join_ns = kj;
-    st->t_probe_ns = kp;
-    if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns = (int64_t)(ms * 1e6);
-    if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns = (int64_t)(ms * 1e6);
+    if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
+    if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
     st->t_total_ns = now_ns() - t0;
   }
   return 0;
+}
+
+static int check_batch_args(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax, yrwi_hit* out,
+                            int32_t* nout) {
+  if (!ctx || (nq > 0 && (!q || !out || !nout)) || nq < 0 || kmax < 1 || kmax > YRWI_MAX_K) return YRWI_E_ARG;
+  return 0;
+}
+
+// wait until no asynchronous batch is in flight (their statuses stay recorded)
+static void drain(yrwi_ctx* ctx) {
+  for (Lane* L : ctx->lanes) L->wait();
+}
+
+extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax, yrwi_hit* out,
+                                int32_t* nout, yrwi_stats* st) {
+  if (int rc = check_batch_args(ctx, q, nq, kmax, out, nout)) return rc;
+  if (nq == 0) {
+    if (st) std::memset(st, 0, sizeof(*st));
+    return 0;
+  }
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  const int64_t t0 = now_ns();
+  // contiguous parts of equal query count, one per lane, each planned and run
+  // by its lane's thread (every rank splits a sharded batch identically)
+  const int nl = (int)std::min<int64_t>((int64_t)ctx->lanes.size(), nq);
+  std::vector<yrwi_stats> pst((size_t)nl);
+  for (auto& p : pst) std::memset(&p, 0, sizeof(p));
+  auto cut = [&](int l) { return (int32_t)((int64_t)nq * l / nl); };
+  auto part = [=, &pst](int l) {
+    Lane* L = ctx->lanes[(size_t)l];
+    L->rc = run_batch_part(ctx, L, q + cut(l), cut(l + 1) - cut(l), kmax, out + (size_t)cut(l) * kmax, nout + cut(l),
+                           st ? &pst[(size_t)l] : nullptr);
+  };
+  for (int l = 1; l < nl; l++) ctx->lanes[(size_t)l]->submit([=] { part(l); });
+  part(0);  // lane 0 on the calling thread (its worker is idle after drain)
+  int rc = 0;
+  for (int l = 0; l < nl; l++) {
+    Lane* L = ctx->lanes[(size_t)l];
+    if (l > 0) L->wait();
+    if (L->rc && !rc) rc = ctx->take(L, L->rc);
+  }
+  if (rc) return rc;
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    for (const yrwi_stats& p : pst) {
+      st->postings_in += p.postings_in;
+      st->joined += p.joined;
+      st->bytes_alg += p.bytes_alg;
+      st->bytes_join += p.bytes_join;
+      st->bytes_probe += p.bytes_probe;
+      st->t_join_ns += p.t_join_ns;
+      st->t_probe_ns += p.t_probe_ns;
+      st->t_norm_ns += p.t_norm_ns;
+      st->t_score_ns += p.t_score_ns;
+      st->n_join_launches += p.n_join_launches;
+      st->n_enum_steps += p.n_enum_steps;
+      st->n_test_steps += p.n_test_steps;
+    }
+    st->t_total_ns = now_ns() - t0;
+  }
+  return 0;
+}
+
+extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                                       yrwi_hit* out, int32_t* nout, yrwi_stats* st, int64_t* ticket) {
+  if (int rc = check_batch_args(ctx, q, nq, kmax, out, nout)) return rc;
+  if (!ticket) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  const int64_t t = ctx->next_ticket;
+  Lane* L = ctx->lanes[(size_t)(t % (int64_t)ctx->lanes.size())];
+  L->wait();  // the lane's previous batch (its status is already recorded)
+  ctx->next_ticket++;
+  L->submit([=] {
+    if (st) std::memset(st, 0, sizeof(*st));
+    const int rc = nq == 0 ? 0 : run_batch_part(ctx, L, q, nq, kmax, out, nout, st);
+    {
+      std::lock_guard<std::mutex> lk(ctx->st_mu);
+      ctx->status[t] = {rc, rc ? L->err : std::string()};
+    }
+    L->done = t;
+  });
+  *ticket = t;
+  return 0;
+}
+
+extern "C" int yrwi_query_batch_wait(yrwi_ctx* ctx, int64_t ticket) {
+  if (!ctx || ticket < 0 || ticket >= ctx->next_ticket) return YRWI_E_ARG;
+  Lane* L = ctx->lanes[(size_t)(ticket % (int64_t)ctx->lanes.size())];
+  L->wait();  // a lane runs its tickets in order; the next one is not submitted before this returns
+  std::lock_guard<std::mutex> lk(ctx->st_mu);
+  auto it = ctx->status.find(ticket);
+  if (it == ctx->status.end()) return ctx->fail(YRWI_E_ARG, "unknown or already collected ticket");
+  const int rc = it->second.first;
+  if (rc) ctx->err = it->second.second;
+  ctx->status.erase(it);
+  return rc;
+}
+
+extern "C" int yrwi_host_alloc(yrwi_ctx* ctx, size_t bytes, void** p) {
+  if (!ctx || !p || bytes == 0) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) return ctx->fail(YRWI_E_NOMEM, "hipHostMalloc");
+  std::lock_guard<std::mutex> lk(ctx->hostreg.mu);
+  ctx->hostreg.bufs.push_back({static_cast<uint8_t*>(h), bytes});
+  *p = h;
+  return 0;
+}
+
+extern "C" int yrwi_host_free(yrwi_ctx* ctx, void* p) {
+  if (!ctx || !p) return YRWI_E_ARG;
+  drain(ctx);
+  std::lock_guard<std::mutex> lk(ctx->hostreg.mu);
+  auto& v = ctx->hostreg.bufs;
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i].first == p) {
+      hipHostFree(p);
+      v.erase(v.begin() + (long)i);
+      return 0;
+    }
+  return ctx->fail(YRWI_E_ARG, "not a yrwi_host_alloc buffer");
 }
 
 extern "C" int yrwi_query(yrwi_ctx* ctx, const yrwi_query_desc* q, yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
@@ -1050,11 +1358,13 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
   d.max_distance = max_distance;
   d.k = 1;
   d.now_ms = now_ms;
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
   std::vector<Plan> plans(1);
-  int rc = plan_query(ctx, d, &plans[0]);
+  int rc = ctx->take(L, plan_query(ctx, L, d, &plans[0]));
   if (rc) return rc;
-  if (begin_pass(ctx)) return YRWI_E_HIP;
-  rc = run_join_phase(ctx, plans, nullptr, nullptr);
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  rc = ctx->take(L, run_join_phase(L, plans, nullptr, nullptr));
   if (rc) return rc;
   const Plan& P = plans[0];
   if (P.empty || P.cont.n == 0) {
@@ -1085,11 +1395,13 @@ extern "C" int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_
   if (m <= 0) return 0;
   if (m > MAX_LIST) return ctx->fail(YRWI_E_LIMIT, "container longer than 53,687,091 rows");
   hipSetDevice(ctx->device);
-  if (begin_pass(ctx)) return YRWI_E_HIP;
-  uint8_t* rows = arena_alloc<uint8_t>(ctx, m * 40);
-  uint64_t* khi = arena_alloc<uint64_t>(ctx, m);
-  uint8_t* klo = arena_alloc<uint8_t>(ctx, m);
-  int32_t* derr = arena_alloc<int32_t>(ctx, 1);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  uint8_t* rows = arena_alloc<uint8_t>(L, m * 40);
+  uint64_t* khi = arena_alloc<uint64_t>(L, m);
+  uint8_t* klo = arena_alloc<uint8_t>(L, m);
+  int32_t* derr = arena_alloc<int32_t>(L, 1);
   if (!rows || !khi || !klo || !derr) return ctx->fail(YRWI_E_NOMEM, "arena");
   HIPCHK(ctx, hipMemcpyAsync(rows, rows40, (size_t)m * 40, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(derr, 0, 4, ctx->stream));
@@ -1114,5 +1426,5 @@ extern "C" int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_
                          : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
                                std::chrono::system_clock::now().time_since_epoch()).count();
   P.k = 1;
-  return run_rank_phase(ctx, plans, 1, nullptr, nullptr, score_out, nullptr, nullptr, false);
+  return ctx->take(L, run_rank_phase(L, plans, 1, nullptr, nullptr, score_out, nullptr, nullptr, false));
 }

@@ -145,6 +145,9 @@ class RWIIndex:
 
     def close(self):
         if self._h:
+            for p in getattr(self, "_pinned", []):
+                _lib.lib().yrwi_host_free(self._h, p)
+            self._pinned = []
             _lib.lib().yrwi_close(self._h)
             self._h = None
 
@@ -237,6 +240,25 @@ class RWIIndex:
     def search_batch_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> None:
         """Zero-marshalling batch call for benchmarks (pre-built ctypes arrays)."""
         _check(self._h, _lib.lib().yrwi_query_batch(self._h, cq, nq, kmax, hits, nout, ctypes.byref(st)))
+
+    # ---- asynchronous batches (yrwi_query_batch_submit / _wait) ----
+    def submit_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> int:
+        """Start a batch; the ctypes buffers must stay alive until wait(ticket)."""
+        t = ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_query_batch_submit(self._h, cq, nq, kmax, hits, nout, ctypes.byref(st),
+                                                           ctypes.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        _check(self._h, _lib.lib().yrwi_query_batch_wait(self._h, ticket))
+
+    def host_array(self, ctype, n: int):
+        """A ctypes array of n `ctype` in pinned host memory (GPU writes results into it directly)."""
+        p = ctypes.c_void_p()
+        _check(self._h, _lib.lib().yrwi_host_alloc(self._h, ctypes.sizeof(ctype) * max(1, n), ctypes.byref(p)))
+        arr = (ctype * max(1, n)).from_address(p.value)
+        self._pinned = getattr(self, "_pinned", []) + [p.value]
+        return arr
 
 
 def unique_id() -> bytes:
