@@ -118,6 +118,29 @@ int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, 
 int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
 
+/* ---- YaCy on-disk index ---- */
+/* Loads BLOB heap files of the RWI (records [int32 reclen][12-byte term hash]
+ * [exported RowSet], HeapWriter.java:114-124, RowCollection.java:209-224) into
+ * device memory.  Files are folded oldest first with RowSet.mergeEnum (the older
+ * file's row wins on equal url hashes; ReferenceContainerArray.get :305-322);
+ * lists already in the context act as the RAM cache and are merged below the
+ * files (IndexCell.get :353-386).  A sharded context keeps only its url-hash
+ * range.  With YRWI_LOAD_ORDER_BY_NAME the files are ordered by the
+ * <prefix>.<yyyyMMddHHmmssSSS>.blob stamp and others are ignored
+ * (ArrayStack.java:182-229); otherwise `paths` is taken as oldest first.
+ * Malformed records are skipped as HeapReader does; a term whose RowSet export
+ * is inconsistent (importRowSet's SpaceExceededException) keeps only its RAM
+ * list, as does a term with malformed rows; both are counted in dropped_terms. */
+#define YRWI_LOAD_ORDER_BY_NAME 1
+typedef struct yrwi_load_stats {
+  int64_t files, records, free_records, bad_keys;
+  int64_t terms;          /* lists stored (replaced or new) */
+  int64_t postings;       /* rows in those lists */
+  int64_t dropped_terms;
+} yrwi_load_stats;
+int yrwi_load_heaps(yrwi_ctx* ctx, const char* const* paths, int32_t npaths, int32_t flags,
+                    yrwi_load_stats* st);
+
 /* ---- query hot path ---- */
 /* TermSearch + joinExcludeContainers + normalizeWith + cardinal + rwiStack top-k
  * (SearchEvent.RWIProcess.run :612-631 -> addRWIs :673-836), canonical

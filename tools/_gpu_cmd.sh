@@ -1,3 +1,2 @@
 set -e
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench.json 2>gpurun_out/bench.err

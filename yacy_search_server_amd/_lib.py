@@ -54,6 +54,11 @@ class CStats(ctypes.Structure):
                 ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64)]
 
 
+class CLoadStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
+                                              "dropped_terms")]
+
+
 # every symbol include/yrwi.h declares, with its ctypes signature
 _VP = ctypes.c_void_p
 SIGNATURES = {
@@ -81,6 +86,8 @@ SIGNATURES = {
     "yrwi_query_batch_wait": (ctypes.c_int, [_VP, ctypes.c_int64]),
     "yrwi_host_alloc": (ctypes.c_int, [_VP, ctypes.c_size_t, ctypes.POINTER(_VP)]),
     "yrwi_host_free": (ctypes.c_int, [_VP, _VP]),
+    "yrwi_load_heaps": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.POINTER(CLoadStats)]),
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),

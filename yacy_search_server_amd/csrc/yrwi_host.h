@@ -1,0 +1,343 @@
+// yrwi_host.h -- host-side structures shared by libyrwi's host translation
+// units (yrwi_host.cpp: contexts, planning, query execution; yrwi_heap.cpp:
+// BLOB heap loader).  Internal; the public ABI is include/yrwi.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <unordered_map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "yrwi_internal.h"
+
+namespace yrwi {
+
+constexpr int64_t MAX_LIST = 53687091;  // RowSet.importRowSet: 2^31 bytes of 40-byte rows
+
+// Base64Order.enhancedCoder alphabet index (Base64Order.java:38,54), -1 if not in it
+struct AhpTable {
+  int8_t v[256];
+  constexpr AhpTable() : v() {
+    const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    for (int i = 0; i < 256; i++) v[i] = -1;
+    for (int i = 0; i < 64; i++) v[(uint8_t)a[i]] = (int8_t)i;
+  }
+};
+inline constexpr AhpTable AHP_T{};
+#define AHP AHP_T.v
+
+struct KeyT {
+  uint64_t hi;
+  uint32_t lo;
+  bool operator<(const KeyT& o) const { return hi < o.hi || (hi == o.hi && lo < o.lo); }
+  bool operator==(const KeyT& o) const { return hi == o.hi && lo == o.lo; }
+};
+
+inline bool key_of(const uint8_t* h, KeyT* k) {
+  uint64_t x = 0;
+  for (int j = 0; j < 10; j++) {
+    if (AHP[h[j]] < 0) return false;
+    x = (x << 6) | (uint64_t)AHP[h[j]];
+  }
+  if (AHP[h[10]] < 0 || AHP[h[11]] < 0) return false;
+  uint32_t c10 = (uint32_t)AHP[h[10]], c11 = (uint32_t)AHP[h[11]];
+  k->hi = (x << 4) | (c10 >> 2);
+  k->lo = ((c10 & 3u) << 6) | c11;
+  return true;
+}
+
+// Java int arithmetic
+inline int32_t add32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+inline int32_t mul32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+inline int log2j(int32_t x) {
+  int l = 0;
+  while (x > 0) { x >>= 1; l++; }
+  return l;
+}
+
+struct ListRec {
+  uint64_t* khi = nullptr;
+  uint8_t* klo = nullptr;
+  uint8_t* rows = nullptr;
+  int64_t n = 0;
+  DList dl() const { return DList{khi, klo, rows, n}; }
+};
+
+// bump allocator over device chunks
+struct Arena {
+  std::vector<std::pair<uint8_t*, size_t>> chunks;
+  size_t used = 0, cur = 0, total_used = 0, min_chunk;
+  explicit Arena(size_t mc) : min_chunk(mc) {}
+  uint8_t* alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (bytes == 0) bytes = 256;
+    while (cur < chunks.size() && used + bytes > chunks[cur].second) {
+      cur++;
+      used = 0;
+    }
+    if (cur >= chunks.size()) {
+      size_t sz = std::max(bytes, min_chunk);
+      void* p = nullptr;
+      if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
+      chunks.push_back({(uint8_t*)p, sz});
+      cur = chunks.size() - 1;
+      used = 0;
+    }
+    uint8_t* p = chunks[cur].first + used;
+    used += bytes;
+    total_used += bytes;
+    return p;
+  }
+  // only call when no kernel uses arena memory any more
+  void reset() {
+    if (chunks.size() > 1) {
+      size_t need = total_used + (1 << 20);
+      for (auto& c : chunks) hipFree(c.first);
+      chunks.clear();
+      void* p = nullptr;
+      if (hipMalloc(&p, std::max(need, min_chunk)) == hipSuccess)
+        chunks.push_back({(uint8_t*)p, std::max(need, min_chunk)});
+    }
+    used = 0;
+    cur = 0;
+    total_used = 0;
+  }
+  size_t capacity() const {
+    size_t s = 0;
+    for (auto& c : chunks) s += c.second;
+    return s;
+  }
+  void release() {
+    for (auto& c : chunks) hipFree(c.first);
+    chunks.clear();
+  }
+};
+
+struct Plan {
+  bool empty = true;
+  std::vector<const ListRec*> seq;   // fold order
+  std::vector<const ListRec*> excl;  // exclusion lists (empty: no exclusion)
+  int32_t maxd = YRWI_MAX_DISTANCE_ANY, k = 0;
+  yrwi_profile prof{};
+  uint8_t lang[2] = {0, 0};
+  int32_t lang_ok = 0;
+  int64_t now_ms = 0;
+  int64_t postings_in = 0;
+  // runtime container
+  DList cont{nullptr, nullptr, nullptr, 0};
+  uint8_t* removed = nullptr;
+};
+
+
+struct KeyHash {
+  size_t operator()(const KeyT& k) const { return (size_t)(k.hi * 0x9E3779B97F4A7C15ull) ^ k.lo; }
+};
+
+// pinned host staging for the per-batch uploads (pageable copies would block)
+struct Stage {
+  uint8_t* p = nullptr;
+  size_t cap = 0, used = 0;
+};
+
+// Pinned host buffers handed out by yrwi_host_alloc: results whose destination
+// lies inside one are written there by the GPU directly (no staging copy).
+struct HostRegistry {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, size_t>> bufs;
+  bool contains(const void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    const uint8_t* q = static_cast<const uint8_t*>(p);
+    for (auto& b : bufs)
+      if (q >= b.first && q + bytes <= b.first + b.second) return true;
+    return false;
+  }
+};
+
+// One execution lane: a HIP stream with its own scratch arena, pinned staging,
+// events and (sharded) communicator.  A batch is split over the lanes and each
+// lane runs its part from its own host thread, so one lane's host planning and
+// synchronisation overlap the other lane's kernels (and latency-bound kernels
+// of the two lanes share the device).
+struct Lane {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  Stage stage;
+  Stage out_stage;           // pinned landing buffer for results
+  int64_t probe_ratio = 16;  // YRWI_PROBE_RATIO, read once per call
+  Arena arena{(size_t)256 << 20};
+  std::string err;
+  std::vector<hipEvent_t> evpool;
+  size_t evnext = 0;
+  HostRegistry* hostreg = nullptr;
+  hipEvent_t sync_ev = nullptr;
+  bool own_stream = true;
+  // persistent worker thread; `done` = last finished async ticket
+  int64_t done = -1;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool busy = false, quit = false;
+  int rc = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  hipEvent_t event() {
+    if (evnext >= evpool.size()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      evpool.push_back(e);
+    }
+    return evpool[evnext++];
+  }
+  void start_worker() {
+    th = std::thread([this] {
+      hipSetDevice(device);
+      std::unique_lock<std::mutex> lk(mu);
+      while (true) {
+        cv.wait(lk, [this] { return busy || quit; });
+        if (quit) return;
+        lk.unlock();
+        job();
+        lk.lock();
+        busy = false;
+        cv.notify_all();
+      }
+    });
+  }
+  void submit(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu);
+    job = std::move(f);
+    busy = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !busy; });
+  }
+  void stop() {
+    if (!th.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+      cv.notify_all();
+    }
+    th.join();
+  }
+};
+
+struct CtxBase {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;  // == lanes[0]->stream (index uploads)
+  std::vector<Lane*> lanes;
+  HostRegistry hostreg;
+  // asynchronous batches: ticket t runs on lane t % lanes; finished status by ticket
+  int64_t next_ticket = 0;
+  std::mutex st_mu;
+  std::unordered_map<int64_t, std::pair<int, std::string>> status;
+  std::unordered_map<KeyT, ListRec, KeyHash> lists;
+  Arena index_mem{(size_t)1 << 30};
+  std::string err;
+  int64_t npostings = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  // a lane's error becomes the context's
+  int take(Lane* l, int rc) {
+    if (rc) err = l->err;
+    return rc;
+  }
+};
+
+void drain(CtxBase* ctx);
+
+#define HIPCHK(ctx, x)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (x);                                                              \
+    if (_e != hipSuccess) return (ctx)->fail(YRWI_E_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class T>
+inline T* arena_alloc(Lane* ctx, int64_t count) {
+  return reinterpret_cast<T*>(ctx->arena.alloc((size_t)std::max<int64_t>(count, 1) * sizeof(T)));
+}
+
+// Wait for this lane's work so far: an event, not a stream sync, so lanes that
+// share one stream do not wait for work the other lane enqueues later.
+inline hipError_t lane_sync(Lane* L) {
+  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
+    return hipErrorOutOfMemory;
+  hipError_t e = hipEventRecord(L->sync_ev, L->stream);
+  return e != hipSuccess ? e : hipEventSynchronize(L->sync_ev);
+}
+
+// pinned buffer of at least `bytes` (contents dropped on growth); nullptr on failure
+inline uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
+  if (bytes > S->cap) {
+    if (drain && lane_sync(ctx) != hipSuccess) return nullptr;
+    if (S->p) hipHostFree(S->p);
+    S->p = nullptr;
+    S->cap = std::max<size_t>(std::max<size_t>(2 * S->cap, bytes), (size_t)4 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&S->p), S->cap, hipHostMallocDefault) != hipSuccess) {
+      S->cap = 0;
+      ctx->fail(YRWI_E_HIP, "pinned host allocation failed");
+      return nullptr;
+    }
+  }
+  return S->p;
+}
+
+template <class T>
+inline int upload(Lane* ctx, T* dst, const std::vector<T>& v) {
+  if (v.empty()) return 0;
+  const size_t bytes = v.size() * sizeof(T);
+  Stage& S = ctx->stage;
+  size_t off = (S.used + 255) & ~(size_t)255;
+  if (off + bytes > S.cap) {
+    // copies still read the old buffer: drain them, then grow
+    HIPCHK(ctx, lane_sync(ctx));
+    if (S.p) HIPCHK(ctx, hipHostFree(S.p));
+    S.p = nullptr;
+    S.cap = std::max<size_t>(std::max<size_t>(2 * S.cap, bytes + 256), (size_t)4 << 20);
+    HIPCHK(ctx, hipHostMalloc(reinterpret_cast<void**>(&S.p), S.cap, hipHostMallocDefault));
+    off = 0;
+  }
+  std::memcpy(S.p + off, v.data(), bytes);
+  HIPCHK(ctx, hipMemcpyAsync(dst, S.p + off, bytes, hipMemcpyHostToDevice, ctx->stream));
+  S.used = off + bytes;
+  return 0;
+}
+
+// start of a device pass: nothing is in flight any more, scratch can be reused
+inline int begin_pass(Lane* ctx) {
+  HIPCHK(ctx, lane_sync(ctx));
+  ctx->arena.reset();
+  ctx->stage.used = 0;
+  ctx->evnext = 0;
+  const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
+  ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
+  return 0;
+}
+
+}  // namespace yrwi
+
+// the opaque context of the C ABI
+struct yrwi_ctx : yrwi::CtxBase {};

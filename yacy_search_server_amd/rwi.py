@@ -162,6 +162,15 @@ class RWIIndex:
         rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, 40)
         _check(self._h, _lib.lib().yrwi_put_list(self._h, bytes(term), rows.ctypes.data, len(rows), 1 if sorted else 0))
 
+    def load_heaps(self, paths: Sequence[str], order_by_name: bool = False) -> "_lib.CLoadStats":
+        """Load YaCy BLOB heap files (IndexCell's ReferenceContainerArray) into the index;
+        lists already present act as the RAM cache (the files' rows win)."""
+        arr = (ctypes.c_char_p * max(1, len(paths)))(*[p.encode() for p in paths])
+        st = _lib.CLoadStats()
+        _check(self._h, _lib.lib().yrwi_load_heaps(self._h, arr, len(paths), 1 if order_by_name else 0,
+                                                   ctypes.byref(st)))
+        return st
+
     def get_size(self, term: bytes) -> int:
         n = ctypes.c_int64()
         _check(self._h, _lib.lib().yrwi_list_size(self._h, bytes(term), ctypes.byref(n)))
