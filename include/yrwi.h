@@ -67,6 +67,28 @@ typedef struct yrwi_hit {
   int64_t score;    /* ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265) */
 } yrwi_hit;
 
+/* Per-query constraints that SearchEvent.addRWIs applies before a posting enters
+ * rwiStack (SearchEvent.java:736-806), and the doubledom pull order of
+ * pullOneRWI(skipDoubleDom) (:1297-1394).  Normalisation still covers the whole
+ * joined container; these only decide which postings are ranked. */
+typedef struct yrwi_filter {
+  uint8_t constraint[4];        /* QueryParams.constraint as Bitfield bytes (bit j: byte j>>3, bit j&7) */
+  int32_t has_constraint;       /* constraint != null; testFlags :2459-2474 */
+  int32_t all_of_constraint;    /* QueryParams.allofconstraint */
+  int32_t contentdom;           /* ContentDomain code: -1 ALL, 0 TEXT, 1 IMAGE, 2 AUDIO, 3 VIDEO, 4 APP */
+  int32_t strict_contentdom;    /* QueryParams.isStrictContentDom(): test the doctype, not the flags */
+  char language[8];             /* QueryModifier.language, NUL terminated; "" = any */
+  uint8_t sitehash[6];          /* QueryModifier.sitehash: host hash = url-hash chars 6..11 */
+  uint8_t alt_sitehash[6];      /* DigestURL.hosthash of the www./non-www. variant (:716-718) */
+  int32_t has_sitehash, has_alt_sitehash;
+  const uint8_t* siteexcludes;  /* nsiteexcludes * 6 bytes (QueryParams.siteexcludes); used without sitehash */
+  int32_t nsiteexcludes;
+  const uint8_t* urlhashes;     /* nurlhashes * 12 bytes already in SearchEvent.urlhashes (doublecheck) */
+  int32_t nurlhashes;
+  int32_t skip_double_dom;      /* results in pullOneRWI(true) order: new hosts first (stack bound 3000) */
+  int32_t* flagcount;           /* out: SearchEvent.flagcount[32] over the postings past the doublecheck, or NULL */
+} yrwi_filter;
+
 /* A query: QueryGoal include/exclude word hashes (QueryGoal.java:229-240) plus
  * QueryParams.maxDistance, the ranking profile and the target language. */
 typedef struct yrwi_query_desc {
@@ -79,6 +101,7 @@ typedef struct yrwi_query_desc {
   const yrwi_profile* profile;
   char language[8];           /* ReferenceOrder.language, NUL terminated (any length) */
   int64_t now_ms;             /* System.currentTimeMillis() of the request; 0 = now */
+  const yrwi_filter* filter;  /* NULL: unconstrained query */
 } yrwi_query_desc;
 
 typedef struct yrwi_stats {

@@ -906,23 +906,140 @@ class ReverseQueue:
 MAX_RESULTS_RWI = 3000  # SearchEvent.java:118
 
 
+class QueryFilter:
+    """The per-query constraints addRWIs applies before a posting enters rwiStack
+    (SearchEvent.java:736-806) and the doubledom pull order (:1297-1394).
+    Defaults reproduce the unconstrained query."""
+
+    def __init__(self, constraint: Optional[bytes] = None, all_of_constraint: bool = False, contentdom: int = 0,
+                 strict_contentdom: bool = False, language: str = "", sitehash: Optional[bytes] = None,
+                 alt_sitehash: Optional[bytes] = None, siteexcludes: Sequence[bytes] = (),
+                 urlhashes: Sequence[bytes] = (), skip_double_dom: bool = False):
+        self.constraint = Bitfield(constraint) if constraint is not None else None  # QueryParams.constraint
+        self.all_of_constraint = all_of_constraint
+        self.contentdom = contentdom          # ContentDomain code (Classification.java:47-52)
+        self.strict_contentdom = strict_contentdom
+        self.language = language              # QueryModifier.language
+        self.sitehash = sitehash              # QueryModifier.sitehash
+        self.alt_sitehash = alt_sitehash      # acceptableAlternativeSitehash (:716-718)
+        self.siteexcludes = set(siteexcludes)
+        self.urlhashes = set(urlhashes)       # SearchEvent.urlhashes (doublecheck)
+        self.skip_double_dom = skip_double_dom
+        self.flagcount = [0] * 32             # SearchEvent.flagcount
+
+    def test_flags(self, flags: Bitfield) -> bool:  # SearchEvent.testFlags :2459-2474
+        if self.constraint is None:
+            return True
+        if self.all_of_constraint:
+            for i in range(32):
+                if self.constraint.get(i) and not flags.get(i):
+                    return False
+            return True
+        for i in range(32):
+            if self.constraint.get(i) and flags.get(i):
+                return True
+        return False
+
+    def admit(self, e: "Vars") -> bool:
+        """addRWIs pollloop body up to rwiStack.put (:736-806); True = put on the stack."""
+        if e.urlHash in self.urlhashes:       # doublecheck (:736-740)
+            return False
+        flags = e.flags
+        for j in range(32):                   # flag counts (:743-746)
+            if flags.get(j):
+                self.flagcount[j] += 1
+        if not self.test_flags(flags):        # (:749-752)
+            return False
+        if self.contentdom > 0:               # (:755-775), Tokenizer flags :51-56, Response.DT_*
+            t = chr(e.type)
+            if self.strict_contentdom:
+                bad = ((self.contentdom == 2 and t != "a") or (self.contentdom == 3 and t != "m") or
+                       (self.contentdom == 1 and t != "i") or (self.contentdom == 4 and not flags.get(23)))
+            else:
+                bad = ((self.contentdom == 2 and not flags.get(21)) or (self.contentdom == 3 and not flags.get(22)) or
+                       (self.contentdom == 1 and not flags.get(20)) or (self.contentdom == 4 and not flags.get(23)))
+            if bad:
+                return False
+        if self.language:                      # (:778-784): modifier.language.equals(getLanguageString())
+            lang = e.language.decode("latin-1") if e.language is not None else None
+            if self.language != lang:
+                return False
+        h = e.hosthash()                       # (:790-802)
+        if self.sitehash is None:
+            if h in self.siteexcludes:
+                return False
+        elif h != self.sitehash and (self.alt_sitehash is None or h != self.alt_sitehash):
+            return False
+        self.urlhashes.add(e.urlHash)          # urlhashes.putUnique (:805)
+        return True
+
+
+def pull_double_dom(items: List[Tuple[bytes, int]], n: int) -> List[Tuple[bytes, int]]:
+    """pullOneRWI(skipDoubleDom = true) repeated n times over a settled rwiStack
+    (SearchEvent.java:1297-1394).  items: the stack, best first.  Each round polls
+    at most 10 stack entries; the first whose host has no doubleDomCache entry is
+    returned (and creates one), the others go to their host's queue.  If none was
+    returned, the best head of the host queues is returned and a host whose queue
+    becomes empty leaves the cache.  The reference picks that head by weight over
+    a ConcurrentHashMap walk; equal weights are resolved here by stack position
+    (the earliest queued entry), which is the best head under the stack order."""
+    out: List[Tuple[bytes, int]] = []
+    cache: Dict[bytes, List[int]] = {}  # host -> queued stack positions
+    queued: List[int] = []              # all queued positions, in push order (= stack order)
+    i = 0
+    while len(out) < n:
+        c = 0
+        got = None
+        while i < len(items) and c < 10:
+            pos = i
+            i += 1
+            c += 1
+            h = items[pos][0][6:12]
+            if h not in cache:
+                cache[h] = []
+                got = pos
+                break
+            cache[h].append(pos)
+            queued.append(pos)
+        if got is not None:
+            out.append(items[got])
+            continue
+        if not cache or not queued:
+            break
+        pos = queued.pop(0)
+        h = items[pos][0][6:12]
+        cache[h].remove(pos)
+        if not cache[h]:
+            del cache[h]
+        out.append(items[pos])
+    return out
+
+
 def rank(container: List[bytes], profile: RankingProfile, language: str, now_ms: int,
-         maxsize: int = MAX_RESULTS_RWI) -> List[Tuple[bytes, int]]:
-    """normalizeWith + addRWIs poll loop (SearchEvent.java:697-816), default
-    query (no doublecheck hits, no constraint/contentdom/language/site filter)."""
+         maxsize: int = MAX_RESULTS_RWI, filt: Optional[QueryFilter] = None) -> List[Tuple[bytes, int]]:
+    """normalizeWith + addRWIs poll loop (SearchEvent.java:697-816).  Without
+    `filt` the query is unconstrained (no doublecheck hits, no constraint /
+    contentdom / language / site filter).  Normalisation covers the whole
+    container; the filters only decide what enters the stack."""
     if not container:
         return []
     order = ReferenceOrder(profile, language)
     entries = order.normalize_with(container, now_ms)
     q = ReverseQueue(maxsize)
     for e in entries:
+        if filt is not None and not filt.admit(e):
+            continue
         q.put(order.cardinal(e), e.urlHash)
     return [(h, w) for (w, _, h) in q.items]
 
 
 def search(index: Dict[bytes, List[bytes]], include: Iterable[bytes], exclude: Iterable[bytes],
            profile: RankingProfile, language: str = "en", max_distance: int = 2147483647,
-           now_ms: int = 0, k: int = 100) -> List[Tuple[bytes, int]]:
-    """End-to-end canonical RWI query: TermSearch -> normalise -> cardinal -> top-k."""
+           now_ms: int = 0, k: int = 100, filt: Optional[QueryFilter] = None) -> List[Tuple[bytes, int]]:
+    """End-to-end canonical RWI query: TermSearch -> normalise -> cardinal -> top-k
+    (with `filt`: addRWIs constraints, and the doubledom pull order if requested)."""
     c = term_search(index, include, exclude, max_distance, now_ms)
-    return rank(c, profile, language, now_ms)[:k]
+    stack = rank(c, profile, language, now_ms, filt=filt)
+    if filt is not None and filt.skip_double_dom:
+        return pull_double_dom(stack, k)
+    return stack[:k]

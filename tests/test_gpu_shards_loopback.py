@@ -1,0 +1,111 @@
+"""Sharded libyrwi path on ONE GPU through the in-process loopback transport.
+
+RCCL refuses two ranks on one device (tests/test_gpu_multirank.py skips on a
+one-GPU box), so these tests open `world` shard contexts in one process, each
+driven by its own thread, joined by a loopback group id (yrwi_coll.cpp).  Every
+step of the sharded path runs as in production -- vertical-DHT url-hash shards,
+ShardSum all-gather + ordered combine, the authority host-count owner exchange,
+flag-count all-reduce, the cross-shard top-k merge and the doubledom pull -- only
+the transport is a device-to-device copy instead of RCCL.  Results must be
+bit-exact against the single-container oracle."""
+
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import java_literal as jl
+import oracle as orc
+from yacy_search_server_amd import Query, QueryFilter, RankingProfile, RWIIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+NOW = 20741 * 86400000 + 31337
+
+
+def _loop_id():
+    return b"YRWI-LOOPBACK\0" + os.urandom(114)
+
+
+def _run_shards(full, world, make_batch):
+    """Open `world` shards of `full` on GPU 0, run make_batch(part) on each from its
+    own thread; returns per-rank (batch, results)."""
+    uid = _loop_id()
+    parts = [synth.build_index(full.shard(r, world)) for r in range(world)]
+    ixs = [None] * world
+    out = [None] * world
+    errs = []
+
+    def opener(r):
+        try:
+            ixs[r] = RWIIndex(0, shard=(r, world, uid))
+            p = parts[r]
+            for t in range(full.n_terms):
+                if p.sizes[t]:
+                    ixs[r].add(p.hashes[t], p.list_rows(t))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    def runner(r):
+        try:
+            batch = make_batch(parts[r])
+            out[r] = (batch, ixs[r].search_batch(batch))
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+
+    for fn in (opener, runner):
+        ths = [threading.Thread(target=fn, args=(r,)) for r in range(world)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=300)
+        assert not errs, errs
+    for ix in ixs:
+        ix.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_shards_bit_exact(world):
+    full = synth.preset("small")
+    qs = synth.queries(full, 24, 1, 4, 1, qseed=41)
+    c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")  # authority -> host-count exchange
+
+    def make_batch(part):
+        return [Query([part.hashes[t] for t in inc], [part.hashes[t] for t in exc], now_ms=NOW, k=100,
+                      profile=(c5 if i % 2 else None)) for i, (inc, exc) in enumerate(qs)]
+
+    res = _run_shards(full, world, make_batch)
+    whole = synth.build_index(full).as_dict()
+    for r, (batch, got) in enumerate(res):
+        for qi, (q, g) in enumerate(zip(batch, got)):
+            prof = orc.profile_from(q.profile) if q.profile is not None else None
+            exp = orc.search(whole, q.include, q.exclude, profile=prof, now_ms=NOW, k=100)
+            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, (r, qi)
+
+
+def test_loopback_shards_filters_and_doubledom():
+    world = 2
+    full = synth.preset("tiny")
+    idx = synth.build_index(full)
+    big = [int(t) for t in np.argsort(-idx.sizes)[:3]]
+    rng = np.random.default_rng(5)
+    hosts = sorted({bytes(r[6:12]) for r in idx.rows[rng.integers(0, len(idx.rows), 100)]})
+    kws = [dict(constraint=b"\0\0\x10\x01"), dict(language="de"), dict(siteexcludes=hosts[:30]),
+           dict(skip_double_dom=True), dict(skip_double_dom=True, contentdom=1)]
+    queries = [([big[0]], []), ([big[1]], [big[2]]), ([big[0], big[2]], [])]
+    cases = [(inc, exc, kw, k) for (inc, exc) in queries for kw in kws for k in (10, 100)]
+
+    def make_batch(part):  # every rank gets its own filter objects (flag counts come back per rank)
+        return [Query([part.hashes[t] for t in inc], [part.hashes[t] for t in exc], now_ms=NOW, k=k,
+                      filter=QueryFilter(**kw)) for (inc, exc, kw, k) in cases]
+
+    res = _run_shards(full, world, make_batch)
+    lit = {h: [bytes(x) for x in rows] for h, rows in idx.as_dict().items()}
+    for r, (batch, got) in enumerate(res):
+        for (inc, exc, kw, k), q, g in zip(cases, batch, got):
+            lf = jl.QueryFilter(**kw)
+            e = jl.search(lit, q.include, q.exclude, jl.RankingProfile(), "en", now_ms=NOW, k=k, filt=lf)
+            assert [(h.urlhash, h.score) for h in g] == e, (r, kw, k)
+            assert q.filter.flagcount == lf.flagcount, (r, kw, k)

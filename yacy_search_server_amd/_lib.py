@@ -37,12 +37,23 @@ class CHit(ctypes.Structure):
     _fields_ = [("urlhash", ctypes.c_uint8 * 12), ("tiebreak", ctypes.c_int32), ("score", ctypes.c_int64)]
 
 
+class CFilter(ctypes.Structure):
+    _fields_ = [("constraint", ctypes.c_uint8 * 4), ("has_constraint", ctypes.c_int32),
+                ("all_of_constraint", ctypes.c_int32), ("contentdom", ctypes.c_int32),
+                ("strict_contentdom", ctypes.c_int32), ("language", ctypes.c_char * 8),
+                ("sitehash", ctypes.c_uint8 * 6), ("alt_sitehash", ctypes.c_uint8 * 6),
+                ("has_sitehash", ctypes.c_int32), ("has_alt_sitehash", ctypes.c_int32),
+                ("siteexcludes", ctypes.c_void_p), ("nsiteexcludes", ctypes.c_int32),
+                ("urlhashes", ctypes.c_void_p), ("nurlhashes", ctypes.c_int32),
+                ("skip_double_dom", ctypes.c_int32), ("flagcount", ctypes.POINTER(ctypes.c_int32))]
+
+
 class CQuery(ctypes.Structure):
     _fields_ = [("incl", ctypes.c_void_p), ("nincl", ctypes.c_int32),
                 ("excl", ctypes.c_void_p), ("nexcl", ctypes.c_int32),
                 ("max_distance", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("profile", ctypes.POINTER(CProfile)), ("language", ctypes.c_char * 8),
-                ("now_ms", ctypes.c_int64)]
+                ("now_ms", ctypes.c_int64), ("filter", ctypes.POINTER(CFilter))]
 
 
 class CStats(ctypes.Structure):

@@ -141,6 +141,9 @@ static void close_lanes(yrwi_ctx* ctx) {
   }
   if (!ctx->lanes.empty() && ctx->lanes[0]->comm) ncclCommDestroy(ctx->lanes[0]->comm);
   for (Lane* L : ctx->lanes) {
+    if (L->loop) loop_leave(L->loop);
+    for (auto e : L->coll_ev)
+      if (e) hipEventDestroy(e);
     L->arena.release();
     for (auto e : L->evpool) hipEventDestroy(e);
     if (L->stage.p) hipHostFree(L->stage.p);
@@ -193,7 +196,22 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
   int rc = open_common(device, rank, world, out);
   if (rc) return rc;
   yrwi_ctx* ctx = *out;
-  if (world > 1) {
+  if (world > 1 && std::memcmp(nccl_id, LOOP_TAG, sizeof(LOOP_TAG)) == 0) {
+    // in-process loopback group (tests: several shards on one GPU), one per lane
+    bool ok = true;
+    for (size_t l = 0; ok && l < ctx->lanes.size(); l++) {
+      uint8_t id[128];
+      std::memcpy(id, nccl_id, 128);
+      id[127] ^= (uint8_t)l;
+      ctx->lanes[l]->loop = loop_join(id, world, rank);
+      ok = ctx->lanes[l]->loop != nullptr;
+    }
+    if (!ok) {
+      yrwi_close(ctx);
+      *out = nullptr;
+      return YRWI_E_ARG;
+    }
+  } else if (world > 1) {
     ncclUniqueId u;
     std::memcpy(&u, nccl_id, 128);
     ncclComm_t c0 = nullptr;
@@ -313,6 +331,12 @@ static int plan_query(const yrwi_ctx* ix, Lane* ctx, const yrwi_query_desc& d, P
   }
   if (d.nincl < 0 || d.nexcl < 0 || d.nincl > YRWI_MAX_TERMS || d.nexcl > YRWI_MAX_TERMS)
     return ctx->fail(YRWI_E_ARG, "too many terms");
+  P->filter = d.filter;
+  if (const yrwi_filter* F = d.filter) {
+    if (F->nsiteexcludes < 0 || F->nurlhashes < 0 || (F->nsiteexcludes > 0 && !F->siteexcludes) ||
+        (F->nurlhashes > 0 && !F->urlhashes))
+      return ctx->fail(YRWI_E_ARG, "filter: bad siteexcludes / urlhashes");
+  }
   // HandleSet: sorted (Base64Order) set of term hashes
   KeyT inc[YRWI_MAX_TERMS], exc[YRWI_MAX_TERMS];
   int ninc = 0, nexc = 0;
@@ -540,8 +564,7 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   HIPCHK(ctx, hipMemsetAsync(d_gmax, 0, nq * 4, ctx->stream));
   if (upload(ctx, d_sb, slot_base)) return YRWI_E_HIP;
   if (launch_host_count(d_hkeys, nslots, W, d_ocnt, ctx->stream)) return ctx->fail(YRWI_E_HIP, "host count");
-  if (ncclAllGather(d_ocnt, d_M, W, ncclUint32, ctx->comm, ctx->stream) != ncclSuccess)
-    return ctx->fail(YRWI_E_RCCL, "allgather of host message counts");
+  if (int rc = coll_allgather(ctx, d_ocnt, d_M, (size_t)W * 4)) return rc;
   std::vector<uint32_t> M((size_t)W * W);
   HIPCHK(ctx, hipMemcpyAsync(M.data(), d_M, M.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, lane_sync(ctx));
@@ -571,33 +594,59 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   HIPCHK(ctx, hipMemsetAsync(d_ovals, 0, ocap * 4, ctx->stream));
   if (launch_host_pack(d_hkeys, d_hcnt, d_sb, nq, nslots, W, d_cur, d_send, d_sslot, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "host pack");
-  if (ncclGroupStart() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group");
-  for (int p = 0; p < W; p++) {
-    size_t sn = (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * sizeof(HostMsg);
-    size_t rn = (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * sizeof(HostMsg);
-    if (sn && ncclSend(d_send + soff[(size_t)p], sn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
-      return ctx->fail(YRWI_E_RCCL, "send host messages");
-    if (rn && ncclRecv(d_recv + roff[(size_t)p], rn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
-      return ctx->fail(YRWI_E_RCCL, "recv host messages");
+  {
+    std::vector<Xfer> snd, rcv;
+    for (int p = 0; p < W; p++) {
+      snd.push_back({p, d_send + soff[(size_t)p], (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * sizeof(HostMsg)});
+      rcv.push_back({p, d_recv + roff[(size_t)p], (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * sizeof(HostMsg)});
+    }
+    if (int rc = coll_exchange(ctx, snd, rcv)) return rc;
   }
-  if (ncclGroupEnd() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group end");
   if (launch_host_owner(d_recv, nrecv, d_okeys, d_ovals, ocap - 1, d_gmax, d_reply, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "host owner");
-  if (ncclAllReduce(d_gmax, d_gmax, nq, ncclInt32, ncclMax, ctx->comm, ctx->stream) != ncclSuccess)
-    return ctx->fail(YRWI_E_RCCL, "allreduce max host count");
-  if (ncclGroupStart() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group");
-  for (int p = 0; p < W; p++) {
-    size_t rn = (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * 4;  // replies to what p sent me
-    size_t sn = (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * 4;  // totals for what I sent p
-    if (rn && ncclSend(d_reply + roff[(size_t)p], rn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
-      return ctx->fail(YRWI_E_RCCL, "send host totals");
-    if (sn && ncclRecv(d_back + soff[(size_t)p], sn, ncclChar, p, ctx->comm, ctx->stream) != ncclSuccess)
-      return ctx->fail(YRWI_E_RCCL, "recv host totals");
+  if (int rc = coll_allreduce_i32(ctx, d_gmax, (size_t)nq, true)) return rc;
+  {
+    std::vector<Xfer> snd, rcv;  // replies to what p sent me; totals for what I sent p
+    for (int p = 0; p < W; p++) {
+      snd.push_back({p, d_reply + roff[(size_t)p], (size_t)(roff[(size_t)p + 1] - roff[(size_t)p]) * 4});
+      rcv.push_back({p, d_back + soff[(size_t)p], (size_t)(soff[(size_t)p + 1] - soff[(size_t)p]) * 4});
+    }
+    if (int rc = coll_exchange(ctx, snd, rcv)) return rc;
   }
-  if (ncclGroupEnd() != ncclSuccess) return ctx->fail(YRWI_E_RCCL, "group end");
   if (launch_host_apply(d_back, d_sslot, nsend, d_hcnt, d_ss, d_gmax, nq, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "host apply");
   return 0;
+}
+
+// pullOneRWI(skipDoubleDom) over a merged stack (SearchEvent.java:1297-1394), as
+// k_doubledom does on one GPU: the sharded path merges the shard stacks here.
+static int32_t pull_double_dom(const yrwi_hit* st, int32_t n, int32_t want, yrwi_hit* out) {
+  auto host = [&](int32_t i) {
+    uint64_t h = 0;
+    for (int j = 6; j < 12; j++) h = (h << 6) | (uint64_t)(AHP[st[i].urlhash[j]] & 63);
+    return h;
+  };
+  std::unordered_map<uint64_t, int32_t> queued;  // host in doubleDomCache -> queued entries
+  std::vector<int32_t> fifo;
+  size_t qh = 0;
+  int32_t i = 0, m = 0;
+  while (m < want) {
+    int32_t got = -1;
+    for (int c = 0; i < n && c < 10; c++) {
+      const int32_t pos = i++;
+      auto it = queued.find(host(pos));
+      if (it == queued.end()) { queued[host(pos)] = 0; got = pos; break; }
+      it->second++;
+      fifo.push_back(pos);
+    }
+    if (got >= 0) { out[m++] = st[got]; continue; }
+    if (qh == fifo.size()) break;
+    const int32_t pos = fifo[qh++];
+    auto it = queued.find(host(pos));
+    if (--it->second == 0) queued.erase(it);
+    out[m++] = st[pos];
+  }
+  return m;
 }
 
 // Normalise (+ cross-shard exchange), then either score+top-k (hits) or all scores.
@@ -628,6 +677,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.k = P.k;
     R.want_authority = P.prof.coeff_authority > 12 && R.n > 0;
     R.idx_tag = W > 1 ? (uint32_t)ctx->rank << 28 : 0u;
+    R.doubledom = P.filter && P.filter->skip_double_dom ? 1 : 0;
+    R.kout = P.k;
+    if (R.doubledom) R.k = YRWI_MAX_K;  // pullOneRWI draws from the whole rwiStack (max_results_rwi)
     // identical on every rank (same queries): decides the collective host-count exchange
     if (P.prof.coeff_authority > 12) any_auth = true;
     if (R.want_authority) {
@@ -661,6 +713,101 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       R.hcnt = d_hcnt + slot_base[(size_t)qi];
     }
   }
+  // addRWIs constraints: one FilterQ per filtered query, key arrays and flag counters
+  std::vector<int> fidx((size_t)nq, -1);
+  int nf = 0;
+  bool any_dd = false, any_flagcount = false;
+  for (int qi = 0; qi < nq; qi++) {
+    if (plans[(size_t)qi].filter) fidx[(size_t)qi] = nf++;
+    if (rq[(size_t)qi].doubledom) any_dd = true;
+    if (plans[(size_t)qi].filter && plans[(size_t)qi].filter->flagcount) any_flagcount = true;
+  }
+  int32_t* d_flag = nullptr;
+  if (nf > 0) {
+    std::vector<FilterQ> fq((size_t)nf);
+    std::vector<uint64_t> sx, uh;
+    std::vector<uint8_t> ul;
+    std::vector<int64_t> sx0((size_t)nf), uh0((size_t)nf);
+    for (int qi = 0; qi < nq; qi++) {
+      if (fidx[(size_t)qi] < 0) continue;
+      const yrwi_filter& F = *plans[(size_t)qi].filter;
+      FilterQ& G = fq[(size_t)fidx[(size_t)qi]];
+      std::memset(&G, 0, sizeof(G));
+      std::memcpy(G.constraint, F.constraint, 4);
+      G.has_constraint = F.has_constraint != 0;
+      G.all_of = F.all_of_constraint != 0;
+      G.contentdom = F.contentdom;
+      G.strict = F.strict_contentdom != 0;
+      const size_t ll = strnlen(F.language, sizeof(F.language));
+      G.lang_len = (int32_t)ll;
+      std::memcpy(G.lang, F.language, ll);
+      auto host_key = [](const uint8_t* h, uint64_t* k) {
+        uint64_t x = 0;
+        for (int j = 0; j < 6; j++) {
+          if (AHP[h[j]] < 0) return false;
+          x = (x << 6) | (uint64_t)AHP[h[j]];
+        }
+        *k = x;
+        return true;
+      };
+      // a host hash outside the alphabet matches no row (rows are validated)
+      G.has_site = F.has_sitehash != 0;
+      G.has_alt = F.has_alt_sitehash != 0 && host_key(F.alt_sitehash, &G.altsite);
+      if (G.has_site && !host_key(F.sitehash, &G.site)) G.site = ~0ull;
+      sx0[(size_t)fidx[(size_t)qi]] = (int64_t)sx.size();
+      std::vector<uint64_t> v;
+      for (int i = 0; i < F.nsiteexcludes; i++) {
+        uint64_t k;
+        if (host_key(F.siteexcludes + 6 * i, &k)) v.push_back(k);
+      }
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      G.nsiteex = (int64_t)v.size();
+      sx.insert(sx.end(), v.begin(), v.end());
+      uh0[(size_t)fidx[(size_t)qi]] = (int64_t)uh.size();
+      std::vector<KeyT> u;
+      for (int i = 0; i < F.nurlhashes; i++) {
+        KeyT k;
+        if (key_of(F.urlhashes + 12 * i, &k)) u.push_back(k);
+      }
+      std::sort(u.begin(), u.end());
+      u.erase(std::unique(u.begin(), u.end()), u.end());
+      G.nurl = (int64_t)u.size();
+      for (auto& k : u) { uh.push_back(k.hi); ul.push_back((uint8_t)k.lo); }
+    }
+    FilterQ* d_fq = arena_alloc<FilterQ>(ctx, nf);
+    uint64_t* d_sx = arena_alloc<uint64_t>(ctx, (int64_t)sx.size());
+    uint64_t* d_uh = arena_alloc<uint64_t>(ctx, (int64_t)uh.size());
+    uint8_t* d_ul = arena_alloc<uint8_t>(ctx, (int64_t)ul.size());
+    d_flag = any_flagcount ? arena_alloc<int32_t>(ctx, (int64_t)nf * 32) : nullptr;
+    if (!d_fq || !d_sx || !d_uh || !d_ul || (any_flagcount && !d_flag)) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (d_flag) HIPCHK(ctx, hipMemsetAsync(d_flag, 0, (size_t)nf * 32 * 4, ctx->stream));
+    for (int qi = 0; qi < nq; qi++) {
+      const int f = fidx[(size_t)qi];
+      if (f < 0) continue;
+      FilterQ& G = fq[(size_t)f];
+      G.siteex = d_sx + sx0[(size_t)f];
+      G.url_hi = d_uh + uh0[(size_t)f];
+      G.url_lo = d_ul + uh0[(size_t)f];
+      G.flagcount = plans[(size_t)qi].filter->flagcount ? d_flag + (int64_t)f * 32 : nullptr;
+      rq[(size_t)qi].filt = d_fq + f;
+    }
+    if (upload(ctx, d_fq, fq) || upload(ctx, d_sx, sx) || upload(ctx, d_uh, uh) || upload(ctx, d_ul, ul))
+      return YRWI_E_HIP;
+  }
+  // flag counters back to the callers' filters (summed over the shards)
+  auto flagcounts_out = [&]() -> int {
+    if (!d_flag) return 0;
+    if (W > 1)
+      if (int rc = coll_allreduce_i32(ctx, d_flag, (size_t)nf * 32, false)) return rc;
+    std::vector<int32_t> h((size_t)nf * 32);
+    HIPCHK(ctx, hipMemcpyAsync(h.data(), d_flag, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, lane_sync(ctx));
+    for (int qi = 0; qi < nq; qi++)
+      if (fidx[(size_t)qi] >= 0 && plans[(size_t)qi].filter->flagcount)
+        std::memcpy(plans[(size_t)qi].filter->flagcount, &h[(size_t)fidx[(size_t)qi] * 32], 32 * 4);
+    return 0;
+  };
   RankQ* d_q = arena_alloc<RankQ>(ctx, nq);
   int64_t* d_cb = arena_alloc<int64_t>(ctx, nq);
   ChunkSum* d_cs = arena_alloc<ChunkSum>(ctx, chunks);
@@ -681,8 +828,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     if (rc2) return rc2;
   }
   if (W > 1) {
-    if (ncclAllGather(d_ss, d_all, sizeof(ShardSum) * nq, ncclChar, ctx->comm, ctx->stream) != ncclSuccess)
-      return ctx->fail(YRWI_E_RCCL, "allgather of shard summaries");
+    if (int rc = coll_allgather(ctx, d_ss, d_all, sizeof(ShardSum) * nq)) return rc;
   }
   if (launch_combine(d_q, nq, d_all, W, d_norm, ctx->stream)) return ctx->fail(YRWI_E_HIP, "combine launch");
   if (tm) { tm->tn = ctx->event(); hipEventRecord(tm->tn, ctx->stream); }
@@ -765,9 +911,11 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   }
   const Cand** d_fptr = arena_alloc<const Cand*>(ctx, nq);
   const int32_t** d_fcnt = arena_alloc<const int32_t*>(ctx, nq);
-  // one GPU: k_emit writes the results straight into pinned host memory -- the
-  // caller's buffer when it came from yrwi_host_alloc, else this lane's landing
-  // buffer (then copied out per query)
+  // one GPU: k_emit / k_doubledom write the results straight into pinned host
+  // memory -- the caller's buffer when it came from yrwi_host_alloc, else this
+  // lane's landing buffer (then copied out per query).  Sharded: every shard's
+  // list (the whole stack for doubledom queries) is gathered and merged.
+  const int32_t kint = (W > 1 && any_dd) ? std::max<int32_t>(kmax, YRWI_MAX_K) : kmax;
   const size_t hb = sizeof(yrwi_hit) * (size_t)nq * kmax, hb_al = (hb + 255) & ~(size_t)255;
   const size_t nb = sizeof(int32_t) * (size_t)nq;
   yrwi_hit* d_hits = nullptr;
@@ -787,12 +935,15 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hits), hp, 0));
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));
   } else {
-    d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);
+    d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
     d_nout = arena_alloc<int32_t>(ctx, nq);
   }
   if (!d_fptr || !d_fcnt || !d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
-  if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, ctx->stream)) return ctx->fail(YRWI_E_HIP, "emit launch");
+  if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_hits, d_nout, W > 1 ? 1 : 0, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "emit launch");
+  if (W == 1 && any_dd && launch_doubledom(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "doubledom launch");
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
   if (W == 1) {
     HIPCHK(ctx, lane_sync(ctx));
@@ -802,30 +953,28 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
         std::memcpy(h_hits + (size_t)qi * kmax, land + sizeof(yrwi_hit) * (size_t)qi * kmax,
                     sizeof(yrwi_hit) * (size_t)std::max(0, std::min(h_nout[qi], kmax)));
     }
-    return 0;
+    return flagcounts_out();
   }
-  // ---- multi-GPU: gather every shard's top-k, merge in shard (= url hash) order
-  yrwi_hit* d_allh = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax * W);
+  // ---- multi-GPU: gather every shard's list, merge in shard (= url hash) order
+  yrwi_hit* d_allh = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint * W);
   int32_t* d_alln = arena_alloc<int32_t>(ctx, (int64_t)nq * W);
   if (!d_allh || !d_alln) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (ncclGroupStart() != ncclSuccess ||
-      ncclAllGather(d_hits, d_allh, sizeof(yrwi_hit) * nq * kmax, ncclChar, ctx->comm, ctx->stream) != ncclSuccess ||
-      ncclAllGather(d_nout, d_alln, sizeof(int32_t) * nq, ncclChar, ctx->comm, ctx->stream) != ncclSuccess ||
-      ncclGroupEnd() != ncclSuccess)
-    return ctx->fail(YRWI_E_RCCL, "allgather of top-k lists");
-  std::vector<yrwi_hit> allh((size_t)nq * kmax * W);
+  if (int rc = coll_allgather(ctx, d_hits, d_allh, sizeof(yrwi_hit) * nq * kint)) return rc;
+  if (int rc = coll_allgather(ctx, d_nout, d_alln, sizeof(int32_t) * nq)) return rc;
+  std::vector<yrwi_hit> allh((size_t)nq * kint * W);
   std::vector<int32_t> alln((size_t)nq * W);
   HIPCHK(ctx, hipMemcpyAsync(allh.data(), d_allh, allh.size() * sizeof(yrwi_hit), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(alln.data(), d_alln, alln.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   std::vector<NormState> nsh((size_t)nq);
   HIPCHK(ctx, hipMemcpyAsync(nsh.data(), d_norm, nq * sizeof(NormState), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, lane_sync(ctx));
+  std::vector<yrwi_hit> v, stack;
   for (int qi = 0; qi < nq; qi++) {
     if (nsh[(size_t)qi].D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
-    std::vector<yrwi_hit> v;
+    v.clear();
     for (int s = 0; s < W; s++) {
       int32_t n = alln[(size_t)s * nq + qi];
-      const yrwi_hit* src = &allh[((size_t)s * nq + qi) * kmax];
+      const yrwi_hit* src = &allh[((size_t)s * nq + qi) * kint];
       v.insert(v.end(), src, src + n);
     }
     // stable: among equal (score, hashCode) the lower shard (smaller url hash) stays first
@@ -833,18 +982,20 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       if (a.score != b.score) return a.score > b.score;
       return a.tiebreak > b.tiebreak;
     });
-    int32_t n = 0;
-    const int32_t kq = std::min(plans[(size_t)qi].k, kmax);
-    for (size_t i = 0; i < v.size() && n < kq; i++) {
-      if (n > 0 && v[i].score == h_hits[(size_t)qi * kmax + n - 1].score &&
-          v[i].tiebreak == h_hits[(size_t)qi * kmax + n - 1].tiebreak)
-        continue;
-      h_hits[(size_t)qi * kmax + n] = v[i];
-      n++;
+    const RankQ& R = rq[(size_t)qi];
+    const int32_t kq = std::min(R.k, kint);  // the merged stack (TreeSet dedupe)
+    stack.clear();
+    for (size_t i = 0; i < v.size() && (int32_t)stack.size() < kq; i++) {
+      if (!stack.empty() && v[i].score == stack.back().score && v[i].tiebreak == stack.back().tiebreak) continue;
+      stack.push_back(v[i]);
     }
-    h_nout[qi] = n;
+    yrwi_hit* dst = h_hits + (size_t)qi * kmax;
+    const int32_t want = std::min(R.kout, kmax);
+    h_nout[qi] = R.doubledom ? pull_double_dom(stack.data(), (int32_t)stack.size(), want, dst)
+                             : (int32_t)std::min<size_t>(stack.size(), (size_t)want);
+    if (!R.doubledom) std::copy(stack.begin(), stack.begin() + h_nout[qi], dst);
   }
-  return 0;
+  return flagcounts_out();
 }
 
 static int64_t now_ns() {

@@ -136,6 +136,7 @@ struct Plan {
   int32_t lang_ok = 0;
   int64_t now_ms = 0;
   int64_t postings_in = 0;
+  const yrwi_filter* filter = nullptr;  // addRWIs constraints (nullptr: none)
   // runtime container
   DList cont{nullptr, nullptr, nullptr, 0};
   uint8_t* removed = nullptr;
@@ -166,6 +167,8 @@ struct HostRegistry {
   }
 };
 
+struct LoopGroup;  // in-process shard group (yrwi_coll.cpp)
+
 // One execution lane: a HIP stream with its own scratch arena, pinned staging,
 // events and (sharded) communicator.  A batch is split over the lanes and each
 // lane runs its part from its own host thread, so one lane's host planning and
@@ -175,6 +178,8 @@ struct Lane {
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
+  LoopGroup* loop = nullptr;  // test transport instead of comm (yrwi_coll.cpp)
+  hipEvent_t coll_ev[2] = {nullptr, nullptr};
   Stage stage;
   Stage out_stage;           // pinned landing buffer for results
   int64_t probe_ratio = 16;  // YRWI_PROBE_RATIO, read once per call
@@ -336,6 +341,21 @@ inline int begin_pass(Lane* ctx) {
   ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
   return 0;
 }
+
+// ---- collectives between url-hash shards (yrwi_coll.cpp): RCCL over xGMI, or
+// the in-process loopback group that lets tests run several shards on one GPU.
+struct Xfer {
+  int peer;
+  void* ptr;
+  size_t bytes;
+};
+int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
+int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op);    // in place; sum or max
+int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs);  // grouped send/recv
+// loopback groups: a 128-byte id starting with this tag names an in-process group
+constexpr char LOOP_TAG[] = "YRWI-LOOPBACK";
+LoopGroup* loop_join(const uint8_t id[128], int world, int rank);
+void loop_leave(LoopGroup* g);
 
 }  // namespace yrwi
 

@@ -128,6 +128,23 @@ enum : int {
   F_POSINPHRASE, F_POSOFPHRASE, F_URLLENGTH, F_URLCOMPS, F_WORDSINTITLE
 };
 
+// Device copy of a query's yrwi_filter (SearchEvent.addRWIs constraints).
+struct FilterQ {
+  uint8_t constraint[4];
+  int32_t has_constraint, all_of;
+  int32_t contentdom, strict;
+  uint8_t lang[8];
+  int32_t lang_len;          // 0: any language
+  int32_t has_site, has_alt;
+  uint64_t site, altsite;    // 36-bit host keys (alphabet index per char of url-hash chars 6..11)
+  const uint64_t* siteex;    // sorted host keys
+  int64_t nsiteex;
+  const uint64_t* url_hi;    // sorted url keys of the doublecheck set
+  const uint8_t* url_lo;
+  int64_t nurl;
+  int32_t* flagcount;        // 32 device counters or nullptr
+};
+
 struct RankQ {
   const uint8_t* rows;     // container rows (sorted by url hash)
   const uint8_t* removed;  // exclusion marks or nullptr
@@ -144,7 +161,10 @@ struct RankQ {
   uint32_t* hcnt;
   uint64_t hmask;
   uint32_t idx_tag;        // shard << 28, OR-ed into candidate indices
-  int32_t pad;
+  int32_t kout;            // results wanted (k is the stack bound: 3000 with doubledom)
+  const FilterQ* filt;     // addRWIs constraints or nullptr
+  int32_t doubledom;       // results in pullOneRWI(skipDoubleDom) order
+  int32_t pad2;
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -191,8 +211,15 @@ int topq_capacity(int32_t keff);
 // in_stride, counts d_in_cnt), k = gk[g]; output list g at d_out + g*keff, count d_out_cnt[g]
 int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
                 const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* stream);
+// stack_mode: doubledom queries emit their whole stack (sharded merge) instead of
+// leaving them to launch_doubledom
 int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int stack_mode, void* stream);
+// out[i] = sum or max over r of all[r * n + i] (loopback allreduce)
+int launch_reduce_i32(const int32_t* all, int world, int64_t n, int32_t* out, int max_op, void* stream);
+// pullOneRWI(skipDoubleDom) order of the final stacks of the doubledom queries
+int launch_doubledom(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
+                     int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
 int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* stream);
 

@@ -1376,6 +1376,72 @@ __device__ __forceinline__ void radix_pick(const int32_t* sHist, int32_t rem, in
 // chunk's keys differ, LDS histograms); only keys >= T -- a prefix of the sorted
 // chunk -- are sorted.  If the TreeSet dedupe leaves fewer than kq classes in
 // that prefix, the whole chunk is sorted instead (exact either way).
+// ------------------------------------------------ addRWIs constraints (filter)
+// SearchEvent.addRWIs pollloop (SearchEvent.java:736-806) for one posting:
+// doublecheck, flag counts, testFlags (:2459-2474), contentdom (Tokenizer flags
+// :51-56, Response.DT_*), modifier.language, sitehash / siteexcludes.
+__device__ __forceinline__ bool sorted_has_u64(const uint64_t* __restrict__ a, int64_t n, uint64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && a[lo] == x;
+}
+
+__device__ __forceinline__ bool flag_bit(const Row& r, int j) { return (r.b(O_Z + (j >> 3)) >> (j & 7)) & 1u; }
+
+// returns true if the posting enters the stack; counts flags into sFlag (LDS) when asked
+__device__ __forceinline__ bool admit(const FilterQ& F, const Row& r, int32_t* sFlag) {
+  if (F.nurl) {  // doublecheck: url already in SearchEvent.urlhashes
+    uint64_t hi;
+    uint32_t lo;
+    row_key(r, hi, lo);
+    int64_t a = 0, b = F.nurl;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      const uint64_t mh = F.url_hi[m];
+      if (mh < hi || (mh == hi && (uint32_t)F.url_lo[m] < lo)) a = m + 1; else b = m;
+    }
+    if (a < F.nurl && F.url_hi[a] == hi && (uint32_t)F.url_lo[a] == lo) return false;
+  }
+  if (sFlag) {
+    const uint32_t z = (r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24));
+    for (uint32_t m = z; m; m &= m - 1) atomicAdd(&sFlag[__ffs(m) - 1], 1);
+  }
+  if (F.has_constraint) {
+    bool ok = F.all_of ? true : false;
+    for (int j = 0; j < 32; j++) {
+      const bool c = (F.constraint[j >> 3] >> (j & 7)) & 1u;
+      if (!c) continue;
+      if (F.all_of) { if (!flag_bit(r, j)) { ok = false; break; } }
+      else if (flag_bit(r, j)) { ok = true; break; }
+    }
+    if (!ok) return false;
+  }
+  if (F.contentdom > 0) {
+    const uint32_t t = r.b(O_D);
+    bool bad;
+    if (F.strict)
+      bad = (F.contentdom == 2 && t != 'a') || (F.contentdom == 3 && t != 'm') || (F.contentdom == 1 && t != 'i') ||
+            (F.contentdom == 4 && !flag_bit(r, 23));
+    else
+      bad = (F.contentdom == 2 && !flag_bit(r, 21)) || (F.contentdom == 3 && !flag_bit(r, 22)) ||
+            (F.contentdom == 1 && !flag_bit(r, 20)) || (F.contentdom == 4 && !flag_bit(r, 23));
+    if (bad) return false;
+  }
+  if (F.lang_len > 0) {  // modifier.language.equals(getLanguageString()): a 2-char string
+    if (F.lang_len != 2 || r.b(O_L) != F.lang[0] || r.b(O_L + 1) != F.lang[1]) return false;
+  }
+  const uint64_t h = host36(r);
+  if (!F.has_site) {
+    if (F.nsiteex && sorted_has_u64(F.siteex, F.nsiteex, h)) return false;
+  } else if (h != F.site && (!F.has_alt || h != F.altsite)) {
+    return false;
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
                                                         const int32_t* __restrict__ chunk_q,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
@@ -1387,12 +1453,16 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ int32_t sSel[3];
   __shared__ uint64_t sRed[8];
   __shared__ NormState sN;
+  __shared__ int32_t sFlag[32];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   if (tid == 0) sN = norm[qi];
+  if (tid < 32) sFlag[tid] = 0;
   __syncthreads();
+  const FilterQ* F = Q.filt;
+  int32_t* flagc = (F && F->flagcount) ? sFlag : nullptr;
   const int64_t c = b - Q.chunk_base;
   // strided element map (neighbouring lanes read neighbouring rows); order is
   // irrelevant here, the candidate key carries the container index
@@ -1407,6 +1477,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     z[s] = 0;
     if (e < Q.n && !(Q.removed && Q.removed[e])) {
       const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+      if (F && !admit(*F, r, flagc)) continue;
       const Feat t = decode(r);
       const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
       const int64_t score = cardinal(r, t, sN, Q, hc);
@@ -1420,7 +1491,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   }
   const int32_t kq = Q.k < kc ? Q.k : kc;
   int32_t nv;
-  (void)block_excl_sum<CHUNK_THREADS>(nvl, sScan, &nv);
+  (void)block_excl_sum<CHUNK_THREADS>(nvl, sScan, &nv);  // (its barriers also order the sFlag atomics)
+  if (flagc && tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
   if (kq <= 0 || nv == 0) {
     if (tid == 0) cand_cnt[b] = 0;
     return;
@@ -1674,10 +1746,13 @@ __global__ __launch_bounds__(TOPQ_THREADS) void k_topq(const int64_t* __restrict
 
 __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* __restrict__ fin,
                        const int32_t* const* __restrict__ fin_cnt, int32_t kmax, yrwi_hit* __restrict__ hits,
-                       int32_t* __restrict__ nout) {
+                       int32_t* __restrict__ nout, int stack_mode) {
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
-  const int32_t n = min(*fin_cnt[qi], min(Q.k, kmax));
+  // doubledom queries: k_doubledom writes the pull order, or (stack_mode, sharded)
+  // the whole stack goes out for the cross-shard merge
+  if (Q.doubledom && !stack_mode) return;
+  const int32_t n = min(*fin_cnt[qi], min(Q.doubledom ? Q.k : Q.kout, kmax));
   const Cand* f = fin[qi];
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const Cand cd = f[i];
@@ -1690,6 +1765,82 @@ __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* 
     hits[(int64_t)qi * kmax + i] = h;
   }
   if (threadIdx.x == 0) nout[qi] = n;
+}
+
+// pullOneRWI(skipDoubleDom = true) repeated kout times over the settled stack
+// (SearchEvent.java:1297-1394).  Each round polls up to 10 stack entries; the
+// first one of a host without a doubleDomCache entry is returned (the host gets
+// an entry), the others are queued on their host.  A round that returns nothing
+// takes the best queued entry -- the earliest queued one, since the stack is in
+// rank order (equal weights: the earliest) -- and a host whose queue
+// runs empty leaves the cache.  The queues together are one FIFO in stack order.
+// One workgroup per query: hosts are interned in an LDS hash table in parallel,
+// then lane 0 replays the pull sequence on small LDS arrays.
+constexpr int DD_SLOTS = 8192;  // > 2 * YRWI_MAX_K
+
+__global__ __launch_bounds__(64) void k_doubledom(const RankQ* __restrict__ qs, const Cand* const* __restrict__ fin,
+                                                  const int32_t* const* __restrict__ fin_cnt, int32_t kmax,
+                                                  yrwi_hit* __restrict__ hits, int32_t* __restrict__ nout) {
+  __shared__ unsigned long long sKey[DD_SLOTS];
+  __shared__ uint16_t sCnt[DD_SLOTS];     // queued entries of the host
+  __shared__ uint8_t sSeen[DD_SLOTS];     // host has a doubleDomCache entry
+  __shared__ uint16_t sHost[YRWI_MAX_K];  // stack position -> host slot
+  __shared__ uint16_t sFifo[YRWI_MAX_K];
+  __shared__ uint16_t sOut[YRWI_MAX_K];
+  __shared__ int32_t sN;
+  const int qi = blockIdx.x;
+  const RankQ& Q = qs[qi];
+  if (!Q.doubledom) return;
+  const int32_t n = min(*fin_cnt[qi], (int32_t)YRWI_MAX_K);
+  const Cand* f = fin[qi];
+  for (int i = threadIdx.x; i < DD_SLOTS; i += 64) { sKey[i] = 0; sCnt[i] = 0; sSeen[i] = 0; }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const uint32_t idx = ~(uint32_t)f[i].k2 & 0x0FFFFFFFu;
+    const uint64_t key = host36(load_row(Q.rows + (int64_t)idx * YRWI_ROW_BYTES)) + 1;
+    uint32_t slot = (uint32_t)mix64(key) & (DD_SLOTS - 1);
+    while (true) {
+      const unsigned long long prev = atomicCAS(&sKey[slot], 0ull, (unsigned long long)key);
+      if (prev == 0ull || prev == key) break;
+      slot = (slot + 1) & (DD_SLOTS - 1);
+    }
+    sHost[i] = (uint16_t)slot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t want = min(Q.kout, kmax);
+    int32_t out = 0, i = 0, qh = 0, qt = 0;
+    while (out < want) {
+      int32_t got = -1;
+      for (int c = 0; i < n && c < 10; c++) {
+        const int32_t pos = i++;
+        const int h = sHost[pos];
+        if (!sSeen[h]) { sSeen[h] = 1; got = pos; break; }
+        sCnt[h]++;
+        sFifo[qt++] = (uint16_t)pos;
+      }
+      if (got >= 0) { sOut[out++] = (uint16_t)got; continue; }
+      if (qh == qt) break;
+      const int32_t pos = sFifo[qh++];
+      const int h = sHost[pos];
+      if (--sCnt[h] == 0) sSeen[h] = 0;
+      sOut[out++] = (uint16_t)pos;
+    }
+    sN = out;
+  }
+  __syncthreads();
+  const int32_t m = sN;
+  for (int o = threadIdx.x; o < m; o += 64) {
+    const Cand cd = f[sOut[o]];
+    const uint32_t idx = ~(uint32_t)cd.k2 & 0x0FFFFFFFu;
+    const uint8_t* r = Q.rows + (int64_t)idx * YRWI_ROW_BYTES;
+    yrwi_hit h;
+    for (int j = 0; j < 12; j++) h.urlhash[j] = r[j];
+    h.tiebreak = (int32_t)((uint32_t)(cd.k2 >> 32) ^ 0x80000000u);
+    h.score = (int64_t)(cd.k1 ^ 0x8000000000000000ull);
+    hits[(int64_t)qi * kmax + o] = h;
+  }
+  if (threadIdx.x == 0) nout[qi] = m;
 }
 
 // all scores of a container (yrwi_normalize_score)
@@ -1919,10 +2070,35 @@ int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk
   return rc(hipGetLastError());
 }
 
+__global__ void k_reduce_i32(const int32_t* __restrict__ all, int world, int64_t n, int32_t* __restrict__ out,
+                             int max_op) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t v = all[i];
+  for (int r = 1; r < world; r++) {
+    const int32_t x = all[(int64_t)r * n + i];
+    v = max_op ? (x > v ? x : v) : (int32_t)((uint32_t)v + (uint32_t)x);
+  }
+  out[i] = v;
+}
+
+int launch_reduce_i32(const int32_t* all, int world, int64_t n, int32_t* out, int max_op, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_reduce_i32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), all, world, n, out, max_op);
+  return rc(hipGetLastError());
+}
+
+int launch_doubledom(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
+                     int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
+  if (nq <= 0) return 0;
+  hipLaunchKernelGGL(k_doubledom, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_final, d_final_cnt, kmax, d_hits, d_nout);
+  return rc(hipGetLastError());
+}
+
 int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int stack_mode, void* st) {
   hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, kmax,
-                     d_hits, d_nout);
+                     d_hits, d_nout, stack_mode);
   return rc(hipGetLastError());
 }
 

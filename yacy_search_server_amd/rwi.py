@@ -26,7 +26,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import CHit, CProfile, CQuery, CStats, YrwiError
+from ._lib import CFilter, CHit, CProfile, CQuery, CStats, YrwiError
 
 INTEGER_MAX = 2147483647
 MAX_RESULTS_RWI = 3000  # SearchEvent.java:118
@@ -102,6 +102,47 @@ class Hit:
     tiebreak: int   # ByteArray.hashCode(urlhash)
 
 
+class QueryFilter:
+    """SearchEvent.addRWIs constraints (SearchEvent.java:736-806) and the doubledom
+    pull order (pullOneRWI, :1297-1394); see yrwi_filter in include/yrwi.h.
+    After a search, `flagcount` holds SearchEvent.flagcount (32 counters)."""
+
+    def __init__(self, constraint: Optional[bytes] = None, all_of_constraint: bool = False, contentdom: int = 0,
+                 strict_contentdom: bool = False, language: str = "", sitehash: Optional[bytes] = None,
+                 alt_sitehash: Optional[bytes] = None, siteexcludes: Sequence[bytes] = (),
+                 urlhashes: Sequence[bytes] = (), skip_double_dom: bool = False):
+        c = CFilter()
+        if constraint is not None:
+            c.constraint[:] = list(bytes(constraint)[:4].ljust(4, b"\0"))
+            c.has_constraint = 1
+        c.all_of_constraint = int(all_of_constraint)
+        c.contentdom = contentdom
+        c.strict_contentdom = int(strict_contentdom)
+        c.language = language.encode()[:7]
+        if sitehash is not None:
+            c.sitehash[:] = list(bytes(sitehash)[:6])
+            c.has_sitehash = 1
+        if alt_sitehash is not None:
+            c.alt_sitehash[:] = list(bytes(alt_sitehash)[:6])
+            c.has_alt_sitehash = 1
+        sx = b"".join(bytes(h) for h in siteexcludes)
+        uh = b"".join(bytes(h) for h in urlhashes)
+        self._sx = ctypes.create_string_buffer(sx, max(1, len(sx)))
+        self._uh = ctypes.create_string_buffer(uh, max(1, len(uh)))
+        c.siteexcludes = ctypes.cast(self._sx, ctypes.c_void_p)
+        c.nsiteexcludes = len(siteexcludes)
+        c.urlhashes = ctypes.cast(self._uh, ctypes.c_void_p)
+        c.nurlhashes = len(urlhashes)
+        c.skip_double_dom = int(skip_double_dom)
+        self._flags = (ctypes.c_int32 * 32)()
+        c.flagcount = ctypes.cast(self._flags, ctypes.POINTER(ctypes.c_int32))
+        self.c = c
+
+    @property
+    def flagcount(self) -> List[int]:
+        return list(self._flags)
+
+
 @dataclass
 class Query:
     include: Sequence[bytes]
@@ -111,6 +152,7 @@ class Query:
     profile: Optional[RankingProfile] = None
     language: str = "en"
     now_ms: int = 0
+    filter: Optional[QueryFilter] = None
 
 
 def _check(ctx, rc: int):
@@ -208,8 +250,8 @@ class RWIIndex:
     # ---- full query: TermSearch -> normalise -> cardinal -> top-k ----
     def search(self, include: Sequence[bytes], exclude: Sequence[bytes] = (), profile: Optional[RankingProfile] = None,
                language: str = "en", max_distance: int = INTEGER_MAX, now_ms: int = 0, k: int = 100,
-               stats: Optional[CStats] = None) -> List[Hit]:
-        return self.search_batch([Query(include, exclude, max_distance, k, profile, language, now_ms)],
+               stats: Optional[CStats] = None, filter: Optional[QueryFilter] = None) -> List[Hit]:
+        return self.search_batch([Query(include, exclude, max_distance, k, profile, language, now_ms, filter)],
                                  stats=stats)[0]
 
     def search_batch(self, queries: Sequence[Query], stats: Optional[CStats] = None,
@@ -236,6 +278,9 @@ class RWIIndex:
             arr[i].profile = ctypes.pointer(prof.c)
             arr[i].language = q.language.encode()[:7]
             arr[i].now_ms = q.now_ms
+            if q.filter is not None:
+                keep.append(q.filter)
+                arr[i].filter = ctypes.pointer(q.filter.c)
         hits = (CHit * (nq * kmax))()
         nout = (ctypes.c_int32 * nq)()
         st = stats if stats is not None else CStats()
