@@ -1,2 +1,3 @@
 set -e
-timeout -k 10 300 python -u -m pytest tests/test_gpu_shards_loopback.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/gputest_lb.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest.log 2>&1
+timeout -k 10 200 python bench.py --no-cpu --latency 50 > gpurun_out/bench.json 2>gpurun_out/bench.err

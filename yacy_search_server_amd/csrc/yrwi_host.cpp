@@ -618,37 +618,6 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   return 0;
 }
 
-// pullOneRWI(skipDoubleDom) over a merged stack (SearchEvent.java:1297-1394), as
-// k_doubledom does on one GPU: the sharded path merges the shard stacks here.
-static int32_t pull_double_dom(const yrwi_hit* st, int32_t n, int32_t want, yrwi_hit* out) {
-  auto host = [&](int32_t i) {
-    uint64_t h = 0;
-    for (int j = 6; j < 12; j++) h = (h << 6) | (uint64_t)(AHP[st[i].urlhash[j]] & 63);
-    return h;
-  };
-  std::unordered_map<uint64_t, int32_t> queued;  // host in doubleDomCache -> queued entries
-  std::vector<int32_t> fifo;
-  size_t qh = 0;
-  int32_t i = 0, m = 0;
-  while (m < want) {
-    int32_t got = -1;
-    for (int c = 0; i < n && c < 10; c++) {
-      const int32_t pos = i++;
-      auto it = queued.find(host(pos));
-      if (it == queued.end()) { queued[host(pos)] = 0; got = pos; break; }
-      it->second++;
-      fifo.push_back(pos);
-    }
-    if (got >= 0) { out[m++] = st[got]; continue; }
-    if (qh == fifo.size()) break;
-    const int32_t pos = fifo[qh++];
-    auto it = queued.find(host(pos));
-    if (--it->second == 0) queued.erase(it);
-    out[m++] = st[pos];
-  }
-  return m;
-}
-
 // Normalise (+ cross-shard exchange), then either score+top-k (hits) or all scores.
 static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrwi_hit* h_hits,
                           int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
@@ -911,19 +880,19 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   }
   const Cand** d_fptr = arena_alloc<const Cand*>(ctx, nq);
   const int32_t** d_fcnt = arena_alloc<const int32_t*>(ctx, nq);
-  // one GPU: k_emit / k_doubledom write the results straight into pinned host
-  // memory -- the caller's buffer when it came from yrwi_host_alloc, else this
-  // lane's landing buffer (then copied out per query).  Sharded: every shard's
-  // list (the whole stack for doubledom queries) is gathered and merged.
-  const int32_t kint = (W > 1 && any_dd) ? std::max<int32_t>(kmax, YRWI_MAX_K) : kmax;
+  // Results go straight into pinned host memory -- the caller's buffer when it
+  // came from yrwi_host_alloc, else this lane's landing buffer (then copied out
+  // per query).  One GPU: k_emit writes them (doubledom queries: their stacks,
+  // ordered by k_pull).  Sharded: every shard's stack is gathered, merged on the
+  // device (k_gmerge_*) and pulled (k_pull); every rank ends with the same lists.
+  const int32_t kint = any_dd ? YRWI_MAX_K : kmax;  // stack stride
   const size_t hb = sizeof(yrwi_hit) * (size_t)nq * kmax, hb_al = (hb + 255) & ~(size_t)255;
   const size_t nb = sizeof(int32_t) * (size_t)nq;
   yrwi_hit* d_hits = nullptr;
   int32_t* d_nout = nullptr;
+  const bool direct = ctx->hostreg && ctx->hostreg->contains(h_hits, hb) && ctx->hostreg->contains(h_nout, nb);
   uint8_t* land = nullptr;
-  bool direct = false;
-  if (W == 1) {
-    direct = ctx->hostreg && ctx->hostreg->contains(h_hits, hb) && ctx->hostreg->contains(h_nout, nb);
+  {
     void* hp = h_hits;
     void* np = h_nout;
     if (!direct) {
@@ -934,66 +903,52 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     }
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hits), hp, 0));
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));
-  } else {
-    d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
-    d_nout = arena_alloc<int32_t>(ctx, nq);
   }
-  if (!d_fptr || !d_fcnt || !d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (!d_fptr || !d_fcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
-  if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_hits, d_nout, W > 1 ? 1 : 0, ctx->stream))
-    return ctx->fail(YRWI_E_HIP, "emit launch");
-  if (W == 1 && any_dd && launch_doubledom(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, ctx->stream))
-    return ctx->fail(YRWI_E_HIP, "doubledom launch");
-  if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
+  std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
   if (W == 1) {
-    HIPCHK(ctx, lane_sync(ctx));
-    if (!direct) {
-      std::memcpy(h_nout, land + hb_al, nb);
-      for (int qi = 0; qi < nq; qi++)
-        std::memcpy(h_hits + (size_t)qi * kmax, land + sizeof(yrwi_hit) * (size_t)qi * kmax,
-                    sizeof(yrwi_hit) * (size_t)std::max(0, std::min(h_nout[qi], kmax)));
+    if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, 0, ctx->stream))
+      return ctx->fail(YRWI_E_HIP, "emit launch");
+    if (any_dd) {
+      yrwi_hit* d_stack = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
+      int32_t* d_scnt = arena_alloc<int32_t>(ctx, nq);
+      if (!d_stack || !d_scnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_stack, d_scnt, 2, ctx->stream) ||
+          launch_pull(d_q, nq, d_stack, d_scnt, kint, 1, kmax, d_hits, d_nout, ctx->stream))
+        return ctx->fail(YRWI_E_HIP, "doubledom launch");
     }
-    return flagcounts_out();
+  } else {
+    yrwi_hit* d_mine = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
+    int32_t* d_mcnt = arena_alloc<int32_t>(ctx, nq);
+    yrwi_hit* d_allh = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint * W);
+    int32_t* d_alln = arena_alloc<int32_t>(ctx, (int64_t)nq * W);
+    uint32_t* d_slot = arena_alloc<uint32_t>(ctx, (int64_t)nq * kint * W);
+    uint8_t* d_dup = arena_alloc<uint8_t>(ctx, (int64_t)nq * kint * W);
+    yrwi_hit* d_stack = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
+    int32_t* d_scnt = arena_alloc<int32_t>(ctx, nq);
+    if (!d_mine || !d_mcnt || !d_allh || !d_alln || !d_slot || !d_dup || !d_stack || !d_scnt)
+      return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_mine, d_mcnt, 1, ctx->stream))
+      return ctx->fail(YRWI_E_HIP, "emit launch");
+    if (int rc = coll_allgather(ctx, d_mine, d_allh, sizeof(yrwi_hit) * (size_t)nq * kint)) return rc;
+    if (int rc = coll_allgather(ctx, d_mcnt, d_alln, sizeof(int32_t) * (size_t)nq)) return rc;
+    if (launch_gmerge(d_q, d_allh, d_alln, W, nq, kint, d_slot, d_dup, d_stack, d_scnt, ctx->stream) ||
+        launch_pull(d_q, nq, d_stack, d_scnt, kint, 0, kmax, d_hits, d_nout, ctx->stream))
+      return ctx->fail(YRWI_E_HIP, "shard merge launch");
+    hD.resize((size_t)nq);
+    HIPCHK(ctx, hipMemcpy2DAsync(hD.data(), sizeof(int32_t), reinterpret_cast<const uint8_t*>(d_norm) + offsetof(NormState, D),
+                                 sizeof(NormState), sizeof(int32_t), (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
   }
-  // ---- multi-GPU: gather every shard's list, merge in shard (= url hash) order
-  yrwi_hit* d_allh = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint * W);
-  int32_t* d_alln = arena_alloc<int32_t>(ctx, (int64_t)nq * W);
-  if (!d_allh || !d_alln) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (int rc = coll_allgather(ctx, d_hits, d_allh, sizeof(yrwi_hit) * nq * kint)) return rc;
-  if (int rc = coll_allgather(ctx, d_nout, d_alln, sizeof(int32_t) * nq)) return rc;
-  std::vector<yrwi_hit> allh((size_t)nq * kint * W);
-  std::vector<int32_t> alln((size_t)nq * W);
-  HIPCHK(ctx, hipMemcpyAsync(allh.data(), d_allh, allh.size() * sizeof(yrwi_hit), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(alln.data(), d_alln, alln.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-  std::vector<NormState> nsh((size_t)nq);
-  HIPCHK(ctx, hipMemcpyAsync(nsh.data(), d_norm, nq * sizeof(NormState), hipMemcpyDeviceToHost, ctx->stream));
+  if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
   HIPCHK(ctx, lane_sync(ctx));
-  std::vector<yrwi_hit> v, stack;
-  for (int qi = 0; qi < nq; qi++) {
-    if (nsh[(size_t)qi].D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
-    v.clear();
-    for (int s = 0; s < W; s++) {
-      int32_t n = alln[(size_t)s * nq + qi];
-      const yrwi_hit* src = &allh[((size_t)s * nq + qi) * kint];
-      v.insert(v.end(), src, src + n);
-    }
-    // stable: among equal (score, hashCode) the lower shard (smaller url hash) stays first
-    std::stable_sort(v.begin(), v.end(), [](const yrwi_hit& a, const yrwi_hit& b) {
-      if (a.score != b.score) return a.score > b.score;
-      return a.tiebreak > b.tiebreak;
-    });
-    const RankQ& R = rq[(size_t)qi];
-    const int32_t kq = std::min(R.k, kint);  // the merged stack (TreeSet dedupe)
-    stack.clear();
-    for (size_t i = 0; i < v.size() && (int32_t)stack.size() < kq; i++) {
-      if (!stack.empty() && v[i].score == stack.back().score && v[i].tiebreak == stack.back().tiebreak) continue;
-      stack.push_back(v[i]);
-    }
-    yrwi_hit* dst = h_hits + (size_t)qi * kmax;
-    const int32_t want = std::min(R.kout, kmax);
-    h_nout[qi] = R.doubledom ? pull_double_dom(stack.data(), (int32_t)stack.size(), want, dst)
-                             : (int32_t)std::min<size_t>(stack.size(), (size_t)want);
-    if (!R.doubledom) std::copy(stack.begin(), stack.begin() + h_nout[qi], dst);
+  for (int32_t D : hD)
+    if (D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
+  if (!direct) {
+    std::memcpy(h_nout, land + hb_al, nb);
+    for (int qi = 0; qi < nq; qi++)
+      std::memcpy(h_hits + (size_t)qi * kmax, land + sizeof(yrwi_hit) * (size_t)qi * kmax,
+                  sizeof(yrwi_hit) * (size_t)std::max(0, std::min(h_nout[qi], kmax)));
   }
   return flagcounts_out();
 }

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <thread>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <map>
 #include <unordered_map>

@@ -211,15 +211,19 @@ int topq_capacity(int32_t keff);
 // in_stride, counts d_in_cnt), k = gk[g]; output list g at d_out + g*keff, count d_out_cnt[g]
 int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
                 const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* stream);
-// stack_mode: doubledom queries emit their whole stack (sharded merge) instead of
-// leaving them to launch_doubledom
+// mode 0: first kout hits of the non-doubledom queries; 1: every query's stack
+// (k hits); 2: only the doubledom queries' stacks
 int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int stack_mode, void* stream);
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int mode, void* stream);
 // out[i] = sum or max over r of all[r * n + i] (loopback allreduce)
 int launch_reduce_i32(const int32_t* all, int world, int64_t n, int32_t* out, int max_op, void* stream);
-// pullOneRWI(skipDoubleDom) order of the final stacks of the doubledom queries
-int launch_doubledom(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                     int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
+// results from stacks (stride kint): pullOneRWI(skipDoubleDom) order for doubledom
+// queries, the first kout entries for the others (only_dd: doubledom queries only)
+int launch_pull(const RankQ* d_q, int32_t nq, const yrwi_hit* d_stack, const int32_t* d_scnt, int32_t kint,
+                int only_dd, int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* stream);
+// merge of gathered shard stacks allh[world][nq][kint] into stack[nq][kint] (TreeSet in shard order)
+int launch_gmerge(const RankQ* d_q, const yrwi_hit* d_allh, const int32_t* d_alln, int world, int32_t nq, int32_t kint,
+                  uint32_t* d_slot, uint8_t* d_dup, yrwi_hit* d_stack, int32_t* d_scnt, void* stream);
 int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* stream);
 

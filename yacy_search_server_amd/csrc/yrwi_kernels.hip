@@ -1744,15 +1744,19 @@ __global__ __launch_bounds__(TOPQ_THREADS) void k_topq(const int64_t* __restrict
   if (tid == 0) out_cnt[g] = emitted;
 }
 
+// Emit final candidates as yrwi_hit records.  mode EMIT_OUT: queries without
+// doubledom, their first kout hits to `hits`; EMIT_STACK: every query's stack
+// (k hits, the doubledom bound), input of the shard merge; EMIT_STACK_DD: only
+// the doubledom queries' stacks (k_pull orders them).
+enum : int { EMIT_OUT = 0, EMIT_STACK = 1, EMIT_STACK_DD = 2 };
+
 __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* __restrict__ fin,
                        const int32_t* const* __restrict__ fin_cnt, int32_t kmax, yrwi_hit* __restrict__ hits,
-                       int32_t* __restrict__ nout, int stack_mode) {
+                       int32_t* __restrict__ nout, int mode) {
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
-  // doubledom queries: k_doubledom writes the pull order, or (stack_mode, sharded)
-  // the whole stack goes out for the cross-shard merge
-  if (Q.doubledom && !stack_mode) return;
-  const int32_t n = min(*fin_cnt[qi], min(Q.doubledom ? Q.k : Q.kout, kmax));
+  if ((mode == EMIT_OUT && Q.doubledom) || (mode == EMIT_STACK_DD && !Q.doubledom)) return;
+  const int32_t n = min(*fin_cnt[qi], min(mode == EMIT_OUT ? Q.kout : Q.k, kmax));
   const Cand* f = fin[qi];
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const Cand cd = f[i];
@@ -1767,6 +1771,74 @@ __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* 
   if (threadIdx.x == 0) nout[qi] = n;
 }
 
+// ------------------------------------------------ cross-shard merge (sharded)
+// Gathered per-shard stacks allh[s][q][0, alln[s][q]) (each in rwiStack order)
+// are merged as one TreeSet fed in url-hash (= shard) order: order (score desc,
+// hashCode desc, shard asc); an entry whose (score, hashCode) already occurs in
+// a lower shard is rejected.  k_gmerge_rank places every entry at its merged
+// position (its index + the entries of the other shards ahead of it);
+// k_gmerge_out compacts the survivors into the query's merged stack.
+__device__ __forceinline__ bool hit_before(const yrwi_hit& x, int64_t score, int32_t tb, bool ties_first) {
+  return x.score > score || (x.score == score && (x.tiebreak > tb || (ties_first && x.tiebreak == tb)));
+}
+
+__global__ void k_gmerge_rank(const yrwi_hit* __restrict__ allh, const int32_t* __restrict__ alln, int W, int nq,
+                              int32_t kint, uint32_t* __restrict__ slot, uint8_t* __restrict__ dup) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)W * kint;
+  if (t >= per * nq) return;
+  const int q = (int)(t / per);
+  const int s = (int)((t % per) / kint);
+  const int32_t i = (int32_t)(t % kint);
+  if (i >= alln[(int64_t)s * nq + q]) return;
+  const yrwi_hit me = allh[((int64_t)s * nq + q) * kint + i];
+  int64_t pos = i;
+  uint8_t d = 0;
+  for (int s2 = 0; s2 < W; s2++) {
+    if (s2 == s) continue;
+    const yrwi_hit* L = allh + ((int64_t)s2 * nq + q) * kint;
+    const int32_t n2 = alln[(int64_t)s2 * nq + q];
+    const bool ties_first = s2 < s;  // a lower shard's equal key precedes
+    int32_t lo = 0, hi = n2;         // first element not before me
+    while (lo < hi) {
+      const int32_t m = (lo + hi) >> 1;
+      if (hit_before(L[m], me.score, me.tiebreak, ties_first)) lo = m + 1; else hi = m;
+    }
+    pos += lo;
+    if (ties_first && lo > 0 && L[lo - 1].score == me.score && L[lo - 1].tiebreak == me.tiebreak) d = 1;
+  }
+  slot[(int64_t)q * per + pos] = (uint32_t)(s * kint + i);
+  dup[(int64_t)q * per + pos] = d;
+}
+
+__global__ __launch_bounds__(256) void k_gmerge_out(const RankQ* __restrict__ qs, const yrwi_hit* __restrict__ allh,
+                                                    const int32_t* __restrict__ alln, int W, int nq, int32_t kint,
+                                                    const uint32_t* __restrict__ slot, const uint8_t* __restrict__ dup,
+                                                    yrwi_hit* __restrict__ stack, int32_t* __restrict__ scnt) {
+  __shared__ int32_t sScan[4];
+  const int q = blockIdx.x;
+  const RankQ& Q = qs[q];
+  const int64_t per = (int64_t)W * kint;
+  int32_t T = 0;
+  for (int s = 0; s < W; s++) T += alln[(int64_t)s * nq + q];
+  const int32_t lim = min(Q.k, kint);
+  int32_t base = 0;
+  for (int32_t c0 = 0; c0 < T && base < lim; c0 += 256) {
+    const int32_t p = c0 + (int32_t)threadIdx.x;
+    const int keep = (p < T && !dup[(int64_t)q * per + p]) ? 1 : 0;
+    int32_t tot;
+    const int32_t off = block_excl_sum256(keep, sScan, &tot);
+    if (keep && base + off < lim) {
+      const uint32_t sl = slot[(int64_t)q * per + p];
+      const int s = (int)(sl / (uint32_t)kint), i = (int)(sl % (uint32_t)kint);
+      stack[(int64_t)q * kint + base + off] = allh[((int64_t)s * nq + q) * kint + i];
+    }
+    base += tot;
+  }
+  if (threadIdx.x == 0) scnt[q] = min(base, lim);
+}
+
+// ------------------------------------------------ result pulling
 // pullOneRWI(skipDoubleDom = true) repeated kout times over the settled stack
 // (SearchEvent.java:1297-1394).  Each round polls up to 10 stack entries; the
 // first one of a host without a doubleDomCache entry is returned (the host gets
@@ -1775,12 +1847,20 @@ __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* 
 // rank order (equal weights: the earliest) -- and a host whose queue
 // runs empty leaves the cache.  The queues together are one FIFO in stack order.
 // One workgroup per query: hosts are interned in an LDS hash table in parallel,
-// then lane 0 replays the pull sequence on small LDS arrays.
+// then lane 0 replays the pull sequence on small LDS arrays.  Queries without
+// doubledom just copy the first kout entries (only_dd = 0).
 constexpr int DD_SLOTS = 8192;  // > 2 * YRWI_MAX_K
 
-__global__ __launch_bounds__(64) void k_doubledom(const RankQ* __restrict__ qs, const Cand* const* __restrict__ fin,
-                                                  const int32_t* const* __restrict__ fin_cnt, int32_t kmax,
-                                                  yrwi_hit* __restrict__ hits, int32_t* __restrict__ nout) {
+__device__ __forceinline__ uint64_t hit_host36(const yrwi_hit& h) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 6; j < 12; j++) x = (x << 6) | (uint64_t)(ahpla(h.urlhash[j]) & 63);
+  return x;
+}
+
+__global__ __launch_bounds__(64) void k_pull(const RankQ* __restrict__ qs, const yrwi_hit* __restrict__ stack,
+                                             const int32_t* __restrict__ scnt, int32_t kint, int only_dd,
+                                             int32_t kmax, yrwi_hit* __restrict__ hits, int32_t* __restrict__ nout) {
   __shared__ unsigned long long sKey[DD_SLOTS];
   __shared__ uint16_t sCnt[DD_SLOTS];     // queued entries of the host
   __shared__ uint8_t sSeen[DD_SLOTS];     // host has a doubleDomCache entry
@@ -1790,14 +1870,20 @@ __global__ __launch_bounds__(64) void k_doubledom(const RankQ* __restrict__ qs, 
   __shared__ int32_t sN;
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
-  if (!Q.doubledom) return;
-  const int32_t n = min(*fin_cnt[qi], (int32_t)YRWI_MAX_K);
-  const Cand* f = fin[qi];
+  if (only_dd && !Q.doubledom) return;
+  const yrwi_hit* st = stack + (int64_t)qi * kint;
+  const int32_t n = min(scnt[qi], min((int32_t)YRWI_MAX_K, kint));
+  const int32_t want = min(Q.kout, kmax);
+  if (!Q.doubledom) {
+    const int32_t m = min(n, want);
+    for (int o = threadIdx.x; o < m; o += 64) hits[(int64_t)qi * kmax + o] = st[o];
+    if (threadIdx.x == 0) nout[qi] = m;
+    return;
+  }
   for (int i = threadIdx.x; i < DD_SLOTS; i += 64) { sKey[i] = 0; sCnt[i] = 0; sSeen[i] = 0; }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += 64) {
-    const uint32_t idx = ~(uint32_t)f[i].k2 & 0x0FFFFFFFu;
-    const uint64_t key = host36(load_row(Q.rows + (int64_t)idx * YRWI_ROW_BYTES)) + 1;
+    const uint64_t key = hit_host36(st[i]) + 1;
     uint32_t slot = (uint32_t)mix64(key) & (DD_SLOTS - 1);
     while (true) {
       const unsigned long long prev = atomicCAS(&sKey[slot], 0ull, (unsigned long long)key);
@@ -1808,7 +1894,6 @@ __global__ __launch_bounds__(64) void k_doubledom(const RankQ* __restrict__ qs, 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int32_t want = min(Q.kout, kmax);
     int32_t out = 0, i = 0, qh = 0, qt = 0;
     while (out < want) {
       int32_t got = -1;
@@ -1830,18 +1915,10 @@ __global__ __launch_bounds__(64) void k_doubledom(const RankQ* __restrict__ qs, 
   }
   __syncthreads();
   const int32_t m = sN;
-  for (int o = threadIdx.x; o < m; o += 64) {
-    const Cand cd = f[sOut[o]];
-    const uint32_t idx = ~(uint32_t)cd.k2 & 0x0FFFFFFFu;
-    const uint8_t* r = Q.rows + (int64_t)idx * YRWI_ROW_BYTES;
-    yrwi_hit h;
-    for (int j = 0; j < 12; j++) h.urlhash[j] = r[j];
-    h.tiebreak = (int32_t)((uint32_t)(cd.k2 >> 32) ^ 0x80000000u);
-    h.score = (int64_t)(cd.k1 ^ 0x8000000000000000ull);
-    hits[(int64_t)qi * kmax + o] = h;
-  }
+  for (int o = threadIdx.x; o < m; o += 64) hits[(int64_t)qi * kmax + o] = st[sOut[o]];
   if (threadIdx.x == 0) nout[qi] = m;
 }
+
 
 // all scores of a container (yrwi_normalize_score)
 __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
@@ -2088,17 +2165,29 @@ int launch_reduce_i32(const int32_t* all, int world, int64_t n, int32_t* out, in
   return rc(hipGetLastError());
 }
 
-int launch_doubledom(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                     int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
+int launch_pull(const RankQ* d_q, int32_t nq, const yrwi_hit* d_stack, const int32_t* d_scnt, int32_t kint,
+                int only_dd, int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, void* st) {
   if (nq <= 0) return 0;
-  hipLaunchKernelGGL(k_doubledom, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_final, d_final_cnt, kmax, d_hits, d_nout);
+  hipLaunchKernelGGL(k_pull, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_stack, d_scnt, kint, only_dd, kmax, d_hits,
+                     d_nout);
+  return rc(hipGetLastError());
+}
+
+int launch_gmerge(const RankQ* d_q, const yrwi_hit* d_allh, const int32_t* d_alln, int world, int32_t nq, int32_t kint,
+                  uint32_t* d_slot, uint8_t* d_dup, yrwi_hit* d_stack, int32_t* d_scnt, void* st) {
+  if (nq <= 0) return 0;
+  const int64_t n = (int64_t)nq * world * kint;
+  hipLaunchKernelGGL(k_gmerge_rank, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), d_allh, d_alln, world, nq,
+                     kint, d_slot, d_dup);
+  hipLaunchKernelGGL(k_gmerge_out, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, d_allh, d_alln, world, nq, kint, d_slot,
+                     d_dup, d_stack, d_scnt);
   return rc(hipGetLastError());
 }
 
 int launch_emit(const RankQ* d_q, int32_t nq, const Cand* const* d_final, const int32_t* const* d_final_cnt,
-                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int stack_mode, void* st) {
+                int32_t kmax, yrwi_hit* d_hits, int32_t* d_nout, int mode, void* st) {
   hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, kmax,
-                     d_hits, d_nout, stack_mode);
+                     d_hits, d_nout, mode);
   return rc(hipGetLastError());
 }
 
