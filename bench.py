@@ -152,6 +152,10 @@ def main():
         if idx.sizes[t]:
             ix.add(idx.hashes[t], idx.list_rows(t))
     log(f"rank {rank}: index resident in {time.time() - t0:.1f}s, stats {ix.stats()}")
+    t0 = time.time()
+    ix.build_url_ids()
+    t_dict = time.time() - t0
+    log(f"rank {rank}: url dictionary built in {t_dict:.3f}s")
 
     qs = synth.queries(full, args.nq, args.terms, args.terms, 0)
     now_ms = 20741 * 86400000
@@ -243,6 +247,11 @@ def main():
 
     roof = roofline(iso, "k_join")
     roof["measured"] = "HIP events around each launch, separate pass of the timed batch with 1 batch in flight"
+    # BASELINE.md §4 counts 12 B per posting key; the join streams 4-byte url ids
+    # (DESIGN.md §3), so the HBM bytes it moves are far fewer: that rate is here
+    if roof.get("traffic") and roof["mean_launch_us"]:
+        roof["traffic_GBps"] = round(roof["traffic"] / (roof["mean_launch_us"] * 1e-6) / 1e9, 1)
+        roof["traffic_frac"] = round(roof["traffic_GBps"] / HBM_PEAK_GBS, 4)
     roof_probe = roofline(iso, "k_probe")
     roof_timed = roofline(timed, "k_join")
     roof_timed["measured"] = "HIP events around each launch inside the timed region (2 lanes overlap)"
@@ -284,6 +293,7 @@ def main():
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
             "inflight": args.inflight,
+            "url_dictionary_build_s": round(t_dict, 3),
         }
         print(json.dumps(out))
     ix.close()

@@ -139,6 +139,10 @@ const char* yrwi_last_error(yrwi_ctx* ctx);
  * sorts (duplicate url hashes: the first occurrence wins, RowSet.mergeEnum). */
 int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted);
 int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n);
+/* Builds the url dictionary (url hash -> order-preserving 32-bit url id, the
+ * join key in HBM) now instead of at the next query; the index is immutable
+ * for queries until the next put_list / load_heaps. */
+int yrwi_build_url_ids(yrwi_ctx* ctx);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
 
 /* ---- YaCy on-disk index ---- */

@@ -234,6 +234,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   hipSetDevice(ctx->device);
   close_lanes(ctx);
   ctx->index_mem.release();
+  if (ctx->uid_all) hipFree(ctx->uid_all);
   delete ctx;
 }
 
@@ -249,7 +250,7 @@ extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_
   drain(ctx);  // in-flight batches read the list table
   if (n == 0) {
     auto it = ctx->lists.find(tk);
-    if (it != ctx->lists.end()) { ctx->npostings -= it->second.n; ctx->lists.erase(it); }
+    if (it != ctx->lists.end()) { ctx->npostings -= it->second.n; ctx->lists.erase(it); ctx->uid_dirty = true; }
     return 0;
   }
   std::vector<uint8_t> tmp;
@@ -290,7 +291,15 @@ extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_
   if (it != ctx->lists.end()) ctx->npostings -= it->second.n;
   ctx->lists[tk] = L;
   ctx->npostings += n;
+  ctx->uid_dirty = true;
   return 0;
+}
+
+extern "C" int yrwi_build_url_ids(yrwi_ctx* ctx) {
+  if (!ctx) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  return ensure_url_ids(ctx);
 }
 
 extern "C" int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n) {
@@ -466,9 +475,8 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.now_ms = P.now_ms;
       int64_t cap = std::min(J.A.n, J.B.n);
       J.out_rows = arena_alloc<uint8_t>(ctx, cap * 40);
-      J.out_khi = arena_alloc<uint64_t>(ctx, cap);
-      J.out_klo = arena_alloc<uint8_t>(ctx, cap);
-      if (!J.out_rows || !J.out_khi || !J.out_klo) return ctx->fail(YRWI_E_NOMEM, "arena");
+      J.out_uid = arena_alloc<uint32_t>(ctx, cap);
+      if (!J.out_rows || !J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (st) {
         st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
@@ -490,12 +498,14 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
     ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
     uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
+    uint32_t* d_puid = arena_alloc<uint32_t>(ctx, tiles * JOIN_MAXM);
     int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
     int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
-    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_cnt || !d_off) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_cnt || !d_off)
+      return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
     hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
-    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_cnt, d_off, false,
+    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
                          ctx->stream, e0, em, e1))
       return ctx->fail(YRWI_E_HIP, "join launch");
     if (tm) tm->kjoin.push_back({e0, em, e1});
@@ -505,7 +515,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     HIPCHK(ctx, lane_sync(ctx));
     for (int j = 0; j < nj; j++) {
       Plan& P = plans[(size_t)owner[(size_t)j]];
-      P.cont = DList{jobs[(size_t)j].out_khi, jobs[(size_t)j].out_klo, jobs[(size_t)j].out_rows, mh[(size_t)j]};
+      P.cont = DList{nullptr, nullptr, jobs[(size_t)j].out_rows, mh[(size_t)j], jobs[(size_t)j].out_uid};
     }
   }
   // exclusion (excludeContainers :373-388): mark container rows present in an exclude list
@@ -541,7 +551,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
       if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, true,
+      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr, true,
                            ctx->stream, nullptr, nullptr, nullptr))
         return ctx->fail(YRWI_E_HIP, "exclude launch");
     }
@@ -1012,6 +1022,7 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   }
   hipSetDevice(ctx->device);
   drain(ctx);
+  if (int rc = ensure_url_ids(ctx)) return rc;
   const int64_t t0 = now_ns();
   // contiguous parts of equal query count, one per lane, each planned and run
   // by its lane's thread (every rank splits a sharded batch identically)
@@ -1059,6 +1070,10 @@ extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, 
   if (int rc = check_batch_args(ctx, q, nq, kmax, out, nout)) return rc;
   if (!ticket) return YRWI_E_ARG;
   hipSetDevice(ctx->device);
+  if (ctx->uid_dirty) {  // the index changed: nothing can be in flight (put_list drained)
+    drain(ctx);
+    if (int rc = ensure_url_ids(ctx)) return rc;
+  }
   const int64_t t = ctx->next_ticket;
   Lane* L = ctx->lanes[(size_t)(t % (int64_t)ctx->lanes.size())];
   L->wait();  // the lane's previous batch (its status is already recorded)
@@ -1135,6 +1150,7 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
   d.k = 1;
   d.now_ms = now_ms;
   drain(ctx);
+  if (int rc0 = ensure_url_ids(ctx)) return rc0;
   Lane* L = ctx->lanes[0];
   std::vector<Plan> plans(1);
   int rc = ctx->take(L, plan_query(ctx, L, d, &plans[0]));

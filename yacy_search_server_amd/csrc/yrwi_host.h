@@ -74,7 +74,8 @@ struct ListRec {
   uint8_t* klo = nullptr;
   uint8_t* rows = nullptr;
   int64_t n = 0;
-  DList dl() const { return DList{khi, klo, rows, n}; }
+  uint32_t* uid = nullptr;  // url ids (rebuilt with the url dictionary)
+  DList dl() const { return DList{khi, klo, rows, n, uid}; }
 };
 
 // bump allocator over device chunks
@@ -259,6 +260,11 @@ struct CtxBase {
   std::unordered_map<int64_t, std::pair<int, std::string>> status;
   std::unordered_map<KeyT, ListRec, KeyHash> lists;
   Arena index_mem{(size_t)1 << 30};
+  // url dictionary (yrwi_dict.hip): every list's uid array is a slice of uid_all;
+  // rebuilt before the next query after any list changed
+  bool uid_dirty = true;
+  uint32_t* uid_all = nullptr;
+  size_t uid_cap = 0;
   std::string err;
   int64_t npostings = 0;
 
@@ -350,6 +356,9 @@ struct Xfer {
   void* ptr;
   size_t bytes;
 };
+// (re)build the url dictionary and every list's url ids if the index changed
+int ensure_url_ids(CtxBase* ctx);
+
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op);    // in place; sum or max
 int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs);  // grouped send/recv

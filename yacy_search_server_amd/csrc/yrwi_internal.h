@@ -27,11 +27,16 @@ constexpr int64_t DAY_MS = 86400000LL;
 // hi = key >> 8 (chars 0..9 and the top 4 bits of char 10), lo = key & 0xFF.
 
 // A sorted posting list / container on the device (SoA keys + AoS rows).
+// uid: the url id of each posting -- its url hash's rank in the context's url
+// dictionary (yrwi_dict.hip), so uid order == url-hash order and the joins
+// compare and stream 4-byte ids instead of 9-byte keys.  khi/klo (the 72-bit
+// key) are kept on index lists only (validation, dictionary build, loader).
 struct DList {
   const uint64_t* khi;
   const uint8_t* klo;
   const uint8_t* rows;  // 40-byte WordReferenceRow
   int64_t n;
+  const uint32_t* uid;
 };
 
 // Feature rule of a join step (ReferenceContainer.joinConstructive :406-416).
@@ -57,8 +62,7 @@ struct JoinQ {
   int32_t algo;        // JoinAlgo
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   uint8_t* removed;    // JM_MARK target (indexed like A)
-  uint64_t* out_khi;   // compacted output container (capacity min(nA, nB))
-  uint8_t* out_klo;
+  uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
   uint8_t* out_rows;
   int64_t now_ms;
   int64_t* m_out;      // number of output rows (written by the scan kernel)
@@ -68,10 +72,8 @@ struct JoinQ {
 // range [a0, a0+na) and B range [b0, b0+nb) plus one lookahead B key (nbl = nb+1
 // unless B is exhausted), with direct key pointers so k_join needs no job lookup.
 struct TileDesc {
-  const uint64_t* ah;
-  const uint8_t* al;
-  const uint64_t* bh;
-  const uint8_t* bl;
+  const uint32_t* a;  // url ids of A and B
+  const uint32_t* b;
   int64_t a0, b0;
   int32_t na, nb, nbl, job;
   int32_t maxd, pad;
@@ -193,7 +195,7 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
-                     uint2* d_pairs,
+                     uint2* d_pairs, uint32_t* d_pair_uid,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
                      void* ev_mid, void* ev_end);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

@@ -193,11 +193,6 @@ __global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t
 // =========================================================== join: partition
 // One thread per merge tile: the merge-path split of the tile's first and last
 // diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
-__device__ __forceinline__ bool key_le_at(const DList& A, int64_t i, const DList& B, int64_t j) {
-  const uint64_t ah = A.khi[i], bh = B.khi[j];
-  return ah < bh || (ah == bh && A.klo[i] <= B.klo[j]);
-}
-
 __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
                             int64_t total_tiles, TileDesc* __restrict__ desc) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,6 +200,8 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   const int j = find_job(tile_base, njobs, b);
   const JoinQ& J = jobs[j];
   const int64_t nA = J.A.n, nB = J.B.n;
+  const uint32_t* __restrict__ A = J.A.uid;
+  const uint32_t* __restrict__ B = J.B.uid;
   const int64_t d0 = (b - tile_base[j]) * JOIN_TILE;
   const int64_t d1 = d0 + JOIN_TILE < nA + nB ? d0 + JOIN_TILE : nA + nB;
   int64_t lo0 = d0 - nB > 0 ? d0 - nB : 0, hi0 = d0 < nA ? d0 : nA;
@@ -212,18 +209,16 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   while (lo0 < hi0 || lo1 < hi1) {
     if (lo0 < hi0) {
       const int64_t mid = (lo0 + hi0) >> 1;
-      if (key_le_at(J.A, mid, J.B, d0 - 1 - mid)) lo0 = mid + 1; else hi0 = mid;
+      if (A[mid] <= B[d0 - 1 - mid]) lo0 = mid + 1; else hi0 = mid;
     }
     if (lo1 < hi1) {
       const int64_t mid = (lo1 + hi1) >> 1;
-      if (key_le_at(J.A, mid, J.B, d1 - 1 - mid)) lo1 = mid + 1; else hi1 = mid;
+      if (A[mid] <= B[d1 - 1 - mid]) lo1 = mid + 1; else hi1 = mid;
     }
   }
   TileDesc D;
-  D.ah = J.A.khi;
-  D.al = J.A.klo;
-  D.bh = J.B.khi;
-  D.bl = J.B.klo;
+  D.a = A;
+  D.b = B;
   D.a0 = lo0;
   D.b0 = d0 - lo0;
   D.na = (int32_t)(lo1 - lo0);
@@ -255,53 +250,36 @@ __device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint
 constexpr int JOIN_SLOTS = (JOIN_TILE + 1 + JOIN_THREADS - 1) / JOIN_THREADS;  // 2049 items max per tile
 
 struct TileKeys {
-  uint64_t h[JOIN_SLOTS];
-  uint32_t l[JOIN_SLOTS];
+  uint32_t k[JOIN_SLOTS];
 };
 
-__device__ uint64_t g_pad_h[1];
-__device__ uint8_t g_pad_l[1];
+__device__ uint32_t g_pad_k[1];
 
 // global (address space 1) pointers: flat loads would also count in lgkmcnt and
 // every LDS wait of the merge would then wait for the prefetch as well
-typedef __attribute__((address_space(1))) const uint64_t gu64c;
 typedef __attribute__((address_space(1))) const uint32_t gu32c;
 
-// Branch-free address select: one load per slot, so no wait is forced before the
-// merge.  klo bytes are read as the aligned dword that holds them (key arrays are
-// 256-byte aligned allocations rounded up to 256 bytes, so the dword is in bounds):
-// a full-width loaded register is carried to the next iteration without a
-// narrowing instruction that would wait for the load.
+// Branch-free address select: one load per slot, so no wait is forced before the merge.
 __device__ __forceinline__ void tile_load(const TileDesc& D, TileKeys& K) {
 #pragma unroll
   for (int s = 0; s < JOIN_SLOTS; s++) {
     const int x = threadIdx.x + s * JOIN_THREADS;
-    const uint64_t* ph = g_pad_h;
-    const uint8_t* pl = g_pad_l;
-    if (x < D.na) {
-      ph = D.ah + D.a0 + x;
-      pl = D.al + D.a0 + x;
-    } else if (x < D.na + D.nbl) {
-      ph = D.bh + D.b0 + (x - D.na);
-      pl = D.bl + D.b0 + (x - D.na);
-    }
-    K.h[s] = *(gu64c*)ph;
-    K.l[s] = *(gu32c*)((uintptr_t)pl & ~(uintptr_t)3);
+    const uint32_t* p = g_pad_k;
+    if (x < D.na) p = D.a + D.a0 + x;
+    else if (x < D.na + D.nbl) p = D.b + D.b0 + (x - D.na);
+    K.k[s] = *(gu32c*)p;
   }
 }
 
 __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
                                                       const TileDesc* __restrict__ desc, int64_t ntiles,
-                                                      uint2* __restrict__ pairs, int32_t* __restrict__ tile_cnt,
-                                                      int mark) {
-  // A keys at [0, na), B keys (+ lookahead) at [JOIN_TILE, JOIN_TILE + nbl), one pad slot
-  __shared__ uint64_t sH[2 * JOIN_TILE + 2];
-  __shared__ uint8_t sL[2 * JOIN_TILE + 2];
+                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
+                                                      int32_t* __restrict__ tile_cnt, int mark) {
+  // A ids at [0, na), B ids (+ lookahead) at [JOIN_TILE, JOIN_TILE + nbl), one pad slot
+  __shared__ uint32_t sK[2 * JOIN_TILE + 2];
   __shared__ int32_t sScan[4];
-  const uint64_t* sAh = sH;
-  const uint64_t* sBh = sH + JOIN_TILE;
-  const uint8_t* sAl = sL;
-  const uint8_t* sBl = sL + JOIN_TILE;
+  const uint32_t* sA = sK;
+  const uint32_t* sB = sK + JOIN_TILE;
 
   // Tile descriptors travel through VGPRs (lane i holds dword i, read with
   // v_readlane when due): a scalar load would share lgkmcnt with LDS traffic and
@@ -331,13 +309,11 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 #pragma unroll
     for (int s = 0; s < JOIN_SLOTS; s++) {
       const int x = threadIdx.x + s * JOIN_THREADS;
-      const int64_t gi = x < na ? Dc.a0 + x : Dc.b0 + (x - na);
       const int slot = x < na ? x : (x < na + nbl ? JOIN_TILE + (x - na) : 2 * JOIN_TILE + 1);
-      sH[slot] = K.h[s];
-      sL[slot] = (uint8_t)(K.l[s] >> (8 * (gi & 3)));
+      sK[slot] = K.k[s];
     }
     __syncthreads();
-    // prefetch: keys of the next tile, descriptor of the one after
+    // prefetch: ids of the next tile, descriptor of the one after
     const int64_t a0 = Dc.a0, b0 = Dc.b0;
     const int jc = Dc.job, maxd = Dc.maxd;
     if (b + G < ntiles) {
@@ -353,32 +329,34 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
       int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
       while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        int bj = dd0 - 1 - mid;
-        if (key_le(sAh[mid], sAl[mid], sBh[bj], sBl[bj])) lo = mid + 1; else hi = mid;
+        if (sA[mid] <= sB[dd0 - 1 - mid]) lo = mid + 1; else hi = mid;
       }
       ia = lo;
       ib = dd0 - lo;
     }
     int32_t ma[JOIN_IPT], mb[JOIN_IPT];
+    uint32_t mu[JOIN_IPT];
     uint32_t mbits = 0;
+    uint32_t ka = ia < na ? sA[ia] : 0xFFFFFFFFu, kb = sB[ib];
 #pragma unroll
     for (int s = 0; s < JOIN_IPT; s++) {
       ma[s] = 0;
       mb[s] = 0;
+      mu[s] = 0;
       if (dd0 + s < dtot) {
-        bool takeA;
-        if (ia >= na) takeA = false;
-        else if (ib >= nb) takeA = true;
-        else takeA = key_le(sAh[ia], sAl[ia], sBh[ib], sBl[ib]);
+        const bool takeA = ia < na && (ib >= nb || ka <= kb);
         if (takeA) {
-          if (ib < nbl && sAh[ia] == sBh[ib] && sAl[ia] == sBl[ib]) {
+          if (ib < nbl && ka == kb) {
             ma[s] = ia;
             mb[s] = ib;
+            mu[s] = ka;
             mbits |= 1u << s;
           }
           ia++;
+          ka = ia < na ? sA[ia] : 0xFFFFFFFFu;
         } else {
           ib++;
+          kb = sB[ib];
         }
       }
     }
@@ -407,10 +385,12 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
       int32_t tot;
       int32_t off = block_excl_sum256(cnt, sScan, &tot);
       uint2* out = pairs + b * (int64_t)JOIN_MAXM;
+      uint32_t* outu = pair_uid + b * (int64_t)JOIN_MAXM;
 #pragma unroll
       for (int s = 0; s < JOIN_IPT; s++) {
         if (mbits & (1u << s)) {
           out[off] = make_uint2((uint32_t)(a0 + ma[s]), (uint32_t)(b0 + mb[s]));
+          outu[off] = mu[s];
           off++;
         }
       }
@@ -428,13 +408,10 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 // thread, all tiles in parallel); k_probe binary-searches each key inside its
 // tile's range.  Output and mark semantics are k_join's.
 
-__device__ __forceinline__ int64_t lower_bound_key(const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
-                                                   int64_t lo, int64_t hi, uint64_t h, uint32_t l) {
+__device__ __forceinline__ int64_t lower_bound_uid(const uint32_t* __restrict__ u, int64_t lo, int64_t hi, uint32_t x) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    const uint64_t mh = kh[mid];
-    const bool less = mh < h || (mh == h && (uint32_t)kl[mid] < l);
-    if (less) lo = mid + 1; else hi = mid;
+    if (u[mid] < x) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
@@ -449,20 +426,17 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const int64_t s0 = (tile0 + t - tile_base[j]) * PROBE_TILE;
   const int64_t s1 = s0 + PROBE_TILE < Sm.n ? s0 + PROBE_TILE : Sm.n;
-  const uint64_t h0 = Sm.khi[s0], h1 = Sm.khi[s1 - 1];
-  const uint32_t l0 = Sm.klo[s0], l1 = Sm.klo[s1 - 1];
-  // lower bound of the first key, upper bound (lower bound of key + 1) of the last
+  const uint32_t k0 = Sm.uid[s0], k1 = Sm.uid[s1 - 1];
+  // lower bound of the first id, upper bound of the last
   int64_t lo0 = 0, hi0 = Lg.n, lo1 = 0, hi1 = Lg.n;
   while (lo0 < hi0 || lo1 < hi1) {
     if (lo0 < hi0) {
       const int64_t mid = (lo0 + hi0) >> 1;
-      const uint64_t mh = Lg.khi[mid];
-      if (mh < h0 || (mh == h0 && (uint32_t)Lg.klo[mid] < l0)) lo0 = mid + 1; else hi0 = mid;
+      if (Lg.uid[mid] < k0) lo0 = mid + 1; else hi0 = mid;
     }
     if (lo1 < hi1) {
       const int64_t mid = (lo1 + hi1) >> 1;
-      const uint64_t mh = Lg.khi[mid];
-      if (mh < h1 || (mh == h1 && (uint32_t)Lg.klo[mid] <= l1)) lo1 = mid + 1; else hi1 = mid;
+      if (Lg.uid[mid] <= k1) lo1 = mid + 1; else hi1 = mid;
     }
   }
   ProbeDesc D;
@@ -476,8 +450,8 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
 __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
-                                                     uint2* __restrict__ pairs, int32_t* __restrict__ tile_cnt,
-                                                     int mark) {
+                                                     uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
+                                                     int32_t* __restrict__ tile_cnt, int mark) {
   __shared__ int32_t sScan[4];
   const int64_t t = blockIdx.x;
   const int64_t b = tile0 + t;
@@ -489,12 +463,12 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const int64_t i = s0 + threadIdx.x;
   bool hit = false;
   int64_t jl = 0;
+  uint32_t key = 0;
   if (i < Sm.n) {
     // the upper levels of the 256 searches share lines of the range (L2 hits)
-    const uint64_t h = Sm.khi[i];
-    const uint32_t l = Sm.klo[i];
-    jl = lower_bound_key(Lg.khi, Lg.klo, D.lo, D.hi, h, l);
-    hit = jl < D.hi && Lg.khi[jl] == h && (uint32_t)Lg.klo[jl] == l;
+    key = Sm.uid[i];
+    jl = lower_bound_uid(Lg.uid, D.lo, D.hi, key);
+    hit = jl < D.hi && Lg.uid[jl] == key;
   }
   const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
   if (hit && !mark && J.maxd < 65535) {
@@ -506,7 +480,10 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   }
   int32_t tot;
   const int32_t off = block_excl_sum256(hit ? 1 : 0, sScan, &tot);
-  if (hit) pairs[b * (int64_t)JOIN_MAXM + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
+  if (hit) {
+    pairs[b * (int64_t)JOIN_MAXM + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
+    pair_uid[b * (int64_t)JOIN_MAXM + off] = key;
+  }
   if (threadIdx.x == 0) tile_cnt[b] = tot;
 }
 
@@ -591,11 +568,12 @@ __device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo
 
 // One workgroup per COMPACT_TILES consecutive tiles: the tiles' matches are
 // concatenated (LDS prefix of their counts) and spread over all 256 threads.
-// The output key is recomputed from the gathered row (no key gathers).
+// The output url id comes with the pair (written by k_join / k_probe).
 constexpr int COMPACT_TILES = 16;
 
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
+                                                 const uint32_t* __restrict__ pair_uid,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
@@ -626,17 +604,14 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     }
     const int i = m - sPre[lo];
     const JoinQ& J = jobs[sJob[lo]];
-    const uint2 pr = pairs[(t0 + lo) * (int64_t)JOIN_MAXM + i];
+    const int64_t pi = (t0 + lo) * (int64_t)JOIN_MAXM + i;
+    const uint2 pr = pairs[pi];
     const int64_t o = sOff[lo] + i;
     const uint8_t* ra = J.A.rows + (int64_t)pr.x * YRWI_ROW_BYTES;
     const uint8_t* rb = J.B.rows + (int64_t)pr.y * YRWI_ROW_BYTES;
     const Row r = joined_row(ra, rb, J.mode, J.now_ms);
-    uint64_t kh;
-    uint32_t kl;
-    row_key(r, kh, kl);
     store_row(J.out_rows + o * YRWI_ROW_BYTES, r);
-    J.out_khi[o] = kh;
-    J.out_klo[o] = (uint8_t)kl;
+    J.out_uid[o] = pair_uid[pi];
   }
 }
 
@@ -2029,7 +2004,8 @@ int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t*
 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
-                     uint2* d_pairs, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* st, void* ev0,
+                     uint2* d_pairs, uint32_t* d_pair_uid, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark,
+                     void* st, void* ev0,
                      void* evm, void* ev1) {
   if (total_tiles <= 0) return 0;
   static int join_grid = 0;  // resident k_join workgroups on the whole device
@@ -2052,17 +2028,17 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
-                       S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_tile_cnt, mark ? 1 : 0);
+                       S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_tile_cnt, mark ? 1 : 0);
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_cnt, mark ? 1 : 0);
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off);
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
-                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_tile_cnt, d_tile_off);
+                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_cnt, d_tile_off);
   }
   return rc(hipGetLastError());
 }

@@ -134,7 +134,7 @@ struct DevList {
   uint8_t* klo = nullptr;
   uint8_t* rows = nullptr;
   int64_t n = 0;
-  DList dl() const { return DList{khi, klo, rows, n}; }
+  DList dl() const { return DList{khi, klo, rows, n, nullptr}; }
 };
 
 }  // namespace
@@ -387,6 +387,7 @@ extern "C" int yrwi_load_heaps(yrwi_ctx* ctx, const char* const* paths, int32_t 
     if (has_ram) ctx->npostings -= it->second.n;
     ctx->lists[T.first] = R;
     ctx->npostings += R.n;
+    ctx->uid_dirty = true;
     S.terms++;
     S.postings += R.n;
   }

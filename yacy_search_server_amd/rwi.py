@@ -213,6 +213,10 @@ class RWIIndex:
                                                    ctypes.byref(st)))
         return st
 
+    def build_url_ids(self) -> None:
+        """Build the url dictionary now (else the next query does)."""
+        _check(self._h, _lib.lib().yrwi_build_url_ids(self._h))
+
     def get_size(self, term: bytes) -> int:
         n = ctypes.c_int64()
         _check(self._h, _lib.lib().yrwi_list_size(self._h, bytes(term), ctypes.byref(n)))
