@@ -243,43 +243,46 @@ __device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint
 }
 
 // ============================================================ join: tiles
-// Persistent workgroups walk the merge tiles t = blockIdx.x + k*gridDim.x.  The
-// keys of the next tile are loaded into registers while the current tile is
-// merged out of LDS (and its descriptor two tiles ahead), so every workgroup
-// keeps one tile of key loads in flight for the whole kernel.
 constexpr int JOIN_SLOTS = (JOIN_TILE + 1 + JOIN_THREADS - 1) / JOIN_THREADS;  // 2049 items max per tile
 
 struct TileKeys {
-  uint32_t k[JOIN_SLOTS];
+  uint32_t a[JOIN_SLOTS], b[JOIN_SLOTS];
 };
-
-__device__ uint32_t g_pad_k[1];
 
 // global (address space 1) pointers: flat loads would also count in lgkmcnt and
 // every LDS wait of the merge would then wait for the prefetch as well
 typedef __attribute__((address_space(1))) const uint32_t gu32c;
 
-// Branch-free address select: one load per slot, so no wait is forced before the merge.
+// Tile id loads through two buffer descriptors (A range, B range + lookahead):
+// slot x reads A[x] and B[x - na]; the range check returns 0 for the side that
+// is out of bounds (or both, past the tile), so the id is the OR of the two and
+// there is no per-slot address select.  Descriptor fields are wave-uniform
+// (TileDesc arrives through v_readlane).
 __device__ __forceinline__ void tile_load(const TileDesc& D, TileKeys& K) {
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(D.a + D.a0), 0, D.na * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(D.b + D.b0), 0, D.nbl * 4, 0x00020000);
 #pragma unroll
   for (int s = 0; s < JOIN_SLOTS; s++) {
     const int x = threadIdx.x + s * JOIN_THREADS;
-    const uint32_t* p = g_pad_k;
-    if (x < D.na) p = D.a + D.a0 + x;
-    else if (x < D.na + D.nbl) p = D.b + D.b0 + (x - D.na);
-    K.k[s] = *(gu32c*)p;
+    K.a[s] = __builtin_amdgcn_raw_buffer_load_b32(ra, x * 4, 0, 0);
+    K.b[s] = __builtin_amdgcn_raw_buffer_load_b32(rb, (x - D.na) * 4, 0, 0);
   }
 }
 
+// Persistent workgroups walk the merge tiles t = blockIdx.x + k*gridDim.x, the
+// ids of the next tile loading while the current one is merged out of LDS.
+// LDS holds the tile's A ids at [0, na) and B ids (+ lookahead) at [na, na+nbl).
+// Each thread finds its 8-item diagonal by binary search, then merges; it keeps
+// only two bit masks (took-A, match) and rebuilds the indices of its (rare)
+// matches afterwards.
 __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
                                                       const TileDesc* __restrict__ desc, int64_t ntiles,
                                                       uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                       int32_t* __restrict__ tile_cnt, int mark) {
-  // A ids at [0, na), B ids (+ lookahead) at [JOIN_TILE, JOIN_TILE + nbl), one pad slot
-  __shared__ uint32_t sK[2 * JOIN_TILE + 2];
+  __shared__ uint32_t sK[JOIN_SLOTS * JOIN_THREADS];
   __shared__ int32_t sScan[4];
-  const uint32_t* sA = sK;
-  const uint32_t* sB = sK + JOIN_TILE;
 
   // Tile descriptors travel through VGPRs (lane i holds dword i, read with
   // v_readlane when due): a scalar load would share lgkmcnt with LDS traffic and
@@ -304,14 +307,8 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
   tile_load(Dc, K);
   for (; b < ntiles; b += G) {
     const int na = Dc.na, nb = Dc.nb, nbl = Dc.nbl;
-    // branch-free LDS fill (a branchy one would leave the prefetch registers "maybe
-    // pending" on skipped paths and force waits in the middle of the next prefetch)
 #pragma unroll
-    for (int s = 0; s < JOIN_SLOTS; s++) {
-      const int x = threadIdx.x + s * JOIN_THREADS;
-      const int slot = x < na ? x : (x < na + nbl ? JOIN_TILE + (x - na) : 2 * JOIN_TILE + 1);
-      sK[slot] = K.k[s];
-    }
+    for (int s = 0; s < JOIN_SLOTS; s++) sK[threadIdx.x + s * JOIN_THREADS] = K.a[s] | K.b[s];
     __syncthreads();
     // prefetch: ids of the next tile, descriptor of the one after
     const int64_t a0 = Dc.a0, b0 = Dc.b0;
@@ -321,78 +318,62 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
       dnext = desc_fetch(b + 2 * G);
       tile_load(Dc, K);
     }
-
+    const uint32_t* sB = sK + na;
     const int dd0 = threadIdx.x * JOIN_IPT;
     const int dtot = na + nb;
-    int ia = 0, ib = 0;
-    if (dd0 < dtot) {
-      int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (sA[mid] <= sB[dd0 - 1 - mid]) lo = mid + 1; else hi = mid;
-      }
-      ia = lo;
-      ib = dd0 - lo;
+    int lo = dd0 - nb > 0 ? dd0 - nb : 0, hi = dd0 < na ? dd0 : na;
+    if (dd0 >= dtot) lo = hi = 0;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sK[mid] <= sB[dd0 - 1 - mid]) lo = mid + 1; else hi = mid;
     }
-    int32_t ma[JOIN_IPT], mb[JOIN_IPT];
-    uint32_t mu[JOIN_IPT];
-    uint32_t mbits = 0;
-    uint32_t ka = ia < na ? sA[ia] : 0xFFFFFFFFu, kb = sB[ib];
+    const int ia0 = lo, ib0 = dd0 - lo;
+    int ia = ia0, ib = ib0;
+    uint32_t ka = sK[ia], kb = sB[ib];
+    uint32_t tbits = 0, mbits = 0;
+    const int nstep = dtot - dd0 < JOIN_IPT ? dtot - dd0 : JOIN_IPT;
 #pragma unroll
     for (int s = 0; s < JOIN_IPT; s++) {
-      ma[s] = 0;
-      mb[s] = 0;
-      mu[s] = 0;
-      if (dd0 + s < dtot) {
+      if (s < nstep) {
         const bool takeA = ia < na && (ib >= nb || ka <= kb);
-        if (takeA) {
-          if (ib < nbl && ka == kb) {
-            ma[s] = ia;
-            mb[s] = ib;
-            mu[s] = ka;
-            mbits |= 1u << s;
-          }
-          ia++;
-          ka = ia < na ? sA[ia] : 0xFFFFFFFFu;
-        } else {
-          ib++;
-          kb = sB[ib];
-        }
+        const bool m = takeA && ib < nbl && ka == kb;
+        tbits |= (uint32_t)takeA << s;
+        mbits |= (uint32_t)m << s;
+        ia += takeA;
+        ib += !takeA;
+        ka = sK[ia];
+        kb = sB[ib];
       }
     }
+    // index of the A / B element of step s
+    auto a_at = [&](int s) { return ia0 + __popc(tbits & ((1u << s) - 1u)); };
+    auto b_at = [&](int s) { return ib0 + s - __popc(tbits & ((1u << s) - 1u)); };
     // maxDistance filter (ReferenceContainer.java:442,482; distance <= 65535 always)
     // and exclusion marks need the job's rows; plain joins never touch the job
     if ((mark || maxd < 65535) && __syncthreads_or(mbits != 0)) {
       const JoinQ& J = jobs[jc];
-      if (mbits && !mark) {
-#pragma unroll
-        for (int s = 0; s < JOIN_IPT; s++) {
-          if (mbits & (1u << s)) {
-            const uint8_t* ra = J.A.rows + (a0 + ma[s]) * YRWI_ROW_BYTES;
-            const uint8_t* rb = J.B.rows + (b0 + mb[s]) * YRWI_ROW_BYTES;
-            if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << s);
-          }
+      for (uint32_t m = mbits; m; m &= m - 1) {
+        const int st = __ffs(m) - 1;
+        if (mark) {
+          J.removed[a0 + a_at(st)] = 1;
+        } else {
+          const uint8_t* ra = J.A.rows + (a0 + a_at(st)) * YRWI_ROW_BYTES;
+          const uint8_t* rb = J.B.rows + (b0 + b_at(st)) * YRWI_ROW_BYTES;
+          if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << st);
         }
-      }
-      if (mark) {
-#pragma unroll
-        for (int s = 0; s < JOIN_IPT; s++)
-          if (mbits & (1u << s)) J.removed[a0 + ma[s]] = 1;
       }
     }
     if (!mark) {
-      const int32_t cnt = __popc(mbits);
       int32_t tot;
-      int32_t off = block_excl_sum256(cnt, sScan, &tot);
+      int32_t off = block_excl_sum256(__popc(mbits), sScan, &tot);
       uint2* out = pairs + b * (int64_t)JOIN_MAXM;
       uint32_t* outu = pair_uid + b * (int64_t)JOIN_MAXM;
-#pragma unroll
-      for (int s = 0; s < JOIN_IPT; s++) {
-        if (mbits & (1u << s)) {
-          out[off] = make_uint2((uint32_t)(a0 + ma[s]), (uint32_t)(b0 + mb[s]));
-          outu[off] = mu[s];
-          off++;
-        }
+      for (uint32_t m = mbits; m; m &= m - 1) {
+        const int st = __ffs(m) - 1;
+        const int ai = a_at(st);
+        out[off] = make_uint2((uint32_t)(a0 + ai), (uint32_t)(b0 + b_at(st)));
+        outu[off] = sK[ai];
+        off++;
       }
       if (threadIdx.x == 0) tile_cnt[b] = tot;
     }
