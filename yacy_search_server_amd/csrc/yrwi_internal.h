@@ -122,6 +122,9 @@ struct NormState {
   int32_t maxdom;
   int64_t nvalid;
   double tf_mn, tf_mx;
+  // fl(1 / divisor) of cardinal's normalisations (0 where max == min): fields
+  // [0, NF), then date (va), then worddistance (D) -- see qdiv in yrwi_kernels.hip
+  double rcp[NF + 2];
 };
 
 // Field indices inside mn/mx.

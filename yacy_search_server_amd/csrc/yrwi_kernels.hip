@@ -491,11 +491,9 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
 // ============================================================ join: compact
 // Joined row: J5 (WordReferenceVars.join :465-499) + J6 (toRowEntry :301-322 ->
 // WordReferenceRow ctor :116-161).
-__device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, int mode, int64_t now_ms) {
-  Row o;
+// J5 + J6 on loaded rows: for by-test modes `o` is already the large side's row
+__device__ __forceinline__ Row joined_row_of(Row o, const Row& B, int mode, int64_t now_ms) {
   if (mode == JM_ENUM) {
-    o = load_row(ra);
-    const Row B = load_row(rb);
     int pa = (int)o.u16(O_T), pb = (int)B.u16(O_T);
     int pos = 0, post = pa;
     bool has = false;
@@ -522,10 +520,8 @@ __device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, 
     o.set(O_P, (uint32_t)p >> 8); o.set(O_P + 1, (uint32_t)p);
     o.set(O_C, (uint32_t)c);
     o.set(O_I, (uint32_t)dist);
-  } else {
-    // by test: the large row joined with itself -> its own features, stored distance
-    o = load_row(mode == JM_TEST_LARGE_B ? rb : ra);
   }
+  // by test: the large row joined with itself -> its own features, stored distance
   const int32_t mddlm = clamp_days((int32_t)o.u16(O_A), now_ms);
   const int32_t mddct = micro_date_days(now_ms);
   int32_t fresh = add32(mddlm, mul32(sub32(mddct, mddlm), 2));
@@ -535,6 +531,13 @@ __device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, 
   o.set(O_G, 0);
   o.set(O_K, 0);
   return o;
+}
+
+__device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, int mode, int64_t now_ms) {
+  const Row a = load_row(mode == JM_TEST_LARGE_B ? rb : ra);
+  Row b{};
+  if (mode == JM_ENUM) b = load_row(rb);
+  return joined_row_of(a, b, mode, now_ms);
 }
 
 // url-hash key of a row (bytes 0..11), as k_validate computes it for the index
@@ -549,8 +552,22 @@ __device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo
 
 // One workgroup per COMPACT_TILES consecutive tiles: the tiles' matches are
 // concatenated (LDS prefix of their counts) and spread over all 256 threads.
-// The output url id comes with the pair (written by k_join / k_probe).
+// The output url id comes with the pair (written by k_join / k_probe).  Each
+// thread takes COMPACT_UNROLL matches at a time and issues all their pair and
+// row loads before combining any of them: the gathers are latency-bound, so
+// more of them in flight per thread is what moves the rows.
 constexpr int COMPACT_TILES = 16;
+constexpr int COMPACT_UNROLL = 4;
+
+struct CompactJob {
+  const uint8_t* ar;
+  const uint8_t* br;
+  uint8_t* orows;
+  uint32_t* ouid;
+  int64_t now_ms;
+  int64_t off;
+  int32_t mode, pad;
+};
 
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
@@ -558,8 +575,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
-  __shared__ int32_t sJob[COMPACT_TILES];
-  __shared__ int64_t sOff[COMPACT_TILES];
+  __shared__ CompactJob sJ[COMPACT_TILES];
   const int64_t t0 = (int64_t)blockIdx.x * COMPACT_TILES;
   if (threadIdx.x < 64) {
     const int64_t t = t0 + threadIdx.x;
@@ -567,8 +583,15 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     if (threadIdx.x < COMPACT_TILES && t < ntiles) {
       c = tile_cnt[t];
       if (c) {
-        sJob[threadIdx.x] = find_job(tile_base, njobs, t);
-        sOff[threadIdx.x] = tile_off[t];
+        const JoinQ& J = jobs[find_job(tile_base, njobs, t)];
+        CompactJob& X = sJ[threadIdx.x];
+        X.ar = J.A.rows;
+        X.br = J.B.rows;
+        X.orows = J.out_rows;
+        X.ouid = J.out_uid;
+        X.now_ms = J.now_ms;
+        X.off = tile_off[t];
+        X.mode = J.mode;
       }
     }
     const int32_t inc = wave_incl_sum(c);
@@ -577,22 +600,44 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
   }
   __syncthreads();
   const int32_t total = sPre[COMPACT_TILES];
-  for (int m = threadIdx.x; m < total; m += blockDim.x) {
-    int lo = 0, hi = COMPACT_TILES - 1;  // largest lt with sPre[lt] <= m
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (sPre[mid] <= m) lo = mid; else hi = mid - 1;
+  for (int m0 = threadIdx.x; m0 < total; m0 += COMPACT_UNROLL * 256) {
+    int tl[COMPACT_UNROLL];
+    int64_t pi[COMPACT_UNROLL];
+    uint2 pr[COMPACT_UNROLL];
+    uint32_t uid[COMPACT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      const int m = m0 + u * 256;
+      tl[u] = -1;
+      if (m < total) {
+        int lo = 0, hi = COMPACT_TILES - 1;  // largest lt with sPre[lt] <= m
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sPre[mid] <= m) lo = mid; else hi = mid - 1;
+        }
+        tl[u] = lo;
+        pi[u] = (t0 + lo) * (int64_t)JOIN_MAXM + (m - sPre[lo]);
+        pr[u] = pairs[pi[u]];
+        uid[u] = pair_uid[pi[u]];
+      }
     }
-    const int i = m - sPre[lo];
-    const JoinQ& J = jobs[sJob[lo]];
-    const int64_t pi = (t0 + lo) * (int64_t)JOIN_MAXM + i;
-    const uint2 pr = pairs[pi];
-    const int64_t o = sOff[lo] + i;
-    const uint8_t* ra = J.A.rows + (int64_t)pr.x * YRWI_ROW_BYTES;
-    const uint8_t* rb = J.B.rows + (int64_t)pr.y * YRWI_ROW_BYTES;
-    const Row r = joined_row(ra, rb, J.mode, J.now_ms);
-    store_row(J.out_rows + o * YRWI_ROW_BYTES, r);
-    J.out_uid[o] = pair_uid[pi];
+    Row A[COMPACT_UNROLL], B[COMPACT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      if (tl[u] < 0) continue;
+      const CompactJob& X = sJ[tl[u]];
+      A[u] = load_row(X.mode == JM_TEST_LARGE_B ? X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES
+                                                 : X.ar + (int64_t)pr[u].x * YRWI_ROW_BYTES);
+      if (X.mode == JM_ENUM) B[u] = load_row(X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES);
+    }
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      if (tl[u] < 0) continue;
+      const CompactJob& X = sJ[tl[u]];
+      const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
+      store_row(X.orows + o * YRWI_ROW_BYTES, joined_row_of(A[u], B[u], X.mode, X.now_ms));
+      X.ouid[o] = uid[u];
+    }
   }
 }
 
@@ -1153,10 +1198,24 @@ __global__ void k_combine(const RankQ* __restrict__ qs, int nq, const ShardSum* 
     N.va_mn = N.va_mx = 0;
     N.tf_mn = N.tf_mx = 0.0;
   }
+  for (int f = 0; f < NF; f++) N.rcp[f] = N.mx[f] != N.mn[f] ? 1.0 / (double)(N.mx[f] - N.mn[f]) : 0.0;
+  N.rcp[NF] = N.va_mx != N.va_mn ? 1.0 / (double)(N.va_mx - N.va_mn) : 0.0;
+  N.rcp[NF + 1] = N.D != 0 ? 1.0 / (double)N.D : 0.0;
   norm[qi] = N;
 }
 
 // ------------------------------------------------------------------ scoring
+// Java int division n / d (truncation toward zero) for |n| < 2^24 and
+// 0 < d < 2^24, with r = fl(1/d): |n|*r carries an error below 2^-28 and the
+// 2^-26 bias lifts exact quotients above their integer while a true fraction
+// (at least 1/d > 2^-24 below the next integer) stays below it, so the
+// truncation equals the integer quotient.  Every normalised term of cardinal
+// has |(t - min) << 8| <= 65535 * 256 < 2^24 and max - min <= 65535.
+__device__ __forceinline__ int32_t qdiv(int32_t n, double r) {
+  const int32_t q = (int32_t)fma((double)(n < 0 ? -n : n), r, 0x1p-26);
+  return n < 0 ? -q : q;
+}
+
 // ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265), settled min/max.
 __device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const NormState& N, const RankQ& Q,
                                             int32_t hcount) {
@@ -1164,30 +1223,35 @@ __device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const N
   int32_t tfterm = 0;
   if (!(N.tf_mx == N.tf_mn))
     tfterm = shl32(d2i(((t.tf - N.tf_mn) * 256.0) / (N.tf_mx - N.tf_mn)), rk.coeff_termfrequency);
-  auto inv = [](int32_t tv, int32_t lo, int32_t hi, int32_t c) -> int32_t {
+  auto inv = [](int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) -> int32_t {
     if (hi == lo) return 0;
-    return shl32(sub32(256, div32(shl32(sub32(tv, lo), 8), sub32(hi, lo))), c);
+    return shl32(sub32(256, qdiv(shl32(sub32(tv, lo), 8), rc)), c);
   };
-  auto fwd = [](int32_t tv, int32_t lo, int32_t hi, int32_t c) -> int32_t {
+  auto fwd = [](int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) -> int32_t {
     if (hi == lo) return 0;
-    return shl32(div32(shl32(sub32(tv, lo), 8), sub32(hi, lo)), c);
+    return shl32(qdiv(shl32(sub32(tv, lo), 8), rc), c);
   };
   const int dl = ahpla(r.b(11)) & 3;  // DigestURL.domLengthEstimation; << (8/20) == << 0
   const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
   int32_t s = shl32(256 - dln, rk.coeff_domlength);
-  s = add32(s, inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], rk.coeff_urlcomps));
-  s = add32(s, inv(t.f[F_URLLENGTH], N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], rk.coeff_urllength));
-  s = add32(s, inv(t.f[F_POSINTEXT], N.mn[F_POSINTEXT], N.mx[F_POSINTEXT], rk.coeff_posintext));
-  s = add32(s, inv(t.f[F_POSOFPHRASE], N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], rk.coeff_posofphrase));
-  s = add32(s, inv(t.f[F_POSINPHRASE], N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], rk.coeff_posinphrase));
-  s = add32(s, inv(t.od, 0, N.D, rk.coeff_worddistance));
-  s = add32(s, fwd(t.a, N.va_mn, N.va_mx, rk.coeff_date));
-  s = add32(s, fwd(t.f[F_WORDSINTITLE], N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], rk.coeff_wordsintitle));
-  s = add32(s, fwd(t.f[F_WORDSINTEXT], N.mn[F_WORDSINTEXT], N.mx[F_WORDSINTEXT], rk.coeff_wordsintext));
-  s = add32(s, fwd(t.f[F_PHRASESINTEXT], N.mn[F_PHRASESINTEXT], N.mx[F_PHRASESINTEXT], rk.coeff_phrasesintext));
-  s = add32(s, fwd(t.f[F_LLOCAL], N.mn[F_LLOCAL], N.mx[F_LLOCAL], rk.coeff_llocal));
-  s = add32(s, fwd(t.f[F_LOTHER], N.mn[F_LOTHER], N.mx[F_LOTHER], rk.coeff_lother));
-  s = add32(s, fwd(t.f[F_HITCOUNT], N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], rk.coeff_hitcount));
+  s = add32(s, inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], N.rcp[F_URLCOMPS], rk.coeff_urlcomps));
+  s = add32(s, inv(t.f[F_URLLENGTH], N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], N.rcp[F_URLLENGTH], rk.coeff_urllength));
+  s = add32(s, inv(t.f[F_POSINTEXT], N.mn[F_POSINTEXT], N.mx[F_POSINTEXT], N.rcp[F_POSINTEXT], rk.coeff_posintext));
+  s = add32(s, inv(t.f[F_POSOFPHRASE], N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], N.rcp[F_POSOFPHRASE],
+                   rk.coeff_posofphrase));
+  s = add32(s, inv(t.f[F_POSINPHRASE], N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], N.rcp[F_POSINPHRASE],
+                   rk.coeff_posinphrase));
+  s = add32(s, inv(t.od, 0, N.D, N.rcp[NF + 1], rk.coeff_worddistance));
+  s = add32(s, fwd(t.a, N.va_mn, N.va_mx, N.rcp[NF], rk.coeff_date));
+  s = add32(s, fwd(t.f[F_WORDSINTITLE], N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], N.rcp[F_WORDSINTITLE],
+                   rk.coeff_wordsintitle));
+  s = add32(s, fwd(t.f[F_WORDSINTEXT], N.mn[F_WORDSINTEXT], N.mx[F_WORDSINTEXT], N.rcp[F_WORDSINTEXT],
+                   rk.coeff_wordsintext));
+  s = add32(s, fwd(t.f[F_PHRASESINTEXT], N.mn[F_PHRASESINTEXT], N.mx[F_PHRASESINTEXT], N.rcp[F_PHRASESINTEXT],
+                   rk.coeff_phrasesintext));
+  s = add32(s, fwd(t.f[F_LLOCAL], N.mn[F_LLOCAL], N.mx[F_LLOCAL], N.rcp[F_LLOCAL], rk.coeff_llocal));
+  s = add32(s, fwd(t.f[F_LOTHER], N.mn[F_LOTHER], N.mx[F_LOTHER], N.rcp[F_LOTHER], rk.coeff_lother));
+  s = add32(s, fwd(t.f[F_HITCOUNT], N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], N.rcp[F_HITCOUNT], rk.coeff_hitcount));
   int64_t R = add64((int64_t)s, (int64_t)tfterm);  // + tf turns the sum into a long
   if (rk.coeff_authority > 12) {
     int32_t auth = div32(shl32(hcount, 8), add32(1, N.maxdom));  // ReferenceOrder.authority :213-216
