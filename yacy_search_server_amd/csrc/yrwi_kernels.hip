@@ -709,6 +709,11 @@ __device__ __forceinline__ double wave_min_d(double v) {
 
 constexpr int32_t BIG = 0x7FFFFFFF;
 
+// One workgroup per CHUNK container elements.  Rows are read coalesced
+// (element s*256 + tid of the chunk), which is all the order-independent parts
+// need (min/max, tf, host counts); the order-dependent fold of posintext /
+// distance works on thread-consecutive elements, so (valid, p, od) of every
+// element are exchanged through LDS.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
@@ -716,28 +721,44 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ double sD[8];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sFirst[4];
+  __shared__ uint32_t sPO[CHUNK];  // element order: valid << 31 | od << 16 | p
   __shared__ uint32_t sSegP[CHUNK_THREADS * CHUNK_IPT];
   __shared__ uint32_t sSegM[CHUNK_THREADS * CHUNK_IPT];
   __shared__ uint32_t sSegL[CHUNK_THREADS * CHUNK_IPT];
+  __shared__ int32_t sFirstInfo[3];
 
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   const int64_t c = b - Q.chunk_base;
-  const int64_t e0 = c * CHUNK + (int64_t)threadIdx.x * CHUNK_IPT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 
-  bool valid[CHUNK_IPT];
-  Feat F[CHUNK_IPT];
-  int myfirst = BIG;
+  // ---- coalesced pass: order-independent summaries
+  int32_t mn[NF], mx[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
+  int32_t pmax = -1, nval = 0, myfirst = BIG;
+  double tfmn = 1e300, tfmx = -1e300;
+  int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    const int64_t e = e0 + s;
-    valid[s] = e < Q.n && !(Q.removed && Q.removed[e]);
-    if (valid[s]) {
-      Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
-      F[s] = decode(r);
-      if (myfirst == BIG) myfirst = s;
+    const int eo = s * CHUNK_THREADS + (int)threadIdx.x;
+    const int64_t e = c * CHUNK + eo;
+    const bool v = e < Q.n && !(Q.removed && Q.removed[e]);
+    av[s] = -1;
+    uint32_t po = 0;
+    if (v) {
+      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+      const Feat F = decode(r);
+#pragma unroll
+      for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], F.f[f]); mx[f] = max(mx[f], F.f[f]); }
+      tfmn = fmin(tfmn, F.tf);
+      tfmx = fmax(tfmx, F.tf);
+      pmax = max(pmax, F.p);
+      nval++;
+      myfirst = min(myfirst, eo);
+      av[s] = F.a;
+      po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
       if (Q.want_authority) {
         uint64_t key = host36(r) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
@@ -751,40 +772,50 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
           slot = (slot + 1) & Q.hmask;
         }
       }
-    } else {
-      F[s] = Feat{};
     }
+    sPO[eo] = po;
   }
-  // first valid element of the chunk
-  int32_t firstIdx = myfirst == BIG ? BIG : (int32_t)threadIdx.x * CHUNK_IPT + myfirst;
+  // first valid element of the chunk (element order)
+  int32_t firstIdx;
   {
-    int32_t v = wave_min_i(firstIdx);
+    int32_t v = wave_min_i(myfirst);
     if (lane == 0) sFirst[wv] = v;
-    __syncthreads();
+    __syncthreads();  // also publishes sPO
     v = min(min(sFirst[0], sFirst[1]), min(sFirst[2], sFirst[3]));
     __syncthreads();
     firstIdx = v;
   }
-  const int32_t firstT = firstIdx == BIG ? -1 : firstIdx / CHUNK_IPT;
-  const int32_t firstS = firstIdx == BIG ? -1 : firstIdx % CHUNK_IPT;
-
-  // rest = valid elements after the chunk's first one
-  bool rest[CHUNK_IPT];
-  int32_t nval = 0, pmax_rest = -1;
+  // virtualAge over the rest (the chunk's first element is min/max's clone candidate)
+  int32_t vamn = BIG, vamx = -1;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    rest[s] = valid[s] && !((int)threadIdx.x == firstT && s == firstS);
-    nval += valid[s] ? 1 : 0;
-    if (rest[s]) pmax_rest = max(pmax_rest, F[s].p);
+    const int eo = s * CHUNK_THREADS + (int)threadIdx.x;
+    if (av[s] >= 0 && eo != firstIdx) { vamn = min(vamn, av[s]); vamx = max(vamx, av[s]); }
+    if (eo == firstIdx) sFirstInfo[2] = av[s];
   }
-  // local fold segments (records of the prefix max of posintext over the rest)
+
+  // ---- ordered pass on thread-consecutive elements: local fold segments
+  // (records of the prefix max of posintext over the rest)
+  bool rest[CHUNK_IPT];
+  int32_t P[CHUNK_IPT], OD[CHUNK_IPT];
+  int32_t pmax_rest = -1;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int eo = (int)threadIdx.x * CHUNK_IPT + s;
+    const uint32_t po = sPO[eo];
+    P[s] = (int32_t)(po & 0xFFFFu);
+    OD[s] = (int32_t)((po >> 16) & 0xFFu);
+    rest[s] = (po >> 31) && eo != firstIdx;
+    if (rest[s]) pmax_rest = max(pmax_rest, P[s]);
+    if (eo == firstIdx) { sFirstInfo[0] = P[s]; sFirstInfo[1] = OD[s]; }
+  }
   const int32_t lpin = block_excl_max256(pmax_rest, sScan);
   bool isrec[CHUNK_IPT];
   int32_t LP = lpin, nrec = 0;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    isrec[s] = rest[s] && F[s].p > LP;
-    if (isrec[s]) { LP = F[s].p; nrec++; }
+    isrec[s] = rest[s] && P[s] > LP;
+    if (isrec[s]) { LP = P[s]; nrec++; }
   }
   // backward pass: per record, max od and the last positive od (keyed by element
   // position so that a max over keys selects the latest one)
@@ -797,9 +828,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     recM[s] = 0;
     recL[s] = 0;
     if (rest[s]) {
-      accM = max(accM, F[s].od);
-      if (accL == 0 && F[s].od > 0)
-        accL = (((uint32_t)threadIdx.x * CHUNK_IPT + (uint32_t)s + 1u) << 8) | (uint32_t)F[s].od;
+      accM = max(accM, OD[s]);
+      if (accL == 0 && OD[s] > 0)
+        accL = (((uint32_t)threadIdx.x * CHUNK_IPT + (uint32_t)s + 1u) << 8) | (uint32_t)OD[s];
     }
     if (isrec[s]) {
       recM[s] = accM;
@@ -816,7 +847,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 #pragma unroll
     for (int s = 0; s < CHUNK_IPT; s++) {
       if (isrec[s]) {
-        sSegP[o] = (uint32_t)F[s].p;
+        sSegP[o] = (uint32_t)P[s];
         sSegM[o] = (uint32_t)recM[s];
         sSegL[o] = recL[s];
         o++;
@@ -832,22 +863,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __syncthreads();
 
   // block reductions of the min/max fields
-  int32_t mn[NF], mx[NF];
-#pragma unroll
-  for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
-  int32_t vamn = BIG, vamx = -1, pmax = -1;
-  double tfmn = 1e300, tfmx = -1e300;
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {
-    if (valid[s]) {
-#pragma unroll
-      for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], F[s].f[f]); mx[f] = max(mx[f], F[s].f[f]); }
-      tfmn = fmin(tfmn, F[s].tf);
-      tfmx = fmax(tfmx, F[s].tf);
-      pmax = max(pmax, F[s].p);
-    }
-    if (rest[s]) { vamn = min(vamn, F[s].a); vamx = max(vamx, F[s].a); }
-  }
   const int NI = 2 * NF + 4;
   int32_t vals[2 * NF + 4];
 #pragma unroll
@@ -863,13 +878,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     for (int i = 0; i < NI; i++) sI[wv * NI + i] = vals[i];
     sD[wv] = tfmn;
     sD[4 + wv] = tfmx;
-  }
-  // first element info, owned by thread firstT
-  __shared__ int32_t sFirstInfo[3];
-  if ((int)threadIdx.x == firstT) {
-#pragma unroll
-    for (int s = 0; s < CHUNK_IPT; s++)
-      if (s == firstS) { sFirstInfo[0] = F[s].p; sFirstInfo[1] = F[s].od; sFirstInfo[2] = F[s].a; }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
