@@ -103,3 +103,85 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_query(JNIEnv* env
   free(hits);
   return res;
 }
+
+/* IndexCell's BLOB files (ReferenceContainerArray): yrwi_load_heaps; returns the
+ * stats as long[7] {files, records, free_records, bad_keys, terms, postings, dropped_terms}. */
+JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_loadHeaps(JNIEnv* env, jclass c, jlong ctx,
+                                                                        jobjectArray paths, jint byName) {
+  const jsize n = (*env)->GetArrayLength(env, paths);
+  const char** p = (const char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
+  jstring* js = (jstring*)calloc((size_t)(n > 0 ? n : 1), sizeof(jstring));
+  for (jsize i = 0; i < n; i++) {
+    js[i] = (jstring)(*env)->GetObjectArrayElement(env, paths, i);
+    p[i] = (*env)->GetStringUTFChars(env, js[i], NULL);
+  }
+  yrwi_load_stats st;
+  int rc = yrwi_load_heaps((yrwi_ctx*)(intptr_t)ctx, p, n, byName ? YRWI_LOAD_ORDER_BY_NAME : 0, &st);
+  for (jsize i = 0; i < n; i++) (*env)->ReleaseStringUTFChars(env, js[i], p[i]);
+  free(p);
+  free(js);
+  if (rc != 0) return NULL;
+  jlong v[7] = {st.files, st.records, st.free_records, st.bad_keys, st.terms, st.postings, st.dropped_terms};
+  jlongArray res = (*env)->NewLongArray(env, 7);
+  (*env)->SetLongArrayRegion(env, res, 0, 7, v);
+  return res;
+}
+
+/* SearchEvent.addRWIs constraints + pullOneRWI(skipDoubleDom): query with a yrwi_filter.
+ * constraint: 4 Bitfield bytes or null; site / altSite: 6-byte host hashes or null;
+ * siteExcludes: n*6 bytes; urlHashes: n*12 bytes; flagCount: int[32] out or null. */
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_queryFiltered(
+    JNIEnv* env, jclass c, jlong ctx, jbyteArray incl, jint nincl, jbyteArray excl, jint nexcl, jint maxd, jint k,
+    jintArray prof, jstring lang, jlong now, jbyteArray constraint, jboolean allOf, jint contentdom,
+    jboolean strictDom, jstring modLang, jbyteArray site, jbyteArray altSite, jbyteArray siteExcludes,
+    jbyteArray urlHashes, jboolean skipDoubleDom, jintArray flagCount) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  yrwi_filter f;
+  memset(&f, 0, sizeof(f));
+  if (constraint) { (*env)->GetByteArrayRegion(env, constraint, 0, 4, (jbyte*)f.constraint); f.has_constraint = 1; }
+  f.all_of_constraint = allOf;
+  f.contentdom = contentdom;
+  f.strict_contentdom = strictDom;
+  if (modLang) {
+    const char* ml = (*env)->GetStringUTFChars(env, modLang, NULL);
+    strncpy(f.language, ml, sizeof(f.language) - 1);
+    (*env)->ReleaseStringUTFChars(env, modLang, ml);
+  }
+  if (site) { (*env)->GetByteArrayRegion(env, site, 0, 6, (jbyte*)f.sitehash); f.has_sitehash = 1; }
+  if (altSite) { (*env)->GetByteArrayRegion(env, altSite, 0, 6, (jbyte*)f.alt_sitehash); f.has_alt_sitehash = 1; }
+  jbyte* sx = siteExcludes ? (*env)->GetByteArrayElements(env, siteExcludes, NULL) : NULL;
+  jbyte* uh = urlHashes ? (*env)->GetByteArrayElements(env, urlHashes, NULL) : NULL;
+  f.siteexcludes = (const uint8_t*)sx;
+  f.nsiteexcludes = sx ? (*env)->GetArrayLength(env, siteExcludes) / 6 : 0;
+  f.urlhashes = (const uint8_t*)uh;
+  f.nurlhashes = uh ? (*env)->GetArrayLength(env, urlHashes) / 12 : 0;
+  f.skip_double_dom = skipDoubleDom;
+  int32_t fc[32];
+  f.flagcount = flagCount ? fc : NULL;
+  yrwi_query_desc q;
+  memset(&q, 0, sizeof(q));
+  jbyte* ib = (*env)->GetByteArrayElements(env, incl, NULL);
+  jbyte* eb = (*env)->GetByteArrayElements(env, excl, NULL);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  q.incl = (const uint8_t*)ib; q.nincl = nincl;
+  q.excl = (const uint8_t*)eb; q.nexcl = nexcl;
+  q.max_distance = maxd; q.k = k; q.profile = &p; q.now_ms = now; q.filter = &f;
+  strncpy(q.language, l, sizeof(q.language) - 1);
+  yrwi_hit* hits = (yrwi_hit*)malloc(sizeof(yrwi_hit) * (size_t)(k > 0 ? k : 1));
+  int32_t n = 0;
+  int rc = yrwi_query((yrwi_ctx*)(intptr_t)ctx, &q, hits, &n, NULL);
+  (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
+  (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
+  if (sx) (*env)->ReleaseByteArrayElements(env, siteExcludes, sx, JNI_ABORT);
+  if (uh) (*env)->ReleaseByteArrayElements(env, urlHashes, uh, JNI_ABORT);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    if (flagCount) (*env)->SetIntArrayRegion(env, flagCount, 0, 32, (const jint*)fc);
+    res = (*env)->NewByteArray(env, (jsize)(n * (jint)sizeof(yrwi_hit)));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * (jint)sizeof(yrwi_hit)), (const jbyte*)hits);
+  }
+  free(hits);
+  return res;
+}

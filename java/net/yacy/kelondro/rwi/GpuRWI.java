@@ -9,6 +9,8 @@
 //   kelondro/rwi/ReferenceContainer.java:310   -> GpuRWI.joinExclude(...)
 //   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.normalizeScore(...)
 //   search/query/SearchEvent.java:612-631      -> GpuRWI.query(...) (whole local RWI path)
+//   search/query/SearchEvent.java:736-806,1297 -> GpuRWI.queryFiltered(...) (constraints, doubledom)
+//   kelondro/rwi/IndexCell.java:353-386        -> GpuRWI.loadHeaps(...) (BLOB heaps into HBM)
 package net.yacy.kelondro.rwi;
 
 public final class GpuRWI implements AutoCloseable {
@@ -48,6 +50,28 @@ public final class GpuRWI implements AutoCloseable {
                      profile32, language, nowMillis);
     }
 
+    /** IndexCell's BLOB heaps (text.index.*.blob) into the GPU index; lists already
+     *  present act as the RAM cache.  Returns {files, records, free, badKeys, terms,
+     *  postings, droppedTerms}. */
+    public long[] loadHeaps(final String[] heapFiles, final boolean orderByFileName) {
+        return loadHeaps(this.ctx, heapFiles, orderByFileName ? 1 : 0);
+    }
+
+    /** query(...) under SearchEvent.addRWIs constraints (SearchEvent.java:736-806) and,
+     *  with skipDoubleDom, in pullOneRWI order (:1297-1394).  flagCount (int[32] or null)
+     *  receives SearchEvent.flagcount. */
+    public byte[] queryFiltered(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+                                final int[] profile32, final String language, final long nowMillis,
+                                final byte[] constraint, final boolean allOfConstraint, final int contentdom,
+                                final boolean strictContentDom, final String modifierLanguage, final byte[] sitehash,
+                                final byte[] altSitehash, final byte[][] siteexcludes, final byte[][] urlhashes,
+                                final boolean skipDoubleDom, final int[] flagCount) {
+        return queryFiltered(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
+                             maxDistance, k, profile32, language, nowMillis, constraint, allOfConstraint, contentdom,
+                             strictContentDom, modifierLanguage, sitehash, altSitehash, flattenN(siteexcludes, 6),
+                             flattenN(urlhashes, 12), skipDoubleDom, flagCount);
+    }
+
     @Override
     public void close() {
         if (this.ctx != 0) { close(this.ctx); this.ctx = 0; }
@@ -71,6 +95,13 @@ public final class GpuRWI implements AutoCloseable {
         return b;
     }
 
+    private static byte[] flattenN(final byte[][] hashes, final int w) {
+        if (hashes == null) return null;
+        final byte[] b = new byte[w * hashes.length];
+        for (int i = 0; i < hashes.length; i++) System.arraycopy(hashes[i], 0, b, w * i, w);
+        return b;
+    }
+
     private static void check(final int rc) {
         if (rc != 0) throw new IllegalStateException("libyrwi error " + rc);
     }
@@ -84,4 +115,11 @@ public final class GpuRWI implements AutoCloseable {
                                                 long nowMillis);
     private static native byte[] query(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl, int maxDistance,
                                        int k, int[] profile32, String language, long nowMillis);
+    private static native long[] loadHeaps(long ctx, String[] paths, int byName);
+    private static native byte[] queryFiltered(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl,
+                                               int maxDistance, int k, int[] profile32, String language,
+                                               long nowMillis, byte[] constraint, boolean allOf, int contentdom,
+                                               boolean strictDom, String modifierLanguage, byte[] site,
+                                               byte[] altSite, byte[] siteExcludes, byte[] urlHashes,
+                                               boolean skipDoubleDom, int[] flagCount);
 }
