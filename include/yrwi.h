@@ -194,6 +194,25 @@ int yrwi_query_batch_wait(yrwi_ctx* ctx, int64_t ticket);
 int yrwi_host_alloc(yrwi_ctx* ctx, size_t bytes, void** p);
 int yrwi_host_free(yrwi_ctx* ctx, void* p);
 
+/* ---- Solr node stack ---- */
+/* The fields of a URIMetadataNode that ReferenceOrder.cardinal(URIMetadataNode)
+ * reads (ReferenceOrder.java:267-296); the caller extracts them from the Solr
+ * document (URIMetadataNode.java:238-504). */
+typedef struct yrwi_node {
+  uint8_t urlhash[12];    /* t.hash() */
+  int32_t virtual_age;    /* t.virtualAge() = MicroDate.microDateDays(moddate) */
+  int32_t wordsintitle;   /* t.wordsintitle() */
+  int32_t wordcount;      /* t.wordCount() */
+  int32_t llocal, lother; /* t.llocal(), t.lother() */
+  uint8_t flags[4];       /* t.flags() Bitfield bytes */
+  int32_t host_count;     /* ReferenceOrder.doms.get(t.hosthash()) (authority) */
+  char language[8];       /* t.language(), NUL terminated; "" = null */
+} yrwi_node;
+/* scores[i] = cardinal(nodes[i]) under `prof` and the ReferenceOrder language;
+ * maxdomcount is ReferenceOrder.maxdomcount (authority divisor 1 + maxdomcount). */
+int yrwi_score_nodes(yrwi_ctx* ctx, const yrwi_node* nodes, int64_t n, const yrwi_profile* prof,
+                     const char* language, int32_t maxdomcount, int64_t* scores);
+
 /* ---- finer-grained drop-ins mirroring the Java split ---- */
 /* == ReferenceContainer.joinExcludeContainers via TermSearch (ReferenceContainer.java:310,
  *    TermSearch.java:42-70): writes the joined container's rows (sorted) to rows_out. */

@@ -854,6 +854,42 @@ class ReferenceOrder:
 # ---------------------------------------------------------------------------
 
 
+def cardinal_node(order: "ReferenceOrder", urlhash: bytes, virtual_age: int, wordsintitle: int, wordcount: int,
+                  llocal: int, lother: int, flags: bytes, language: Optional[str]) -> int:
+    """ReferenceOrder.cardinal(URIMetadataNode) (ReferenceOrder.java:267-296): the
+    Solr node stack's fallback score.  Every term is a Java int, so the sum wraps
+    as an int before it is widened to long; `language` None is a node without a
+    language (String.equals(null) is false).  The authority term uses the order's
+    host counts (ReferenceOrder.authority :213-216)."""
+    rk = order.ranking
+    f = Bitfield(flags)
+    terms = [
+        ishl(256 - dom_length_normalized(urlhash), rk.coeff_domlength),
+        ishl(virtual_age, rk.coeff_date),
+        ishl(wordsintitle, rk.coeff_wordsintitle),
+        ishl(wordcount, rk.coeff_wordsintext),
+        ishl(llocal, rk.coeff_llocal),
+        ishl(lother, rk.coeff_lother),
+        ishl(order.authority(urlhash[6:12]), rk.coeff_authority) if rk.coeff_authority > 12 else 0,
+        ishl(255, rk.coeff_appurl) if f.get(FLAG_APP_DC_IDENTIFIER) else 0,
+        ishl(255, rk.coeff_app_dc_title) if f.get(FLAG_APP_DC_TITLE) else 0,
+        ishl(255, rk.coeff_app_dc_creator) if f.get(FLAG_APP_DC_CREATOR) else 0,
+        ishl(255, rk.coeff_app_dc_subject) if f.get(FLAG_APP_DC_SUBJECT) else 0,
+        ishl(255, rk.coeff_app_dc_description) if f.get(FLAG_APP_DC_DESCRIPTION) else 0,
+        ishl(255, rk.coeff_appemph) if f.get(FLAG_APP_EMPHASIZED) else 0,
+        ishl(255, rk.coeff_catindexof) if f.get(FLAG_CAT_INDEXOF) else 0,
+        ishl(255, rk.coeff_cathasimage) if f.get(FLAG_CAT_HASIMAGE) else 0,
+        ishl(255, rk.coeff_cathasaudio) if f.get(FLAG_CAT_HASAUDIO) else 0,
+        ishl(255, rk.coeff_cathasvideo) if f.get(FLAG_CAT_HASVIDEO) else 0,
+        ishl(255, rk.coeff_cathasapp) if f.get(FLAG_CAT_HASAPP) else 0,
+        ishl(255, rk.coeff_language) if (language is not None and order.language == language) else 0,
+    ]
+    r = 0
+    for t in terms:
+        r = i32(r + t)
+    return r
+
+
 class ReverseQueue:
     """Bounded TreeSet ordered by ReverseElement.compareTo (:414-425)."""
 

@@ -65,6 +65,12 @@ class CStats(ctypes.Structure):
                 ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64)]
 
 
+class CNode(ctypes.Structure):
+    _fields_ = [("urlhash", ctypes.c_uint8 * 12), ("virtual_age", ctypes.c_int32), ("wordsintitle", ctypes.c_int32),
+                ("wordcount", ctypes.c_int32), ("llocal", ctypes.c_int32), ("lother", ctypes.c_int32),
+                ("flags", ctypes.c_uint8 * 4), ("host_count", ctypes.c_int32), ("language", ctypes.c_char * 8)]
+
+
 class CLoadStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
                                               "dropped_terms")]
@@ -100,6 +106,8 @@ SIGNATURES = {
     "yrwi_host_free": (ctypes.c_int, [_VP, _VP]),
     "yrwi_load_heaps": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int32, ctypes.c_int32,
                                        ctypes.POINTER(CLoadStats)]),
+    "yrwi_score_nodes": (ctypes.c_int, [_VP, ctypes.POINTER(CNode), ctypes.c_int64, ctypes.POINTER(CProfile),
+                                        ctypes.c_char_p, ctypes.c_int32, _VP]),
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),

@@ -1135,6 +1135,32 @@ extern "C" int yrwi_query(yrwi_ctx* ctx, const yrwi_query_desc* q, yrwi_hit* out
   return yrwi_query_batch(ctx, q, 1, kmax, out, nout, st);
 }
 
+extern "C" int yrwi_score_nodes(yrwi_ctx* ctx, const yrwi_node* nodes, int64_t n, const yrwi_profile* prof,
+                                const char* language, int32_t maxdomcount, int64_t* scores) {
+  if (!ctx || n < 0 || (n > 0 && (!nodes || !scores))) return YRWI_E_ARG;
+  if (n == 0) return 0;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  yrwi_profile p;
+  if (prof) p = *prof; else yrwi_profile_default(&p);
+  char lang[8] = {0};
+  if (language) std::strncpy(lang, language, 7);  // ReferenceOrder.language (a String; longer never equals)
+  if (language && std::strlen(language) > 7) std::memset(lang, 0xFF, 7);
+  yrwi_node* d_nodes = arena_alloc<yrwi_node>(L, n);
+  yrwi_profile* d_prof = arena_alloc<yrwi_profile>(L, 1);
+  int64_t* d_sc = arena_alloc<int64_t>(L, n);
+  if (!d_nodes || !d_prof || !d_sc) return ctx->fail(YRWI_E_NOMEM, "arena");
+  HIPCHK(ctx, hipMemcpyAsync(d_nodes, nodes, sizeof(yrwi_node) * (size_t)n, hipMemcpyHostToDevice, L->stream));
+  HIPCHK(ctx, hipMemcpyAsync(d_prof, &p, sizeof(p), hipMemcpyHostToDevice, L->stream));
+  if (launch_score_nodes(d_nodes, n, d_prof, lang, maxdomcount, d_sc, L->stream))
+    return ctx->fail(YRWI_E_HIP, "score_nodes launch");
+  HIPCHK(ctx, hipMemcpyAsync(scores, d_sc, sizeof(int64_t) * (size_t)n, hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  return 0;
+}
+
 extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nincl, const uint8_t* excl,
                                  int32_t nexcl, int32_t max_distance, int64_t now_ms, uint8_t* rows_out,
                                  int64_t cap_rows, int64_t* m) {

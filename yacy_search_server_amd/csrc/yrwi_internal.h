@@ -229,6 +229,9 @@ int launch_pull(const RankQ* d_q, int32_t nq, const yrwi_hit* d_stack, const int
 // merge of gathered shard stacks allh[world][nq][kint] into stack[nq][kint] (TreeSet in shard order)
 int launch_gmerge(const RankQ* d_q, const yrwi_hit* d_allh, const int32_t* d_alln, int world, int32_t nq, int32_t kint,
                   uint32_t* d_slot, uint8_t* d_dup, yrwi_hit* d_stack, int32_t* d_scnt, void* stream);
+// cardinal(URIMetadataNode) of n node records
+int launch_score_nodes(const yrwi_node* d_nodes, int64_t n, const yrwi_profile* d_prof, const char* lang8,
+                       int32_t maxdomcount, int64_t* d_scores, void* stream);
 int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* stream);
 

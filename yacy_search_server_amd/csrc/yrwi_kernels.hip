@@ -2176,6 +2176,55 @@ int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk
   return rc(hipGetLastError());
 }
 
+// ReferenceOrder.cardinal(URIMetadataNode) (ReferenceOrder.java:267-296): all
+// terms are Java ints, summed with int wrap, then widened.  lang: the order's
+// language (8 bytes, NUL padded); a node language equal to it as a string scores.
+__global__ void k_score_nodes(const yrwi_node* __restrict__ nodes, int64_t n, const yrwi_profile* __restrict__ prof,
+                              uint64_t lang, int32_t maxdomcount, int64_t* __restrict__ scores) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const yrwi_node& t = nodes[i];
+  const yrwi_profile& rk = *prof;
+  const uint32_t z = t.flags[0] | ((uint32_t)t.flags[1] << 8) | ((uint32_t)t.flags[2] << 16) |
+                     ((uint32_t)t.flags[3] << 24);
+  const int dl = ahpla(t.urlhash[11]) & 3;
+  const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;  // << (8/20) == << 0
+  int32_t r = shl32(256 - dln, rk.coeff_domlength);
+  r = add32(r, shl32(t.virtual_age, rk.coeff_date));
+  r = add32(r, shl32(t.wordsintitle, rk.coeff_wordsintitle));
+  r = add32(r, shl32(t.wordcount, rk.coeff_wordsintext));
+  r = add32(r, shl32(t.llocal, rk.coeff_llocal));
+  r = add32(r, shl32(t.lother, rk.coeff_lother));
+  if (rk.coeff_authority > 12)
+    r = add32(r, shl32(div32(shl32(t.host_count, 8), add32(1, maxdomcount)), rk.coeff_authority));
+  const int32_t c255 = 255;
+  if (z & (1u << 28)) r = add32(r, shl32(c255, rk.coeff_appurl));
+  if (z & (1u << 25)) r = add32(r, shl32(c255, rk.coeff_app_dc_title));
+  if (z & (1u << 26)) r = add32(r, shl32(c255, rk.coeff_app_dc_creator));
+  if (z & (1u << 27)) r = add32(r, shl32(c255, rk.coeff_app_dc_subject));
+  if (z & (1u << 24)) r = add32(r, shl32(c255, rk.coeff_app_dc_description));
+  if (z & (1u << 29)) r = add32(r, shl32(c255, rk.coeff_appemph));
+  if (z & (1u << 0)) r = add32(r, shl32(c255, rk.coeff_catindexof));
+  if (z & (1u << 20)) r = add32(r, shl32(c255, rk.coeff_cathasimage));
+  if (z & (1u << 21)) r = add32(r, shl32(c255, rk.coeff_cathasaudio));
+  if (z & (1u << 22)) r = add32(r, shl32(c255, rk.coeff_cathasvideo));
+  if (z & (1u << 23)) r = add32(r, shl32(c255, rk.coeff_cathasapp));
+  uint64_t nl = 0;
+  for (int j = 0; j < 8; j++) nl |= (uint64_t)(uint8_t)t.language[j] << (8 * j);
+  if (nl != 0 && nl == lang) r = add32(r, shl32(c255, rk.coeff_language));
+  scores[i] = (int64_t)r;
+}
+
+int launch_score_nodes(const yrwi_node* d_nodes, int64_t n, const yrwi_profile* d_prof, const char* lang8,
+                       int32_t maxdomcount, int64_t* d_scores, void* st) {
+  if (n <= 0) return 0;
+  uint64_t lang = 0;
+  for (int j = 0; j < 8 && lang8[j]; j++) lang |= (uint64_t)(uint8_t)lang8[j] << (8 * j);
+  hipLaunchKernelGGL(k_score_nodes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), d_nodes, n, d_prof, lang,
+                     maxdomcount, d_scores);
+  return rc(hipGetLastError());
+}
+
 __global__ void k_reduce_i32(const int32_t* __restrict__ all, int world, int64_t n, int32_t* __restrict__ out,
                              int max_op) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

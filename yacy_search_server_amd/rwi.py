@@ -251,6 +251,26 @@ class RWIIndex:
                                                         language.encode(), now_ms, out.ctypes.data))
         return out
 
+    # ---- ReferenceOrder.cardinal(URIMetadataNode): the Solr node stack ----
+    def score_nodes(self, nodes: Sequence[dict], profile: Optional[RankingProfile] = None, language: str = "en",
+                    maxdomcount: int = 0) -> np.ndarray:
+        """nodes: dicts with urlhash, virtual_age, wordsintitle, wordcount, llocal, lother,
+        flags (4 bytes), host_count, language (str or None) -- the URIMetadataNode fields
+        cardinal reads (ReferenceOrder.java:267-296)."""
+        n = len(nodes)
+        arr = (_lib.CNode * max(1, n))()
+        for i, d in enumerate(nodes):
+            arr[i].urlhash[:] = list(bytes(d["urlhash"]))
+            for f in ("virtual_age", "wordsintitle", "wordcount", "llocal", "lother", "host_count"):
+                setattr(arr[i], f, int(d.get(f, 0)))
+            arr[i].flags[:] = list(bytes(d.get("flags", b"\0\0\0\0"))[:4])
+            arr[i].language = (d.get("language") or "").encode()[:7]
+        out = np.zeros(max(1, n), dtype=np.int64)
+        prof = profile or RankingProfile()
+        _check(self._h, _lib.lib().yrwi_score_nodes(self._h, arr, n, ctypes.byref(prof._c), language.encode(),
+                                                    maxdomcount, out.ctypes.data))
+        return out[:n]
+
     # ---- full query: TermSearch -> normalise -> cardinal -> top-k ----
     def search(self, include: Sequence[bytes], exclude: Sequence[bytes] = (), profile: Optional[RankingProfile] = None,
                language: str = "en", max_distance: int = INTEGER_MAX, now_ms: int = 0, k: int = 100,
