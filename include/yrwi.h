@@ -42,7 +42,8 @@ enum {
   YRWI_E_NULL_LANGUAGE = -7, /* language cell is 0x0000: the reference throws NPE in
                                 ASCII.getBytes(null) (WordReferenceVars.java:315, ReferenceOrder.java:260) */
   YRWI_E_UNSUPPORTED = -8,
-  YRWI_E_LIMIT = -9          /* list longer than 53,687,091 rows (RowSet.java:90-92) */
+  YRWI_E_LIMIT = -9,         /* list longer than 53,687,091 rows (RowSet.java:90-92) */
+  YRWI_E_CAPACITY = -10      /* search event tables full (max_postings given to yrwi_event_open too small) */
 };
 
 typedef struct yrwi_ctx yrwi_ctx;
@@ -212,6 +213,50 @@ typedef struct yrwi_node {
  * maxdomcount is ReferenceOrder.maxdomcount (authority divisor 1 + maxdomcount). */
 int yrwi_score_nodes(yrwi_ctx* ctx, const yrwi_node* nodes, int64_t n, const yrwi_profile* prof,
                      const char* language, int32_t maxdomcount, int64_t* scores);
+
+/* ---- search events: local + remote containers merged per arrival ---- */
+/* A SearchEvent's RWI side (SearchEvent.java:673-836): containers arrive one
+ * after another -- the local joined container from RWIProcess.run (:612-631) and
+ * each remote peer's result container from Protocol.remoteSearchProcess
+ * (Protocol.java:670-830, addRWIs(container, false, ...) at :802).  Every
+ * arrival continues the event's ReferenceOrder (min/max, max-distance fold,
+ * host counts), is settled over itself and then scored; entries already on the
+ * stack keep their arrival-time scores.  The doublecheck set (SearchEvent.
+ * urlhashes), the flag counts and the rwiStack (bound k) persist in device
+ * memory.  Rows are WordReferenceRow bytes in the container's order (a remote
+ * container is in the order the peer's results arrived). */
+typedef struct yrwi_event yrwi_event;
+/* k: stack bound (<= YRWI_MAX_K; the results kept); filter: constraints, its
+ * urlhashes seed the doublecheck set (NULL: unconstrained; its flagcount and
+ * skip_double_dom are not used -- see yrwi_event_result); max_postings: the
+ * most postings the event will receive (sizes the url and host tables). */
+int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms, int32_t k,
+                    const yrwi_filter* filter, int64_t max_postings, yrwi_event** out);
+typedef struct yrwi_arrival {
+  yrwi_event* ev;
+  const uint8_t* rows40;  /* n rows of 40 bytes */
+  int64_t n;
+  int32_t local;          /* addRWIs(local): statistics only */
+  int32_t rc;             /* out: 0 or YRWI_E_* (HASH, NULL_LANGUAGE, CAPACITY) for this arrival */
+} yrwi_arrival;
+/* Applies arrivals in array order (per event); arrivals of different events run
+ * in parallel, one workgroup per event.  Returns the first nonzero rc. */
+int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr);
+typedef struct yrwi_event_info {
+  int32_t flagcount[32];        /* SearchEvent.flagcount */
+  int64_t postings_in;          /* rows received */
+  int64_t admitted_local;       /* local_rwi_available */
+  int64_t admitted_remote;      /* remote_rwi_available */
+  int64_t remote_arrivals;      /* remote_rwi_peerCount */
+  int32_t maxdomcount;          /* ReferenceOrder.maxdomcount (authority profiles only) */
+  int32_t max_distance;         /* max.distance() of the fold (min.distance() is 0) */
+  int32_t err;                  /* YRWI_E_CAPACITY once the event's tables overflowed */
+  int32_t stack_size;
+} yrwi_event_info;
+/* The stack in rwiStack order (best first), up to maxn entries. */
+int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
+                      yrwi_event_info* info);
+void yrwi_event_close(yrwi_ctx* ctx, yrwi_event* ev);
 
 /* ---- finer-grained drop-ins mirroring the Java split ---- */
 /* == ReferenceContainer.joinExcludeContainers via TermSearch (ReferenceContainer.java:310,

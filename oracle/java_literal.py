@@ -1069,6 +1069,48 @@ def rank(container: List[bytes], profile: RankingProfile, language: str, now_ms:
     return [(h, w) for (w, _, h) in q.items]
 
 
+class SearchEventRWI:
+    """The RWI side of one SearchEvent fed container by container
+    (SearchEvent.addRWIs :673-836, called by RWIProcess.run :612-631 for the
+    local container and by Protocol.remoteSearchProcess :802 for every remote
+    peer).  The ReferenceOrder (min/max, distance fold, doms), the doublecheck
+    set, the flag counts and rwiStack persist between calls; each arrival is
+    normalised completely before its entries are scored (the canonical settled
+    order of DESIGN.md §2, per arrival), so entries keep the score they got when
+    they arrived."""
+
+    def __init__(self, profile: RankingProfile, language: str, now_ms: int,
+                 filt: Optional[QueryFilter] = None, maxsize: int = MAX_RESULTS_RWI):
+        self.order = ReferenceOrder(profile, language)
+        self.filt = filt if filt is not None else QueryFilter()
+        self.now_ms = now_ms
+        self.q = ReverseQueue(maxsize)
+        self.local_available = 0
+        self.remote_available = 0
+        self.remote_peers = 0
+
+    def add_rwis(self, container: List[bytes], local: bool) -> int:
+        if not container:                      # index.isEmpty() -> return 0 (:685)
+            return 0
+        if not local:
+            self.remote_peers += 1
+        entries = self.order.normalize_with(container, self.now_ms)
+        n = 0
+        for e in entries:
+            if not self.filt.admit(e):
+                continue
+            self.q.put(self.order.cardinal(e), e.urlHash)
+            n += 1
+        if local:
+            self.local_available += n
+        else:
+            self.remote_available += n
+        return n
+
+    def stack(self) -> List[Tuple[bytes, int]]:
+        return [(h, w) for (w, _, h) in self.q.items]
+
+
 def search(index: Dict[bytes, List[bytes]], include: Iterable[bytes], exclude: Iterable[bytes],
            profile: RankingProfile, language: str = "en", max_distance: int = 2147483647,
            now_ms: int = 0, k: int = 100, filt: Optional[QueryFilter] = None) -> List[Tuple[bytes, int]]:

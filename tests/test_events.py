@@ -1,0 +1,232 @@
+"""Search events: containers arriving one after another.
+
+SearchEvent.addRWIs (SearchEvent.java:673-836) is called for the local joined
+container (RWIProcess.run :612-631) and for every remote peer's result container
+(Protocol.remoteSearchProcess :670-830, addRWIs(local=false) at :802).  The
+ReferenceOrder, the doublecheck set, the flag counts and rwiStack carry over;
+each arrival is settled over itself before it is scored.
+
+CPU: the literal oracle (oracle/java_literal.SearchEventRWI) against the
+single-container path, and the bounded-TreeSet argument the GPU merge relies
+on (sequential puts into a WeakPriorityBlockingQueue == the top-k of the
+distinct (score, hashCode) classes, earliest arrival wins).
+GPU: libyrwi's k_event_add against the oracle, bit-exact, over random arrival
+sequences (duplicates inside and across arrivals, multi-chunk arrivals,
+filters, authority profiles, zero posintext)."""
+
+import numpy as np
+import pytest
+
+import java_literal as jl
+from yacy_search_server_amd import QueryFilter, RankingProfile, synth
+
+NOW = 20741 * 86400000 + 31337
+
+
+def _rows(a):
+    return [bytes(r) for r in np.asarray(a, dtype=np.uint8).reshape(-1, 40)]
+
+
+def _pool():
+    cfg = synth.preset("tiny")
+    idx = synth.build_index(cfg)
+    return cfg, idx
+
+
+def _arrivals(idx, rng, n_remote, local_term=None, zero_pos=False, big=False):
+    """local container (a whole posting list, sorted) + remote containers built
+    from random rows of random lists (same url under other words: different
+    features), shuffled (arrival order), with duplicates inside an arrival."""
+    out = []
+    if local_term is not None:
+        out.append((np.array(idx.list_rows(local_term)), True))
+    all_rows = np.asarray(idx.rows, dtype=np.uint8)
+    for _ in range(n_remote):
+        m = int(rng.integers(0, 3000 if big else 200))
+        take = rng.integers(0, len(all_rows), m)
+        if m > 4:
+            take[: m // 4] = take[rng.integers(0, m, m // 4)]  # duplicates inside the arrival
+        r = all_rows[take].copy()
+        if m:  # word distances (the 'i' column), so the max-distance fold has work
+            d = rng.random(m) < 0.5
+            r[d, 38] = rng.integers(0, 40, int(d.sum()))
+        if zero_pos and m:
+            z = rng.random(m) < 0.3
+            r[z, 34] = 0
+            r[z, 35] = 0
+        out.append((r, False))
+    return out
+
+
+def test_single_local_arrival_equals_rank():
+    _, idx = _pool()
+    t = int(np.argmax(idx.sizes))
+    c = _rows(idx.list_rows(t))
+    ev = jl.SearchEventRWI(jl.RankingProfile(), "en", NOW)
+    ev.add_rwis(c, True)
+    assert ev.stack() == jl.rank(c, jl.RankingProfile(), "en", NOW)
+
+
+def test_later_arrivals_keep_their_scores_and_doublecheck():
+    _, idx = _pool()
+    order = np.argsort(-idx.sizes)
+    a = _rows(idx.list_rows(int(order[0])))
+    b = _rows(idx.list_rows(int(order[1])))
+    ev = jl.SearchEventRWI(jl.RankingProfile(), "en", NOW)
+    ev.add_rwis(a, True)
+    first = dict(ev.stack())
+    ev.add_rwis(b, False)
+    after = dict(ev.stack())
+    for h, w in after.items():
+        if h in first:
+            assert first[h] == w  # scored at arrival, never re-scored
+    seen = {bytes(r[:12]) for r in a}
+    assert ev.remote_available == len({bytes(r[:12]) for r in b} - seen)
+
+
+def test_bounded_treeset_is_topk_of_earliest_classes():
+    rng = np.random.default_rng(3)
+    for trial in range(200):
+        maxsize = int(rng.integers(1, 12))
+        q = jl.ReverseQueue(maxsize)
+        puts = []
+        for s in range(int(rng.integers(0, 60))):
+            w = int(rng.integers(0, 6))
+            h = bytes(rng.integers(65, 70, 12).astype(np.uint8))
+            puts.append((w, jl.bytearray_hashcode(h), h, s))
+            q.put(w, h)
+        best = {}
+        for w, hc, h, s in puts:
+            if (w, hc) not in best and not any(x[2] == h for x in best.values()):
+                best[(w, hc)] = (w, hc, h, s)
+        ref = sorted(best.values(), key=lambda x: (-x[0], -x[1]))[:maxsize]
+        assert [(x[0], x[2]) for x in ref] == [(w, h) for (w, _, h) in q.items], trial
+
+
+def _check_event(ix, arrivals, profile_fields=None, kw=None, k=100, language="en"):
+    lp = jl.RankingProfile()
+    gp = RankingProfile()
+    for f, v in (profile_fields or {}).items():
+        setattr(lp, f, v)
+        setattr(gp, f, v)
+    lf = jl.QueryFilter(**(kw or {}))
+    gf = QueryFilter(**(kw or {})) if kw is not None else None
+    ref = jl.SearchEventRWI(lp, language, NOW, filt=lf)
+    total = sum(len(r) for r, _ in arrivals)
+    with ix.event(gp, language, NOW, k=k, filter=gf, max_postings=total + 16) as ev:
+        for rows, local in arrivals:
+            ref.add_rwis(_rows(rows), local)
+            ev.add_rwis(rows, local)
+        hits, info = ev.results()
+    exp = ref.stack()[:k]
+    assert [(h.urlhash, h.score) for h in hits] == exp
+    assert list(info.flagcount) == lf.flagcount
+    assert info.postings_in == total
+    assert info.admitted_remote == ref.remote_available
+    assert info.admitted_local == ref.local_available
+    assert info.remote_arrivals == ref.remote_peers
+    mx = ref.order.max
+    assert info.max_distance == (mx.distance() if mx is not None else 0)
+    if lp.coeff_authority > 12:
+        assert info.maxdomcount == ref.order.maxdomcount
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_event_arrivals_bit_exact(seed):
+    from yacy_search_server_amd import RWIIndex
+    _, idx = _pool()
+    rng = np.random.default_rng(seed)
+    order = np.argsort(-idx.sizes)
+    ix = RWIIndex(0)
+    try:
+        arr = _arrivals(idx, rng, 12, local_term=int(order[seed]), zero_pos=(seed == 1))
+        _check_event(ix, arr)
+        _check_event(ix, arr, {"coeff_authority": 14, "coeff_worddistance": 15}, k=3000)
+        _check_event(ix, arr[1:], {"coeff_date": 15, "coeff_posintext": 13}, k=10)
+    finally:
+        ix.close()
+
+
+@pytest.mark.gpu
+def test_event_multichunk_and_filters():
+    from yacy_search_server_amd import RWIIndex
+    _, idx = _pool()
+    rng = np.random.default_rng(11)
+    arr = _arrivals(idx, rng, 6, big=True, zero_pos=True)
+    hosts = sorted({bytes(r[6:12]) for r in np.asarray(idx.rows)[rng.integers(0, len(idx.rows), 80)]})
+    seeds = [bytes(r[:12]) for r in np.asarray(idx.rows)[rng.integers(0, len(idx.rows), 50)]]
+    ix = RWIIndex(0)
+    try:
+        _check_event(ix, arr, k=3000)
+        for kw in (dict(constraint=b"\0\0\x10\x01"), dict(language="de"), dict(siteexcludes=hosts),
+                   dict(sitehash=hosts[0], alt_sitehash=hosts[1]), dict(urlhashes=seeds, contentdom=1),
+                   dict(constraint=b"\x01\0\0\0", all_of_constraint=True, strict_contentdom=True, contentdom=2)):
+            _check_event(ix, arr, {"coeff_authority": 13}, kw=kw, k=200)
+    finally:
+        ix.close()
+
+
+@pytest.mark.gpu
+def test_many_events_one_launch():
+    from yacy_search_server_amd import RWIIndex
+    _, idx = _pool()
+    rng = np.random.default_rng(21)
+    ix = RWIIndex(0)
+    try:
+        nev = 40
+        evs, refs, seqs = [], [], []
+        for e in range(nev):
+            arr = _arrivals(idx, rng, int(rng.integers(1, 6)))
+            seqs.append(arr)
+            evs.append(ix.event(None, "en", NOW, k=50, max_postings=sum(len(r) for r, _ in arr) + 16))
+            refs.append(jl.SearchEventRWI(jl.RankingProfile(), "en", NOW))
+        # interleave: every call carries one arrival of many events (and sometimes two of one)
+        step = 0
+        while any(seqs):
+            batch = []
+            for e in range(nev):
+                take = 2 if (step + e) % 7 == 0 else 1
+                for _ in range(take):
+                    if seqs[e]:
+                        rows, local = seqs[e].pop(0)
+                        refs[e].add_rwis(_rows(rows), local)
+                        batch.append((evs[e], rows, local))
+            ix.add_rwis(batch)
+            step += 1
+        for ev, ref in zip(evs, refs):
+            hits, _ = ev.results()
+            assert [(h.urlhash, h.score) for h in hits] == ref.stack()[:50]
+            ev.close()
+    finally:
+        ix.close()
+
+
+@pytest.mark.gpu
+def test_event_errors():
+    from yacy_search_server_amd import RWIIndex
+    from yacy_search_server_amd._lib import YrwiError
+    _, idx = _pool()
+    rows = np.array(idx.list_rows(int(np.argmax(idx.sizes))))
+    ix = RWIIndex(0)
+    try:
+        with ix.event(None, "en", NOW, k=20, max_postings=len(rows)) as ev:
+            ev.add_rwis(rows[:100], True)
+            before, _ = ev.results()
+            bad = rows[100:110].copy()
+            bad[3, 0] = ord("*")
+            with pytest.raises(YrwiError):
+                ev.add_rwis(bad)
+            nolang = rows[100:110].copy()
+            nolang[5, 22:24] = 0
+            with pytest.raises(YrwiError):
+                ev.add_rwis(nolang)
+            after, info = ev.results()
+            assert after == before and info.postings_in == 100
+        with ix.event(None, "en", NOW, k=20, max_postings=0) as ev:
+            big = np.asarray(idx.rows)
+            with pytest.raises(YrwiError):
+                for s in range(0, len(big), 5000):
+                    ev.add_rwis(big[s:s + 5000])
+    finally:
+        ix.close()

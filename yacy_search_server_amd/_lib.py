@@ -71,6 +71,18 @@ class CNode(ctypes.Structure):
                 ("flags", ctypes.c_uint8 * 4), ("host_count", ctypes.c_int32), ("language", ctypes.c_char * 8)]
 
 
+class CArrival(ctypes.Structure):
+    _fields_ = [("ev", ctypes.c_void_p), ("rows40", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("local", ctypes.c_int32), ("rc", ctypes.c_int32)]
+
+
+class CEventInfo(ctypes.Structure):
+    _fields_ = [("flagcount", ctypes.c_int32 * 32), ("postings_in", ctypes.c_int64),
+                ("admitted_local", ctypes.c_int64), ("admitted_remote", ctypes.c_int64),
+                ("remote_arrivals", ctypes.c_int64), ("maxdomcount", ctypes.c_int32),
+                ("max_distance", ctypes.c_int32), ("err", ctypes.c_int32), ("stack_size", ctypes.c_int32)]
+
+
 class CLoadStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
                                               "dropped_terms")]
@@ -108,6 +120,12 @@ SIGNATURES = {
                                        ctypes.POINTER(CLoadStats)]),
     "yrwi_score_nodes": (ctypes.c_int, [_VP, ctypes.POINTER(CNode), ctypes.c_int64, ctypes.POINTER(CProfile),
                                         ctypes.c_char_p, ctypes.c_int32, _VP]),
+    "yrwi_event_open": (ctypes.c_int, [_VP, ctypes.POINTER(CProfile), ctypes.c_char_p, ctypes.c_int64,
+                                       ctypes.c_int32, ctypes.POINTER(CFilter), ctypes.c_int64, _VP]),
+    "yrwi_event_add": (ctypes.c_int, [_VP, ctypes.POINTER(CArrival), ctypes.c_int32]),
+    "yrwi_event_result": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(CHit), ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CEventInfo)]),
+    "yrwi_event_close": (None, [_VP, _VP]),
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),

@@ -1,0 +1,234 @@
+// yrwi_event.cpp -- search events: one SearchEvent's RWI side receiving
+// containers one after another.  The local joined
+// container and every remote peer's result container go through
+// SearchEvent.addRWIs (SearchEvent.java:673-836; remote: Protocol.java:802) and
+// the event's ReferenceOrder, doublecheck set, flag counts and rwiStack carry
+// over between arrivals.  All of that state lives in device memory; k_event_add
+// (yrwi_kernels.hip) applies a batch of arrivals, one workgroup per event.
+#include "yrwi_host.h"
+
+using namespace yrwi;
+
+struct yrwi_event {
+  EvDev h{};         // host copy of the device descriptor
+  void* mem = nullptr;
+  int32_t k = 0;
+};
+
+namespace {
+
+int ceil_log2(int64_t x) {
+  int l = 0;
+  while ((int64_t(1) << l) < x) l++;
+  return l;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms,
+                               int32_t k, const yrwi_filter* filter, int64_t max_postings, yrwi_event** out) {
+  if (!ctx || !out || k <= 0 || k > YRWI_MAX_K || max_postings < 0) return YRWI_E_ARG;
+  *out = nullptr;
+  if (filter && (filter->nsiteexcludes < 0 || filter->nurlhashes < 0 ||
+                 (filter->nsiteexcludes > 0 && !filter->siteexcludes) || (filter->nurlhashes > 0 && !filter->urlhashes)))
+    return ctx->fail(YRWI_E_ARG, "filter: bad siteexcludes / urlhashes");
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+
+  EvDev h{};
+  RankQ& q = h.q;
+  if (prof) q.prof = *prof; else yrwi_profile_default(&q.prof);
+  const char* lang = language ? language : "";
+  const size_t ll = std::strlen(lang);
+  q.lang_ok = ll == 2;
+  q.lang[0] = ll > 0 ? (uint8_t)lang[0] : 0;
+  q.lang[1] = ll > 1 ? (uint8_t)lang[1] : 0;
+  q.now_ms = now_ms != 0 ? now_ms
+                         : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::system_clock::now().time_since_epoch()).count();
+  q.k = k;
+  q.want_authority = q.prof.coeff_authority > 12;
+  std::vector<uint64_t> siteex;
+  std::vector<KeyT> seeds;
+  if (filter) {
+    build_filterq(*filter, &h.f, &siteex, &seeds);
+    h.f.nurl = 0;  // the doublecheck seeds go into the url set
+    h.f.flagcount = nullptr;
+    h.has_filter = 1;
+  }
+  // url set: EV_SUBS sub-tables, each about 4x its share of the keys
+  const int64_t cap = std::max<int64_t>(max_postings + (int64_t)seeds.size(), 1024);
+  h.ulog = std::max(5, ceil_log2((4 * cap + EV_SUBS - 1) / EV_SUBS));
+  const int64_t uslots = (int64_t)EV_SUBS << h.ulog;
+  const int64_t hslots = q.want_authority ? (int64_t)1 << ceil_log2(2 * cap) : 1;
+  q.hmask = (uint64_t)(hslots - 1);
+
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align256(bytes);
+    return o;
+  };
+  const size_t o_st = take(sizeof(EvState));
+  const size_t o_uk = take((size_t)uslots * 8), o_uv = take((size_t)uslots * 8);
+  const size_t o_hk = take((size_t)hslots * 8), o_hc = take((size_t)hslots * 4);
+  const size_t o_stk = take((size_t)2 * k * sizeof(yrwi_hit));
+  const size_t o_sx = take(std::max<size_t>(siteex.size(), 1) * 8);
+  const size_t o_dev = take(sizeof(EvDev));
+  const size_t o_sh = take(std::max<size_t>(seeds.size(), 1) * 8), o_sl = take(std::max<size_t>(seeds.size(), 1));
+  void* mem = nullptr;
+  if (hipMalloc(&mem, off) != hipSuccess) return ctx->fail(YRWI_E_NOMEM, "event allocation failed");
+  uint8_t* base = static_cast<uint8_t*>(mem);
+  h.st = reinterpret_cast<EvState*>(base + o_st);
+  h.ukey = reinterpret_cast<uint64_t*>(base + o_uk);
+  h.uval = reinterpret_cast<uint64_t*>(base + o_uv);
+  q.hkeys = reinterpret_cast<uint64_t*>(base + o_hk);
+  q.hcnt = reinterpret_cast<uint32_t*>(base + o_hc);
+  h.stack = reinterpret_cast<yrwi_hit*>(base + o_stk);
+  h.f.siteex = reinterpret_cast<uint64_t*>(base + o_sx);
+  EvDev* d_dev = reinterpret_cast<EvDev*>(base + o_dev);
+
+  auto fail = [&](int code, const char* m) {
+    lane_sync(L);
+    hipFree(mem);
+    return ctx->fail(code, m);
+  };
+  hipStream_t s = L->stream;
+  if (hipMemsetAsync(base, 0, off, s) != hipSuccess || hipMemsetAsync(h.uval, 0xFF, (size_t)uslots * 8, s) != hipSuccess)
+    return fail(YRWI_E_HIP, "event init");
+  std::vector<uint64_t> sh;
+  std::vector<uint8_t> sl;
+  for (auto& key : seeds) {
+    sh.push_back(key.hi);
+    sl.push_back((uint8_t)key.lo);
+  }
+  std::vector<EvDev> hv{h};
+  if (upload(L, reinterpret_cast<uint64_t*>(base + o_sx), siteex) || upload(L, d_dev, hv) ||
+      upload(L, reinterpret_cast<uint64_t*>(base + o_sh), sh) || upload(L, base + o_sl, sl))
+    return fail(YRWI_E_HIP, "event upload");
+  if (launch_event_seed(d_dev, reinterpret_cast<uint64_t*>(base + o_sh), base + o_sl, (int64_t)sh.size(), s))
+    return fail(YRWI_E_HIP, "event seed launch");
+  int32_t err = 0;
+  if (hipMemcpyAsync(&err, &h.st->err, 4, hipMemcpyDeviceToHost, s) != hipSuccess || lane_sync(L) != hipSuccess)
+    return fail(YRWI_E_HIP, "event open sync");
+  if (err) return fail(err, "doublecheck seeds exceed the event's url table");
+  yrwi_event* e = new yrwi_event;
+  e->h = h;
+  e->mem = mem;
+  e->k = k;
+  *out = e;
+  return 0;
+}
+
+extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
+  if (!ctx || narr < 0 || (narr > 0 && !arr)) return YRWI_E_ARG;
+  if (narr == 0) return 0;
+  for (int32_t i = 0; i < narr; i++) {
+    arr[i].rc = 0;
+    if (!arr[i].ev || arr[i].n < 0 || arr[i].n >= ((int64_t)1 << 31) || (arr[i].n > 0 && !arr[i].rows40))
+      return ctx->fail(YRWI_E_ARG, "bad arrival");
+  }
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  // group the arrivals by event (first-appearance order), keeping their order inside a group
+  std::unordered_map<const yrwi_event*, int32_t> gid;
+  std::vector<const yrwi_event*> evs;
+  for (int32_t i = 0; i < narr; i++)
+    if (gid.emplace(arr[i].ev, (int32_t)evs.size()).second) evs.push_back(arr[i].ev);
+  std::vector<std::vector<int32_t>> members(evs.size());
+  for (int32_t i = 0; i < narr; i++) members[(size_t)gid[arr[i].ev]].push_back(i);
+  int64_t total = 0;
+  for (int32_t i = 0; i < narr; i++) total += arr[i].n;
+  uint8_t* d_rows = arena_alloc<uint8_t>(L, total * YRWI_ROW_BYTES);
+  EvDev* d_ev = arena_alloc<EvDev>(L, (int64_t)evs.size());
+  EvJob* d_jobs = arena_alloc<EvJob>(L, narr);
+  int32_t* d_jb = arena_alloc<int32_t>(L, (int64_t)evs.size() + 1);
+  int32_t* d_status = arena_alloc<int32_t>(L, narr);
+  if (!d_rows || !d_ev || !d_jobs || !d_jb || !d_status) return ctx->fail(YRWI_E_NOMEM, "arena");
+  // the rows of every arrival, concatenated through pinned staging
+  uint8_t* stg = stage_reserve(L, &L->out_stage, (size_t)std::max<int64_t>(total * YRWI_ROW_BYTES, 4), true);
+  if (!stg) return ctx->take(L, YRWI_E_HIP);
+  std::vector<EvDev> hev;
+  std::vector<EvJob> jobs;
+  std::vector<int32_t> jb{0}, job_arr;
+  int64_t roff = 0;
+  for (size_t g = 0; g < evs.size(); g++) {
+    hev.push_back(evs[g]->h);
+    for (int32_t i : members[g]) {
+      EvJob J{};
+      J.ev = (int32_t)g;
+      J.local = arr[i].local != 0;
+      J.rows = d_rows + roff * YRWI_ROW_BYTES;
+      J.n = arr[i].n;
+      if (arr[i].n) std::memcpy(stg + roff * YRWI_ROW_BYTES, arr[i].rows40, (size_t)arr[i].n * YRWI_ROW_BYTES);
+      roff += arr[i].n;
+      jobs.push_back(J);
+      job_arr.push_back(i);
+    }
+    jb.push_back((int32_t)jobs.size());
+  }
+  hipStream_t s = L->stream;
+  if (total) HIPCHK(ctx, hipMemcpyAsync(d_rows, stg, (size_t)total * YRWI_ROW_BYTES, hipMemcpyHostToDevice, s));
+  if (upload(L, d_ev, hev) || upload(L, d_jobs, jobs) || upload(L, d_jb, jb)) return ctx->take(L, YRWI_E_HIP);
+  if (launch_event_add(d_ev, d_jobs, d_jb, (int32_t)evs.size(), d_status, s))
+    return ctx->fail(YRWI_E_HIP, "event_add launch");
+  std::vector<int32_t> st((size_t)narr);
+  HIPCHK(ctx, hipMemcpyAsync(st.data(), d_status, (size_t)narr * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, lane_sync(L));
+  int first = 0;
+  for (size_t j = 0; j < job_arr.size(); j++) {
+    arr[job_arr[j]].rc = st[j];
+    if (st[j] && !first) first = st[j];
+  }
+  if (first == YRWI_E_HASH) return ctx->fail(first, "arrival: url hash is not well-formed Base64");
+  if (first == YRWI_E_NULL_LANGUAGE) return ctx->fail(first, "arrival: row with empty language cell (reference NPE)");
+  if (first == YRWI_E_CAPACITY) return ctx->fail(first, "event tables full: max_postings too small");
+  return first;
+}
+
+extern "C" int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
+                                 yrwi_event_info* info) {
+  if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out)) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  EvState S;
+  HIPCHK(ctx, hipMemcpyAsync(&S, ev->h.st, sizeof(S), hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  const int32_t n = std::min(S.nstack, maxn);
+  if (n > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(out, ev->h.stack + (int64_t)S.cur * ev->k, sizeof(yrwi_hit) * (size_t)n,
+                               hipMemcpyDeviceToHost, L->stream));
+    HIPCHK(ctx, lane_sync(L));
+  }
+  if (nout) *nout = n;
+  if (info) {
+    std::memcpy(info->flagcount, S.flagcount, sizeof(info->flagcount));
+    info->postings_in = S.nin;
+    info->admitted_local = S.nadmit_local;
+    info->admitted_remote = S.nadmit_remote;
+    info->remote_arrivals = S.nremote;
+    info->maxdomcount = S.maxdom;
+    info->max_distance = (S.hasA && S.P > 0) ? std::abs(S.P - S.A) : 0;
+    info->err = S.err;
+    info->stack_size = S.nstack;
+  }
+  return 0;
+}
+
+extern "C" void yrwi_event_close(yrwi_ctx* ctx, yrwi_event* ev) {
+  if (!ev) return;
+  if (ctx) {
+    hipSetDevice(ctx->device);
+    drain(ctx);
+    lane_sync(ctx->lanes[0]);
+  }
+  hipFree(ev->mem);
+  delete ev;
+}

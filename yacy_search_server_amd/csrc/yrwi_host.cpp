@@ -324,6 +324,52 @@ extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostin
 }
 
 // ================================================================== planning
+// yrwi_filter -> FilterQ (device pointers left null), the sorted unique host keys
+// of siteexcludes and the sorted unique url keys of the doublecheck seed set.
+void yrwi::build_filterq(const yrwi_filter& F, FilterQ* Gp, std::vector<uint64_t>* siteex, std::vector<KeyT>* urls) {
+  FilterQ& G = *Gp;
+  std::memset(&G, 0, sizeof(G));
+  std::memcpy(G.constraint, F.constraint, 4);
+  G.has_constraint = F.has_constraint != 0;
+  G.all_of = F.all_of_constraint != 0;
+  G.contentdom = F.contentdom;
+  G.strict = F.strict_contentdom != 0;
+  const size_t ll = strnlen(F.language, sizeof(F.language));
+  G.lang_len = (int32_t)ll;
+  std::memcpy(G.lang, F.language, ll);
+  auto host_key = [](const uint8_t* h, uint64_t* k) {
+    uint64_t x = 0;
+    for (int j = 0; j < 6; j++) {
+      if (AHP[h[j]] < 0) return false;
+      x = (x << 6) | (uint64_t)AHP[h[j]];
+    }
+    *k = x;
+    return true;
+  };
+  // a host hash outside the alphabet matches no row (rows are validated)
+  G.has_site = F.has_sitehash != 0;
+  G.has_alt = F.has_alt_sitehash != 0 && host_key(F.alt_sitehash, &G.altsite);
+  if (G.has_site && !host_key(F.sitehash, &G.site)) G.site = ~0ull;
+  std::vector<uint64_t>& v = *siteex;
+  v.clear();
+  for (int i = 0; i < F.nsiteexcludes; i++) {
+    uint64_t k;
+    if (host_key(F.siteexcludes + 6 * i, &k)) v.push_back(k);
+  }
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  G.nsiteex = (int64_t)v.size();
+  std::vector<KeyT>& u = *urls;
+  u.clear();
+  for (int i = 0; i < F.nurlhashes; i++) {
+    KeyT k;
+    if (key_of(F.urlhashes + 12 * i, &k)) u.push_back(k);
+  }
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  G.nurl = (int64_t)u.size();
+}
+
 static int plan_query(const yrwi_ctx* ix, Lane* ctx, const yrwi_query_desc& d, Plan* P) {
   P->maxd = d.max_distance;
   P->k = std::min<int32_t>(std::max<int32_t>(d.k, 0), YRWI_MAX_K);
@@ -711,47 +757,12 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       if (fidx[(size_t)qi] < 0) continue;
       const yrwi_filter& F = *plans[(size_t)qi].filter;
       FilterQ& G = fq[(size_t)fidx[(size_t)qi]];
-      std::memset(&G, 0, sizeof(G));
-      std::memcpy(G.constraint, F.constraint, 4);
-      G.has_constraint = F.has_constraint != 0;
-      G.all_of = F.all_of_constraint != 0;
-      G.contentdom = F.contentdom;
-      G.strict = F.strict_contentdom != 0;
-      const size_t ll = strnlen(F.language, sizeof(F.language));
-      G.lang_len = (int32_t)ll;
-      std::memcpy(G.lang, F.language, ll);
-      auto host_key = [](const uint8_t* h, uint64_t* k) {
-        uint64_t x = 0;
-        for (int j = 0; j < 6; j++) {
-          if (AHP[h[j]] < 0) return false;
-          x = (x << 6) | (uint64_t)AHP[h[j]];
-        }
-        *k = x;
-        return true;
-      };
-      // a host hash outside the alphabet matches no row (rows are validated)
-      G.has_site = F.has_sitehash != 0;
-      G.has_alt = F.has_alt_sitehash != 0 && host_key(F.alt_sitehash, &G.altsite);
-      if (G.has_site && !host_key(F.sitehash, &G.site)) G.site = ~0ull;
-      sx0[(size_t)fidx[(size_t)qi]] = (int64_t)sx.size();
       std::vector<uint64_t> v;
-      for (int i = 0; i < F.nsiteexcludes; i++) {
-        uint64_t k;
-        if (host_key(F.siteexcludes + 6 * i, &k)) v.push_back(k);
-      }
-      std::sort(v.begin(), v.end());
-      v.erase(std::unique(v.begin(), v.end()), v.end());
-      G.nsiteex = (int64_t)v.size();
+      std::vector<KeyT> u;
+      build_filterq(F, &G, &v, &u);
+      sx0[(size_t)fidx[(size_t)qi]] = (int64_t)sx.size();
       sx.insert(sx.end(), v.begin(), v.end());
       uh0[(size_t)fidx[(size_t)qi]] = (int64_t)uh.size();
-      std::vector<KeyT> u;
-      for (int i = 0; i < F.nurlhashes; i++) {
-        KeyT k;
-        if (key_of(F.urlhashes + 12 * i, &k)) u.push_back(k);
-      }
-      std::sort(u.begin(), u.end());
-      u.erase(std::unique(u.begin(), u.end()), u.end());
-      G.nurl = (int64_t)u.size();
       for (auto& k : u) { uh.push_back(k.hi); ul.push_back((uint8_t)k.lo); }
     }
     FilterQ* d_fq = arena_alloc<FilterQ>(ctx, nf);

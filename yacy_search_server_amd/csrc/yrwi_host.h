@@ -280,6 +280,8 @@ struct CtxBase {
 };
 
 void drain(CtxBase* ctx);
+// yrwi_filter -> FilterQ (device pointers unset) + sorted unique siteexclude host keys and doublecheck url keys
+void build_filterq(const yrwi_filter& F, FilterQ* G, std::vector<uint64_t>* siteex, std::vector<KeyT>* urls);
 
 #define HIPCHK(ctx, x)                                                                 \
   do {                                                                                \

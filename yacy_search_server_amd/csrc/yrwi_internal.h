@@ -235,4 +235,52 @@ int launch_score_nodes(const yrwi_node* d_nodes, int64_t n, const yrwi_profile* 
 int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
                      const NormState* d_norm, int64_t* d_scores, void* stream);
 
+// ------------------------------------------------ search events
+// A SearchEvent that receives containers one after another (the local RWI
+// process and every remote peer, SearchEvent.addRWIs :673-836 from
+// RWIProcess.run and Protocol.remoteSearchProcess :802): normalisation state,
+// host counts, the doublecheck url set, the flag counts and the rwiStack persist
+// across arrivals in device memory.
+constexpr int EV_THREADS = 256;
+constexpr int EV_CH = 1024;    // arrival rows per chunk (4 per thread)
+constexpr int EV_SUBS = 512;   // url-set sub-tables (9 key bits select one, see uset_slot)
+
+struct EvState {
+  int32_t started;             // ReferenceOrder.min/max exist
+  int32_t P, A, hasA;          // max-distance fold
+  int32_t mn[NF], mx[NF];
+  int32_t va_mn, va_mx;
+  int32_t maxdom;              // ReferenceOrder.maxdomcount
+  int32_t nstack, cur;         // stack entries, current stack half
+  int32_t epoch;               // non-empty arrivals applied
+  int32_t err;                 // YRWI_E_* once a table overflowed (event unusable)
+  int32_t pad;
+  int32_t flagcount[32];       // SearchEvent.flagcount
+  int64_t nin, nadmit_local, nadmit_remote, nremote;
+  double tf_mn, tf_mx;
+};
+
+struct EvDev {
+  RankQ q;          // prof, lang, now_ms, want_authority, host table (hkeys/hcnt/hmask), k = stack bound
+  FilterQ f;        // addRWIs constraints (doublecheck seeds live in the url set)
+  int32_t has_filter, ulog;
+  EvState* st;
+  uint64_t* ukey;   // url set: EV_SUBS << ulog slots
+  uint64_t* uval;   // (epoch << 32) | first admitted index, ~0 = none
+  yrwi_hit* stack;  // 2 * q.k entries (double buffer)
+};
+
+struct EvJob {
+  int32_t ev;       // index into the EvDev array
+  int32_t local;
+  const uint8_t* rows;
+  int64_t n;
+};
+
+// one workgroup per event: jobs [jb[b], jb[b+1]) of the same event, in arrival order; status[j] = 0 / YRWI_E_*
+int launch_event_add(const EvDev* d_ev, const EvJob* d_jobs, const int32_t* d_jb, int32_t nblocks, int32_t* d_status,
+                     void* stream);
+// seeds the url set with the doublecheck urls of the filter (epoch 0)
+int launch_event_seed(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, void* stream);
+
 }  // namespace yrwi

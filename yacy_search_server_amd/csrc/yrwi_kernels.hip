@@ -1419,6 +1419,8 @@ __device__ __forceinline__ bool sorted_has_u64(const uint64_t* __restrict__ a, i
 
 __device__ __forceinline__ bool flag_bit(const Row& r, int j) { return (r.b(O_Z + (j >> 3)) >> (j & 7)) & 1u; }
 
+__device__ __forceinline__ bool passes(const FilterQ& F, const Row& r);
+
 // returns true if the posting enters the stack; counts flags into sFlag (LDS) when asked
 __device__ __forceinline__ bool admit(const FilterQ& F, const Row& r, int32_t* sFlag) {
   if (F.nurl) {  // doublecheck: url already in SearchEvent.urlhashes
@@ -1437,6 +1439,11 @@ __device__ __forceinline__ bool admit(const FilterQ& F, const Row& r, int32_t* s
     const uint32_t z = (r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24));
     for (uint32_t m = z; m; m &= m - 1) atomicAdd(&sFlag[__ffs(m) - 1], 1);
   }
+  return passes(F, r);
+}
+
+// the constraints after the doublecheck and the flag counts (:749-802)
+__device__ __forceinline__ bool passes(const FilterQ& F, const Row& r) {
   if (F.has_constraint) {
     bool ok = F.all_of ? true : false;
     for (int j = 0; j < 32; j++) {
@@ -2274,6 +2281,433 @@ int launch_score_all(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int
   if (total_chunks <= 0) return 0;
   hipLaunchKernelGGL(k_score_all, dim3((unsigned)total_chunks), dim3(256), 0, S(st), d_q, d_chunk_q, d_norm,
                      d_scores);
+  return rc(hipGetLastError());
+}
+
+// ======================================= search events
+// SearchEvent.addRWIs (SearchEvent.java:673-836) applied to one container after
+// another -- the local RWI process and every remote peer's result
+// (Protocol.remoteSearchProcess :670-830 -> addRWIs(local=false) :802).  The
+// per-arrival semantics: normalizeWith continues the event's ReferenceOrder
+// (min/max, max-distance fold, host counts; settled over the arrival before it
+// is scored, as the local path), the doublecheck set, the flag counts and the
+// bounded rwiStack carry over; entries already on the stack keep the score they
+// were given on arrival.  One workgroup owns an event for a launch and applies
+// its arrivals in order, so all event state is touched by one workgroup only.
+
+__device__ __forceinline__ uint64_t ld_dev(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_dev32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Url set of 72-bit url keys with 64-bit CAS: 9 key bits (XOR-mixed with the
+// other 63, a bijection) choose one of EV_SUBS sub-tables and the other 63 bits
+// plus an occupied bit are the stored word, so equal words in one sub-table are
+// equal keys and an insert is one compare-and-swap.
+__device__ __forceinline__ void uset_slot(uint64_t hi, uint32_t lo, int ulog, uint64_t& word, int64_t& base,
+                                          uint32_t& start) {
+  const uint64_t h63 = hi >> 1;
+  const uint32_t b9 = ((uint32_t)(hi & 1u) << 8) | (lo & 0xFFu);
+  const uint64_t m = mix64(h63);
+  base = (int64_t)((b9 ^ (uint32_t)m) & (uint32_t)(EV_SUBS - 1)) << ulog;
+  start = (uint32_t)(m >> 32);
+  word = h63 | (1ull << 63);
+}
+__device__ int64_t uset_insert(uint64_t* key, int ulog, uint64_t hi, uint32_t lo) {
+  uint64_t w;
+  int64_t base;
+  uint32_t st;
+  uset_slot(hi, lo, ulog, w, base, st);
+  const uint32_t mask = (1u << ulog) - 1;
+  for (uint32_t t = 0; t <= mask; t++) {
+    const int64_t s = base + ((st + t) & mask);
+    const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(key + s), 0ull, (unsigned long long)w);
+    if (prev == 0 || prev == w) return s;
+  }
+  return -1;
+}
+__device__ int64_t uset_find(const uint64_t* key, int ulog, uint64_t hi, uint32_t lo) {
+  uint64_t w;
+  int64_t base;
+  uint32_t st;
+  uset_slot(hi, lo, ulog, w, base, st);
+  const uint32_t mask = (1u << ulog) - 1;
+  for (uint32_t t = 0; t <= mask; t++) {
+    const int64_t s = base + ((st + t) & mask);
+    const uint64_t k = ld_dev(key + s);
+    if (k == w) return s;
+    if (k == 0) return -1;
+  }
+  return -1;
+}
+
+// event host counts (ReferenceOrder.doms, ConcurrentScoreMap.inc :184): keys host36 + 1
+__device__ int64_t htab_insert(uint64_t* keys, uint64_t mask, uint64_t key) {
+  uint64_t s = mix64(key) & mask;
+  for (uint64_t t = 0; t <= mask; t++) {
+    const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(keys + s), 0ull, (unsigned long long)key);
+    if (prev == 0 || prev == key) return (int64_t)s;
+    s = (s + 1) & mask;
+  }
+  return -1;
+}
+__device__ int32_t htab_count(const uint64_t* keys, const uint32_t* cnt, uint64_t mask, uint64_t key) {
+  uint64_t s = mix64(key) & mask;
+  for (uint64_t t = 0; t <= mask; t++) {
+    const uint64_t k = ld_dev(keys + s);
+    if (k == key) return (int32_t)ld_dev32(cnt + s);
+    if (k == 0) return 0;
+    s = (s + 1) & mask;
+  }
+  return 0;
+}
+
+__global__ void k_event_seed(const EvDev* __restrict__ ev, const uint64_t* __restrict__ hi,
+                             const uint8_t* __restrict__ lo, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s = uset_insert(ev->ukey, ev->ulog, hi[i], lo[i]);
+  if (s < 0) atomicExch(&ev->st->err, (int32_t)YRWI_E_CAPACITY);
+  else atomicMin(reinterpret_cast<unsigned long long*>(ev->uval + s), 0ull);  // epoch 0: in urlhashes from the start
+}
+
+__global__ __launch_bounds__(EV_THREADS) void k_event_add(const EvDev* __restrict__ evs,
+                                                          const EvJob* __restrict__ jobs,
+                                                          const int32_t* __restrict__ jb,
+                                                          int32_t* __restrict__ status) {
+  __shared__ EvState S;
+  __shared__ NormState N;
+  __shared__ int32_t sP[EV_CH], sO[EV_CH];
+  __shared__ uint64_t sK1[EV_CH], sK2[EV_CH];
+  __shared__ Cand sC[EV_CH];
+  __shared__ int32_t sKeep[EV_CH + 1];
+  __shared__ int32_t sSegM[65], sSegL[65], sSegP[65];
+  __shared__ int32_t sFlag[32];
+  __shared__ int32_t sRedI[EV_THREADS / 64][2 * NF + 2];
+  __shared__ double sRedD[EV_THREADS / 64][2];
+  __shared__ int32_t sScan[16];
+  __shared__ int32_t sMisc[8];  // 0 validation bits, 1 candidates, 2 admitted, 3 max host count, 4 overflow
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j0 = jb[blockIdx.x], j1 = jb[blockIdx.x + 1];
+  const EvDev& E = evs[jobs[j0].ev];
+  const RankQ& Q = E.q;
+  const int32_t K = Q.k;
+  if (tid == 0) S = *E.st;
+  __syncthreads();
+  for (int j = j0; j < j1; j++) {
+    const EvJob J = jobs[j];
+    const int64_t n = J.n;
+    if (S.err || n <= 0) {
+      if (tid == 0) status[j] = S.err;
+      continue;
+    }
+    const uint8_t* rows = J.rows;
+    if (tid < 8) sMisc[tid] = 0;
+    __syncthreads();
+    // ---- validation: Base64 url hashes, a language cell (the reference NPEs on 0x0000)
+    {
+      int bad = 0;
+      for (int64_t i = tid; i < n; i += EV_THREADS) {
+        const Row R = load_row(rows + i * YRWI_ROW_BYTES);
+        for (int q = 0; q < 12; q++) bad |= ahpla(R.b(q)) < 0 ? 1 : 0;
+        if (R.b(O_L) == 0 && R.b(O_L + 1) == 0) bad |= 2;
+      }
+      if (bad) atomicOr(&sMisc[0], bad);
+      __syncthreads();
+      const int verr = sMisc[0];
+      if (verr) {
+        if (tid == 0) status[j] = (verr & 1) ? YRWI_E_HASH : YRWI_E_NULL_LANGUAGE;
+        __syncthreads();
+        continue;
+      }
+    }
+    // ---- normalizeWith over the arrival, continuing the event's min/max (:163-210)
+    const bool first = !S.started;
+    int32_t mn[NF], mx[NF], vmn = BIG, vmx = -1;
+    double tmn = 1e300, tmx = -1e300;
+    for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
+    int32_t fP = S.P, fA = S.A;
+    int fH = S.hasA;
+    for (int64_t c0 = 0; c0 < n; c0 += EV_CH) {
+      const int m = (int)min((int64_t)EV_CH, n - c0);
+      for (int s = 0; s < EV_CH / EV_THREADS; s++) {
+        const int li = s * EV_THREADS + tid;
+        if (li >= m) break;
+        const Row R = load_row(rows + (c0 + li) * YRWI_ROW_BYTES);
+        const Feat t = decode(R);
+        int32_t a = t.a, od = t.od;
+        if (first && c0 == 0 && li == 0) { a = clamp_days(a, Q.now_ms); od = 0; }  // the clone (:357-361)
+        for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], t.f[f]); mx[f] = max(mx[f], t.f[f]); }
+        vmn = min(vmn, a);
+        vmx = max(vmx, a);
+        tmn = fmin(tmn, t.tf);
+        tmx = fmax(tmx, t.tf);
+        sP[li] = t.p;
+        sO[li] = od;
+      }
+      __syncthreads();
+      if (wv == 0) {  // the order-dependent max-distance fold, 64 elements a round
+        if (first && c0 == 0) { fP = sP[0]; fA = 0; fH = 0; }
+        for (int base = 0; base < m; base += 64) {
+          const int i = base + lane;
+          const bool v = i < m;
+          const int32_t p = v ? sP[i] : 0, od = v ? sO[i] : 0;
+          const int32_t Pi = max(fP, wave_incl_max(p));
+          int32_t Pprev = __shfl_up(Pi, 1, 64);
+          if (lane == 0) Pprev = fP;
+          const bool rec = v && Pi > Pprev;  // a new running maximum of posintext starts a segment
+          const uint64_t rm = __ballot(rec);
+          const int seg = __popcll(rm & (lane == 63 ? ~0ull : ((2ull << lane) - 1)));
+          sSegM[lane] = 0;
+          sSegL[lane] = -1;
+          if (lane == 0) { sSegM[64] = 0; sSegL[64] = -1; }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          if (rec) sSegP[seg] = Pi;
+          if (v) {
+            atomicMax(&sSegM[seg], od);
+            if (od > 0) atomicMax(&sSegL[seg], lane);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          const int nseg = __popcll(rm);
+          if (lane == 0) {
+            Fold fd{fP, fA, fH != 0};
+            for (int sg = 0; sg <= nseg; sg++) {
+              const int32_t Ls = sSegL[sg];
+              fd.piece(sg == 0 ? fP : sSegP[sg], sSegM[sg], Ls >= 0 ? sO[base + Ls] : 0);
+            }
+            fP = fd.P;
+            fA = fd.A;
+            fH = fd.hasA ? 1 : 0;
+          }
+          fP = __shfl(fP, 0, 64);
+          fA = __shfl(fA, 0, 64);
+          fH = __shfl(fH, 0, 64);
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      __syncthreads();
+    }
+    for (int f = 0; f < NF; f++) {
+      const int32_t a = wave_min_i(mn[f]), b = wave_max_i(mx[f]);
+      if (lane == 0) { sRedI[wv][f] = a; sRedI[wv][NF + f] = b; }
+    }
+    {
+      const int32_t a = wave_min_i(vmn), b = wave_max_i(vmx);
+      const double c = wave_min_d(tmn), d = wave_max_d(tmx);
+      if (lane == 0) { sRedI[wv][2 * NF] = a; sRedI[wv][2 * NF + 1] = b; sRedD[wv][0] = c; sRedD[wv][1] = d; }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 0; w < EV_THREADS / 64; w++) {
+        for (int f = 0; f < NF; f++) {
+          S.mn[f] = (first && w == 0) ? sRedI[w][f] : min(S.mn[f], sRedI[w][f]);
+          S.mx[f] = (first && w == 0) ? sRedI[w][NF + f] : max(S.mx[f], sRedI[w][NF + f]);
+        }
+        S.va_mn = (first && w == 0) ? sRedI[w][2 * NF] : min(S.va_mn, sRedI[w][2 * NF]);
+        S.va_mx = (first && w == 0) ? sRedI[w][2 * NF + 1] : max(S.va_mx, sRedI[w][2 * NF + 1]);
+        S.tf_mn = (first && w == 0) ? sRedD[w][0] : fmin(S.tf_mn, sRedD[w][0]);
+        S.tf_mx = (first && w == 0) ? sRedD[w][1] : fmax(S.tf_mx, sRedD[w][1]);
+      }
+      S.P = fP;
+      S.A = fA;
+      S.hasA = fH;
+      S.started = 1;
+    }
+    // ---- host counts (doms, maxdomcount; only read by authority)
+    if (Q.want_authority) {
+      int32_t hm = 0, ovf = 0;
+      for (int64_t i = tid; i < n; i += EV_THREADS) {
+        const Row R = load_row(rows + i * YRWI_ROW_BYTES);
+        const int64_t s = htab_insert(Q.hkeys, Q.hmask, host36(R) + 1);
+        if (s < 0) ovf = 1;
+        else hm = max(hm, (int32_t)atomicAdd(Q.hcnt + s, 1u) + 1);
+      }
+      hm = wave_max_i(hm);
+      if (lane == 0 && hm) atomicMax(&sMisc[3], hm);
+      if (ovf) atomicOr(&sMisc[4], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      S.maxdom = max(S.maxdom, sMisc[3]);
+      for (int f = 0; f < NF; f++) { N.mn[f] = S.mn[f]; N.mx[f] = S.mx[f]; }
+      N.va_mn = S.va_mn;
+      N.va_mx = S.va_mx;
+      N.tf_mn = S.tf_mn;
+      N.tf_mx = S.tf_mx;
+      N.maxdom = S.maxdom;
+      N.nvalid = 1;
+      Fold fd{S.P, S.A, S.hasA != 0};
+      N.D = fd.D();
+      for (int f = 0; f < NF; f++) N.rcp[f] = N.mx[f] != N.mn[f] ? 1.0 / (double)(N.mx[f] - N.mn[f]) : 0.0;
+      N.rcp[NF] = N.va_mx != N.va_mn ? 1.0 / (double)(N.va_mx - N.va_mn) : 0.0;
+      N.rcp[NF + 1] = N.D != 0 ? 1.0 / (double)N.D : 0.0;
+    }
+    // ---- doublecheck: the first occurrence of a url passing the constraints is admitted (:736-805)
+    const uint32_t ep = (uint32_t)S.epoch + 1;
+    {
+      int ovf = 0;
+      for (int64_t i = tid; i < n; i += EV_THREADS) {
+        const Row R = load_row(rows + i * YRWI_ROW_BYTES);
+        if (E.has_filter && !passes(E.f, R)) continue;
+        uint64_t hi;
+        uint32_t lo;
+        row_key(R, hi, lo);
+        const int64_t s = uset_insert(E.ukey, E.ulog, hi, lo);
+        if (s < 0) { ovf = 1; continue; }
+        atomicMin(reinterpret_cast<unsigned long long*>(E.uval + s), ((uint64_t)ep << 32) | (uint64_t)i);
+      }
+      if (ovf) atomicOr(&sMisc[4], 1);
+    }
+    __threadfence();
+    __syncthreads();
+    if (sMisc[4]) {  // a table is full: the event is unusable (max_postings too small)
+      if (tid == 0) { S.err = YRWI_E_CAPACITY; status[j] = YRWI_E_CAPACITY; }
+      __syncthreads();
+      continue;
+    }
+    // ---- flag counts, cardinal, rwiStack.put per chunk
+    if (tid < 32) sFlag[tid] = 0;
+    int32_t nadm = 0;
+    for (int64_t c0 = 0; c0 < n; c0 += EV_CH) {
+      const int m = (int)min((int64_t)EV_CH, n - c0);
+      if (tid == 0) sMisc[1] = 0;
+      __syncthreads();
+      for (int s = 0; s < EV_CH / EV_THREADS; s++) {
+        const int li = s * EV_THREADS + tid;
+        if (li >= m) break;
+        const int64_t i = c0 + li;
+        const Row R = load_row(rows + i * YRWI_ROW_BYTES);
+        uint64_t hi;
+        uint32_t lo;
+        row_key(R, hi, lo);
+        const int64_t idx = uset_find(E.ukey, E.ulog, hi, lo);
+        const uint64_t v = idx >= 0 ? ld_dev(E.uval + idx) : ~0ull;
+        if (idx >= 0 && (uint32_t)(v >> 32) < ep) continue;  // already in urlhashes: dropped uncounted
+        const bool found = idx >= 0;
+        const uint32_t fi = found ? (uint32_t)v : 0xFFFFFFFFu;
+        if (!found || (uint32_t)i <= fi) {  // reaches the flag count (later duplicates hit the doublecheck)
+          const uint32_t z = (R.b(O_Z) | (R.b(O_Z + 1) << 8) | (R.b(O_Z + 2) << 16) | (R.b(O_Z + 3) << 24));
+          for (uint32_t mm = z; mm; mm &= mm - 1) atomicAdd(&sFlag[__ffs(mm) - 1], 1);
+        }
+        if (found && (uint32_t)i == fi) {
+          const Feat t = decode(R);
+          const int32_t hc = Q.want_authority ? htab_count(Q.hkeys, Q.hcnt, Q.hmask, host36(R) + 1) : 0;
+          const int64_t sc = cardinal(R, t, N, Q, hc);
+          const int slot = atomicAdd(&sMisc[1], 1);
+          sK1[slot] = (uint64_t)sc ^ 0x8000000000000000ull;
+          sK2[slot] = ((uint64_t)((uint32_t)url_hashcode(R) ^ 0x80000000u) << 32) | (uint64_t)(~(uint32_t)i);
+          nadm++;
+        }
+      }
+      __syncthreads();
+      const int nc = sMisc[1];
+      __syncthreads();  // every thread has nc before the next chunk resets it
+      if (nc == 0) continue;
+      const int NP = pow2_at_least(nc);
+      for (int x = nc + tid; x < NP; x += EV_THREADS) { sK1[x] = 0; sK2[x] = 0; }
+      __syncthreads();
+      bitonic_desc<EV_THREADS>(sK1, sK2, NP);
+      int32_t dist;
+      const int32_t c = dedupe_take<EV_THREADS>(sK1, sK2, NP, K, sC, sScan, &dist);
+      __syncthreads();
+      // merge the chunk's TreeSet classes into the stack: an entry equal in
+      // (score, hashCode) to one already there is rejected (it arrived later)
+      const yrwi_hit* cur = E.stack + (int64_t)S.cur * K;
+      yrwi_hit* nxt = E.stack + (int64_t)(S.cur ^ 1) * K;
+      const int32_t ns = S.nstack;
+      int32_t keep[EV_CH / EV_THREADS], pos[EV_CH / EV_THREADS], nk = 0;
+      for (int q = 0; q < EV_CH / EV_THREADS; q++) {
+        const int x = tid * (EV_CH / EV_THREADS) + q;
+        keep[q] = 0;
+        pos[q] = 0;
+        if (x >= c) continue;
+        const int64_t sc = (int64_t)(sC[x].k1 ^ 0x8000000000000000ull);
+        const int32_t tb = (int32_t)((uint32_t)(sC[x].k2 >> 32) ^ 0x80000000u);
+        int lo = 0, hi = ns;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const int64_t hs = cur[mid].score;
+          const int32_t ht = cur[mid].tiebreak;
+          if (hs > sc || (hs == sc && ht > tb)) lo = mid + 1; else hi = mid;
+        }
+        const bool dup = lo < ns && cur[lo].score == sc && cur[lo].tiebreak == tb;
+        keep[q] = dup ? 0 : 1;
+        pos[q] = lo;
+        nk += keep[q];
+      }
+      int32_t tot;
+      int32_t off = block_excl_sum<EV_THREADS>(nk, sScan, &tot);
+      for (int q = 0; q < EV_CH / EV_THREADS; q++) {
+        const int x = tid * (EV_CH / EV_THREADS) + q;
+        if (x < c) sKeep[x] = off;
+        if (keep[q]) {
+          const int32_t o = off + pos[q];
+          if (o < K) {
+            yrwi_hit h;
+            const uint32_t ai = ~(uint32_t)sC[x].k2;
+            const uint8_t* rr = rows + (int64_t)ai * YRWI_ROW_BYTES;
+            for (int b = 0; b < 12; b++) h.urlhash[b] = rr[b];
+            h.tiebreak = (int32_t)((uint32_t)(sC[x].k2 >> 32) ^ 0x80000000u);
+            h.score = (int64_t)(sC[x].k1 ^ 0x8000000000000000ull);
+            nxt[o] = h;
+          }
+          off++;
+        }
+      }
+      if (tid == 0) sKeep[c] = tot;
+      __syncthreads();
+      for (int y = tid; y < ns; y += EV_THREADS) {
+        const yrwi_hit h = cur[y];
+        int lo = 0, hi = c;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const int64_t cs = (int64_t)(sC[mid].k1 ^ 0x8000000000000000ull);
+          const int32_t ct = (int32_t)((uint32_t)(sC[mid].k2 >> 32) ^ 0x80000000u);
+          if (cs > h.score || (cs == h.score && ct > h.tiebreak)) lo = mid + 1; else hi = mid;
+        }
+        const int32_t o = y + sKeep[lo];
+        if (o < K) nxt[o] = h;
+      }
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) {
+        S.nstack = min(K, ns + tot);
+        S.cur ^= 1;
+      }
+      __syncthreads();
+    }
+    nadm = wave_sum_i(nadm);
+    if (lane == 0 && nadm) atomicAdd(&sMisc[2], nadm);
+    __syncthreads();
+    if (tid < 32) S.flagcount[tid] += sFlag[tid];
+    if (tid == 0) {
+      S.epoch = (int32_t)ep;
+      S.nin += n;
+      if (J.local) S.nadmit_local += sMisc[2];
+      else { S.nadmit_remote += sMisc[2]; S.nremote += 1; }
+      status[j] = 0;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *E.st = S;
+}
+
+int launch_event_add(const EvDev* d_ev, const EvJob* d_jobs, const int32_t* d_jb, int32_t nblocks, int32_t* d_status,
+                     void* st) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(k_event_add, dim3((unsigned)nblocks), dim3(EV_THREADS), 0, S(st), d_ev, d_jobs, d_jb, d_status);
+  return rc(hipGetLastError());
+}
+
+int launch_event_seed(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_event_seed, dim3(nblk(n)), dim3(256), 0, S(st), d_ev, d_hi, d_lo, n);
   return rc(hipGetLastError());
 }
 

@@ -143,6 +143,46 @@ class QueryFilter:
         return list(self._flags)
 
 
+class SearchEvent:
+    """One SearchEvent's RWI side (SearchEvent.addRWIs, SearchEvent.java:673-836):
+    the local container and remote peers' containers (Protocol.java:802) arrive
+    one after another; normalisation, doublecheck set, flag counts and the
+    rwiStack persist on the GPU between arrivals (yrwi_event_* in include/yrwi.h)."""
+
+    def __init__(self, index: "RWIIndex", profile: Optional[RankingProfile], language: str, now_ms: int, k: int,
+                 filter: Optional[QueryFilter], max_postings: int):
+        self._ix = index
+        self.k = k
+        prof = profile or RankingProfile()
+        e = ctypes.c_void_p()
+        fp = ctypes.byref(filter.c) if filter is not None else None
+        _check(index._h, _lib.lib().yrwi_event_open(index._h, ctypes.byref(prof._c), language.encode(), now_ms, k, fp,
+                                                    max_postings, ctypes.byref(e)))
+        self._e = e
+
+    def add_rwis(self, rows: np.ndarray, local: bool = False) -> int:
+        return self._ix.add_rwis([(self, rows, local)])[0]
+
+    def results(self) -> Tuple[List["Hit"], "CEventInfo"]:
+        out = (_lib.CHit * max(1, self.k))()
+        n = ctypes.c_int32()
+        info = _lib.CEventInfo()
+        _check(self._ix._h, _lib.lib().yrwi_event_result(self._ix._h, self._e, out, self.k, ctypes.byref(n),
+                                                         ctypes.byref(info)))
+        return [Hit(bytes(out[i].urlhash), out[i].score, out[i].tiebreak) for i in range(n.value)], info
+
+    def close(self):
+        if self._e and self._ix._h:
+            _lib.lib().yrwi_event_close(self._ix._h, self._e)
+        self._e = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 @dataclass
 class Query:
     include: Sequence[bytes]
@@ -250,6 +290,29 @@ class RWIIndex:
         _check(self._h, _lib.lib().yrwi_normalize_score(self._h, rows.ctypes.data, len(rows), ctypes.byref(prof.c),
                                                         language.encode(), now_ms, out.ctypes.data))
         return out
+
+    # ---- search events: containers arriving one after another ----
+    def event(self, profile: Optional[RankingProfile] = None, language: str = "en", now_ms: int = 0, k: int = 100,
+              filter: Optional[QueryFilter] = None, max_postings: int = 1 << 16) -> "SearchEvent":
+        return SearchEvent(self, profile, language, now_ms, k, filter, max_postings)
+
+    def add_rwis(self, arrivals: Sequence[Tuple["SearchEvent", np.ndarray, bool]]) -> List[int]:
+        """Applies (event, rows (n, 40) uint8, local) arrivals in order, events in
+        parallel (yrwi_event_add); returns the per-arrival codes (raises on the first
+        error)."""
+        arr = (_lib.CArrival * max(1, len(arrivals)))()
+        keep = []
+        for i, (ev, rows, local) in enumerate(arrivals):
+            r = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, 40)
+            keep.append(r)
+            arr[i].ev = ev._e
+            arr[i].rows40 = r.ctypes.data if len(r) else None
+            arr[i].n = len(r)
+            arr[i].local = int(bool(local))
+        rc = _lib.lib().yrwi_event_add(self._h, arr, len(arrivals))
+        codes = [arr[i].rc for i in range(len(arrivals))]
+        _check(self._h, rc)
+        return codes
 
     # ---- ReferenceOrder.cardinal(URIMetadataNode): the Solr node stack ----
     def score_nodes(self, nodes: Sequence[dict], profile: Optional[RankingProfile] = None, language: str = "en",
