@@ -258,6 +258,46 @@ int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn
                       yrwi_event_info* info);
 void yrwi_event_close(yrwi_ctx* ctx, yrwi_event* ev);
 
+/* ---- index abstracts and the secondary search ---- */
+/* AbstractIndex.searchConjunction + WordReferenceFactory.compressIndex for each
+ * term (htroot/yacy/search.java:264-281, SearchEvent.java:505-531;
+ * WordReferenceFactory.java:75-117 without its time limit): "{host:u6u6...,host:...}"
+ * with hosts in String order and url prefixes in container order, minus the urls
+ * of exclude_term's list (NULL: none).  Abstract i is out[offsets[i],
+ * offsets[i+1]); *nout = nterms, or 0 when a term has no list (searchConjunction
+ * returns no containers then). */
+int yrwi_index_abstracts(yrwi_ctx* ctx, const uint8_t* terms, int32_t nterms, const uint8_t* exclude_term,
+                         char* out, int64_t cap, int64_t* offsets, int32_t* nout);
+/* One index abstract received from a peer (Protocol.java:576-596). */
+typedef struct yrwi_abstract {
+  uint8_t word[12];
+  uint8_t peer[12];
+  const char* text;
+  int64_t len;
+} yrwi_abstract;
+/* A secondary search request (SecondarySearchSuperviser.prepareSecondarySearch
+ * :117-196): the peer, the words to ask it for (bit i = words_out[i]) and its urls
+ * (plan_urls[url_off .. url_off + url_n), 12 bytes each, String order). */
+typedef struct yrwi_peer_request {
+  uint8_t peer[12];
+  uint32_t words;
+  int64_t url_off, url_n;
+} yrwi_peer_request;
+/* decompressIndex of every abstract (in arrival order), addAbstract, the
+ * joinConstructive of the words and the requests for the peers other than
+ * mypeer and `checked` (SecondarySearchSuperviser.java:43-196, WordReferenceFactory.
+ * java:125-155, SetTools.java:76-116).  Nothing is planned unless the abstracts
+ * cover exactly nwords_query words.  Outputs: the join (njoin urls in String
+ * order with their peer), words_out (the words in String order, <= 32), the
+ * requests in peer order.  A text that is not a compressIndex abstract fails with
+ * YRWI_E_ARG (the reference would read past its buffer); one without braces is
+ * an empty abstract. */
+int yrwi_secondary_search(yrwi_ctx* ctx, const yrwi_abstract* abs, int32_t nabs, int32_t nwords_query,
+                          const uint8_t mypeer[12], const uint8_t* checked, int32_t nchecked,
+                          uint8_t* join_urls, uint8_t* join_peers, int64_t cap, int64_t* njoin,
+                          yrwi_peer_request* plan, int32_t plan_cap, int32_t* nplan, uint8_t* plan_urls,
+                          uint8_t* words_out, int32_t* nwords);
+
 /* ---- finer-grained drop-ins mirroring the Java split ---- */
 /* == ReferenceContainer.joinExcludeContainers via TermSearch (ReferenceContainer.java:310,
  *    TermSearch.java:42-70): writes the joined container's rows (sorted) to rows_out. */

@@ -1,2 +1,2 @@
 set -e
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_abstracts.py tests/test_events.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/gputest.log 2>&1

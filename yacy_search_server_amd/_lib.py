@@ -83,6 +83,16 @@ class CEventInfo(ctypes.Structure):
                 ("max_distance", ctypes.c_int32), ("err", ctypes.c_int32), ("stack_size", ctypes.c_int32)]
 
 
+class CAbstract(ctypes.Structure):
+    _fields_ = [("word", ctypes.c_uint8 * 12), ("peer", ctypes.c_uint8 * 12), ("text", ctypes.c_void_p),
+                ("len", ctypes.c_int64)]
+
+
+class CPeerRequest(ctypes.Structure):
+    _fields_ = [("peer", ctypes.c_uint8 * 12), ("words", ctypes.c_uint32), ("url_off", ctypes.c_int64),
+                ("url_n", ctypes.c_int64)]
+
+
 class CLoadStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
                                               "dropped_terms")]
@@ -126,6 +136,14 @@ SIGNATURES = {
     "yrwi_event_result": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(CHit), ctypes.c_int32,
                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CEventInfo)]),
     "yrwi_event_close": (None, [_VP, _VP]),
+    "yrwi_index_abstracts": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _VP,
+                                            ctypes.c_int64, _VP, ctypes.POINTER(ctypes.c_int32)]),
+    "yrwi_secondary_search": (ctypes.c_int, [_VP, ctypes.POINTER(CAbstract), ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _VP, _VP,
+                                             ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.POINTER(CPeerRequest), ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_int32), _VP, _VP,
+                                             ctypes.POINTER(ctypes.c_int32)]),
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),

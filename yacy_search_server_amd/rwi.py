@@ -314,6 +314,59 @@ class RWIIndex:
         _check(self._h, rc)
         return codes
 
+    # ---- index abstracts (compressIndex) and the secondary search ----
+    def index_abstracts(self, terms: Sequence[bytes], exclude: Optional[bytes] = None) -> List[bytes]:
+        """searchConjunction + WordReferenceFactory.compressIndex per term; [] when
+        a term has no list."""
+        L = _lib.lib()
+        sizes = [self.get_size(t) for t in terms]
+        cap = sum(14 * n + 2 for n in sizes) + 2
+        out = ctypes.create_string_buffer(max(1, cap))
+        offs = (ctypes.c_int64 * (len(terms) + 1))()
+        nout = ctypes.c_int32()
+        _check(self._h, L.yrwi_index_abstracts(self._h, _hashes(terms), len(terms), exclude, out, cap, offs,
+                                               ctypes.byref(nout)))
+        raw = out.raw
+        return [raw[offs[i]:offs[i + 1]] for i in range(nout.value)]
+
+    def secondary_search(self, abstracts: Sequence[Tuple[bytes, bytes, bytes]], nwords_query: int, mypeer: bytes,
+                         checked: Sequence[bytes] = ()):
+        """abstracts: (word, peer, text) in arrival order.  Returns (join [(url, peer)],
+        words, plan [(peer, urls, words)])."""
+        L = _lib.lib()
+        arr = (_lib.CAbstract * max(1, len(abstracts)))()
+        bufs = []
+        total = 0
+        for i, (w, p, t) in enumerate(abstracts):
+            b = ctypes.create_string_buffer(bytes(t), max(1, len(t)))
+            bufs.append(b)
+            arr[i].word[:] = list(bytes(w))
+            arr[i].peer[:] = list(bytes(p))
+            arr[i].text = ctypes.cast(b, ctypes.c_void_p)
+            arr[i].len = len(t)
+            total += len(t)
+        cap = total // 6 + 1
+        ju = ctypes.create_string_buffer(12 * cap)
+        jp = ctypes.create_string_buffer(12 * cap)
+        pu = ctypes.create_string_buffer(12 * cap)
+        plan = (_lib.CPeerRequest * max(1, len(abstracts)))()
+        wo = ctypes.create_string_buffer(12 * 32)
+        nj = ctypes.c_int64()
+        npl = ctypes.c_int32()
+        nw = ctypes.c_int32()
+        _check(self._h, L.yrwi_secondary_search(self._h, arr, len(abstracts), nwords_query, bytes(mypeer),
+                                                b"".join(bytes(c) for c in checked) or None, len(checked),
+                                                ju, jp, cap, ctypes.byref(nj), plan, len(plan), ctypes.byref(npl),
+                                                pu, wo, ctypes.byref(nw)))
+        words = [wo.raw[12 * i:12 * i + 12] for i in range(nw.value)]
+        join = [(ju.raw[12 * i:12 * i + 12], jp.raw[12 * i:12 * i + 12]) for i in range(nj.value)]
+        reqs = []
+        for i in range(npl.value):
+            r = plan[i]
+            urls = [pu.raw[12 * j:12 * j + 12] for j in range(r.url_off, r.url_off + r.url_n)]
+            reqs.append((bytes(r.peer), urls, [words[b] for b in range(nw.value) if (r.words >> b) & 1]))
+        return join, words, reqs
+
     # ---- ReferenceOrder.cardinal(URIMetadataNode): the Solr node stack ----
     def score_nodes(self, nodes: Sequence[dict], profile: Optional[RankingProfile] = None, language: str = "en",
                     maxdomcount: int = 0) -> np.ndarray:
