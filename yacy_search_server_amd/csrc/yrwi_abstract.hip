@@ -131,44 +131,75 @@ __global__ void k_ss_bad(const uint8_t* __restrict__ t, int64_t nbytes, AbsDesc*
     atomicMin(reinterpret_cast<unsigned long long*>(&A[a].first_bad), (unsigned long long)b);
 }
 
-// one thread per parsed segment: its urls -> (url key, word, abstract) triples
-__global__ void k_ss_parse(const uint8_t* __restrict__ t, int64_t nbytes, AbsDesc* __restrict__ A, int na,
-                           uint64_t* __restrict__ k1, uint64_t* __restrict__ k2, unsigned long long* __restrict__ nent) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbytes) return;
-  const int a = find_abs(A, na, b);
+// A segment starting at b (parsed: before the abstract's first bad start):
+// its url count, or 0; sets the abstract's error for a run the reference would
+// misparse (not a multiple of 6 characters, or not Base64).
+__device__ __forceinline__ int64_t seg_urls(const uint8_t* t, AbsDesc* A, int na, int64_t b, int& a) {
+  a = find_abs(A, na, b);
   const AbsDesc& D = A[a];
   int64_t bend;
-  if (!seg_start(t, D, b, bend) || b >= D.first_bad) return;
-  int hc[6];
+  if (!seg_start(t, D, b, bend) || b >= D.first_bad) return 0;
   bool bad = false;
-  for (int j = 0; j < 6; j++) {
-    hc[j] = acode(t[b + j]);
-    bad |= hc[j] < 0;
-  }
+  for (int j = 0; j < 6; j++) bad |= acode(t[b + j]) < 0;
   int64_t e = b + 7;
   while (e < bend && t[e] != ',') {
     bad |= acode(t[e]) < 0;
     e++;
   }
   const int64_t len = e - (b + 7);
-  if (bad || len % 6) {  // the reference would read past the run (or keep non-Base64 "urls")
+  if (bad || len % 6) {
     atomicOr(&A[a].err, 1);
-    return;
+    return 0;
   }
-  const int64_t cnt = len / 6;
+  return len / 6;
+}
+
+// SS_BYTES text positions per thread: count the urls of the segments starting
+// there, reserve the block's output with one atomic, then write the (url key,
+// word, abstract) triples
+constexpr int SS_BYTES = 16;
+__global__ __launch_bounds__(256) void k_ss_parse(const uint8_t* __restrict__ t, int64_t nbytes,
+                                                  AbsDesc* __restrict__ A, int na, uint64_t* __restrict__ k1,
+                                                  uint64_t* __restrict__ k2, unsigned long long* __restrict__ nent) {
+  __shared__ int64_t sW[4];
+  __shared__ unsigned long long sBase;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t b0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SS_BYTES;
+  int64_t cnt = 0;
+  int a;
+  for (int q = 0; q < SS_BYTES; q++)
+    if (b0 + q < nbytes) cnt += seg_urls(t, A, na, b0 + q, a);
+  int64_t incl = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) sW[wv] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t tot = sW[0] + sW[1] + sW[2] + sW[3];
+    sBase = tot > 0 ? atomicAdd(nent, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  int64_t s0 = (int64_t)sBase + incl - cnt;
+  for (int w = 0; w < wv; w++) s0 += sW[w];
   if (cnt == 0) return;
-  const int64_t s0 = (int64_t)atomicAdd(nent, (unsigned long long)cnt);
-  uint64_t hostpart = 0;  // url chars 6..11 = the host
-  for (int j = 0; j < 6; j++) hostpart = (hostpart << 6) | (uint64_t)hc[j];
-  for (int64_t k = 0; k < cnt; k++) {
-    uint64_t x = 0;
-    for (int j = 0; j < 6; j++) x = (x << 6) | (uint64_t)acode(t[b + 7 + 6 * k + j]);
-    // 72-bit key: chars 0..5 (36 bits), host (36 bits); hi = top 64, lo = low 8
-    const uint64_t hi = (x << 28) | (hostpart >> 8);
-    const uint64_t lo = hostpart & 0xFF;
-    k1[s0 + k] = hi;
-    k2[s0 + k] = (lo << 40) | ((uint64_t)(uint32_t)D.word << 32) | (uint64_t)(uint32_t)a;
+  for (int q = 0; q < SS_BYTES; q++) {
+    const int64_t b = b0 + q;
+    if (b >= nbytes) break;
+    const int64_t c = seg_urls(t, A, na, b, a);
+    if (c == 0) continue;
+    uint64_t hostpart = 0;  // url chars 6..11 = the host
+    for (int j = 0; j < 6; j++) hostpart = (hostpart << 6) | (uint64_t)acode(t[b + j]);
+    const uint32_t w = (uint32_t)A[a].word;
+    for (int64_t k = 0; k < c; k++) {
+      uint64_t x = 0;
+      for (int j = 0; j < 6; j++) x = (x << 6) | (uint64_t)acode(t[b + 7 + 6 * k + j]);
+      // 72-bit key: chars 0..5 (36 bits), host (36 bits); hi = top 64, lo = low 8
+      k1[s0 + k] = (x << 28) | (hostpart >> 8);
+      k2[s0 + k] = ((hostpart & 0xFF) << 40) | ((uint64_t)w << 32) | (uint64_t)(uint32_t)a;
+    }
+    s0 += c;
   }
 }
 
@@ -190,12 +221,18 @@ __device__ __forceinline__ bool same_url(const uint64_t* k1, const uint64_t* k2,
 // per word: distinct urls (the map sizes joinConstructive orders by)
 __global__ void k_ss_count(const uint64_t* __restrict__ k1, const uint64_t* __restrict__ k2, int64_t n,
                            int32_t* __restrict__ wcount, uint32_t* __restrict__ head) {
+  __shared__ int32_t sW[32];
+  if (threadIdx.x < 32) sW[threadIdx.x] = 0;
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t w = (uint32_t)(k2[i] >> 32) & 0xFF;
-  const bool last_w = i == n - 1 || !same_url(k1, k2, i, i + 1) || ((uint32_t)(k2[i + 1] >> 32) & 0xFF) != w;
-  if (last_w) atomicAdd(&wcount[w], 1);
-  head[i] = (i == 0 || !same_url(k1, k2, i, i - 1)) ? 1u : 0u;
+  if (i < n) {
+    const uint32_t w = (uint32_t)(k2[i] >> 32) & 0xFF;
+    const bool last_w = i == n - 1 || !same_url(k1, k2, i, i + 1) || ((uint32_t)(k2[i + 1] >> 32) & 0xFF) != w;
+    if (last_w) atomicAdd(&sW[w], 1);
+    head[i] = (i == 0 || !same_url(k1, k2, i, i - 1)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 && sW[threadIdx.x]) atomicAdd(&wcount[threadIdx.x], sW[threadIdx.x]);
 }
 
 // one thread per url: joined? -> the first join word's peer; words of that peer
@@ -219,7 +256,8 @@ __global__ void k_ss_join(const uint64_t* __restrict__ k1, const uint64_t* __res
   uint32_t pw = 0;
   for (int w = 0; w < 32; w++)
     if ((mask >> w) & 1u && peer_w[w] == p0) pw |= 1u << w;
-  atomicOr(&pmask[p0], pw);
+  // most threads of a wave share the few words masks of a peer: skip repeated global atomics
+  if ((__ldg(&pmask[p0]) & pw) != pw) atomicOr(&pmask[p0], pw);
 }
 
 __global__ void k_ss_flags(const int32_t* __restrict__ jpeer, int64_t n, uint32_t* __restrict__ f) {
@@ -408,7 +446,8 @@ extern "C" int yrwi_secondary_search(yrwi_ctx* ctx, const yrwi_abstract* abs, in
   HIPCHK(ctx, hipMemsetAsync(d_nent, 0, 8, st));
   if (nbytes) {
     hipLaunchKernelGGL(k_ss_bad, dim3(nb(nbytes)), dim3(256), 0, st, d_text, nbytes, d_abs, nabs);
-    hipLaunchKernelGGL(k_ss_parse, dim3(nb(nbytes)), dim3(256), 0, st, d_text, nbytes, d_abs, nabs, k1, k2, d_nent);
+    hipLaunchKernelGGL(k_ss_parse, dim3(nb((nbytes + SS_BYTES - 1) / SS_BYTES)), dim3(256), 0, st, d_text, nbytes, d_abs,
+                       nabs, k1, k2, d_nent);
     HIPCHK(ctx, hipGetLastError());
   }
   unsigned long long nent = 0;

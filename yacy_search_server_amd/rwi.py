@@ -330,9 +330,9 @@ class RWIIndex:
         return [raw[offs[i]:offs[i + 1]] for i in range(nout.value)]
 
     def secondary_search(self, abstracts: Sequence[Tuple[bytes, bytes, bytes]], nwords_query: int, mypeer: bytes,
-                         checked: Sequence[bytes] = ()):
+                         checked: Sequence[bytes] = (), decode: bool = True):
         """abstracts: (word, peer, text) in arrival order.  Returns (join [(url, peer)],
-        words, plan [(peer, urls, words)])."""
+        words, plan [(peer, urls, words)]); with decode=False only (njoin, nplan)."""
         L = _lib.lib()
         arr = (_lib.CAbstract * max(1, len(abstracts)))()
         bufs = []
@@ -358,12 +358,15 @@ class RWIIndex:
                                                 b"".join(bytes(c) for c in checked) or None, len(checked),
                                                 ju, jp, cap, ctypes.byref(nj), plan, len(plan), ctypes.byref(npl),
                                                 pu, wo, ctypes.byref(nw)))
-        words = [wo.raw[12 * i:12 * i + 12] for i in range(nw.value)]
-        join = [(ju.raw[12 * i:12 * i + 12], jp.raw[12 * i:12 * i + 12]) for i in range(nj.value)]
+        if not decode:
+            return nj.value, npl.value
+        wr, jur, jpr, pur = wo.raw, ju.raw, jp.raw, pu.raw  # each .raw is a copy: take them once
+        words = [wr[12 * i:12 * i + 12] for i in range(nw.value)]
+        join = [(jur[12 * i:12 * i + 12], jpr[12 * i:12 * i + 12]) for i in range(nj.value)]
         reqs = []
         for i in range(npl.value):
             r = plan[i]
-            urls = [pu.raw[12 * j:12 * j + 12] for j in range(r.url_off, r.url_off + r.url_n)]
+            urls = [pur[12 * j:12 * j + 12] for j in range(r.url_off, r.url_off + r.url_n)]
             reqs.append((bytes(r.peer), urls, [words[b] for b in range(nw.value) if (r.words >> b) & 1]))
         return join, words, reqs
 
