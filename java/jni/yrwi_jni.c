@@ -185,3 +185,90 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_queryFiltered(
   free(hits);
   return res;
 }
+
+/* ---- search events (SearchEvent.addRWIs per arrival) ---- */
+JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpen(JNIEnv* env, jclass c, jlong ctx, jintArray prof,
+                                                                   jstring lang, jlong now, jint k, jlong maxPostings) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  yrwi_event* ev = NULL;
+  int rc = yrwi_event_open((yrwi_ctx*)(intptr_t)ctx, &p, l, now, k, NULL, maxPostings, &ev);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  return rc == 0 ? (jlong)(intptr_t)ev : 0;
+}
+
+/* addRWIs(container, local): rows = RowSet.chunkcache bytes of the container in its order */
+JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAdd(JNIEnv* env, jclass c, jlong ctx, jlong ev,
+                                                                 jbyteArray rows, jint n, jboolean local) {
+  yrwi_arrival a;
+  memset(&a, 0, sizeof(a));
+  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
+  a.ev = (yrwi_event*)(intptr_t)ev;
+  a.rows40 = (const uint8_t*)p;
+  a.n = n;
+  a.local = local ? 1 : 0;
+  int rc = yrwi_event_add((yrwi_ctx*)(intptr_t)ctx, &a, 1);
+  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  return rc;
+}
+
+/* rwiStack contents (yrwi_hit records) */
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventResult(JNIEnv* env, jclass c, jlong ctx, jlong ev,
+                                                                          jint maxn) {
+  yrwi_hit* hits = (yrwi_hit*)malloc(sizeof(yrwi_hit) * (size_t)(maxn > 0 ? maxn : 1));
+  int32_t n = 0;
+  int rc = yrwi_event_result((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, hits, maxn, &n, NULL);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewByteArray(env, (jsize)(n * (jint)sizeof(yrwi_hit)));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * (jint)sizeof(yrwi_hit)), (const jbyte*)hits);
+  }
+  free(hits);
+  return res;
+}
+
+JNIEXPORT void JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventClose(JNIEnv* env, jclass c, jlong ctx, jlong ev) {
+  yrwi_event_close((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev);
+}
+
+/* ---- index abstracts: compressIndex per term (searchConjunction), joined by '\n' ---- */
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_indexAbstracts(JNIEnv* env, jclass c, jlong ctx,
+                                                                             jbyteArray terms, jint nterms,
+                                                                             jlong cap) {
+  jbyte* tb = (*env)->GetByteArrayElements(env, terms, NULL);
+  char* out = (char*)malloc((size_t)(cap > 0 ? cap : 1));
+  int64_t* off = (int64_t*)calloc((size_t)nterms + 1, sizeof(int64_t));
+  int32_t nout = 0;
+  int rc = yrwi_index_abstracts((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)tb, nterms, NULL, out, cap, off, &nout);
+  (*env)->ReleaseByteArrayElements(env, terms, tb, JNI_ABORT);
+  jbyteArray res = NULL;
+  if (rc == 0) {  /* abstract i = bytes [off[i], off[i+1]) */
+    res = (*env)->NewByteArray(env, (jsize)off[nout]);
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)off[nout], (const jbyte*)out);
+  }
+  free(out);
+  free(off);
+  return res;
+}
+
+/* ---- Solr node stack: cardinal(URIMetadataNode); nodes = packed yrwi_node records ---- */
+JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_scoreNodes(JNIEnv* env, jclass c, jlong ctx,
+                                                                         jbyteArray nodes, jint n, jintArray prof,
+                                                                         jstring lang, jint maxdomcount) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  jbyte* nb = (*env)->GetByteArrayElements(env, nodes, NULL);
+  jlong* sc = (jlong*)malloc(sizeof(jlong) * (size_t)(n > 0 ? n : 1));
+  int rc = yrwi_score_nodes((yrwi_ctx*)(intptr_t)ctx, (const yrwi_node*)nb, n, &p, l, maxdomcount, (int64_t*)sc);
+  (*env)->ReleaseByteArrayElements(env, nodes, nb, JNI_ABORT);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  jlongArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewLongArray(env, n);
+    (*env)->SetLongArrayRegion(env, res, 0, n, sc);
+  }
+  free(sc);
+  return res;
+}

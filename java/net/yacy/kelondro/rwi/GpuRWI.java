@@ -72,6 +72,38 @@ public final class GpuRWI implements AutoCloseable {
                              flattenN(urlhashes, 12), skipDoubleDom, flagCount);
     }
 
+    /** A SearchEvent's rwiStack on the GPU: open once per event, then addRWIs for the
+     *  local container and every remote peer's container (Protocol.java:802); the
+     *  result is the stack in rwiStack order (24-byte records as query()). */
+    public long eventOpen(final int[] profile32, final String language, final long nowMillis, final int k,
+                          final long maxPostings) {
+        return eventOpen(this.ctx, profile32, language, nowMillis, k, maxPostings);
+    }
+
+    public void addRWIs(final long event, final byte[] containerRows, final int n, final boolean local) {
+        check(eventAdd(this.ctx, event, containerRows, n, local));
+    }
+
+    public byte[] eventResult(final long event, final int maxn) {
+        return eventResult(this.ctx, event, maxn);
+    }
+
+    public void eventClose(final long event) {
+        eventClose(this.ctx, event);
+    }
+
+    /** WordReferenceFactory.compressIndex of each include word's list (search.java:264-281):
+     *  the abstracts back to back, each "{...}". */
+    public byte[] indexAbstracts(final byte[][] words, final long capacity) {
+        return indexAbstracts(this.ctx, flatten(words), words.length, capacity);
+    }
+
+    /** ReferenceOrder.cardinal(URIMetadataNode) of packed yrwi_node records (60 bytes each). */
+    public long[] scoreNodes(final byte[] nodes, final int n, final int[] profile32, final String language,
+                             final int maxdomcount) {
+        return scoreNodes(this.ctx, nodes, n, profile32, language, maxdomcount);
+    }
+
     @Override
     public void close() {
         if (this.ctx != 0) { close(this.ctx); this.ctx = 0; }
@@ -122,4 +154,12 @@ public final class GpuRWI implements AutoCloseable {
                                                boolean strictDom, String modifierLanguage, byte[] site,
                                                byte[] altSite, byte[] siteExcludes, byte[] urlHashes,
                                                boolean skipDoubleDom, int[] flagCount);
+    private static native long eventOpen(long ctx, int[] profile32, String language, long nowMillis, int k,
+                                         long maxPostings);
+    private static native int eventAdd(long ctx, long event, byte[] rows, int n, boolean local);
+    private static native byte[] eventResult(long ctx, long event, int maxn);
+    private static native void eventClose(long ctx, long event);
+    private static native byte[] indexAbstracts(long ctx, byte[] words, int nwords, long capacity);
+    private static native long[] scoreNodes(long ctx, byte[] nodes, int n, int[] profile32, String language,
+                                            int maxdomcount);
 }
