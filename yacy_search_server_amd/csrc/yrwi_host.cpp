@@ -842,13 +842,15 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   Cand* d_cand = arena_alloc<Cand>(ctx, std::max<int64_t>(chunks, 1) * kc);
   int32_t* d_ccnt = arena_alloc<int32_t>(ctx, std::max<int64_t>(chunks, 1));
   if (!d_cand || !d_ccnt) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, ctx->stream))
+  // d_zero[0]: a zero count (queries without chunks); d_zero[1]: k_score's redo count
+  int32_t* d_zero = arena_alloc<int32_t>(ctx, 2);
+  int32_t* d_redo = arena_alloc<int32_t>(ctx, std::max<int64_t>(chunks, 1));
+  if (!d_zero || !d_redo) return ctx->fail(YRWI_E_NOMEM, "arena");
+  HIPCHK(ctx, hipMemsetAsync(d_zero, 0, 2 * sizeof(int32_t), ctx->stream));
+  if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
-  int32_t* d_zero = arena_alloc<int32_t>(ctx, 1);
-  if (!d_zero) return ctx->fail(YRWI_E_NOMEM, "arena");
-  HIPCHK(ctx, hipMemsetAsync(d_zero, 0, sizeof(int32_t), ctx->stream));
   std::vector<const Cand*> fptr((size_t)nq);
   std::vector<const int32_t*> fcnt((size_t)nq);
   std::vector<int64_t> lists((size_t)nq), lbase((size_t)nq);

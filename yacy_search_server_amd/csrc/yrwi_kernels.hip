@@ -1477,19 +1477,92 @@ __device__ __forceinline__ bool passes(const FilterQ& F, const Row& r) {
   return true;
 }
 
+// Chunk scoring, two kernels.  k_score (small LDS footprint, so many chunks are
+// resident per CU) handles every chunk whose selected prefix fits SCORE_SMALL
+// entries and survives the TreeSet dedupe with kq classes -- all but chunks with
+// long runs of tied scores or hashCode collisions; it appends the others to a
+// redo list.  k_score_full re-scores those with the whole chunk in LDS.  Flag
+// counts are taken once, by k_score.
+constexpr int SCORE_SMALL = 256;
+
+// score keys of one chunk: a[s] = score ^ 2^63 of element e0 + s*CHUNK_THREADS,
+// bit s of the result set when that element is live and admitted
+template <bool SCORE = true>
+__device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState& N, int64_t e0, int32_t* flagc,
+                                                uint64_t* a, uint64_t* z) {
+  const FilterQ* F = Q.filt;
+  uint32_t vm = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int64_t e = e0 + s * CHUNK_THREADS;
+    a[s] = 0;
+    if (z) z[s] = 0;
+    if (e < Q.n && !(Q.removed && Q.removed[e])) {
+      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
+      if (F && !admit(*F, r, flagc)) continue;
+      if (!SCORE) continue;
+      const Feat t = decode(r);
+      const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
+      a[s] = (uint64_t)cardinal(r, t, N, Q, hc) ^ 0x8000000000000000ull;
+      if (z) z[s] = ((uint64_t)((uint32_t)url_hashcode(r) ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+      vm |= 1u << s;
+    }
+  }
+  return vm;
+}
+
+// MSB-first radix select over the live keys: the largest T with at least kq live keys >= T
+__device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t vm, int32_t kq, int32_t* sHist,
+                                                    int32_t* sSel, uint64_t* sRed) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t mx = 0, mn = ~0ull;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++)
+    if ((vm >> s) & 1u) { mx = a[s] > mx ? a[s] : mx; mn = a[s] < mn ? a[s] : mn; }
+  mx = wave_max_u64(mx);
+  mn = wave_min_u64(mn);
+  if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
+  __syncthreads();
+  uint64_t gmx = sRed[0], gmn = sRed[4];
+  for (int w = 1; w < 4; w++) { gmx = sRed[w] > gmx ? sRed[w] : gmx; gmn = sRed[4 + w] < gmn ? sRed[4 + w] : gmn; }
+  const uint64_t diff = gmx ^ gmn;
+  if (diff == 0) return gmx;
+  int hi = 64 - __clzll((long long)diff);  // keys differ only in bits [0, hi)
+  uint64_t prefix = hi == 64 ? 0 : (gmx >> hi) << hi;
+  int32_t rem = kq;
+  while (hi > 0) {
+    const int lo = hi > 8 ? hi - 8 : 0;
+    const uint32_t wmask = (1u << (hi - lo)) - 1u;
+    sHist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++)
+      if (((vm >> s) & 1u) && (hi == 64 || (a[s] >> hi) == (prefix >> hi)))
+        atomicAdd(&sHist[(uint32_t)(a[s] >> lo) & wmask], 1);
+    __syncthreads();
+    if (tid < 64) radix_pick(sHist, rem, sSel);
+    __syncthreads();
+    prefix |= (uint64_t)sSel[0] << lo;
+    rem = sSel[1];
+    hi = lo;
+  }
+  return prefix;
+}
+
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
                                                         const int32_t* __restrict__ chunk_q,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
-                                                        int32_t* __restrict__ cand_cnt, int32_t kc) {
-  __shared__ uint64_t s1[CHUNK];
-  __shared__ uint64_t s2[CHUNK];
+                                                        int32_t* __restrict__ cand_cnt, int32_t kc,
+                                                        int32_t* __restrict__ redo, int32_t* __restrict__ nredo) {
+  __shared__ uint64_t s1[SCORE_SMALL];
+  __shared__ uint64_t s2[SCORE_SMALL];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sHist[256];
   __shared__ int32_t sSel[3];
   __shared__ uint64_t sRed[8];
   __shared__ NormState sN;
   __shared__ int32_t sFlag[32];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
@@ -1499,99 +1572,126 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const FilterQ* F = Q.filt;
   int32_t* flagc = (F && F->flagcount) ? sFlag : nullptr;
   const int64_t c = b - Q.chunk_base;
-  // strided element map (neighbouring lanes read neighbouring rows); order is
-  // irrelevant here, the candidate key carries the container index
+  // strided element map (neighbouring lanes read neighbouring rows); the
+  // candidate key carries the container index.  The hashCode (tie-break) is only
+  // computed for the selected prefix.
   const int64_t e0 = c * CHUNK + tid;
-  uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
-  int32_t nvl = 0;
-  uint64_t mx = 0, mn = ~0ull;
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {
-    const int64_t e = e0 + s * CHUNK_THREADS;
-    a[s] = 0;
-    z[s] = 0;
-    if (e < Q.n && !(Q.removed && Q.removed[e])) {
-      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
-      if (F && !admit(*F, r, flagc)) continue;
-      const Feat t = decode(r);
-      const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
-      const int64_t score = cardinal(r, t, sN, Q, hc);
-      const int32_t h = url_hashcode(r);
-      a[s] = (uint64_t)score ^ 0x8000000000000000ull;
-      z[s] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
-      nvl++;
-      mx = a[s] > mx ? a[s] : mx;
-      mn = a[s] < mn ? a[s] : mn;
-    }
-  }
+  uint64_t a[CHUNK_IPT];
   const int32_t kq = Q.k < kc ? Q.k : kc;
+  if (kq > SCORE_SMALL) {  // large k (doubledom stacks): only the flag counts here
+    if (flagc) {
+      (void)score_elems<false>(Q, sN, e0, flagc, a, nullptr);
+      __syncthreads();
+      if (tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
+    }
+    if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
+    return;
+  }
+  const uint32_t vm = score_elems(Q, sN, e0, flagc, a, nullptr);
   int32_t nv;
-  (void)block_excl_sum<CHUNK_THREADS>(nvl, sScan, &nv);  // (its barriers also order the sFlag atomics)
+  (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   if (flagc && tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
   if (kq <= 0 || nv == 0) {
     if (tid == 0) cand_cnt[b] = 0;
     return;
   }
-  Cand* out = cand + b * (int64_t)kc;
-  uint64_t T = 0;  // select live keys >= T
-  if (nv > kq) {
-    mx = wave_max_u64(mx);
-    mn = wave_min_u64(mn);
-    if (lane == 0) { sRed[wv] = mx; sRed[4 + wv] = mn; }
-    __syncthreads();
-    uint64_t gmx = sRed[0], gmn = sRed[4];
-    for (int w = 1; w < 4; w++) { gmx = sRed[w] > gmx ? sRed[w] : gmx; gmn = sRed[4 + w] < gmn ? sRed[4 + w] : gmn; }
-    const uint64_t diff = gmx ^ gmn;
-    if (diff == 0) {
-      T = gmx;
-    } else {
-      int hi = 64 - __clzll((long long)diff);  // keys differ only in bits [0, hi)
-      uint64_t prefix = hi == 64 ? 0 : (gmx >> hi) << hi;
-      int32_t rem = kq;
-      while (hi > 0) {
-        const int lo = hi > 8 ? hi - 8 : 0;
-        const uint32_t wmask = (1u << (hi - lo)) - 1u;
-        sHist[tid] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < CHUNK_IPT; s++)
-          if (z[s] && (hi == 64 || (a[s] >> hi) == (prefix >> hi)))
-            atomicAdd(&sHist[(uint32_t)(a[s] >> lo) & wmask], 1);
-        __syncthreads();
-        if (tid < 64) radix_pick(sHist, rem, sSel);
-        __syncthreads();
-        prefix |= (uint64_t)sSel[0] << lo;
-        rem = sSel[1];
-        hi = lo;
-      }
-      T = prefix;
-    }
-  }
-  // compact the selected prefix into LDS and sort it
+  const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed) : 0;
   int32_t mine = 0;
 #pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) mine += (z[s] && a[s] >= T) ? 1 : 0;
+  for (int s = 0; s < CHUNK_IPT; s++) mine += (((vm >> s) & 1u) && a[s] >= T) ? 1 : 0;
   int32_t nsel;
   int32_t off = block_excl_sum<CHUNK_THREADS>(mine, sScan, &nsel);
+  if (nsel > SCORE_SMALL) {  // long run of tied scores at the cut
+    if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++)
-    if (z[s] && a[s] >= T) { s1[off] = a[s]; s2[off] = z[s]; off++; }
+    if (((vm >> s) & 1u) && a[s] >= T) {
+      const int64_t e = e0 + s * CHUNK_THREADS;
+      const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
+      const uint64_t h0 = *reinterpret_cast<const uint64_t*>(r);
+      const uint32_t h1 = *reinterpret_cast<const uint32_t*>(r + 8);
+      int32_t h = 0;  // ByteArray.hashCode (ByteArray.java:80-84)
+#pragma unroll
+      for (int j = 0; j < 8; j++) h = add32(mul32(31, h), (int32_t)((h0 >> (8 * j)) & 0xFF));
+#pragma unroll
+      for (int j = 0; j < 4; j++) h = add32(mul32(31, h), (int32_t)((h1 >> (8 * j)) & 0xFF));
+      s1[off] = a[s];
+      s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+      off++;
+    }
   const int P = pow2_at_least(nsel);
   for (int i = nsel + tid; i < P; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
   __syncthreads();
   bitonic_desc<CHUNK_THREADS>(s1, s2, P);
   int32_t distinct;
-  int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, P, kq, out, sScan, &distinct);
-  if (distinct < kq && nsel < nv) {
-    // the TreeSet dedupe consumed part of the prefix: sort the whole chunk
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < CHUNK_IPT; s++) { s1[tid * CHUNK_IPT + s] = a[s]; s2[tid * CHUNK_IPT + s] = z[s]; }
-    __syncthreads();
-    bitonic_desc<CHUNK_THREADS>(s1, s2, CHUNK);
-    n = dedupe_take<CHUNK_THREADS>(s1, s2, CHUNK, kq, out, sScan, nullptr);
+  Cand* out = cand + b * (int64_t)kc;
+  const int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, P, kq, out, sScan, &distinct);
+  if (distinct < kq && nsel < nv) {  // the TreeSet dedupe consumed part of the prefix
+    if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
+    return;
   }
   if (tid == 0) cand_cnt[b] = n;
+}
+
+// The chunks k_score could not finish, whole chunk in LDS (grid-stride over the redo list).
+__global__ __launch_bounds__(CHUNK_THREADS) void k_score_full(const RankQ* __restrict__ qs,
+                                                             const int32_t* __restrict__ chunk_q,
+                                                             const NormState* __restrict__ norm,
+                                                             Cand* __restrict__ cand, int32_t* __restrict__ cand_cnt,
+                                                             int32_t kc, const int32_t* __restrict__ redo,
+                                                             const int32_t* __restrict__ nredo) {
+  __shared__ uint64_t s1[CHUNK];
+  __shared__ uint64_t s2[CHUNK];
+  __shared__ int32_t sScan[4];
+  __shared__ int32_t sHist[256];
+  __shared__ int32_t sSel[3];
+  __shared__ uint64_t sRed[8];
+  __shared__ NormState sN;
+  const int tid = threadIdx.x;
+  const int32_t nr = *nredo;
+  for (int32_t ri = blockIdx.x; ri < nr; ri += gridDim.x) {
+    const int64_t b = redo[ri];
+    const int qi = chunk_q[b];
+    const RankQ& Q = qs[qi];
+    __syncthreads();  // LDS of the previous chunk
+    if (tid == 0) sN = norm[qi];
+    __syncthreads();
+    const int64_t c = b - Q.chunk_base;
+    const int64_t e0 = c * CHUNK + tid;
+    uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
+    const uint32_t vm = score_elems(Q, sN, e0, nullptr, a, z);  // flags were counted by k_score
+    const int32_t kq = Q.k < kc ? Q.k : kc;
+    int32_t nv;
+    (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);
+    const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed) : 0;
+    int32_t mine = 0;
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++) mine += (((vm >> s) & 1u) && a[s] >= T) ? 1 : 0;
+    int32_t nsel;
+    int32_t off = block_excl_sum<CHUNK_THREADS>(mine, sScan, &nsel);
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++)
+      if (((vm >> s) & 1u) && a[s] >= T) { s1[off] = a[s]; s2[off] = z[s]; off++; }
+    const int P = pow2_at_least(nsel);
+    for (int i = nsel + tid; i < P; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
+    __syncthreads();
+    bitonic_desc<CHUNK_THREADS>(s1, s2, P);
+    Cand* out = cand + b * (int64_t)kc;
+    int32_t distinct;
+    int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, P, kq, out, sScan, &distinct);
+    if (distinct < kq && nsel < nv) {
+      // the TreeSet dedupe consumed part of the prefix: sort the whole chunk
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < CHUNK_IPT; s++) { s1[tid * CHUNK_IPT + s] = a[s]; s2[tid * CHUNK_IPT + s] = z[s]; }
+      __syncthreads();
+      bitonic_desc<CHUNK_THREADS>(s1, s2, CHUNK);
+      n = dedupe_take<CHUNK_THREADS>(s1, s2, CHUNK, kq, out, sScan, nullptr);
+    }
+    if (tid == 0) cand_cnt[b] = n;
+  }
 }
 
 // Top-k of a group of candidate lists (gn[g] <= 64 lists from list gbase[g];
@@ -2153,10 +2253,14 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 }
 
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
-                 const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, void* st) {
+                 const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, int32_t* d_redo,
+                 int32_t* d_nredo, void* st) {
   if (total_chunks <= 0) return 0;
   hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                     d_norm, d_cand, d_cand_cnt, kc);
+                     d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo);
+  const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
+  hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
+                     d_cand_cnt, kc, d_redo, d_nredo);
   return rc(hipGetLastError());
 }
 
