@@ -176,6 +176,35 @@ def test_fold_overflow_paths():
         ix.close()
 
 
+def test_fold_many_record_chunks():
+    """Containers of 100+ chunks whose posintext trends upwards with noise: record
+    chunks (new prefix max) sit between runs of non-record chunks in every batch of
+    64 chunk summaries k_shard_fin folds, some chunks have posintext 0 throughout."""
+    rng = np.random.default_rng(11)
+    for n, step in ((300000, 40), (260000, 400)):
+        rows = np.zeros((n, 40), dtype=np.uint8)
+        alpha = np.frombuffer(jl.ALPHA, dtype=np.uint8)
+        keys = np.arange(1, n + 1, dtype=np.int64) * 977 + 13
+        for j in range(12):
+            rows[:, 11 - j] = alpha[(keys >> (6 * j)) & 63]
+        rows[:, 12:14] = np.frombuffer((15000).to_bytes(2, "big"), dtype=np.uint8)
+        rows[:, 18] = 50
+        rows[:, 21] = ord("t")
+        rows[:, 22:24] = np.frombuffer(b"en", dtype=np.uint8)
+        p = np.minimum(65535, np.arange(n) // step + rng.integers(0, 2500, n))
+        p[(np.arange(n) // 2048) % 7 == 3] = 0
+        rows[:, 34] = (p >> 8) & 0xFF
+        rows[:, 35] = p & 0xFF
+        rows[:, 38] = rng.integers(0, 256, n) * (rng.random(n) < 0.3)
+        rows[:, 33] = rng.integers(1, 20, n)
+        ix = RWIIndex(0)
+        ix.add(b"TERMmany____", rows)
+        got = [(h.urlhash, h.score) for h in ix.search([b"TERMmany____"], now_ms=NOW, k=100)]
+        exp = [(h, s) for h, s, _ in orc.search({b"TERMmany____": rows}, [b"TERMmany____"], now_ms=NOW, k=100)]
+        assert got == exp
+        ix.close()
+
+
 def test_put_list_validation():
     ix = RWIIndex(0)
     good = synth.build_index(synth.preset("dense")).list_rows(0)

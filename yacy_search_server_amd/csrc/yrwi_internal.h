@@ -17,7 +17,7 @@ constexpr int JOIN_MAXM = JOIN_TILE / 2 + 1;  // matches per tile <= min(#A, #B 
 constexpr int CHUNK = 2048;          // container elements per rank/score workgroup
 constexpr int CHUNK_THREADS = 256;
 constexpr int CHUNK_IPT = CHUNK / CHUNK_THREADS;
-constexpr int SEGC = 16;             // fold segments kept per chunk summary
+constexpr int SEGC = 32;             // fold segments kept per chunk summary
 constexpr int SSEG = 128;            // fold segments kept per shard summary
 constexpr int NF = 11;               // min/max int fields (virtualAge handled apart)
 

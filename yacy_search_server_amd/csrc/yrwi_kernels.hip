@@ -986,12 +986,30 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
   }
 }
 
+// what the ordered fold reads of one chunk summary (nvc 0: empty or past the end)
+struct FoldIn {
+  int32_t nvc, pm, Mall, Lall, pf, of, ns, first;
+};
+__device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t nc) {
+  FoldIn f{0, -1, 0, 0, 0, 0, 0, 0};
+  if (c < nc) {
+    const ChunkSum& X = C[c];
+    f.nvc = X.nvalid;
+    f.pm = X.pmax;
+    f.Mall = max(X.od_first, X.M_rest);
+    f.Lall = X.L_rest > 0 ? X.L_rest : (X.od_first > 0 ? X.od_first : 0);
+    f.pf = X.p_first;
+    f.of = X.od_first;
+    f.ns = X.overflow ? -1 : X.nseg;
+    f.first = X.first;
+  }
+  return f;
+}
+
 // one wave per query: ordered combination of the chunk summaries of this shard
 __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, const int64_t* __restrict__ chunk_base,
                                                   const ChunkSum* __restrict__ cs, ShardSum* __restrict__ out) {
   __shared__ uint32_t sSeg[SSEG];
-  __shared__ int32_t sNv[64], sPm[64], sMall[64], sLall[64], sPf[64], sOf[64], sNs[64], sFirst[64];
-  __shared__ uint32_t sSg[64 * SEGC];
   __shared__ int32_t sRw[128];
   const int qi = blockIdx.x;
   const RankQ& Q = qs[qi];
@@ -1000,38 +1018,38 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
   const int64_t nc = Q.nchunks;
   ShardSum& S = out[qi];
 
-  // ---- min / max / counts / first chunk
+  // ---- min / max / counts / first chunk, one pass.  virtualAge over the shard's
+  // rest = chunk rests + first elements of every chunk but the shard's first: each
+  // lane keeps its own first chunk's first element aside until the shard's first
+  // chunk is known.
   int32_t mn[NF], mx[NF];
   for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
   double tfmn = 1e300, tfmx = -1e300;
-  int32_t nv = 0;
-  int64_t firstc = INT64_MAX;
+  int32_t nv = 0, vamn = BIG, vamx = -1, a_lane = -1;
+  int64_t lanec = INT64_MAX;
   for (int64_t c = lane; c < nc; c += 64) {
     const ChunkSum& X = C[c];
     if (X.nvalid == 0) continue;
     nv += X.nvalid;
-    firstc = min(firstc, c);
     for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], X.mn[f]); mx[f] = max(mx[f], X.mx[f]); }
     tfmn = fmin(tfmn, X.tf_mn);
     tfmx = fmax(tfmx, X.tf_mx);
+    vamn = min(vamn, X.va_mn_rest);
+    vamx = max(vamx, X.va_mx_rest);
+    if (lanec == INT64_MAX) {
+      lanec = c;
+      a_lane = X.a_first;
+    } else {
+      vamn = min(vamn, X.a_first);
+      vamx = max(vamx, X.a_first);
+    }
   }
   for (int f = 0; f < NF; f++) { mn[f] = wave_min_i(mn[f]); mx[f] = wave_max_i(mx[f]); }
   tfmn = wave_min_d(tfmn);
   tfmx = wave_max_d(tfmx);
   nv = wave_sum_i(nv);
-  {
-    int32_t lo = (int32_t)(firstc == INT64_MAX ? BIG : firstc);
-    firstc = wave_min_i(lo);
-  }
-  // virtualAge over the shard's rest: chunk rests + first elements of later chunks
-  int32_t vamn = BIG, vamx = -1;
-  for (int64_t c = lane; c < nc; c += 64) {
-    const ChunkSum& X = C[c];
-    if (X.nvalid == 0) continue;
-    vamn = min(vamn, X.va_mn_rest);
-    vamx = max(vamx, X.va_mx_rest);
-    if (c != firstc) { vamn = min(vamn, X.a_first); vamx = max(vamx, X.a_first); }
-  }
+  const int64_t firstc = wave_min_i((int32_t)(lanec == INT64_MAX ? BIG : lanec));
+  if (lanec != INT64_MAX && lanec != firstc) { vamn = min(vamn, a_lane); vamx = max(vamx, a_lane); }
   vamn = wave_min_i(vamn);
   vamx = wave_max_i(vamx);
 
@@ -1039,73 +1057,66 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
   SegList L{sSeg, SSEG, 0, 0, -1};
   if (nv > 0) {
     const ChunkSum& X = C[firstc];
-    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L, sNv, sPm);
+    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L, sRw, sRw + 64);
     else if (lane == 0)
       for (int i = 0; i < X.nseg; i++) L.add((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
   }
   seg_bcast(L);
-  int32_t nseg = L.n, prun = L.prun;
-  for (int64_t c0 = (nv > 0 ? firstc + 1 : nc); c0 < nc; c0 += 64) {
-    const int64_t c = c0 + lane;
-    int32_t nvc = 0, pm = -1, Mall = 0, Lall = 0;
-    if (c < nc) {
-      const ChunkSum& X = C[c];
-      nvc = X.nvalid;
-      pm = X.pmax;
-      Mall = max(X.od_first, X.M_rest);
-      Lall = X.L_rest > 0 ? X.L_rest : (X.od_first > 0 ? X.od_first : 0);
+  // The later chunks, 64 at a time (lane i: chunk c0+i; the next batch is loaded
+  // while this one is folded).  A chunk is a record chunk iff its max posintext
+  // exceeds the running P before it (prefix max over the batch, seeded with
+  // L.prun); only record chunks add pieces of their own.  The chunks between two
+  // record chunks merge into the last piece as one (max od, last positive od),
+  // taken by a segmented scan headed at the record lanes.
+  const int64_t cs0 = nv > 0 ? firstc + 1 : nc;
+  FoldIn cur = fold_in(C, cs0 + lane, nc);
+  for (int64_t c0 = cs0; c0 < nc; c0 += 64) {
+    const FoldIn nxt = fold_in(C, c0 + 64 + lane, nc);
+    const int32_t pinc = wave_incl_max(cur.nvc ? cur.pm : -1);
+    int32_t pex = __shfl_up(pinc, 1, 64);
+    pex = max(lane == 0 ? -1 : pex, L.prun);
+    const bool rec = cur.nvc && cur.pm > pex;
+    const uint64_t heads = __ballot(rec);
+    int32_t m = (cur.nvc && !rec) ? cur.Mall : 0;
+    int32_t key = (cur.nvc && !rec && cur.Lall > 0) ? ((lane + 1) << 8) | cur.Lall : 0;
+    bool hd = rec;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t m2 = __shfl_up(m, o, 64), k2 = __shfl_up(key, o, 64);
+      const bool h2 = __shfl_up((int)hd, o, 64) != 0;
+      if (lane >= o && !hd) { m = max(m, m2); key = max(key, k2); hd = h2; }
     }
-    const bool fast = __all(nvc == 0 || pm <= prun);
-    if (fast) {
-      int32_t m = wave_max_i(nvc ? Mall : 0);
-      // last positive L in lane order
-      int32_t key = (nvc && Lall > 0) ? ((lane + 1) << 8) | Lall : 0;
-      key = wave_max_i(key);
-      if (lane == 0 && (m > 0 || key > 0)) L.add(-1, m, key & 0xFF);  // P=-1 <= prun: merge
-    } else {
-      // stage this batch's summaries in LDS (all lanes, parallel loads), then lane 0
-      // walks them: chunks without a new prefix-max record merge in O(1)
-      if (c < nc) {
-        const ChunkSum& X = C[c];
-        sNv[lane] = nvc;
-        sPm[lane] = pm;
-        sMall[lane] = Mall;
-        sLall[lane] = Lall;
-        sPf[lane] = X.p_first;
-        sOf[lane] = X.od_first;
-        sNs[lane] = X.overflow ? -1 : X.nseg;
-        sFirst[lane] = X.first;
-        for (int s = 0; s < SEGC && s < X.nseg && !X.overflow; s++) sSg[lane * SEGC + s] = X.seg[s];
-      } else {
-        sNv[lane] = 0;
-      }
-      __syncthreads();
-      // loop and branch conditions are wave-uniform (LDS + broadcast state); only
-      // lane 0 mutates L except inside the cooperative rewalk
-      for (int i = 0; i < 64 && c0 + i < nc; i++) {
-        if (sNv[i] == 0) continue;
-        if (sPm[i] <= L.prun) {
-          if (lane == 0 && (sMall[i] > 0 || sLall[i] > 0)) L.add(-1, sMall[i], sLall[i]);
-          continue;
-        }
-        if (lane == 0) L.add(sPf[i], sOf[i], sOf[i]);
-        if (sNs[i] < 0) {
-          seg_bcast(L);
-          rewalk_chunk(Q, c0 + i, sFirst[i], L, sRw, sRw + 64);
-        } else if (lane == 0) {
-          for (int s = 0; s < sNs[i]; s++)
-            L.add((int32_t)(sSg[i * SEGC + s] >> 16), (int32_t)((sSg[i * SEGC + s] >> 8) & 0xFF),
-                  (int32_t)(sSg[i * SEGC + s] & 0xFF));
-        }
+    // run before the first record chunk
+    const int pre_end = heads ? __ffsll((long long)heads) - 2 : 63;
+    if (pre_end >= 0) {
+      const int32_t em = __shfl(m, pre_end, 64), ek = __shfl(key, pre_end, 64);
+      if (lane == 0 && (em > 0 || ek > 0)) L.add(-1, em, ek & 0xFF);
+    }
+    uint64_t hm = heads;
+    while (hm) {  // wave-uniform
+      const int r = __ffsll((long long)hm) - 1;
+      hm &= hm - 1;
+      const int end = hm ? __ffsll((long long)hm) - 2 : 63;
+      const int32_t pf = __shfl(cur.pf, r, 64), of = __shfl(cur.of, r, 64);
+      const int32_t ns = __shfl(cur.ns, r, 64), fi = __shfl(cur.first, r, 64);
+      if (lane == 0) L.add(pf, of, of);
+      if (ns < 0) {
         seg_bcast(L);
+        rewalk_chunk(Q, c0 + r, fi, L, sRw, sRw + 64);
+      } else {
+        const uint32_t sg = lane < ns ? C[c0 + r].seg[lane] : 0u;
+        for (int s = 0; s < ns; s++) {
+          const uint32_t v = __shfl(sg, s, 64);
+          if (lane == 0) L.add((int32_t)(v >> 16), (int32_t)((v >> 8) & 0xFF), (int32_t)(v & 0xFF));
+        }
       }
-      __syncthreads();
+      const int32_t em = __shfl(m, end, 64), ek = __shfl(key, end, 64);
+      if (lane == 0 && (em > 0 || ek > 0)) L.add(-1, em, ek & 0xFF);
+      seg_bcast(L);
     }
     seg_bcast(L);
-    prun = L.prun;
-    nseg = L.n;
+    cur = nxt;
   }
-  (void)nseg;
   __syncthreads();
   if (lane == 0) {
     S.nvalid = nv;
