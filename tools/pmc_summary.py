@@ -22,7 +22,7 @@ def find(pattern):
 
 def short(name):
     for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
-              "k_score_all", "k_score", "k_merge", "k_emit", "k_validate"):
+              "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
             return k
     return name[:40]
