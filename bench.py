@@ -56,13 +56,14 @@ def build_queries(idx_hashes, qs, k, now_ms, prof):
     return arr, keep
 
 
-def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, min_s=10.0):
+def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, prof, label, min_s=10.0):
     """The oracle (reference algorithm restated in C++) on a bounded sample of the
     same query stream: one query per thread (ctypes releases the GIL), like the
     GPU's throughput mode.  threads == 1 is the canonical single-thread restatement."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import threading
     import oracle as orc
+    oprof = orc.profile_from(prof)
     d = {idx.hashes[t]: idx.list_rows(t) for inc, exc in qs for t in inc + exc if idx.sizes[t]}
     lock = threading.Lock()
     state = {"next": 0, "post": 0, "n": 0}
@@ -77,7 +78,8 @@ def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, min_s=10.0):
                     return
                 state["next"] = i + 1
             inc, exc = qs[i % len(qs)]
-            orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=now_ms, k=k)
+            orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], profile=oprof,
+                       now_ms=now_ms, k=k)
             with lock:
                 state["post"] += int(sum(idx.sizes[t] for t in inc + exc))
                 state["n"] += 1
@@ -89,7 +91,7 @@ def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, min_s=10.0):
         t.join()
     dt = time.perf_counter() - t0
     return {"value": state["post"] / dt, "unit": "postings/s", "cores": threads, "kind": "port",
-            "sample": f"{state['n']} queries cycling the {len(qs)} C2 queries ({state['post']} postings, {dt:.1f}s), "
+            "sample": f"{state['n']} queries cycling the {len(qs)} {label} queries ({state['post']} postings, {dt:.1f}s), "
                       f"oracle/yrwi_oracle.cpp, {threads} host thread(s), one query per thread"}
 
 
@@ -109,7 +111,13 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--k", type=int, default=100)
-    ap.add_argument("--terms", type=int, default=2)
+    ap.add_argument("--terms", type=int, default=2, help="include terms per query (minimum)")
+    ap.add_argument("--max-terms", type=int, default=0, help="include terms per query (maximum; default --terms)")
+    ap.add_argument("--exclude", type=int, default=0, help="exclude terms per query")
+    ap.add_argument("--profile", default="default", choices=["default", "custom", "date"],
+                    help="custom = C5's date=15,domlength=15,authority=13,tf=10; date = the /date modifier")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="(1 GPU) run the rank-0 url-hash shard of a W-GPU corpus: the per-GPU slice of C3/C5")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -129,10 +137,18 @@ def main():
         dist = tdist
 
     base = synth.preset(args.config)
-    # weak scaling: an N-times larger corpus, URL-hash range partitioned over the N ranks
-    full = synth.SynthConfig(base.seed, base.n_urls * world, base.n_terms, base.n_hosts * world,
-                             base.n_postings * world)
-    cfg = full.shard(rank, world) if world > 1 else full
+    max_terms = max(args.terms, args.max_terms)
+    if args.shard_of > 1:
+        # the per-GPU slice of a W-GPU corpus (C3/C5 are quoted over 8 GPUs): shard 0 of W
+        if world > 1:
+            raise SystemExit("--shard-of is a one-GPU option")
+        full = base
+        cfg = full.shard(0, args.shard_of)
+    else:
+        # weak scaling: an N-times larger corpus, URL-hash range partitioned over the N ranks
+        full = synth.SynthConfig(base.seed, base.n_urls * world, base.n_terms, base.n_hosts * world,
+                                 base.n_postings * world)
+        cfg = full.shard(rank, world) if world > 1 else full
     t0 = time.time()
     idx = synth.build_index(cfg)
     log(f"rank {rank}: generated {len(idx.rows)} postings in {time.time() - t0:.1f}s")
@@ -157,9 +173,13 @@ def main():
     t_dict = time.time() - t0
     log(f"rank {rank}: url dictionary built in {t_dict:.3f}s")
 
-    qs = synth.queries(full, args.nq, args.terms, args.terms, 0)
+    qs = synth.queries(full, args.nq, args.terms, max_terms, args.exclude)
     now_ms = 20741 * 86400000
     prof = RankingProfile()
+    if args.profile == "custom":  # exercises the authority path (coeff > 12)
+        prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
+    elif args.profile == "date":
+        prof = RankingProfile.date()
     cq, keep = build_queries(idx.hashes, qs, args.k, now_ms, prof)
     kmax = args.k
     # throughput mode: up to `inflight` batches in flight (yrwi_query_batch_submit),
@@ -168,7 +188,7 @@ def main():
     bufs = [(ix.host_array(CHit, args.nq * kmax), ix.host_array(ctypes.c_int32, args.nq), CStats())
             for _ in range(depth)]
     agg = {"postings_in": 0, "bytes_join": 0, "t_join_ns": 0, "n_join": 0, "bytes_alg": 0, "joined": 0,
-           "bytes_probe": 0, "t_probe_ns": 0}
+           "bytes_probe": 0, "t_probe_ns": 0, "t_norm_ns": 0, "t_score_ns": 0, "t_total_ns": 0}
     state = {"depth": depth}
 
     def collect(st):
@@ -180,6 +200,9 @@ def main():
         agg["n_join"] += st.n_join_launches
         agg["bytes_alg"] += st.bytes_alg
         agg["joined"] += st.joined
+        agg["t_norm_ns"] += st.t_norm_ns
+        agg["t_score_ns"] += st.t_score_ns
+        agg["t_total_ns"] += st.t_total_ns
 
     def run_steps(n):
         """n steps (batches); every batch is complete (results in host memory) on return."""
@@ -233,6 +256,7 @@ def main():
     run_steps(max(1, min(args.steps, 5)))
     state["depth"] = depth
     iso = dict(agg)
+    iso["batches"] = max(1, min(args.steps, 5))
     pmc = load_pmc(args.config)
 
     def roofline(a, kernel):
@@ -266,33 +290,70 @@ def main():
             ix.search_batch_raw(ctypes.byref(cq[i]), 1, kmax, one, n1, CStats())
             lat.append((time.perf_counter() - t1) * 1e3)
 
+    # parity spot check of this very workload: the last batch's hits (pinned host
+    # buffers) of the first few queries against the oracle (checker only)
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc
+        oprof = orc.profile_from(prof)
+        hits, nout = bufs[0][0], bufs[0][1]  # the roofline pass above ran last, on bufs[0]
+        nchk = min(args.nq, 16)
+        bad = 0
+        for qi in range(nchk):
+            inc, exc = qs[qi]
+            d = {idx.hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
+            exp = orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], profile=oprof,
+                             now_ms=now_ms, k=args.k)
+            got = [(bytes(hits[qi * kmax + j].urlhash), hits[qi * kmax + j].score) for j in range(nout[qi])]
+            bad += got != [(h, sc) for h, sc, _ in exp]
+        parity = {"queries_checked": nchk, "mismatches": bad, "checker": "oracle/yrwi_oracle.cpp"}
+        if bad:
+            log(f"PARITY MISMATCH on {bad} of {nchk} queries")
+
     cpu = cpu1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
         nthr = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget, nthr)
-        cpu1 = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget / 2, 1)
+        cpu = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget, nthr, prof, args.config)
+        cpu1 = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget / 2, 1, prof, args.config)
 
     if rank == 0:
+        terms_s = f"{args.terms}" if max_terms == args.terms else f"{args.terms}-{max_terms}"
+        excl_s = f" + {args.exclude} excluded" if args.exclude else ""
+        if args.shard_of > 1:
+            corpus_s = (f"url-hash shard 0 of {args.shard_of} ({len(idx.rows) / 1e6:.0f}M postings) of the "
+                        f"{base.n_postings / 1e6:.0f}M-posting corpus ({base.n_urls / 1e6:.0f}M URLs x "
+                        f"{base.n_terms} words)")
+        else:
+            corpus_s = (f"{base.n_postings / 1e6:.0f}M postings ({base.n_urls / 1e6:.0f}M URLs x "
+                        f"{base.n_terms} words) per GPU")
         out = {
             "metric": "postings joined+ranked/sec (node)",
             "value": value, "unit": "postings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int64", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {args.nq} x {args.terms}-term AND queries, default "
-                                   f"RankingProfile, top-{args.k}; {base.n_postings / 1e6:.0f}M postings "
-                                   f"({base.n_urls / 1e6:.0f}M URLs x {base.n_terms} words) per GPU",
+            "config": {"workload": f"{args.config}: {args.nq} x {terms_s}-term AND queries{excl_s}, "
+                                   f"{args.profile} RankingProfile, top-{args.k}; {corpus_s}",
                        "queries_per_step": args.nq, "postings_per_step": total_post / args.steps,
                        "index_postings_total": int(full.n_postings), "parallelism": f"url-hash shards x{world}"},
             "roofline": roof,
             "roofline_probe": roof_probe,
             "roofline_timed": roof_timed,
             "cpu_baseline": cpu,
+            "parity_sample": parity,
             "cpu_baseline_1thread": cpu1,
             "latency_ms": ({"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                             "n": len(lat)} if lat else None),
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
             "inflight": args.inflight,
+            # per batch, from the library's own HIP events (isolated pass): join+probe kernels,
+            # normalisation (reduce..combine), scoring (score..emit); host = call to results
+            "phase_ms": {"join": round(iso["t_join_ns"] / 1e6 / max(1, iso["batches"]), 3),
+                         "probe": round(iso["t_probe_ns"] / 1e6 / max(1, iso["batches"]), 3),
+                         "norm": round(iso["t_norm_ns"] / 1e6 / max(1, iso["batches"]), 3),
+                         "score": round(iso["t_score_ns"] / 1e6 / max(1, iso["batches"]), 3),
+                         "total": round(iso["t_total_ns"] / 1e6 / max(1, iso["batches"]), 3)},
             "url_dictionary_build_s": round(t_dict, 3),
         }
         print(json.dumps(out))

@@ -259,6 +259,23 @@ def test_forced_join_algorithm(corpus, ratio, monkeypatch):
         assert got == [(h, s) for h, s, _ in orc.search(d, ih, eh, now_ms=NOW)]
 
 
+@pytest.mark.parametrize("gb", ["0.000001", "0.002"])
+def test_batch_split_by_scratch_budget(corpus, gb, monkeypatch):
+    """A batch larger than the scratch budget runs as consecutive passes over
+    query ranges (one query per pass at the tiny budget): same hits as the oracle,
+    each query's hits at its own position."""
+    monkeypatch.setenv("YRWI_SCRATCH_GB", gb)
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    qs = synth.queries(cfg, 24, 1, 4, 1, qseed=41)
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=k, now_ms=NOW)
+             for (inc, exc), k in zip(qs, [100, 7, 3000, 1] * 6)]
+    got = ix.search_batch(batch)
+    for qi, (q, g) in enumerate(zip(batch, got)):
+        exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)
+        assert [(h.urlhash, h.score) for h in g] == [(h, s) for h, s, _ in exp], (gb, qi)
+
+
 def _collision_family(base, n_blocks=6):
     """64 url hashes with one Java hashCode: 6 two-char blocks, each either
     (x, y) or (x + 1, y - 31) -- equal 31 * x + y."""

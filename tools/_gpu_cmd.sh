@@ -1,11 +1,8 @@
 set -e
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shards_loopback.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest.log 2>&1
+mkdir -p gpurun_out/cfg gpurun_out/prof
+timeout -k 10 200 python -u bench.py > gpurun_out/cfg/C2_default.json 2> gpurun_out/cfg/C2_default.err
+timeout -k 10 200 python -u bench.py --steps 5 --warmup 1 --no-cpu --latency 0 > gpurun_out/cfg/C2_s5w1.json 2> gpurun_out/cfg/C2_s5w1.err
+timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --latency 20 --config C5 --shard-of 8 --terms 2 --max-terms 4 --profile custom --cpu-budget 6 > gpurun_out/cfg/C5.json 2> gpurun_out/cfg/C5.err
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d /tmp/tp -o run -- python3 $R/tools/tailprobe.py > $R/gpurun_out/tp.log 2>&1
-python3 - > $R/gpurun_out/tp.txt <<'PY'
-import sys; sys.path.insert(0, "/root/repo/tools")
-from kstats_summary import dispatches
-for k in ("k_shard_fin", "k_reduce", "k_compact", "k_join", "k_probe(", "k_score(", "k_topq", "k_emit", "k_partition"):
-    print(k, " ".join("%.0f" % d for d in dispatches("/tmp/tp", k)))
-PY
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/c3 -o run -- python3 $R/bench.py --config C3 --terms 3 --exclude 1 --steps 2 --warmup 1 --no-cpu --latency 0 --inflight 1 > $R/gpurun_out/prof/c3.log 2>&1

@@ -477,7 +477,18 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, PROBE_TILE);
     order[i] = i;
   }
-  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return jobs[a].algo < jobs[b].algo; });
+  // Within each algorithm, jobs that share their larger list run back to back:
+  // queries sample terms by df, so the big lists recur across a batch, and
+  // consecutive tiles over the same list hit in L2 / MALL instead of HBM.  Job
+  // order only changes the schedule (every job owns its output slots).
+  auto big = [&](const JoinQ& J) { return (uintptr_t)(J.A.n >= J.B.n ? J.A.uid : J.B.uid); };
+  auto small = [&](const JoinQ& J) { return (uintptr_t)(J.A.n >= J.B.n ? J.B.uid : J.A.uid); };
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    const JoinQ &x = jobs[a], &y = jobs[b];
+    if (x.algo != y.algo) return x.algo < y.algo;
+    if (big(x) != big(y)) return big(x) < big(y);
+    return small(x) < small(y);
+  });
   std::vector<JoinQ> js;
   std::vector<int> ow;
   tile_base.clear();
@@ -983,35 +994,83 @@ static int64_t now_ns() {
 
 // Plan and run queries q[0, nq) on lane L; results at out (row stride kmax).
 // Every field of *st is this part's own (the caller sums parts).
+// Upper bound of the arena bytes one query takes in a pass: per fold step the
+// tile pair slots (merge: JOIN_MAXM slots of 12 B per JOIN_TILE items, ~6 B per
+// posting; probe: per PROBE_TILE small-side items, ~48 B per posting) and the
+// joined (uid, row) container (<= the smallest list, 44 B per posting), then the
+// rank phase over that container (~72 B per posting).
+static int64_t scratch_estimate(const Plan& P) {
+  if (P.empty || P.seq.empty()) return 4096;
+  int64_t sum = 0, nmin = INT64_MAX;
+  for (const ListRec* l : P.seq) {
+    sum += l->n;
+    nmin = std::min(nmin, l->n);
+  }
+  for (const ListRec* l : P.excl) sum += l->n;
+  return 6 * sum + (92 * (int64_t)(P.seq.size() - 1) + 80) * nmin + 65536;
+}
+
+// Scratch budget of one pass (YRWI_SCRATCH_GB, default 32 GiB per lane).  A
+// batch whose queries need more runs as consecutive passes over query ranges;
+// sharded contexts never split (every rank must issue the same collectives, and
+// the estimate depends on the local shard), so they keep one pass per batch.
+static int64_t scratch_budget(const Lane* L) {
+  if (L->world > 1) return INT64_MAX;
+  const char* e = getenv("YRWI_SCRATCH_GB");
+  const double gb = e ? atof(e) : 32.0;
+  return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
+}
+
 static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
-  std::vector<Plan> plans((size_t)nq);
+  std::vector<Plan> all((size_t)nq);
   for (int i = 0; i < nq; i++) {
-    int rc = plan_query(ix, L, q[i], &plans[(size_t)i]);
+    int rc = plan_query(ix, L, q[i], &all[(size_t)i]);
     if (rc) return rc;
-    if (st) st->postings_in += plans[(size_t)i].postings_in;
+    if (st) st->postings_in += all[(size_t)i].postings_in;
   }
-  if (begin_pass(L)) return YRWI_E_HIP;
-  Timing tm;
-  tm.t0 = L->event();
-  hipEventRecord(tm.t0, L->stream);
-  int rc = run_join_phase(L, plans, st, &tm);
-  if (rc) return rc;
-  tm.tj = L->event();
-  hipEventRecord(tm.tj, L->stream);
-  rc = run_rank_phase(L, plans, kmax, out, nout, nullptr, st, &tm);
-  if (rc) return rc;
-  if (st) {
-    float ms = 0;
-    for (auto& ev : tm.kjoin) {
-      if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_join_ns += (int64_t)(ms * 1e6);
-      if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) st->t_probe_ns += (int64_t)(ms * 1e6);
+  const int64_t budget = scratch_budget(L);
+  for (int g0 = 0; g0 < nq;) {
+    int g1 = g0;
+    int64_t need = 0;
+    while (g1 < nq) {
+      const int64_t e = scratch_estimate(all[(size_t)g1]);
+      if (g1 > g0 && need + e > budget) break;
+      need += e;
+      g1++;
     }
-    if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
-    if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
-    st->t_total_ns = now_ns() - t0;
+    std::vector<Plan> plans(std::make_move_iterator(all.begin() + g0), std::make_move_iterator(all.begin() + g1));
+    if (begin_pass(L)) return YRWI_E_HIP;
+    Timing tm;
+    tm.t0 = L->event();
+    hipEventRecord(tm.t0, L->stream);
+    int rc = run_join_phase(L, plans, st, &tm);
+    if (rc) return rc;
+    tm.tj = L->event();
+    hipEventRecord(tm.tj, L->stream);
+    rc = run_rank_phase(L, plans, kmax, out + (size_t)g0 * kmax, nout + g0, nullptr, st, &tm);
+    if (rc) return rc;
+    if (st) {
+      if (g1 < nq) HIPCHK(L, lane_sync(L));  // the pass's events must be complete before they are reused
+      float ms = 0;
+      for (auto& ev : tm.kjoin) {
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_join_ns += (int64_t)(ms * 1e6);
+        if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) st->t_probe_ns += (int64_t)(ms * 1e6);
+      }
+      if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
+      if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
+    }
+    g0 = g1;
   }
+  // An arena that had to grow consolidates now, while this batch's caller still
+  // waits for it, not at the start of the lane's next batch (one hipFree +
+  // hipMalloc of the whole scratch costs milliseconds).
+  if (L->arena.chunks.size() > 1) {
+    HIPCHK(L, lane_sync(L));
+    L->arena.reset();
+  }
+  if (st) st->t_total_ns = now_ns() - t0;
   return 0;
 }
 
