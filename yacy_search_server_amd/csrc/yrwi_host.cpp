@@ -1021,8 +1021,19 @@ static int64_t scratch_budget(const Lane* L) {
   return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
 }
 
+static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                           yrwi_hit* out, int32_t* nout, yrwi_stats* st);
+
 static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
+  L->enter();
+  const int rc = run_batch_part_(ix, L, q, nq, kmax, out, nout, st);
+  L->leave();
+  return rc;
+}
+
+static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
+                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
   std::vector<Plan> all((size_t)nq);
   for (int i = 0; i < nq; i++) {
@@ -1069,6 +1080,10 @@ static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q,
   if (L->arena.chunks.size() > 1) {
     HIPCHK(L, lane_sync(L));
     L->arena.reset();
+    // the lanes share one workload: idle lanes take the same size now, so their
+    // first batch does not pay for growing (single-lane sharded contexts: none)
+    for (Lane* o : ix->lanes)
+      if (o != L) o->try_reserve(L->arena.capacity());
   }
   if (st) st->t_total_ns = now_ns() - t0;
   return 0;

@@ -91,7 +91,7 @@ struct Arena {
       used = 0;
     }
     if (cur >= chunks.size()) {
-      size_t sz = std::max(bytes, min_chunk);
+      size_t sz = std::max(std::max(bytes, min_chunk), capacity());  // geometric: few hipMallocs
       void* p = nullptr;
       if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
       chunks.push_back({(uint8_t*)p, sz});
@@ -116,6 +116,15 @@ struct Arena {
     used = 0;
     cur = 0;
     total_used = 0;
+  }
+  // one chunk of at least `bytes` (no allocation in use: call between passes)
+  void reserve(size_t bytes) {
+    if (capacity() >= bytes && chunks.size() <= 1) return;
+    for (auto& c : chunks) hipFree(c.first);
+    chunks.clear();
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max(bytes, min_chunk)) == hipSuccess) chunks.push_back({(uint8_t*)p, std::max(bytes, min_chunk)});
+    used = cur = total_used = 0;
   }
   size_t capacity() const {
     size_t s = 0;
@@ -199,6 +208,9 @@ struct Lane {
   std::condition_variable cv;
   std::function<void()> job;
   bool busy = false, quit = false;
+  // active: a batch runs on this lane (worker or calling thread); reserving:
+  // another lane's thread is sizing this lane's arena (see share_arena_size)
+  bool active = false, reserving = false;
   int rc = 0;
 
   int fail(int code, const std::string& m) {
@@ -236,7 +248,30 @@ struct Lane {
   }
   void wait() {
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [this] { return !busy; });
+    cv.wait(lk, [this] { return !busy && !reserving; });
+  }
+  void enter() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !reserving; });
+    active = true;
+  }
+  void leave() {
+    std::lock_guard<std::mutex> lk(mu);
+    active = false;
+    cv.notify_all();
+  }
+  // size this (idle) lane's arena from another thread; false if the lane is in use
+  bool try_reserve(size_t bytes) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (busy || active || reserving) return false;
+      reserving = true;
+    }
+    arena.reserve(bytes);
+    std::lock_guard<std::mutex> lk(mu);
+    reserving = false;
+    cv.notify_all();
+    return true;
   }
   void stop() {
     if (!th.joinable()) return;
