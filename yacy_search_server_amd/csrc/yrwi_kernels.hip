@@ -556,6 +556,33 @@ __device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo
 // thread takes COMPACT_UNROLL matches at a time and issues all their pair and
 // row loads before combining any of them: the gathers are latency-bound, so
 // more of them in flight per thread is what moves the rows.
+// Gather loads of k_compact.  Every list and container starts 256-B aligned and
+// its allocation is rounded up to 256 B, so a row (40 B at an 8-B aligned
+// offset) lies inside the three 16-B aligned blocks starting at floor16(p):
+// three dwordx4 loads replace five dwordx2 loads, and the block past the row
+// (p % 16 == 0) is still inside the allocation.  The joined row needs only
+// bytes 16..23 and 32..39 of the B row (J5: u w p / c t r o), two loads.
+__device__ __forceinline__ Row load_row_wide(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(a & ~(uintptr_t)15);
+  const ulonglong2 x = q[0], y = q[1], z = q[2];
+  const bool odd = (a & 15) != 0;  // row starts at byte 8 of the first block
+  Row r;
+  r.w[0] = odd ? x.y : x.x;
+  r.w[1] = odd ? y.x : x.y;
+  r.w[2] = odd ? y.y : y.x;
+  r.w[3] = odd ? z.x : y.y;
+  r.w[4] = odd ? z.y : z.x;
+  return r;
+}
+__device__ __forceinline__ Row load_row_join_side(const uint8_t* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  Row r{};
+  r.w[2] = q[2];
+  r.w[4] = q[4];
+  return r;
+}
+
 constexpr int COMPACT_TILES = 16;
 constexpr int COMPACT_UNROLL = 4;
 
@@ -626,9 +653,9 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
-      A[u] = load_row(X.mode == JM_TEST_LARGE_B ? X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES
-                                                 : X.ar + (int64_t)pr[u].x * YRWI_ROW_BYTES);
-      if (X.mode == JM_ENUM) B[u] = load_row(X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES);
+      A[u] = load_row_wide(X.mode == JM_TEST_LARGE_B ? X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES
+                                                      : X.ar + (int64_t)pr[u].x * YRWI_ROW_BYTES);
+      if (X.mode == JM_ENUM) B[u] = load_row_join_side(X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
