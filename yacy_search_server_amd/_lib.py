@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyrwi.so")
+LIB_PATH = os.environ.get("YRWI_LIB") or os.path.join(_HERE, "libyrwi.so")  # YRWI_LIB: kernel-variant builds
 
 PROFILE_FIELDS = [
     "coeff_domlength", "coeff_date", "coeff_wordsintitle", "coeff_wordsintext",

@@ -583,8 +583,14 @@ __device__ __forceinline__ Row load_row_join_side(const uint8_t* p) {
   return r;
 }
 
-constexpr int COMPACT_TILES = 16;
-constexpr int COMPACT_UNROLL = 4;
+#ifndef YRWI_COMPACT_TILES
+#define YRWI_COMPACT_TILES 16
+#endif
+#ifndef YRWI_COMPACT_UNROLL
+#define YRWI_COMPACT_UNROLL 4
+#endif
+constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
+constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
 
 struct CompactJob {
   const uint8_t* ar;
