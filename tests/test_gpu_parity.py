@@ -259,6 +259,49 @@ def test_forced_join_algorithm(corpus, ratio, monkeypatch):
         assert got == [(h, s) for h, s, _ in orc.search(d, ih, eh, now_ms=NOW)]
 
 
+def _keyed_rows(keys, seed):
+    """Valid 40-B rows whose url hashes are jl.key_to_hash(key) (ascending keys -> sorted list)."""
+    rng = np.random.default_rng(seed)
+    n = len(keys)
+    rows = np.zeros((n, 40), dtype=np.uint8)
+    for i, k in enumerate(keys):
+        rows[i, :12] = np.frombuffer(jl.key_to_hash(int(k) << 20 | 7), dtype=np.uint8)
+    rows[:, 12:14] = np.frombuffer((15000).to_bytes(2, "big"), dtype=np.uint8)
+    rows[:, 18] = 50
+    rows[:, 21] = ord("t")
+    rows[:, 22:24] = np.frombuffer(b"en", dtype=np.uint8)
+    p = rng.integers(1, 3000, n)
+    rows[:, 34] = (p >> 8) & 0xFF
+    rows[:, 35] = p & 0xFF
+    rows[:, 33] = rng.integers(1, 20, n)
+    rows[:, 38] = rng.integers(0, 40, n)
+    return rows
+
+
+@pytest.mark.parametrize("nab", [(2048, 2048), (2047, 2050), (4095, 4097), (6000, 6289), (12288, 1)])
+def test_merge_tile_boundaries(nab, monkeypatch):
+    """Merge-path tiles (forced) over lists whose combined length sits on and
+    around multiples of the tile size, every B key matching: matches on both
+    sides of each tile split and the lookahead element must all be joined once."""
+    monkeypatch.setenv("YRWI_PROBE_RATIO", "1000000000")
+    na, nb = nab
+    a = _keyed_rows(np.arange(na), 1)
+    b = _keyed_rows(np.arange(0, 2 * nb, 2)[:nb], 2)
+    d = {b"TERMtileA___": a, b"TERMtileB___": b}
+    ix = RWIIndex(0)
+    try:
+        for h, r in d.items():
+            ix.add(h, r)
+        q = [b"TERMtileA___", b"TERMtileB___"]
+        for md in (2147483647, 100):
+            assert np.array_equal(ix.term_search(q, [], md, NOW), orc.term_search(d, q, [], md, NOW)), md
+            assert np.array_equal(ix.term_search(q[:1], q[1:], md, NOW), orc.term_search(d, q[:1], q[1:], md, NOW))
+        got = [(h.urlhash, h.score) for h in ix.search(q, now_ms=NOW, k=300)]
+        assert got == [(h, s) for h, s, _ in orc.search(d, q, now_ms=NOW, k=300)]
+    finally:
+        ix.close()
+
+
 @pytest.mark.parametrize("gb", ["0.000001", "0.002"])
 def test_batch_split_by_scratch_budget(corpus, gb, monkeypatch):
     """A batch larger than the scratch budget runs as consecutive passes over

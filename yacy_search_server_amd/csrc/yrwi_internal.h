@@ -9,7 +9,10 @@
 namespace yrwi {
 
 // ---------------------------------------------------------------- geometry
-constexpr int JOIN_TILE = 2048;      // merge-path items per join workgroup
+#ifndef YRWI_JOIN_TILE
+#define YRWI_JOIN_TILE 4096
+#endif
+constexpr int JOIN_TILE = YRWI_JOIN_TILE;  // merge-path items per join workgroup
 constexpr int JOIN_THREADS = 256;
 constexpr int JOIN_IPT = JOIN_TILE / JOIN_THREADS;
 constexpr int JOIN_MAXM = JOIN_TILE / 2 + 1;  // matches per tile <= min(#A, #B + 1)

@@ -243,7 +243,7 @@ __device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint
 }
 
 // ============================================================ join: tiles
-constexpr int JOIN_SLOTS = (JOIN_TILE + 1 + JOIN_THREADS - 1) / JOIN_THREADS;  // 2049 items max per tile
+constexpr int JOIN_SLOTS = (JOIN_TILE + 1 + JOIN_THREADS - 1) / JOIN_THREADS;  // JOIN_TILE + 1 items max per tile
 
 struct TileKeys {
   uint32_t a[JOIN_SLOTS], b[JOIN_SLOTS];
@@ -584,7 +584,7 @@ __device__ __forceinline__ Row load_row_join_side(const uint8_t* p) {
 }
 
 #ifndef YRWI_COMPACT_TILES
-#define YRWI_COMPACT_TILES 16
+#define YRWI_COMPACT_TILES 4
 #endif
 #ifndef YRWI_COMPACT_UNROLL
 #define YRWI_COMPACT_UNROLL 4
