@@ -1,0 +1,19 @@
+#!/bin/bash
+# Merge-vs-probe threshold sweep (YRWI_PROBE_RATIO) on the GPU box: bench line + kernel averages per ratio.
+set -e
+R=$(pwd)
+mkdir -p $R/gpurun_out/ratio
+cd /tmp && export TMPDIR=/tmp
+for P in ${RATIOS:-8 16 32 64 128}; do
+  YRWI_PROBE_RATIO=$P timeout -k 10 200 python3 $R/bench.py --cpu-budget 1 --latency 0 > $R/gpurun_out/ratio/$P.json 2> $R/gpurun_out/ratio/$P.err
+  rm -rf /tmp/kv
+  YRWI_PROBE_RATIO=$P timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kv -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 > /tmp/kv.log 2>&1
+  python3 - ratio$P $R/gpurun_out/ratio/$P.json <<'PY' >> $R/gpurun_out/ratio/summary.txt
+import csv, glob, json, sys
+f = glob.glob("/tmp/kv/**/*kernel_stats.csv", recursive=True)[0]
+k = {r["Name"].split("(")[0]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f))}
+b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+print(sys.argv[1], "ms/step %.3f" % b["ms_per_step"], "mismatch %s" % (b.get("parity_sample") or {}).get("mismatches"), " ".join("%s %.1f" % (n.split("::")[-1], v) for n, v in k.items() if n.split("::")[-1] in ("k_compact", "k_join", "k_probe", "k_partition", "k_probe_part")))
+PY
+done
+cat $R/gpurun_out/ratio/summary.txt
