@@ -15,7 +15,7 @@ import csv, glob, json, sys
 f = glob.glob("/tmp/kv/**/*kernel_stats.csv", recursive=True)[0]
 k = {r["Name"].split("(")[0]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f))}
 b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(sys.argv[1], "ms/step %.3f" % b["ms_per_step"], "mismatch %s" % (b.get("parity_sample") or {}).get("mismatches"), " ".join("%s %.1f" % (n.split("::")[-1], v) for n, v in k.items() if n.split("::")[-1] in ("k_compact", "k_join", "k_score", "k_probe", "k_partition")))
+print(sys.argv[1], "ms/step %.3f" % b["ms_per_step"], "mismatch %s" % (b.get("parity_sample") or {}).get("mismatches"), " ".join("%s %.1f" % (n.split("::")[-1], v) for n, v in k.items() if n.split("::")[-1] in ("k_compact", "k_join", "k_score", "k_probe", "k_partition", "k_score_full")))
 PY
 done
 cat $R/gpurun_out/var/summary.txt

@@ -1528,6 +1528,11 @@ __device__ __forceinline__ bool passes(const FilterQ& F, const Row& r) {
 // redo list.  k_score_full re-scores those with the whole chunk in LDS.  Flag
 // counts are taken once, by k_score.
 constexpr int SCORE_SMALL = 256;
+#ifndef YRWI_SCORE_CAP
+#define YRWI_SCORE_CAP 128
+#endif
+constexpr int SCORE_CAP = YRWI_SCORE_CAP;  // early-exit bound of k_score's radix select (0: exact kq-th key)
+static_assert(SCORE_CAP <= SCORE_SMALL, "the selected prefix must fit k_score's LDS");
 
 // score keys of one chunk: a[s] = score ^ 2^63 of element e0 + s*CHUNK_THREADS,
 // bit s of the result set when that element is live and admitted
@@ -1555,9 +1560,13 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
   return vm;
 }
 
-// MSB-first radix select over the live keys: the largest T with at least kq live keys >= T
+// MSB-first radix select over the live keys: the largest T with at least kq live keys >= T.
+// With cap > 0 the select stops at the first digit whose bin takes the count of
+// keys >= the bin's lowest key to at most cap: T is then that lowest key, a
+// threshold with kq..cap keys above it (k_score sorts whatever T selects, so any
+// such T is exact for it; fewer passes, each 3 barriers and a histogram).
 __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t vm, int32_t kq, int32_t* sHist,
-                                                    int32_t* sSel, uint64_t* sRed) {
+                                                    int32_t* sSel, uint64_t* sRed, int32_t cap = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t mx = 0, mn = ~0ull;
 #pragma unroll
@@ -1587,6 +1596,7 @@ __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t 
     if (tid < 64) radix_pick(sHist, rem, sSel);
     __syncthreads();
     prefix |= (uint64_t)sSel[0] << lo;
+    if (cap > 0 && kq - sSel[1] + sSel[2] <= cap) return prefix;  // keys above the bin + the whole bin
     rem = sSel[1];
     hi = lo;
   }
@@ -1639,7 +1649,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (tid == 0) cand_cnt[b] = 0;
     return;
   }
-  const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed) : 0;
+  const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed, SCORE_CAP) : 0;
   int32_t mine = 0;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) mine += (((vm >> s) & 1u) && a[s] >= T) ? 1 : 0;
