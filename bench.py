@@ -188,7 +188,7 @@ def main():
     bufs = [(ix.host_array(CHit, args.nq * kmax), ix.host_array(ctypes.c_int32, args.nq), CStats())
             for _ in range(depth)]
     agg = {"postings_in": 0, "bytes_join": 0, "t_join_ns": 0, "n_join": 0, "bytes_alg": 0, "joined": 0,
-           "bytes_probe": 0, "t_probe_ns": 0, "t_norm_ns": 0, "t_score_ns": 0, "t_total_ns": 0}
+           "bytes_probe": 0, "t_probe_ns": 0, "bytes_compact": 0, "t_compact_ns": 0, "t_norm_ns": 0, "t_score_ns": 0, "t_total_ns": 0}
     state = {"depth": depth}
 
     def collect(st):
@@ -197,6 +197,8 @@ def main():
         agg["t_join_ns"] += st.t_join_ns
         agg["bytes_probe"] += st.bytes_probe
         agg["t_probe_ns"] += st.t_probe_ns
+        agg["bytes_compact"] += st.bytes_compact
+        agg["t_compact_ns"] += st.t_compact_ns
         agg["n_join"] += st.n_join_launches
         agg["bytes_alg"] += st.bytes_alg
         agg["joined"] += st.joined
@@ -260,7 +262,8 @@ def main():
     pmc = load_pmc(args.config)
 
     def roofline(a, kernel):
-        tkey, bkey = ("t_join_ns", "bytes_join") if kernel == "k_join" else ("t_probe_ns", "bytes_probe")
+        tkey, bkey = {"k_join": ("t_join_ns", "bytes_join"), "k_probe": ("t_probe_ns", "bytes_probe"),
+                      "k_compact": ("t_compact_ns", "bytes_compact")}[kernel]
         t = a[tkey] / max(1, a["n_join"]) * 1e-9
         bpl = a[bkey] / max(1, a["n_join"])
         ach = bpl / t / 1e9 if t > 0 else 0.0
@@ -269,15 +272,22 @@ def main():
                 "traffic": pmc.get(f"{kernel}_hbm_bytes_per_launch") if pmc else None,
                 "kernel": kernel, "bytes_per_launch_alg": int(bpl), "mean_launch_us": round(t * 1e6, 2)}
 
-    roof = roofline(iso, "k_join")
+    def with_traffic(r):
+        if r.get("traffic") and r["mean_launch_us"]:
+            r["traffic_GBps"] = round(r["traffic"] / (r["mean_launch_us"] * 1e-6) / 1e9, 1)
+            r["traffic_frac"] = round(r["traffic_GBps"] / HBM_PEAK_GBS, 4)
+        return r
+
+    # The dominant kernel is k_compact (the row gathers of the joined container):
+    # its algorithmic bytes are the rows it must read and write; the PMC traffic
+    # beside it shows the sector cost of gathering sparse 40-B rows.
+    roof = with_traffic(roofline(iso, "k_compact"))
     roof["measured"] = "HIP events around each launch, separate pass of the timed batch with 1 batch in flight"
     # BASELINE.md §4 counts 12 B per posting key; the join streams 4-byte url ids
-    # (DESIGN.md §3), so the HBM bytes it moves are far fewer: that rate is here
-    if roof.get("traffic") and roof["mean_launch_us"]:
-        roof["traffic_GBps"] = round(roof["traffic"] / (roof["mean_launch_us"] * 1e-6) / 1e9, 1)
-        roof["traffic_frac"] = round(roof["traffic_GBps"] / HBM_PEAK_GBS, 4)
-    roof_probe = roofline(iso, "k_probe")
-    roof_timed = roofline(timed, "k_join")
+    # (DESIGN.md §3), so the HBM bytes it moves are far fewer than its K
+    roof_join = with_traffic(roofline(iso, "k_join"))
+    roof_probe = with_traffic(roofline(iso, "k_probe"))
+    roof_timed = roofline(timed, "k_compact")
     roof_timed["measured"] = "HIP events around each launch inside the timed region (2 lanes overlap)"
 
     # single-query latency (host call -> top-k in host memory)
@@ -337,6 +347,7 @@ def main():
                        "queries_per_step": args.nq, "postings_per_step": total_post / args.steps,
                        "index_postings_total": int(full.n_postings), "parallelism": f"url-hash shards x{world}"},
             "roofline": roof,
+            "roofline_join": roof_join,
             "roofline_probe": roof_probe,
             "roofline_timed": roof_timed,
             "cpu_baseline": cpu,

@@ -63,12 +63,10 @@ def main(tag, config):
             d["write_kb_per_launch"] = write[k]["WRITE_SIZE"] / nw[k]
         if "fetch_kb_per_launch_raw" in d and "write_kb_per_launch" in d:
             d["hbm_bytes_per_launch"] = (2 * d["fetch_kb_per_launch_raw"] + d["write_kb_per_launch"]) * 1024
-    kj = out["kernels"].get("k_join", {})
-    out["k_join_hbm_bytes_per_launch"] = kj.get("hbm_bytes_per_launch")
-    out["k_join_avg_ns"] = kj.get("avg_ns")
-    kp = out["kernels"].get("k_probe", {})
-    out["k_probe_hbm_bytes_per_launch"] = kp.get("hbm_bytes_per_launch")
-    out["k_probe_avg_ns"] = kp.get("avg_ns")
+    for name in ("k_compact", "k_join", "k_probe"):
+        kd = out["kernels"].get(name, {})
+        out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
+        out[name + "_avg_ns"] = kd.get("avg_ns")
     for log in ("kt.log", "fetch.log", "write.log"):
         p = os.path.join(base, log)
         if os.path.exists(p):

@@ -461,6 +461,7 @@ static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
 struct Timing {
   // per join step: before k_join, between k_join and k_probe, after k_probe
   std::vector<std::array<hipEvent_t, 3>> kjoin;
+  std::vector<std::array<hipEvent_t, 2>> kcompact;  // around each k_compact launch
   hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
 };
 
@@ -562,14 +563,20 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
     hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
+    hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
     if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
-                         ctx->stream, e0, em, e1))
+                         ctx->stream, e0, em, e1, c0, c1))
       return ctx->fail(YRWI_E_HIP, "join launch");
-    if (tm) tm->kjoin.push_back({e0, em, e1});
+    if (tm) {
+      tm->kjoin.push_back({e0, em, e1});
+      tm->kcompact.push_back({c0, c1});
+    }
     if (st) st->n_join_launches++;
     mh.assign((size_t)nj, 0);
     HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, lane_sync(ctx));
+    if (st)  // k_compact per joined row: pair + id, the row(s) it gathers, row + id written
+      for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 136 : 96);
     for (int j = 0; j < nj; j++) {
       Plan& P = plans[(size_t)owner[(size_t)j]];
       P.cont = DList{nullptr, nullptr, jobs[(size_t)j].out_rows, mh[(size_t)j], jobs[(size_t)j].out_uid};
@@ -1069,6 +1076,8 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_join_ns += (int64_t)(ms * 1e6);
         if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) st->t_probe_ns += (int64_t)(ms * 1e6);
       }
+      for (auto& ev : tm.kcompact)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_compact_ns += (int64_t)(ms * 1e6);
       if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
       if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
     }
@@ -1141,6 +1150,8 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->bytes_probe += p.bytes_probe;
       st->t_join_ns += p.t_join_ns;
       st->t_probe_ns += p.t_probe_ns;
+      st->bytes_compact += p.bytes_compact;
+      st->t_compact_ns += p.t_compact_ns;
       st->t_norm_ns += p.t_norm_ns;
       st->t_score_ns += p.t_score_ns;
       st->n_join_launches += p.n_join_launches;

@@ -193,7 +193,7 @@ struct Lane {
   hipEvent_t coll_ev[2] = {nullptr, nullptr};
   Stage stage;
   Stage out_stage;           // pinned landing buffer for results
-  int64_t probe_ratio = 16;  // YRWI_PROBE_RATIO, read once per call
+  int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
   Arena arena{(size_t)256 << 20};
   std::string err;
   std::vector<hipEvent_t> evpool;
@@ -382,7 +382,7 @@ inline int begin_pass(Lane* ctx) {
   ctx->stage.used = 0;
   ctx->evnext = 0;
   const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
-  ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16;
+  ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)8;
   return 0;
 }
 

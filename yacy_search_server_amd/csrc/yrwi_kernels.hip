@@ -389,6 +389,11 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 // thread, all tiles in parallel); k_probe binary-searches each key inside its
 // tile's range.  Output and mark semantics are k_join's.
 
+#ifndef YRWI_PROBE_LDS
+#define YRWI_PROBE_LDS 4096
+#endif
+#define PROBE_LDS YRWI_PROBE_LDS  // large-list range (ids) a probe tile stages in LDS; 0: always gather
+
 __device__ __forceinline__ int64_t lower_bound_uid(const uint32_t* __restrict__ u, int64_t lo, int64_t hi, uint32_t x) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
@@ -434,6 +439,9 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                      int32_t* __restrict__ tile_cnt, int mark) {
   __shared__ int32_t sScan[4];
+#if PROBE_LDS > 0
+  __shared__ uint32_t sL[PROBE_LDS];
+#endif
   const int64_t t = blockIdx.x;
   const int64_t b = tile0 + t;
   const ProbeDesc D = pdesc[t];
@@ -445,6 +453,26 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   bool hit = false;
   int64_t jl = 0;
   uint32_t key = 0;
+#if PROBE_LDS > 0
+  const int64_t R = D.hi - D.lo;  // workgroup-uniform
+  if (R <= PROBE_LDS) {
+    // short range: read it once, coalesced, and search in LDS -- 4 B per range
+    // id instead of the two or three sector gathers per key of the lower levels
+    const uint32_t* __restrict__ g = Lg.uid + D.lo;
+    for (int x = threadIdx.x; x < (int)R; x += PROBE_TILE) sL[x] = g[x];
+    if (i < Sm.n) key = Sm.uid[i];
+    __syncthreads();
+    if (i < Sm.n) {
+      int lo = 0, hi = (int)R;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sL[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      jl = D.lo + lo;
+      hit = lo < (int)R && sL[lo] == key;
+    }
+  } else
+#endif
   if (i < Sm.n) {
     // the upper levels of the 256 searches share lines of the range (L2 hits)
     key = Sm.uid[i];
@@ -2220,7 +2248,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark,
                      void* st, void* ev0,
-                     void* evm, void* ev1) {
+                     void* evm, void* ev1, void* evc0, void* evc1) {
   if (total_tiles <= 0) return 0;
   static int join_grid = 0;  // resident k_join workgroups on the whole device
   if (!join_grid) {
@@ -2251,8 +2279,10 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off);
+    if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
                        S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_cnt, d_tile_off);
+    if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
   }
   return rc(hipGetLastError());
 }
