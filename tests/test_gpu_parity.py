@@ -435,3 +435,23 @@ def test_async_batches_pinned_and_pageable(corpus):
             assert got == [(h, s) for h, s, _ in exp]
     with pytest.raises(Exception):
         ix.wait(tickets[0][0])  # a ticket is collected once
+
+
+def test_stats_compact_accounting(corpus):
+    """yrwi_stats: a two-term query joins in one step, so k_compact's algorithmic
+    bytes are the joined rows times 136 (enumeration) or 96 (by test), and its
+    HIP-event time is positive whenever rows were joined."""
+    from yacy_search_server_amd._lib import CStats
+    cfg, idx, ix = corpus
+    seen = 0
+    for inc, _ in synth.queries(cfg, 12, 2, 2, 0, qseed=77):
+        if len(set(inc)) < 2:
+            continue
+        st = CStats()
+        ix.search_batch([Query([idx.hashes[t] for t in inc], [], k=20, now_ms=NOW)], stats=st)
+        if st.joined == 0:
+            continue
+        seen += 1
+        assert st.bytes_compact in (136 * st.joined, 96 * st.joined), (st.bytes_compact, st.joined)
+        assert st.t_compact_ns > 0
+    assert seen > 0
