@@ -74,6 +74,9 @@ def load():
         lib.yo_join_dispatch.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]
         lib.yo_fold_order.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         lib.yo_profile_default.argtypes = [ctypes.POINTER(YoProfile)]
+        lib.yo_join_step.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         _lib = lib
     return _lib
 
@@ -172,6 +175,23 @@ def join_dispatch(n1: int, n2: int) -> Tuple[bool, bool]:
     s = ctypes.c_int32(0)
     bt = load().yo_join_dispatch(n1, n2, ctypes.byref(s))
     return bool(bt), bool(s.value)
+
+
+def join_step(r1: np.ndarray, r2: np.ndarray, mode: int, max_distance: int = 2147483647,
+              now_ms: int = 0) -> np.ndarray:
+    """One joinConstructive step with a forced dispatch (0 enumeration, 1 by test
+    small=r1, 2 by test small=r2); see yo_join_step."""
+    lib = load()
+    a = np.ascontiguousarray(r1, dtype=np.uint8).reshape(-1, 40)
+    b = np.ascontiguousarray(r2, dtype=np.uint8).reshape(-1, 40)
+    cap = max(1, min(len(a), len(b)))
+    out = np.zeros((cap, 40), dtype=np.uint8)
+    m = ctypes.c_int64(0)
+    rc = lib.yo_join_step(a.ctypes.data if len(a) else None, len(a), b.ctypes.data if len(b) else None, len(b),
+                          mode, max_distance, now_ms, out.ctypes.data, cap, ctypes.byref(m))
+    if rc != 0:
+        raise RuntimeError(f"yo_join_step rc={rc}")
+    return out[:m.value].copy()
 
 
 def fold_order(sizes: Sequence[int]) -> List[int]:

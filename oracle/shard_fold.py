@@ -9,7 +9,9 @@ composition reproduces the single-container fold of ReferenceOrder exactly
 (WordReferenceVars.min/max :383-455, the distance fold :431-445).
 """
 
-from typing import List, Tuple
+from typing import Callable, Dict, List, Sequence, Tuple
+
+import numpy as np
 
 import java_literal as jl
 
@@ -91,6 +93,106 @@ def combine(summaries: List[dict], now_ms: int) -> Tuple[dict, dict, Tuple[float
             piece(Pj, M, L)
     D = abs(P - A) if (hasA and P > 0) else 0
     return mn, mx, tf, vmn, vmx, D
+
+
+def _b64key(h: bytes):
+    return [jl.AHPLA[c] for c in h]
+
+
+def shard_term_search(local: Dict[bytes, np.ndarray], incl: Sequence[bytes], excl: Sequence[bytes],
+                      max_distance: int, now_ms: int, allsum: Callable[[List[int]], List[int]]) -> np.ndarray:
+    """TermSearch + joinExcludeContainers on ONE url-hash shard, the way libyrwi
+    runs it (yrwi_host.cpp plan_query / run_join_phase).
+
+    Every decision the reference takes on container sizes is taken on the GLOBAL
+    sizes -- the sum over shards, obtained with ``allsum`` (element-wise sum of a
+    list of ints over all ranks; every rank makes the same sequence of calls):
+      J1  a missing include term empties the result, a missing exclude term
+          disables exclusion (AbstractIndex.java:108-127);
+      J2  the fold order (int)(size*1000 + i) (ReferenceContainer.java:334-366);
+      J3  the dispatch of every step, including the size of the intermediate
+          joined container (:406-416).
+    The rows joined are the shard's own, so the concatenation of the shards'
+    results in shard order is the single-container result."""
+    import oracle as orc
+    inc = sorted({bytes(h) for h in incl}, key=_b64key)
+    exc = sorted({bytes(h) for h in excl}, key=_b64key)
+    empty = np.zeros((0, 40), dtype=np.uint8)
+    lists = {h: (local[h] if h in local else empty) for h in inc + exc}
+    g = allsum([len(lists[h]) for h in inc + exc])
+    gi, ge = g[:len(inc)], g[len(inc):]
+    if not inc or min(gi) == 0:
+        return empty
+    use_excl = len(exc) > 0 and min(ge) > 0
+    order = orc.fold_order(gi)
+    acc, acc_g = lists[inc[order[0]]], gi[order[0]]
+    for j in order[1:]:
+        if acc_g == 0:
+            break
+        bt, small_is_1 = orc.join_dispatch(acc_g, gi[j])
+        mode = (1 if small_is_1 else 2) if bt else 0
+        acc = orc.join_step(acc, lists[inc[j]], mode, max_distance, now_ms)
+        acc_g = allsum([len(acc)])[0]
+    if acc_g == 0 or len(acc) == 0:
+        return empty
+    if use_excl:
+        keep = np.ones(len(acc), dtype=bool)
+        ak = [bytes(r[:12]) for r in acc]
+        for h in exc:
+            ex = {bytes(r[:12]) for r in lists[h]}
+            keep &= np.array([k not in ex for k in ak], dtype=bool)
+        acc = acc[keep]
+    return acc
+
+
+def lockstep_allsum(world: int):
+    """allsum callables for `world` threads simulating the ranks in one process."""
+    import threading
+    bar = threading.Barrier(world)
+    slots: List[List[int]] = [None] * world  # type: ignore[list-item]
+    out: List[List[int]] = [None]  # type: ignore[list-item]
+
+    def make(rank: int):
+        def allsum(v: List[int]) -> List[int]:
+            slots[rank] = list(v)
+            if bar.wait() == 0:
+                out[0] = [sum(x) for x in zip(*slots)]
+            bar.wait()
+            res = list(out[0])
+            bar.wait()
+            return res
+        return allsum
+    return [make(r) for r in range(world)]
+
+
+def sharded_term_search(parts: List[Dict[bytes, np.ndarray]], incl, excl, max_distance: int = 2147483647,
+                        now_ms: int = 0, protocol: str = "global") -> List[np.ndarray]:
+    """All shards of one query in one process.  protocol "global" is libyrwi's
+    (shard_term_search); "local" plans every shard on its own list sizes (the
+    round-1 behaviour, kept to show what it breaks)."""
+    import threading
+    import oracle as orc
+    W = len(parts)
+    if protocol == "local":
+        return [orc.term_search(p, incl, excl, max_distance, now_ms) for p in parts]
+    fns = lockstep_allsum(W)
+    res: List[np.ndarray] = [None] * W  # type: ignore[list-item]
+    errs = []
+
+    def run(r):
+        try:
+            res[r] = shard_term_search(parts[r], incl, excl, max_distance, now_ms, fns[r])
+        except Exception as e:  # pragma: no cover - surfaced below
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise RuntimeError(errs[0])
+    return res
 
 
 def shard_of(urlhash: bytes, world: int) -> int:

@@ -687,6 +687,34 @@ int yo_fold_order(const int64_t* sizes, int n, int32_t* order_out) {
   return k;
 }
 
+// One joinConstructive step (:397-417) with the dispatch given by the caller:
+// mode 0 = joinConstructiveByEnumeration(i1, i2) (:448-489), 1 = by test with
+// small = i1 / large = i2, 2 = by test with small = i2 / large = i1 (:419-446).
+// The sharded protocol (oracle/shard_fold.py) takes the dispatch from the GLOBAL
+// container sizes and joins the shard-local rows with it.  Returns 0, -1 when
+// `cap` rows are too few, -7 on an empty language cell.
+int yo_join_step(const uint8_t* r1, int64_t n1, const uint8_t* r2, int64_t n2, int32_t mode,
+                 int32_t max_distance, int64_t now_ms, uint8_t* rows_out, int64_t cap, int64_t* m_out) {
+  *m_out = 0;
+  Container a, b, res;
+  a.ext = r1;
+  a.n = n1;
+  b.ext = r2;
+  b.n = n2;
+  Err err;
+  bool ok = true;
+  if (n1 > 0 && n2 > 0) {
+    if (mode == 1) ok = join_by_test(a, b, max_distance, now_ms, &res, &err);
+    else if (mode == 2) ok = join_by_test(b, a, max_distance, now_ms, &res, &err);
+    else ok = join_by_enum(a, b, max_distance, now_ms, &res, &err);
+  }
+  if (!ok) return err.code;
+  if (res.n > cap) return -1;
+  if (res.n > 0) std::memcpy(rows_out, res.rows.data(), (size_t)res.n * ROW);
+  *m_out = res.n;
+  return 0;
+}
+
 // Full canonical query: term search -> normalise -> cardinal -> top-k.
 int yo_search(const yo_list* incl, int nincl, const yo_list* excl, int nexcl, int32_t max_distance,
               const yo_profile* prof, const char* lang, int64_t now_ms, int32_t k, yo_hit* out,

@@ -109,3 +109,109 @@ def test_loopback_shards_filters_and_doubledom():
             e = jl.search(lit, q.include, q.exclude, jl.RankingProfile(), "en", now_ms=NOW, k=k, filt=lf)
             assert [(h.urlhash, h.score) for h in g] == e, (r, kw, k)
             assert q.filter.flagcount == lf.flagcount, (r, kw, k)
+
+
+def _run_parts(parts, world, fn):
+    """parts: per-rank {term hash: rows}; fn(rank, RWIIndex) runs on every rank's own
+    thread (the same call sequence on every rank); returns the per-rank results."""
+    uid = _loop_id()
+    ixs = [None] * world
+    out = [None] * world
+    errs = []
+
+    def opener(r):
+        try:
+            ixs[r] = RWIIndex(0, shard=(r, world, uid))
+            for h, rows in parts[r].items():
+                ixs[r].add(h, rows)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    def runner(r):
+        try:
+            out[r] = fn(r, ixs[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+
+    for f in (opener, runner):
+        ths = [threading.Thread(target=f, args=(r,)) for r in range(world)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=300)
+        assert not errs, errs
+    for ix in ixs:
+        ix.close()
+    return out
+
+
+def _flip_band_queries(full, whole, parts, nq, seed):
+    """Queries whose result a shard-local plan would get wrong (the J2/J3 decisions
+    flip on local sizes), found with the oracle, plus a few ordinary ones."""
+    import shard_fold as sf
+    flip, plain = [], []
+    for nex in (0, 1, 2):
+        for inc, exc in synth.queries(full, nq, 2, 3, nex, qseed=seed + nex):
+            ih = [synth.term_hash(full, t) for t in inc]
+            eh = [synth.term_hash(full, t) for t in exc]
+            ref = orc.term_search(whole, ih, eh, 2147483647, NOW)
+            loc = [np.asarray(x).reshape(-1, 40) for x in sf.sharded_term_search(parts, ih, eh, 2147483647, NOW, "local")]
+            same = np.array_equal(np.concatenate(loc) if loc else np.zeros((0, 40), np.uint8), ref)
+            (plain if same else flip).append((ih, eh))
+    return flip, plain[:8]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_flip_band_global_planning(world):
+    """Sharded planning on GLOBAL list sizes (J1 existence, J2 fold order, J3 dispatch of
+    every step): the queries that shard-local planning gets wrong are bit-exact, both the
+    joined containers (yrwi_join_exclude per shard, concatenated in shard order) and the
+    ranked top-100."""
+    full = synth.preset("small")
+    whole = synth.build_index(full).as_dict()
+    parts = [synth.build_index(full.shard(r, world)).as_dict() for r in range(world)]
+    flip, plain = _flip_band_queries(full, whole, parts, 300, 7)
+    assert flip, "no query in the dispatch flip band"
+    cases = flip + plain
+
+    def fn(r, ix):
+        rows = [ix.term_search(ih, eh, now_ms=NOW) for ih, eh in cases]
+        hits = ix.search_batch([Query(ih, eh, now_ms=NOW, k=100) for ih, eh in cases])
+        return rows, hits
+
+    res = _run_parts(parts, world, fn)
+    for qi, (ih, eh) in enumerate(cases):
+        ref = orc.term_search(whole, ih, eh, 2147483647, NOW)
+        got = np.concatenate([res[r][0][qi].reshape(-1, 40) for r in range(world)])
+        assert np.array_equal(got, ref), ("join", qi, qi < len(flip))
+        exp = orc.search(whole, ih, eh, now_ms=NOW, k=100)
+        for r in range(world):
+            assert [(h.urlhash, h.score, h.tiebreak) for h in res[r][1][qi]] == exp, ("top-k", r, qi)
+
+
+def test_loopback_exclude_term_absent_from_a_shard():
+    """Two exclude terms, one of them held by a single shard: exclusion stays on for
+    every shard (J1 is decided on global sizes); a globally absent exclude term turns
+    all exclusion off on every shard."""
+    world = 8
+    full = synth.preset("small")
+    whole = synth.build_index(full).as_dict()
+    parts = [synth.build_index(full.shard(r, world)).as_dict() for r in range(world)]
+    sizes = synth.counts(full)
+    big = [int(t) for t in np.argsort(-sizes)[:3]]
+    hs = [synth.term_hash(full, t) for t in big]
+    rare = b"rareTERMxxxA"
+    rows = parts[3][hs[0]][::3].copy()
+    whole[rare] = rows
+    parts[3][rare] = rows
+    ih = [hs[0], hs[1]]
+    cases = [(ih, [rare, hs[2]]), (ih, [rare]), (ih, [b"AAAAAAAAAAAA", hs[2]]), ([hs[0], hs[2]], [rare])]
+
+    def fn(r, ix):
+        return ix.search_batch([Query(i, e, now_ms=NOW, k=100) for i, e in cases])
+
+    res = _run_parts(parts, world, fn)
+    for qi, (i, e) in enumerate(cases):
+        exp = orc.search(whole, i, e, now_ms=NOW, k=100)
+        for r in range(world):
+            assert [(h.urlhash, h.score, h.tiebreak) for h in res[r][qi]] == exp, (r, qi)

@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, preset, out_q):
+def _worker(rank, world, port, preset, nq, out_q):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -33,18 +33,33 @@ def _worker(rank, world, port, preset, out_q):
         now = 20741 * 86400000 + 99
         prof = orc.default_profile()
         fails = []
-        for qi, (inc, exc) in enumerate(synth.queries(full, 12, 1, 3, 1, qseed=5)):
+        import torch
+
+        def gsum(v):
+            t = torch.tensor(v, dtype=torch.int64)
+            dist.all_reduce(t)
+            return [int(x) for x in t.tolist()]
+
+        pd = part.as_dict()
+        wd = whole.as_dict()
+        for qi, (inc, exc) in enumerate(synth.queries(full, nq, 1, 3, 1, qseed=5)):
             ih = [whole.hashes[t] for t in inc]
             eh = [whole.hashes[t] for t in exc]
-            mine = orc.term_search(part.as_dict(), ih, eh, 2147483647, now)
+            # the shard-local join with the global-size protocol (libyrwi's plan_batch / run_join_phase)
+            mine = sf.shard_term_search(pd, ih, eh, 2147483647, now, gsum)
             # every url of my part maps to my shard
             for r in mine:
                 assert sf.shard_of(bytes(r[:12]), world) == rank
+            # the shards' containers, concatenated in shard order, are the single container
+            cat = [None] * world
+            dist.all_gather_object(cat, mine.tobytes())
+            if b"".join(cat) != orc.term_search(wd, ih, eh, 2147483647, now).tobytes():
+                fails.append((qi, "join"))
             summ = sf.shard_summary([bytes(r) for r in mine])
             allsum = [None] * world
             dist.all_gather_object(allsum, summ)
             mn, mx, tf, vmn, vmx, D = sf.combine(allsum, now)
-            ref_rows = orc.term_search(whole.as_dict(), ih, eh, 2147483647, now)
+            ref_rows = orc.term_search(wd, ih, eh, 2147483647, now)
             if len(ref_rows) == 0:
                 assert all(s["n"] == 0 for s in allsum)
                 continue
@@ -83,15 +98,15 @@ def _worker(rank, world, port, preset, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_normalisation_and_topk_merge(world):
+@pytest.mark.parametrize("world,preset,nq", [(2, "dense", 12), (4, "dense", 12), (2, "small", 40)])
+def test_sharded_normalisation_and_topk_merge(world, preset, nq):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + world * 7 + os.getpid() % 500
-    procs = [ctx.Process(target=_worker, args=(r, world, port, "dense", q)) for r in range(world)]
+    port = 29500 + world * 7 + len(preset) * 131 + os.getpid() % 500
+    procs = [ctx.Process(target=_worker, args=(r, world, port, preset, nq, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=600) for _ in procs]
+    res = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     for rank, fails in res:

@@ -393,47 +393,119 @@ static int plan_query(const yrwi_ctx* ix, Lane* ctx, const yrwi_query_desc& d, P
       return ctx->fail(YRWI_E_ARG, "filter: bad siteexcludes / urlhashes");
   }
   // HandleSet: sorted (Base64Order) set of term hashes
-  KeyT inc[YRWI_MAX_TERMS], exc[YRWI_MAX_TERMS];
   int ninc = 0, nexc = 0;
   for (int i = 0; i < d.nincl; i++)
-    if (!key_of(d.incl + 12 * i, &inc[ninc++])) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
+    if (!key_of(d.incl + 12 * i, &P->inc[ninc++])) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
   for (int i = 0; i < d.nexcl; i++)
-    if (!key_of(d.excl + 12 * i, &exc[nexc++])) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
-  std::sort(inc, inc + ninc);
-  ninc = (int)(std::unique(inc, inc + ninc) - inc);
-  std::sort(exc, exc + nexc);
-  nexc = (int)(std::unique(exc, exc + nexc) - exc);
+    if (!key_of(d.excl + 12 * i, &P->exc[nexc++])) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
+  std::sort(P->inc, P->inc + ninc);
+  ninc = (int)(std::unique(P->inc, P->inc + ninc) - P->inc);
+  std::sort(P->exc, P->exc + nexc);
+  nexc = (int)(std::unique(P->exc, P->exc + nexc) - P->exc);
+  P->ninc = ninc;
+  P->nexc = nexc;
+  auto local = [&](const KeyT& k) -> const ListRec* {
+    auto it = ix->lists.find(k);
+    return (it == ix->lists.end() || it->second.n == 0) ? nullptr : &it->second;
+  };
+  for (int i = 0; i < ninc; i++) P->linc[i] = local(P->inc[i]);
+  for (int i = 0; i < nexc; i++) P->lexc[i] = local(P->exc[i]);
   P->empty = true;
   P->postings_in = 0;
-  if (ninc == 0) return 0;
-  const ListRec* incl[YRWI_MAX_TERMS];
-  for (int i = 0; i < ninc; i++) {
-    auto it = ix->lists.find(inc[i]);
-    if (it == ix->lists.end() || it->second.n == 0) return 0;  // conjunction: any missing term -> empty
-    incl[i] = &it->second;
-  }
-  bool use_excl = nexc > 0;
+  for (int i = 0; i < ninc; i++) P->postings_in += P->linc[i] ? P->linc[i]->n : 0;
+  for (int i = 0; i < nexc; i++) P->postings_in += P->lexc[i] ? P->lexc[i]->n : 0;
+  return 0;
+}
+
+// A list of a query term that this url-hash shard does not hold.
+static const ListRec kAbsentList{};
+
+// The size-dependent decisions of TermSearch / joinContainers, taken on the
+// GLOBAL list sizes ng_inc / ng_exc (one context: its own sizes; url-hash
+// shards: the sum over all shards, so every shard takes the decisions the single
+// container would -- AbstractIndex.java:108-127, ReferenceContainer.java:334-366):
+//   J1  any include term without postings empties the result; any exclude term
+//       without postings disables the exclusion;
+//   J2  fold order by (int)(size*1000 + count), a later put overwriting an
+//       equal key.
+// The lists joined are the shard's own (absent ones are empty).
+static void plan_finish(Plan* P, const int64_t* ng_inc, const int64_t* ng_exc) {
+  P->empty = true;
+  P->seq.clear();
+  P->seq_ng.clear();
   P->excl.clear();
-  for (int i = 0; i < nexc && use_excl; i++) {
-    auto it = ix->lists.find(exc[i]);
-    if (it == ix->lists.end() || it->second.n == 0) use_excl = false;
-    else P->excl.push_back(&it->second);
-  }
-  if (!use_excl) P->excl.clear();
+  if (P->ninc == 0) return;
+  for (int i = 0; i < P->ninc; i++)
+    if (ng_inc[i] == 0) return;  // conjunction: any missing term -> empty
+  bool use_excl = P->nexc > 0;
+  for (int i = 0; i < P->nexc; i++)
+    if (ng_exc[i] == 0) use_excl = false;
+  if (use_excl)
+    for (int i = 0; i < P->nexc; i++)
+      if (P->lexc[i]) P->excl.push_back(P->lexc[i]);
   // joinContainers: TreeMap<Long>((int)(size*1000 + count)); put overwrites equal keys
   std::pair<int32_t, int> tm[YRWI_MAX_TERMS];
-  for (int c = 0; c < ninc; c++) tm[c] = {add32(mul32((int32_t)incl[c]->n, 1000), c), c};
-  std::stable_sort(tm, tm + ninc, [](const std::pair<int32_t, int>& a, const std::pair<int32_t, int>& b) {
+  for (int c = 0; c < P->ninc; c++) tm[c] = {add32(mul32((int32_t)ng_inc[c], 1000), c), c};
+  std::stable_sort(tm, tm + P->ninc, [](const std::pair<int32_t, int>& a, const std::pair<int32_t, int>& b) {
     return a.first < b.first;
   });
-  P->seq.clear();
-  for (int i = 0; i < ninc; i++) {
-    if (i + 1 < ninc && tm[i + 1].first == tm[i].first) continue;  // the later put wins
-    P->seq.push_back(incl[tm[i].second]);
+  for (int i = 0; i < P->ninc; i++) {
+    if (i + 1 < P->ninc && tm[i + 1].first == tm[i].first) continue;  // the later put wins
+    const int c = tm[i].second;
+    P->seq.push_back(P->linc[c] ? P->linc[c] : &kAbsentList);
+    P->seq_ng.push_back(ng_inc[c]);
   }
-  for (int i = 0; i < ninc; i++) P->postings_in += incl[i]->n;
-  for (auto* l : P->excl) P->postings_in += l->n;
   P->empty = false;
+}
+
+// Element-wise sum of v over the url-hash shards (every rank passes vectors of
+// the same length, in the same sequence of calls); identity on one context.
+static int allsum_host(Lane* L, std::vector<int64_t>& v) {
+  if (L->world <= 1 || v.empty()) return 0;
+  const size_t n = v.size();
+  int64_t* d_v = arena_alloc<int64_t>(L, (int64_t)n);
+  int64_t* d_all = arena_alloc<int64_t>(L, (int64_t)n * L->world);
+  if (!d_v || !d_all) return L->fail(YRWI_E_NOMEM, "arena");
+  if (upload(L, d_v, v)) return YRWI_E_HIP;
+  if (int rc = coll_allgather(L, d_v, d_all, n * sizeof(int64_t))) return rc;
+  std::vector<int64_t> all(n * (size_t)L->world);
+  HIPCHK(L, hipMemcpyAsync(all.data(), d_all, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(L, lane_sync(L));
+  for (size_t i = 0; i < n; i++) {
+    int64_t s = 0;
+    for (int r = 0; r < L->world; r++) s += all[(size_t)r * n + i];
+    v[i] = s;
+  }
+  return 0;
+}
+
+// plan_finish for a batch: global term sizes from one exchange of the local
+// sizes of the batch's distinct terms (sharded), or the local sizes (one context).
+static int plan_batch(Lane* L, std::vector<Plan>& plans) {
+  std::unordered_map<KeyT, size_t, KeyHash> slot;
+  std::vector<int64_t> sz;
+  auto slot_of = [&](const KeyT& k, const ListRec* l) {
+    auto it = slot.find(k);
+    if (it != slot.end()) return it->second;
+    slot.emplace(k, sz.size());
+    sz.push_back(l ? l->n : 0);
+    return sz.size() - 1;
+  };
+  // first-appearance order over the batch's queries: identical on every rank
+  std::vector<std::array<size_t, 2 * YRWI_MAX_TERMS>> idx(plans.size());
+  for (size_t q = 0; q < plans.size(); q++) {
+    Plan& P = plans[q];
+    for (int i = 0; i < P.ninc; i++) idx[q][(size_t)i] = slot_of(P.inc[i], P.linc[i]);
+    for (int i = 0; i < P.nexc; i++) idx[q][(size_t)(YRWI_MAX_TERMS + i)] = slot_of(P.exc[i], P.lexc[i]);
+  }
+  if (int rc = allsum_host(L, sz)) return rc;
+  for (size_t q = 0; q < plans.size(); q++) {
+    Plan& P = plans[q];
+    int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
+    for (int i = 0; i < P.ninc; i++) gi[i] = sz[idx[q][(size_t)i]];
+    for (int i = 0; i < P.nexc; i++) ge[i] = sz[idx[q][(size_t)(YRWI_MAX_TERMS + i)]];
+    plan_finish(&P, gi, ge);
+  }
   return 0;
 }
 
@@ -509,26 +581,129 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
   if (!owner.empty()) owner.swap(ow);
 }
 
-// Run the join/exclusion phase of all plans; leaves each plan's container in P.cont.
-static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
-  for (auto& P : plans) {
-    if (P.empty) { P.cont = DList{nullptr, nullptr, nullptr, 0}; continue; }
-    P.cont = P.seq[0]->dl();
+// One fold step's join jobs: layout, launch, joined sizes back to the plans.
+static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>& jobs, std::vector<int>& owner,
+                         yrwi_stats* st, Timing* tm) {
+  std::vector<int64_t> tile_base;
+  int nmerge;
+  int64_t merge_tiles, tiles;
+  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+  const int nj = (int)jobs.size();
+  if (st)
+    for (const JoinQ& J : jobs)  // a probe job reads at most the galloping bound, whatever the reference dispatch
+      (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) +=
+          step_bytes(J.algo == JA_MERGE ? J.mode : (int32_t)JM_TEST_LARGE_A, J.A.n, J.B.n);
+  int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
+  for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
+  JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
+  int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
+  TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
+  ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
+  uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
+  uint32_t* d_puid = arena_alloc<uint32_t>(ctx, tiles * JOIN_MAXM);
+  int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
+  int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
+  if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_cnt || !d_off)
+    return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
+  hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
+  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
+                       ctx->stream, e0, em, e1, c0, c1))
+    return ctx->fail(YRWI_E_HIP, "join launch");
+  if (tm) {
+    tm->kjoin.push_back({e0, em, e1});
+    tm->kcompact.push_back({c0, c1});
   }
-  size_t maxsteps = 0;
-  for (auto& P : plans) if (!P.empty) maxsteps = std::max(maxsteps, P.seq.size() - 1);
-  std::vector<int64_t> mh;
-  for (size_t s = 0; s < maxsteps; s++) {
-    std::vector<JoinQ> jobs;
-    std::vector<int> owner;
-    std::vector<int64_t> tile_base;
-    for (size_t qi = 0; qi < plans.size(); qi++) {
-      Plan& P = plans[qi];
-      if (P.empty || P.seq.size() <= s + 1 || P.cont.n == 0) continue;
+  if (st) st->n_join_launches++;
+  std::vector<int64_t> mh((size_t)nj, 0);
+  HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, lane_sync(ctx));
+  if (st)  // k_compact per joined row: pair + id, the row(s) it gathers, row + id written
+    for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 136 : 96);
+  for (int j = 0; j < nj; j++) {
+    Plan& P = plans[(size_t)owner[(size_t)j]];
+    P.cont = DList{nullptr, nullptr, jobs[(size_t)j].out_rows, mh[(size_t)j], jobs[(size_t)j].out_uid};
+  }
+  return 0;
+}
+
+// exclusion (excludeContainers :373-388): mark container rows present in an exclude list
+static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st) {
+  std::vector<JoinQ> jobs;
+  std::vector<int> owner;
+  std::vector<int64_t> tile_base;
+  for (auto& P : plans) {
+    P.removed = nullptr;
+    if (P.empty || P.cont.n == 0 || P.excl.empty()) continue;
+    P.removed = arena_alloc<uint8_t>(ctx, P.cont.n);
+    if (!P.removed) return ctx->fail(YRWI_E_NOMEM, "arena");
+    HIPCHK(ctx, hipMemsetAsync(P.removed, 0, (size_t)P.cont.n, ctx->stream));
+    for (auto* E : P.excl) {
       JoinQ J{};
       J.A = P.cont;
-      J.B = P.seq[s + 1]->dl();
-      J.mode = dispatch_mode(J.A.n, J.B.n);
+      J.B = E->dl();
+      J.mode = JM_MARK;
+      J.maxd = YRWI_MAX_DISTANCE_ANY;
+      J.removed = P.removed;
+      if (st) st->bytes_alg += 12 * E->n;
+      jobs.push_back(J);
+    }
+  }
+  if (jobs.empty()) return 0;
+  int nmerge;
+  int64_t merge_tiles, tiles;
+  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+  const int nj = (int)jobs.size();
+  JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
+  int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
+  TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
+  ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
+  if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr, true,
+                       ctx->stream, nullptr, nullptr, nullptr))
+    return ctx->fail(YRWI_E_HIP, "exclude launch");
+  return 0;
+}
+
+// Run the join/exclusion phase of all plans; leaves each plan's container in P.cont.
+// Every fold step's dispatch (J3) is taken on the global sizes of its two
+// containers: the next list's (Plan.seq_ng) and the accumulated container's,
+// which after the first step is the sum over the shards of their joined rows
+// (one exchange per step that some query continues past; none on one context).
+static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
+  const size_t nq = plans.size();
+  std::vector<int64_t> acc_g(nq, 0);  // global size of each query's accumulated container
+  for (size_t qi = 0; qi < nq; qi++) {
+    Plan& P = plans[qi];
+    if (P.empty) { P.cont = DList{nullptr, nullptr, nullptr, 0}; continue; }
+    P.cont = P.seq[0]->dl();
+    acc_g[qi] = P.seq_ng[0];
+  }
+  // a query steps at s while it has a list left and its global container is not empty
+  auto steps = [&](size_t qi, size_t s) {
+    const Plan& P = plans[qi];
+    return !P.empty && P.seq.size() > s + 1 && acc_g[qi] > 0;
+  };
+  for (size_t s = 0;; s++) {
+    std::vector<JoinQ> jobs;
+    std::vector<int> owner;
+    bool any = false, more = false;  // some query steps now / after this step (global decisions)
+    for (size_t qi = 0; qi < nq; qi++) {
+      if (!steps(qi, s)) continue;
+      any = true;
+      Plan& P = plans[qi];
+      if (P.seq.size() > s + 2) more = true;
+      const DList B = P.seq[s + 1]->dl();
+      if (P.cont.n == 0 || B.n == 0) {  // nothing of this shard survives the step
+        P.cont = DList{nullptr, nullptr, nullptr, 0};
+        continue;
+      }
+      JoinQ J{};
+      J.A = P.cont;
+      J.B = B;
+      J.mode = dispatch_mode(acc_g[qi], P.seq_ng[s + 1]);
       J.maxd = P.maxd;
       J.now_ms = P.now_ms;
       int64_t cap = std::min(J.A.n, J.B.n);
@@ -542,85 +717,20 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       jobs.push_back(J);
       owner.push_back((int)qi);
     }
-    if (jobs.empty()) break;
-    int nmerge;
-    int64_t merge_tiles, tiles;
-    layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
-    const int nj = (int)jobs.size();
-    if (st)
-      for (const JoinQ& J : jobs) (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) += step_bytes(J.mode, J.A.n, J.B.n);
-    int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
-    for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
-    JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
-    int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-    TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
-    ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
-    uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
-    uint32_t* d_puid = arena_alloc<uint32_t>(ctx, tiles * JOIN_MAXM);
-    int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
-    int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
-    if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_cnt || !d_off)
-      return ctx->fail(YRWI_E_NOMEM, "arena");
-    if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-    hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
-    hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
-    if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
-                         ctx->stream, e0, em, e1, c0, c1))
-      return ctx->fail(YRWI_E_HIP, "join launch");
-    if (tm) {
-      tm->kjoin.push_back({e0, em, e1});
-      tm->kcompact.push_back({c0, c1});
-    }
-    if (st) st->n_join_launches++;
-    mh.assign((size_t)nj, 0);
-    HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, lane_sync(ctx));
-    if (st)  // k_compact per joined row: pair + id, the row(s) it gathers, row + id written
-      for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 136 : 96);
-    for (int j = 0; j < nj; j++) {
-      Plan& P = plans[(size_t)owner[(size_t)j]];
-      P.cont = DList{nullptr, nullptr, jobs[(size_t)j].out_rows, mh[(size_t)j], jobs[(size_t)j].out_uid};
-    }
+    if (!any) break;
+    if (!jobs.empty())
+      if (int rc = run_join_jobs(ctx, plans, jobs, owner, st, tm)) return rc;
+    if (!more) break;
+    // the accumulated containers' global sizes decide the next step's dispatch
+    std::vector<int64_t> v(nq, 0);
+    std::vector<char> stepped(nq, 0);
+    for (size_t qi = 0; qi < nq; qi++)
+      if (steps(qi, s)) { v[qi] = plans[qi].cont.n; stepped[qi] = 1; }
+    if (int rc = allsum_host(ctx, v)) return rc;
+    for (size_t qi = 0; qi < nq; qi++)
+      if (stepped[qi]) acc_g[qi] = v[qi];
   }
-  // exclusion (excludeContainers :373-388): mark container rows present in an exclude list
-  {
-    std::vector<JoinQ> jobs;
-    std::vector<int> owner;
-    std::vector<int64_t> tile_base;
-    for (auto& P : plans) {
-      P.removed = nullptr;
-      if (P.empty || P.cont.n == 0 || P.excl.empty()) continue;
-      P.removed = arena_alloc<uint8_t>(ctx, P.cont.n);
-      if (!P.removed) return ctx->fail(YRWI_E_NOMEM, "arena");
-      HIPCHK(ctx, hipMemsetAsync(P.removed, 0, (size_t)P.cont.n, ctx->stream));
-      for (auto* E : P.excl) {
-        JoinQ J{};
-        J.A = P.cont;
-        J.B = E->dl();
-        J.mode = JM_MARK;
-        J.maxd = YRWI_MAX_DISTANCE_ANY;
-        J.removed = P.removed;
-        if (st) st->bytes_alg += 12 * E->n;
-        jobs.push_back(J);
-      }
-    }
-    if (!jobs.empty()) {
-      int nmerge;
-      int64_t merge_tiles, tiles;
-      layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
-      const int nj = (int)jobs.size();
-      JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
-      int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-      TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
-      ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
-      if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
-      if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
-      if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr, true,
-                           ctx->stream, nullptr, nullptr, nullptr))
-        return ctx->fail(YRWI_E_HIP, "exclude launch");
-    }
-  }
-  return 0;
+  return run_exclusion(ctx, plans, st);
 }
 
 // Global host counts for authority (ReferenceOrder.java:176-216) across url-hash
@@ -1048,6 +1158,9 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
     if (rc) return rc;
     if (st) st->postings_in += all[(size_t)i].postings_in;
   }
+  // J1/J2 on global list sizes (one exchange of the batch's term sizes when sharded)
+  if (begin_pass(L)) return YRWI_E_HIP;
+  if (int rc = plan_batch(L, all)) return rc;
   const int64_t budget = scratch_budget(L);
   for (int g0 = 0; g0 < nq;) {
     int g1 = g0;
@@ -1060,14 +1173,20 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
     }
     std::vector<Plan> plans(std::make_move_iterator(all.begin() + g0), std::make_move_iterator(all.begin() + g1));
     if (begin_pass(L)) return YRWI_E_HIP;
+    // HIP events (per-kernel timing) only when the caller asked for statistics
     Timing tm;
-    tm.t0 = L->event();
-    hipEventRecord(tm.t0, L->stream);
-    int rc = run_join_phase(L, plans, st, &tm);
+    Timing* tmp = st ? &tm : nullptr;
+    if (tmp) {
+      tm.t0 = L->event();
+      hipEventRecord(tm.t0, L->stream);
+    }
+    int rc = run_join_phase(L, plans, st, tmp);
     if (rc) return rc;
-    tm.tj = L->event();
-    hipEventRecord(tm.tj, L->stream);
-    rc = run_rank_phase(L, plans, kmax, out + (size_t)g0 * kmax, nout + g0, nullptr, st, &tm);
+    if (tmp) {
+      tm.tj = L->event();
+      hipEventRecord(tm.tj, L->stream);
+    }
+    rc = run_rank_phase(L, plans, kmax, out + (size_t)g0 * kmax, nout + g0, nullptr, st, tmp);
     if (rc) return rc;
     if (st) {
       if (g1 < nq) HIPCHK(L, lane_sync(L));  // the pass's events must be complete before they are reused
@@ -1280,6 +1399,7 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
   int rc = ctx->take(L, plan_query(ctx, L, d, &plans[0]));
   if (rc) return rc;
   if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  if ((rc = ctx->take(L, plan_batch(L, plans)))) return rc;
   rc = ctx->take(L, run_join_phase(L, plans, nullptr, nullptr));
   if (rc) return rc;
   const Plan& P = plans[0];

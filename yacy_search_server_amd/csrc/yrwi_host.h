@@ -138,9 +138,15 @@ struct Arena {
 };
 
 struct Plan {
-  bool empty = true;
-  std::vector<const ListRec*> seq;   // fold order
-  std::vector<const ListRec*> excl;  // exclusion lists (empty: no exclusion)
+  bool empty = true;                 // no result anywhere (J1 on global sizes)
+  std::vector<const ListRec*> seq;   // fold order; a list absent from this shard is an empty ListRec
+  std::vector<int64_t> seq_ng;       // global size of each seq list (sum over shards)
+  std::vector<const ListRec*> excl;  // this shard's exclusion lists (empty: no exclusion)
+  // term keys (HandleSet order) and their lists on this shard (nullptr: absent)
+  int ninc = 0, nexc = 0;
+  KeyT inc[YRWI_MAX_TERMS], exc[YRWI_MAX_TERMS];
+  const ListRec* linc[YRWI_MAX_TERMS];
+  const ListRec* lexc[YRWI_MAX_TERMS];
   int32_t maxd = YRWI_MAX_DISTANCE_ANY, k = 0;
   yrwi_profile prof{};
   uint8_t lang[2] = {0, 0};
