@@ -1,59 +1,116 @@
 """bench.py -- RWI query hot path throughput on MI355X (BASELINE.json metric).
 
-Workload (a "step"): one batch of the C2 query set -- 1000 two-term AND queries,
-default RankingProfile, top-100 -- over the synthetic C2 index (10M URLs x 10k
-words, 100M postings per GPU), run end to end through libyrwi: join ->
+Headline workload (a "step"): one batch of the C2 query set -- 1000 two-term AND
+queries, default RankingProfile, top-100 -- over the synthetic C2 index (10M URLs
+x 10k words, 100M postings per GPU), run end to end through libyrwi: join ->
 normalise -> cardinal -> top-k, results back in host memory.
 
-N > 1 GPUs (one process per GPU): the index is YaCy's vertical DHT partition
-by url hash (Distribution.java:153-158); every rank holds a C2-sized shard of an
-N-times larger corpus (weak scaling) and every query runs on all shards, with
-RCCL exchanging the normalisation summaries and the per-shard top-k lists.
+N GPUs: `python bench.py --gpus N` starts N rank processes itself (one per GPU,
+before anything touches a GPU); under torchrun the ranks come from the
+environment.  The index is YaCy's vertical DHT partition by url hash
+(Distribution.java:153-158):
+  --scaling weak (default)  every rank holds a C2-sized shard of an N-times larger
+                            corpus (per-GPU work fixed: the driver's 1/2/4/8 series);
+  --scaling strong          the configured corpus (fixed) is split over the N ranks.
+Every query runs on every shard; RCCL exchanges the term sizes, the
+normalisation summaries and the per-shard top-k lists.
 
 value = sum over ranks of the postings of all queries (include + exclude list
 lengths) / max-over-ranks wall time of the K timed steps.
+
+After the headline the default run measures the other BASELINE configs as
+extra legs on the same GPUs: C3 (1B postings, 3-term AND + 1
+exclude, split over the N ranks: strong scaling), C4 (4096 concurrent 2-4 term
+queries over the C3 index) and C5 (the custom and /date RankingProfiles over the
+per-GPU 625M-posting slice of the 5B corpus).  `--legs none` skips them.
 """
 
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, ROOT)
-
-from yacy_search_server_amd import RWIIndex, RankingProfile, synth  # noqa: E402
-from yacy_search_server_amd._lib import CHit, CQuery, CStats  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+NOW_MS = 20741 * 86400000
 
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def build_queries(idx_hashes, qs, k, now_ms, prof):
-    nq = len(qs)
-    arr = (CQuery * nq)()
-    keep = [prof]
-    for i, (inc, exc) in enumerate(qs):
-        ib = ctypes.create_string_buffer(b"".join(idx_hashes[t] for t in inc), 12 * max(1, len(inc)))
-        eb = ctypes.create_string_buffer(b"".join(idx_hashes[t] for t in exc), 12 * max(1, len(exc)))
-        keep += [ib, eb]
-        arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
-        arr[i].nincl = len(inc)
-        arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
-        arr[i].nexcl = len(exc)
-        arr[i].max_distance = 2147483647
-        arr[i].k = k
-        arr[i].profile = ctypes.pointer(prof.c)
-        arr[i].language = b"en"
-        arr[i].now_ms = now_ms
-    return arr, keep
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--terms", type=int, default=2, help="include terms per query (minimum)")
+    ap.add_argument("--max-terms", type=int, default=0, help="include terms per query (maximum; default --terms)")
+    ap.add_argument("--exclude", type=int, default=0, help="exclude terms per query")
+    ap.add_argument("--profile", default="default", choices=["default", "custom", "date"],
+                    help="custom = C5's date=15,domlength=15,authority=13,tf=10; date = the /date modifier")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="(1 GPU) run the rank-0 url-hash shard of a W-GPU corpus: the per-GPU slice of C3/C5")
+    ap.add_argument("--legs", default="C3,C4,C5", help="extra BASELINE configs after the headline, or 'none'")
+    ap.add_argument("--leg-steps", type=int, default=5)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--latency", type=int, default=100, help="single-query latency samples")
+    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (throughput mode)")
+    ap.add_argument("--dry-run", action="store_true", help="ranks + rendezvous only (gloo, no GPU): launcher test")
+    return ap.parse_args(argv)
+
+
+# --------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the
+    environment), started as children before anything here touches a GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+# ------------------------------------------------------------------- baselines
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores():
+    """(threads used, affinity cores, why): every core of this process's affinity,
+    capped by the host-thread share the machine gives this job (OMP_NUM_THREADS /
+    MAX_JOBS, set to the per-GPU share on the GPU boxes)."""
+    aff = len(os.sched_getaffinity(0))
+    share = [int(os.environ[v]) for v in ("OMP_NUM_THREADS", "MAX_JOBS") if os.environ.get(v, "").isdigit()]
+    if share and min(share) < aff:
+        return min(share), aff, f"host-thread share of this job (OMP_NUM_THREADS={min(share)}) of {aff} affinity cores"
+    return aff, aff, "all affinity cores"
 
 
 def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, prof, label, min_s=10.0):
@@ -91,6 +148,7 @@ def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, prof, label, min_s=10.0)
         t.join()
     dt = time.perf_counter() - t0
     return {"value": state["post"] / dt, "unit": "postings/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{state['n']} queries cycling the {len(qs)} {label} queries ({state['post']} postings, {dt:.1f}s), "
                       f"oracle/yrwi_oracle.cpp, {threads} host thread(s), one query per thread"}
 
@@ -99,42 +157,197 @@ def load_pmc(config):
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if os.path.exists(path):
         with open(path) as f:
-            return json.load(f)
+            d = json.load(f)
+        d["_file"] = os.path.relpath(path, ROOT)
+        return d
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2")
-    ap.add_argument("--nq", type=int, default=1000)
-    ap.add_argument("--k", type=int, default=100)
-    ap.add_argument("--terms", type=int, default=2, help="include terms per query (minimum)")
-    ap.add_argument("--max-terms", type=int, default=0, help="include terms per query (maximum; default --terms)")
-    ap.add_argument("--exclude", type=int, default=0, help="exclude terms per query")
-    ap.add_argument("--profile", default="default", choices=["default", "custom", "date"],
-                    help="custom = C5's date=15,domlength=15,authority=13,tf=10; date = the /date modifier")
-    ap.add_argument("--shard-of", type=int, default=1,
-                    help="(1 GPU) run the rank-0 url-hash shard of a W-GPU corpus: the per-GPU slice of C3/C5")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--latency", type=int, default=100, help="single-query latency samples")
-    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (throughput mode)")
-    args = ap.parse_args()
+# ------------------------------------------------------------------ the runner
+class Runner:
+    """One index resident on this rank's GPU and query batches run over it."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    def __init__(self, args, rank, world, local, dist):
+        self.args, self.rank, self.world, self.local, self.dist = args, rank, world, local, dist
+        self.ix = None
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def open_index(self, cfg):
+        from yacy_search_server_amd import RWIIndex, synth, unique_id
+        t0 = time.time()
+        idx = synth.build_index(cfg)
+        log(f"rank {self.rank}: generated {len(idx.rows)} postings in {time.time() - t0:.1f}s")
+        if self.world > 1:
+            import torch
+            uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+            if self.rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
+            self.dist.broadcast(uid, 0)
+            ix = RWIIndex(self.local, shard=(self.rank, self.world, bytes(uid.cpu().numpy())))
+        else:
+            ix = RWIIndex(self.local)
+        t0 = time.time()
+        for t in range(cfg.n_terms):
+            if idx.sizes[t]:
+                ix.add(idx.hashes[t], idx.list_rows(t))
+        log(f"rank {self.rank}: index resident in {time.time() - t0:.1f}s, stats {ix.stats()}")
+        t0 = time.time()
+        ix.build_url_ids()
+        t_dict = time.time() - t0
+        log(f"rank {self.rank}: url dictionary and ranking records built in {t_dict:.3f}s")
+        self.ix = ix
+        return idx, t_dict
+
+    def close(self):
+        if self.ix is not None:
+            self.ix.close()
+            self.ix = None
+
+    def measure(self, qs, hashes, prof, nq, k, steps, warmup, inflight, isolated=True):
+        """warmup + `steps` timed batches (max over ranks), then an isolated pass
+        (one batch in flight) whose library statistics give the per-kernel times."""
+        import ctypes
+        import torch
+        from yacy_search_server_amd._lib import CHit, CQuery, CStats
+        ix = self.ix
+        arr = (CQuery * nq)()
+        keep = [prof]
+        for i, (inc, exc) in enumerate(qs):
+            ib = ctypes.create_string_buffer(b"".join(hashes[t] for t in inc), 12 * max(1, len(inc)))
+            eb = ctypes.create_string_buffer(b"".join(hashes[t] for t in exc), 12 * max(1, len(exc)))
+            keep += [ib, eb]
+            arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
+            arr[i].nincl = len(inc)
+            arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
+            arr[i].nexcl = len(exc)
+            arr[i].max_distance = 2147483647
+            arr[i].k = k
+            arr[i].profile = ctypes.pointer(prof.c)
+            arr[i].language = b"en"
+            arr[i].now_ms = NOW_MS
+        depth = max(1, inflight)
+        bufs = [(ix.host_array(CHit, nq * k), ix.host_array(ctypes.c_int32, nq), CStats()) for _ in range(depth)]
+        fields = [f for f, _ in CStats._fields_ if f != "reserved"]
+        agg = {f: 0 for f in fields}
+        state = {"depth": depth}
+
+        def collect(st):
+            for f in fields:
+                agg[f] += getattr(st, f)
+
+        def run_steps(n):
+            d = state["depth"]
+            pending = []
+            for i in range(n):
+                b = bufs[i % d]
+                if len(pending) == d:
+                    t, bst = pending.pop(0)
+                    ix.wait(t)
+                    collect(bst)
+                pending.append((ix.submit_raw(arr, nq, k, b[0], b[1], b[2]), b[2]))
+            for t, bst in pending:
+                ix.wait(t)
+                collect(bst)
+
+        run_steps(warmup)
+        for f in agg:
+            agg[f] = 0
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_steps(steps)
+        torch.cuda.synchronize()  # every batch was waited for; this brackets the device too
+        self.barrier()
+        dt = time.perf_counter() - t0
+        total_post = float(agg["postings_in"])
+        if self.dist is not None:
+            tt = torch.tensor([dt, total_post], dtype=torch.float64, device="cuda")
+            tmax = tt[:1].clone()
+            self.dist.all_reduce(tmax, op=self.dist.ReduceOp.MAX)
+            self.dist.all_reduce(tt)
+            dt = float(tmax.item())
+            total_post = float(tt[1].item())
+        timed = dict(agg)
+        iso = None
+        if isolated:
+            # the same batch with one in flight: the library's HIP-event times are
+            # then each kernel's alone (in the timed region two lanes share the GPU)
+            for f in agg:
+                agg[f] = 0
+            state["depth"] = 1
+            nb = max(1, min(steps, 5))
+            run_steps(nb)
+            iso = dict(agg)
+            iso["batches"] = nb
+        return {"dt": dt, "steps": steps, "total_post": total_post, "timed": timed, "iso": iso, "bufs": bufs,
+                "arr": arr, "keep": keep}
+
+
+def roofline_path(iso, pmc, head_of_pmc):
+    """Path-level roofline: B = sum K + 12 sum
+    n_excl + 23 t m_out algorithmic bytes per batch over the batch's kernel time
+    (HIP events around every group of launches, t_kernels_ns)."""
+    nb = max(1, iso["batches"])
+    t = iso["t_kernels_ns"] / nb * 1e-9
+    b = iso["bytes_alg"] / nb
+    ach = b / t / 1e9 if t > 0 else 0.0
+    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+         "kernel": "query path (k_partition .. k_emit, every kernel of one batch)",
+         "bytes_per_batch_alg": int(b), "kernel_us_per_batch": round(t * 1e6, 1),
+         "measured": "HIP events around every group of back-to-back launches of the batch (t_kernels_ns), "
+                     "isolated pass with one batch in flight"}
+    if pmc and pmc.get("path_hbm_bytes_per_batch"):
+        r["traffic"] = pmc["path_hbm_bytes_per_batch"]
+        r["traffic_source"] = f"{pmc['_file']} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {pmc.get('tag')}, " \
+                              f"commit {pmc.get('head', head_of_pmc)})"
+    return r
+
+
+def roofline_kernels(iso, pmc):
+    """Per-kernel lines: the kernel's share of the §8(d) bytes (alg_bytes) and the
+    bytes its data layout makes it move (phys_bytes: 4-byte url ids in the joins,
+    32-byte ranking records in k_compact); frac = phys rate / peak."""
+    n = max(1, iso["n_join_launches"])
+    out = {}
+
+    def line(name, t_ns, alg, phys):
+        t = t_ns / n * 1e-9
+        if t <= 0:
+            return
+        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / n), "alg_GBps": round(alg / n / t / 1e9, 1),
+             "phys_bytes": int(phys / n), "phys_GBps": round(phys / n / t / 1e9, 1),
+             "frac": round(phys / n / t / 1e9 / HBM_PEAK_GBS, 4)}
+        kd = (pmc or {}).get("kernels", {}).get(name, {})
+        if kd.get("hbm_bytes_per_launch"):
+            e["traffic"] = kd["hbm_bytes_per_launch"]
+        out[name] = e
+
+    # k_join: K = 12 B per key of the merge jobs; it streams 4-byte url ids
+    line("k_join", iso["t_join_ns"], iso["bytes_join"], iso["bytes_join"] / 3)
+    # k_probe: the galloping bound of the skewed jobs (it reads at most that, in leaf lines)
+    line("k_probe", iso["t_probe_ns"], iso["bytes_probe"], iso["bytes_probe"] / 3)
+    # k_compact: 23 B of features per term and joined posting; it moves bytes_compact (96 B per joined row)
+    line("k_compact", iso["t_compact_ns"], 46 * iso["joined"], iso["bytes_compact"])
+    return out
+
+
+def run(args, rank, world, local):
+    import numpy as np
     import torch
+    sys.path.insert(0, ROOT)
+    from yacy_search_server_amd import RankingProfile, synth
+
     torch.cuda.set_device(local)
+    dist = None
     if world > 1:
         import torch.distributed as tdist
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
+    R = Runner(args, rank, world, local, dist)
 
     base = synth.preset(args.config)
     max_terms = max(args.terms, args.max_terms)
@@ -144,178 +357,58 @@ def main():
             raise SystemExit("--shard-of is a one-GPU option")
         full = base
         cfg = full.shard(0, args.shard_of)
+    elif args.scaling == "strong":
+        full = base
+        cfg = full.shard(rank, world) if world > 1 else full
     else:
         # weak scaling: an N-times larger corpus, URL-hash range partitioned over the N ranks
         full = synth.SynthConfig(base.seed, base.n_urls * world, base.n_terms, base.n_hosts * world,
                                  base.n_postings * world)
         cfg = full.shard(rank, world) if world > 1 else full
-    t0 = time.time()
-    idx = synth.build_index(cfg)
-    log(f"rank {rank}: generated {len(idx.rows)} postings in {time.time() - t0:.1f}s")
-
-    if world > 1:
-        import torch
-        from yacy_search_server_amd import unique_id
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
-        dist.broadcast(uid, 0)
-        ix = RWIIndex(local, shard=(rank, world, bytes(uid.cpu().numpy())))
-    else:
-        ix = RWIIndex(local)
-    t0 = time.time()
-    for t in range(cfg.n_terms):
-        if idx.sizes[t]:
-            ix.add(idx.hashes[t], idx.list_rows(t))
-    log(f"rank {rank}: index resident in {time.time() - t0:.1f}s, stats {ix.stats()}")
-    t0 = time.time()
-    ix.build_url_ids()
-    t_dict = time.time() - t0
-    log(f"rank {rank}: url dictionary built in {t_dict:.3f}s")
+    idx, t_dict = R.open_index(cfg)
 
     qs = synth.queries(full, args.nq, args.terms, max_terms, args.exclude)
-    now_ms = 20741 * 86400000
     prof = RankingProfile()
     if args.profile == "custom":  # exercises the authority path (coeff > 12)
         prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
     elif args.profile == "date":
         prof = RankingProfile.date()
-    cq, keep = build_queries(idx.hashes, qs, args.k, now_ms, prof)
-    kmax = args.k
-    # throughput mode: up to `inflight` batches in flight (yrwi_query_batch_submit),
-    # each on its own lane, results landing in pinned host buffers
-    depth = max(1, args.inflight)
-    bufs = [(ix.host_array(CHit, args.nq * kmax), ix.host_array(ctypes.c_int32, args.nq), CStats())
-            for _ in range(depth)]
-    agg = {"postings_in": 0, "bytes_join": 0, "t_join_ns": 0, "n_join": 0, "bytes_alg": 0, "joined": 0,
-           "bytes_probe": 0, "t_probe_ns": 0, "bytes_compact": 0, "t_compact_ns": 0, "t_norm_ns": 0, "t_score_ns": 0, "t_total_ns": 0}
-    state = {"depth": depth}
-
-    def collect(st):
-        agg["postings_in"] += st.postings_in
-        agg["bytes_join"] += st.bytes_join
-        agg["t_join_ns"] += st.t_join_ns
-        agg["bytes_probe"] += st.bytes_probe
-        agg["t_probe_ns"] += st.t_probe_ns
-        agg["bytes_compact"] += st.bytes_compact
-        agg["t_compact_ns"] += st.t_compact_ns
-        agg["n_join"] += st.n_join_launches
-        agg["bytes_alg"] += st.bytes_alg
-        agg["joined"] += st.joined
-        agg["t_norm_ns"] += st.t_norm_ns
-        agg["t_score_ns"] += st.t_score_ns
-        agg["t_total_ns"] += st.t_total_ns
-
-    def run_steps(n):
-        """n steps (batches); every batch is complete (results in host memory) on return."""
-        depth = state["depth"]
-        pending = []
-        for i in range(n):
-            b = bufs[i % depth]
-            if len(pending) == depth:
-                t, bst = pending.pop(0)
-                ix.wait(t)
-                collect(bst)
-            pending.append((ix.submit_raw(cq, args.nq, kmax, b[0], b[1], b[2]), b[2]))
-        for t, bst in pending:
-            ix.wait(t)
-            collect(bst)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    run_steps(args.warmup)
-    for k in agg:
-        agg[k] = 0
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_steps(args.steps)
-    torch.cuda.synchronize()  # every batch was waited for; this brackets the device too
-    barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        pp = torch.tensor([agg["postings_in"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(pp)
-        total_post = float(pp.item())
-    else:
-        total_post = float(agg["postings_in"])
-    value = total_post / dt
-    ms_per_step = dt / args.steps * 1e3
-
-    timed = dict(agg)
-    # Roofline pass: the same batch, one in flight (no concurrent lane), so the
-    # HIP-event duration of each k_join / k_probe launch is that kernel's alone.
-    # (In the timed region two lanes overlap and share HBM: "roofline_timed".)
-    for k in agg:
-        agg[k] = 0
-    state["depth"] = 1
-    run_steps(max(1, min(args.steps, 5)))
-    state["depth"] = depth
-    iso = dict(agg)
-    iso["batches"] = max(1, min(args.steps, 5))
-    pmc = load_pmc(args.config)
-
-    def roofline(a, kernel):
-        tkey, bkey = {"k_join": ("t_join_ns", "bytes_join"), "k_probe": ("t_probe_ns", "bytes_probe"),
-                      "k_compact": ("t_compact_ns", "bytes_compact")}[kernel]
-        t = a[tkey] / max(1, a["n_join"]) * 1e-9
-        bpl = a[bkey] / max(1, a["n_join"])
-        ach = bpl / t / 1e9 if t > 0 else 0.0
-        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get(f"{kernel}_hbm_bytes_per_launch") if pmc else None,
-                "kernel": kernel, "bytes_per_launch_alg": int(bpl), "mean_launch_us": round(t * 1e6, 2)}
-
-    def with_traffic(r):
-        if r.get("traffic") and r["mean_launch_us"]:
-            r["traffic_GBps"] = round(r["traffic"] / (r["mean_launch_us"] * 1e-6) / 1e9, 1)
-            r["traffic_frac"] = round(r["traffic_GBps"] / HBM_PEAK_GBS, 4)
-        return r
-
-    # The dominant kernel is k_compact (the row gathers of the joined container):
-    # its algorithmic bytes are the rows it must read and write; the PMC traffic
-    # beside it shows the sector cost of gathering sparse 40-B rows.
-    roof = with_traffic(roofline(iso, "k_compact"))
-    roof["measured"] = "HIP events around each launch, separate pass of the timed batch with 1 batch in flight"
-    # BASELINE.md §4 counts 12 B per posting key; the join streams 4-byte url ids
-    # (DESIGN.md §3), so the HBM bytes it moves are far fewer than its K
-    roof_join = with_traffic(roofline(iso, "k_join"))
-    roof_probe = with_traffic(roofline(iso, "k_probe"))
-    roof_timed = roofline(timed, "k_compact")
-    roof_timed["measured"] = "HIP events around each launch inside the timed region (2 lanes overlap)"
+    M = R.measure(qs, idx.hashes, prof, args.nq, args.k, args.steps, args.warmup, args.inflight)
+    value = M["total_post"] / M["dt"]
+    ms_per_step = M["dt"] / args.steps * 1e3
+    iso, timed = M["iso"], M["timed"]
+    pmc = load_pmc(args.config) if world == 1 and args.shard_of == 1 else None
+    roof = roofline_path(iso, pmc, None)
+    kern = roofline_kernels(iso, pmc)
 
     # single-query latency (host call -> top-k in host memory)
     lat = []
     if rank == 0 and world == 1 and args.latency > 0:
-        one = (CHit * kmax)()
+        import ctypes
+        from yacy_search_server_amd._lib import CHit, CStats
+        one = (CHit * args.k)()
         n1 = (ctypes.c_int32 * 1)()
         for i in range(min(args.latency, args.nq)):
             t1 = time.perf_counter()
-            ix.search_batch_raw(ctypes.byref(cq[i]), 1, kmax, one, n1, CStats())
+            R.ix.search_batch_raw(ctypes.byref(M["arr"][i]), 1, args.k, one, n1, CStats())
             lat.append((time.perf_counter() - t1) * 1e3)
 
     # parity spot check of this very workload: the last batch's hits (pinned host
-    # buffers) of the first few queries against the oracle (checker only)
+    # buffers) of the first queries against the oracle (checker only)
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
         oprof = orc.profile_from(prof)
-        hits, nout = bufs[0][0], bufs[0][1]  # the roofline pass above ran last, on bufs[0]
-        nchk = min(args.nq, 16)
+        hits, nout = M["bufs"][0][0], M["bufs"][0][1]  # the isolated pass ran last, on bufs[0]
+        nchk = min(args.nq, 64)
         bad = 0
         for qi in range(nchk):
             inc, exc = qs[qi]
             d = {idx.hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
             exp = orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], profile=oprof,
-                             now_ms=now_ms, k=args.k)
-            got = [(bytes(hits[qi * kmax + j].urlhash), hits[qi * kmax + j].score) for j in range(nout[qi])]
+                             now_ms=NOW_MS, k=args.k)
+            got = [(bytes(hits[qi * args.k + j].urlhash), hits[qi * args.k + j].score) for j in range(nout[qi])]
             bad += got != [(h, sc) for h, sc, _ in exp]
         parity = {"queries_checked": nchk, "mismatches": bad, "checker": "oracle/yrwi_oracle.cpp"}
         if bad:
@@ -323,54 +416,168 @@ def main():
 
     cpu = cpu1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        nthr = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
-        cpu = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget, nthr, prof, args.config)
-        cpu1 = cpu_baseline(idx, qs, now_ms, args.k, args.cpu_budget / 2, 1, prof, args.config)
+        nthr, aff, why = host_cores()
+        cpu = cpu_baseline(idx, qs, NOW_MS, args.k, args.cpu_budget, nthr, prof, args.config)
+        cpu["cores_why"] = why
+        cpu["affinity_cores"] = aff
+        cpu1 = cpu_baseline(idx, qs, NOW_MS, args.k, args.cpu_budget / 2, 1, prof, args.config)
+    R.close()
+    shard_postings = len(idx.rows)
+    del idx
+
+    legs = {}
+    if args.legs and args.legs != "none" and args.shard_of == 1:
+        for leg in [x.strip() for x in args.legs.split(",") if x.strip()]:
+            try:
+                legs.update(run_leg(R, leg, args, rank, world))
+            except Exception as e:  # a leg never sinks the headline line
+                log(f"leg {leg} failed: {e!r}")
+                legs[leg] = {"error": repr(e)}
+                R.close()
 
     if rank == 0:
         terms_s = f"{args.terms}" if max_terms == args.terms else f"{args.terms}-{max_terms}"
         excl_s = f" + {args.exclude} excluded" if args.exclude else ""
         if args.shard_of > 1:
-            corpus_s = (f"url-hash shard 0 of {args.shard_of} ({len(idx.rows) / 1e6:.0f}M postings) of the "
+            corpus_s = (f"url-hash shard 0 of {args.shard_of} ({shard_postings / 1e6:.0f}M postings) of the "
                         f"{base.n_postings / 1e6:.0f}M-posting corpus ({base.n_urls / 1e6:.0f}M URLs x "
                         f"{base.n_terms} words)")
+        elif args.scaling == "strong":
+            corpus_s = (f"{base.n_postings / 1e6:.0f}M postings ({base.n_urls / 1e6:.0f}M URLs x {base.n_terms} words) "
+                        f"split over {world} GPU(s)")
         else:
             corpus_s = (f"{base.n_postings / 1e6:.0f}M postings ({base.n_urls / 1e6:.0f}M URLs x "
                         f"{base.n_terms} words) per GPU")
+        nbi = max(1, iso["batches"])
         out = {
             "metric": "postings joined+ranked/sec (node)",
             "value": value, "unit": "postings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "int64", "data": "synthetic",
             "config": {"workload": f"{args.config}: {args.nq} x {terms_s}-term AND queries{excl_s}, "
                                    f"{args.profile} RankingProfile, top-{args.k}; {corpus_s}",
-                       "queries_per_step": args.nq, "postings_per_step": total_post / args.steps,
+                       "queries_per_step": args.nq, "postings_per_step": M["total_post"] / args.steps,
                        "index_postings_total": int(full.n_postings), "parallelism": f"url-hash shards x{world}"},
             "roofline": roof,
-            "roofline_join": roof_join,
-            "roofline_probe": roof_probe,
-            "roofline_timed": roof_timed,
+            "roofline_kernels": kern,
             "cpu_baseline": cpu,
-            "parity_sample": parity,
             "cpu_baseline_1thread": cpu1,
+            "parity_sample": parity,
             "latency_ms": ({"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                             "n": len(lat)} if lat else None),
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
             "inflight": args.inflight,
             # per batch, from the library's own HIP events (isolated pass): join+probe kernels,
-            # normalisation (reduce..combine), scoring (score..emit); host = call to results
-            "phase_ms": {"join": round(iso["t_join_ns"] / 1e6 / max(1, iso["batches"]), 3),
-                         "probe": round(iso["t_probe_ns"] / 1e6 / max(1, iso["batches"]), 3),
-                         "norm": round(iso["t_norm_ns"] / 1e6 / max(1, iso["batches"]), 3),
-                         "score": round(iso["t_score_ns"] / 1e6 / max(1, iso["batches"]), 3),
-                         "total": round(iso["t_total_ns"] / 1e6 / max(1, iso["batches"]), 3)},
+            # normalisation (reduce..combine), scoring (score..emit), all kernels; host = call to results
+            "phase_ms": {"join": round(iso["t_join_ns"] / 1e6 / nbi, 3),
+                         "probe": round(iso["t_probe_ns"] / 1e6 / nbi, 3),
+                         "compact": round(iso["t_compact_ns"] / 1e6 / nbi, 3),
+                         "norm": round(iso["t_norm_ns"] / 1e6 / nbi, 3),
+                         "score": round(iso["t_score_ns"] / 1e6 / nbi, 3),
+                         "kernels": round(iso["t_kernels_ns"] / 1e6 / nbi, 3),
+                         "host_total": round(iso["t_total_ns"] / 1e6 / nbi, 3)},
             "url_dictionary_build_s": round(t_dict, 3),
+            "legs": legs or None,
         }
-        print(json.dumps(out))
-    ix.close()
+        print(json.dumps(out), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+LEG_DESC = {
+    "C3": "1B postings Zipf (100M URLs x 10k words), 1000 x 3-term AND + 1 excluded term, default profile, top-100",
+    "C4": "4096 concurrent 2-4 term AND queries over the C3 index, default profile, top-100, one batch per step",
+    "C5": "per-GPU slice (url-hash shards of the 8-way partition) of the 5B-posting corpus (500M URLs x 100k words), "
+          "1000 x 2-4 term AND, custom profile date=15,domlength=15,authority=13,tf=10 and the /date profile",
+}
+
+
+def run_leg(R, leg, args, rank, world):
+    """An extra BASELINE config on the same ranks: C3 / C4 strong-scale the fixed
+    1B corpus over the N ranks; C5 gives every rank one 625M-posting url-hash shard
+    of the 8-way partition of the 5B corpus."""
+    from yacy_search_server_amd import RankingProfile, synth
+    res = {}
+    if leg in ("C3", "C4"):
+        full = synth.preset("C3")
+        cfg = full.shard(rank, world) if world > 1 else full
+        if getattr(R, "leg_cfg", None) != ("C3", rank, world):
+            R.close()
+            R.open_index(cfg)
+            R.leg_cfg = ("C3", rank, world)
+        if leg == "C3":
+            qs = synth.queries(full, 1000, 3, 3, 1)
+        else:
+            qs = synth.queries(full, 4096, 2, 4, 0, qseed=full.seed ^ 0xC4)
+        hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
+        M = R.measure(qs, hashes, RankingProfile(), len(qs), 100, args.leg_steps, 1, args.inflight, isolated=True)
+        res[leg] = _leg_line(M, leg, len(qs), world, "strong")
+    elif leg == "C5":
+        full = synth.preset("C5")
+        parts = max(8, world)
+        R.close()
+        R.leg_cfg = None
+        R.open_index(full.shard(rank, parts))
+        qs = synth.queries(full, 1000, 2, 4, 0)
+        hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
+        custom = RankingProfile()
+        custom.coeff_date, custom.coeff_domlength, custom.coeff_authority, custom.coeff_termfrequency = 15, 15, 13, 10
+        for name, prof in (("C5_custom", custom), ("C5_date", RankingProfile.date())):
+            M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 1, args.inflight, isolated=True)
+            res[name] = _leg_line(M, "C5", len(qs), world, "weak")
+        R.close()
+    else:
+        raise ValueError(f"unknown leg {leg}")
+    return res
+
+
+def _leg_line(M, leg, nq, world, scaling):
+    iso = M["iso"]
+    nb = max(1, iso["batches"])
+    t = iso["t_kernels_ns"] / nb * 1e-9
+    b = iso["bytes_alg"] / nb
+    return {"workload": LEG_DESC[leg], "value": M["total_post"] / M["dt"], "unit": "postings/s", "n_gpus": world,
+            "scaling": scaling, "steps": M["steps"], "ms_per_step": M["dt"] / M["steps"] * 1e3,
+            "postings_per_step": M["total_post"] / M["steps"], "queries_per_step": nq,
+            "roofline": {"achieved": round(b / t / 1e9, 1) if t > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None,
+                         "kernel_us_per_batch": round(t * 1e6, 1), "bytes_per_batch_alg": int(b)},
+            "joined_per_step": M["timed"]["joined"] / M["steps"]}
+
+
+def dry_run(args, rank, world):
+    """Launcher check without a GPU: every rank joins a gloo group and rank 0 prints
+    the JSON line's identity fields."""
+    import torch
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+        t = torch.tensor([rank + 1.0])
+        tdist.all_reduce(t)
+        tdist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": "postings joined+ranked/sec (node)", "dry_run": True, "n_gpus": world,
+                          "ranks_sum": float(t.item()) if world > 1 else 1.0, "scaling": args.scaling,
+                          "steps": args.steps, "warmup": args.warmup}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"--gpus {args.gpus} but WORLD_SIZE {world}: measuring {world} rank(s)")
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
+    run(args, rank, world, local)
 
 
 if __name__ == "__main__":

@@ -115,9 +115,12 @@ typedef struct yrwi_stats {
   int32_t n_join_launches, n_enum_steps, n_test_steps, reserved;
   int64_t bytes_probe;   /* sum K over the skewed (probe) join jobs, timed in t_probe_ns */
   int64_t t_probe_ns;    /* device time of the k_probe launches */
-  int64_t bytes_compact; /* k_compact algorithmic bytes: per joined row 12 B pair + url id read, 40 B row of
-                            each side read (one side for by-test steps), 44 B row + url id written */
+  int64_t bytes_compact; /* bytes k_compact moves: per joined row 12 B pair + url id read, the 32-B ranking
+                            record of the accumulated side and 16 B of the joined side's (by-test steps: one
+                            32-B record) read, 32-B record + url id written */
   int64_t t_compact_ns;  /* device time of the k_compact launches */
+  int64_t t_kernels_ns;  /* device time of all the batch's kernel launches (HIP events around every group of
+                            back-to-back launches; host waits and collectives excluded) */
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

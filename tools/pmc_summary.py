@@ -22,7 +22,7 @@ def find(pattern):
 
 def short(name):
     for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
-              "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate"):
+              "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
             return k
     return name[:40]
@@ -63,6 +63,24 @@ def main(tag, config):
             d["write_kb_per_launch"] = write[k]["WRITE_SIZE"] / nw[k]
         if "fetch_kb_per_launch_raw" in d and "write_kb_per_launch" in d:
             d["hbm_bytes_per_launch"] = (2 * d["fetch_kb_per_launch_raw"] + d["write_kb_per_launch"]) * 1024
+    # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
+    # (k_combine runs once per batch pass); index build, uploads and fills excluded
+    path = ("k_partition", "k_probe_part", "k_join", "k_probe", "k_scan_tiles", "k_compact", "k_reduce",
+            "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq", "k_emit")
+    nb = out["kernels"].get("k_combine", {}).get("calls")
+    if nb:
+        tot = 0.0
+        for k in path:
+            kd = out["kernels"].get(k, {})
+            if kd.get("hbm_bytes_per_launch") and kd.get("calls"):
+                tot += kd["hbm_bytes_per_launch"] * kd["calls"]
+        out["path_hbm_bytes_per_batch"] = tot / nb
+        out["batches_profiled"] = nb
+    import subprocess
+    try:
+        out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
+    except Exception:
+        pass
     for name in ("k_compact", "k_join", "k_probe"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")

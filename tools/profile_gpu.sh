@@ -7,7 +7,7 @@
 set -e
 TAG=${1:-r01}
 shift || true
-ARGS=${@:---steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1}
+ARGS=${@:---steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 --legs none}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof/$TAG
 mkdir -p $OUT

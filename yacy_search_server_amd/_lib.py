@@ -63,7 +63,8 @@ class CStats(ctypes.Structure):
                 ("n_join_launches", ctypes.c_int32), ("n_enum_steps", ctypes.c_int32),
                 ("n_test_steps", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64),
-                ("bytes_compact", ctypes.c_int64), ("t_compact_ns", ctypes.c_int64)]
+                ("bytes_compact", ctypes.c_int64), ("t_compact_ns", ctypes.c_int64),
+                ("t_kernels_ns", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):

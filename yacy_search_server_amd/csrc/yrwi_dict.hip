@@ -57,6 +57,18 @@ __global__ void k_dict_scatter(const uint32_t* __restrict__ rank1, const uint32_
   if (j < n) uid[pos[j]] = rank1[j] - 1u;
 }
 
+// the key of every url id: the first posting of each run of equal keys
+__global__ void k_dict_keys(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rank1,
+                            const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
+                            const uint32_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ dkhi,
+                            uint8_t* __restrict__ dklo) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || !flag[j]) return;
+  const uint32_t u = rank1[j] - 1u;
+  dkhi[u] = kh[j];
+  dklo[u] = kl[pos[j]];
+}
+
 unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 struct DevBuf {
@@ -94,6 +106,13 @@ int ensure_url_ids(CtxBase* ctx) {
   if (n == 0) {
     ctx->uid_dirty = false;
     return 0;
+  }
+  // ranking records of lists that have none yet (new or replaced lists)
+  for (ListRec* L : lists) {
+    if (L->feat || L->n == 0) continue;
+    L->feat = reinterpret_cast<uint64_t*>(ctx->index_mem.alloc((size_t)L->n * FEAT_BYTES));
+    if (!L->feat) return ctx->fail(YRWI_E_NOMEM, "ranking record allocation");
+    if (launch_features(L->rows, L->n, L->feat, st)) return ctx->fail(YRWI_E_HIP, "features launch");
   }
   std::vector<DictSeg> segs;
   std::vector<int64_t> off;
@@ -135,6 +154,26 @@ int ensure_url_ids(CtxBase* ctx) {
   hipLaunchKernelGGL(k_dict_flags, dim3(nb(n)), dim3(256), 0, st, kh, pos, kl, n, flag);
   HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp, t3, flag, rank1, ni, st));
   hipLaunchKernelGGL(k_dict_scatter, dim3(nb(n)), dim3(256), 0, st, rank1, pos, n, ctx->uid_all);
+  uint32_t nurls = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&nurls, rank1 + (n - 1), 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if ((size_t)nurls > ctx->dict_cap) {
+    if (ctx->dkhi) hipFree(ctx->dkhi);
+    if (ctx->dklo) hipFree(ctx->dklo);
+    ctx->dkhi = nullptr;
+    ctx->dklo = nullptr;
+    ctx->dict_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->dkhi), (size_t)nurls * 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&ctx->dklo), (size_t)nurls) != hipSuccess)
+      return ctx->fail(YRWI_E_NOMEM, "url dictionary allocation");
+    ctx->dict_cap = nurls;
+  }
+  ctx->nurls = nurls;
+  for (Lane* L : ctx->lanes) {  // no batch is in flight while the dictionary is rebuilt
+    L->dkhi = ctx->dkhi;
+    L->dklo = ctx->dklo;
+  }
+  hipLaunchKernelGGL(k_dict_keys, dim3(nb(n)), dim3(256), 0, st, flag, rank1, kh, kl, pos, n, ctx->dkhi, ctx->dklo);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipStreamSynchronize(st));  // scratch is freed on return
   ctx->uid_dirty = false;

@@ -235,6 +235,8 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   close_lanes(ctx);
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
+  if (ctx->dkhi) hipFree(ctx->dkhi);
+  if (ctx->dklo) hipFree(ctx->dklo);
   delete ctx;
 }
 
@@ -482,6 +484,15 @@ static int allsum_host(Lane* L, std::vector<int64_t>& v) {
 // plan_finish for a batch: global term sizes from one exchange of the local
 // sizes of the batch's distinct terms (sharded), or the local sizes (one context).
 static int plan_batch(Lane* L, std::vector<Plan>& plans) {
+  if (L->world <= 1) {  // one context: its own sizes are the global ones
+    for (Plan& P : plans) {
+      int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
+      for (int i = 0; i < P.ninc; i++) gi[i] = P.linc[i] ? P.linc[i]->n : 0;
+      for (int i = 0; i < P.nexc; i++) ge[i] = P.lexc[i] ? P.lexc[i]->n : 0;
+      plan_finish(&P, gi, ge);
+    }
+    return 0;
+  }
   std::unordered_map<KeyT, size_t, KeyHash> slot;
   std::vector<int64_t> sz;
   auto slot_of = [&](const KeyT& k, const ListRec* l) {
@@ -534,8 +545,24 @@ struct Timing {
   // per join step: before k_join, between k_join and k_probe, after k_probe
   std::vector<std::array<hipEvent_t, 3>> kjoin;
   std::vector<std::array<hipEvent_t, 2>> kcompact;  // around each k_compact launch
+  // around every group of back-to-back kernel launches of the batch (no host
+  // synchronisation inside a span): their sum is the batch's kernel time
+  std::vector<std::array<hipEvent_t, 2>> spans;
   hipEvent_t t0 = nullptr, tj = nullptr, tn = nullptr, ts = nullptr;
 };
+
+static hipEvent_t span_open(Lane* L, Timing* tm) {
+  if (!tm) return nullptr;
+  hipEvent_t e = L->event();
+  hipEventRecord(e, L->stream);
+  return e;
+}
+static void span_close(Lane* L, Timing* tm, hipEvent_t b) {
+  if (!tm) return;
+  hipEvent_t e = L->event();
+  hipEventRecord(e, L->stream);
+  tm->spans.push_back({b, e});
+}
 
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
@@ -608,28 +635,31 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
+  hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
                        ctx->stream, e0, em, e1, c0, c1))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
     tm->kcompact.push_back({c0, c1});
+    tm->spans.push_back({sp, c1});
   }
   if (st) st->n_join_launches++;
   std::vector<int64_t> mh((size_t)nj, 0);
   HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, lane_sync(ctx));
-  if (st)  // k_compact per joined row: pair + id, the row(s) it gathers, row + id written
-    for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 136 : 96);
+  if (st)  // k_compact per joined row: pair + id read, the records it gathers (32 B, + 16 B of the joined
+           // side for enumeration steps), record + id written
+    for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 96 : 80);
   for (int j = 0; j < nj; j++) {
     Plan& P = plans[(size_t)owner[(size_t)j]];
-    P.cont = DList{nullptr, nullptr, jobs[(size_t)j].out_rows, mh[(size_t)j], jobs[(size_t)j].out_uid};
+    P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], jobs[(size_t)j].out_uid, jobs[(size_t)j].out_feat};
   }
   return 0;
 }
 
 // exclusion (excludeContainers :373-388): mark container rows present in an exclude list
-static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st) {
+static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   std::vector<JoinQ> jobs;
   std::vector<int> owner;
   std::vector<int64_t> tile_base;
@@ -661,9 +691,11 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st) {
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
   if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr, true,
                        ctx->stream, nullptr, nullptr, nullptr))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
+  span_close(ctx, tm, sp);
   return 0;
 }
 
@@ -707,9 +739,9 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.maxd = P.maxd;
       J.now_ms = P.now_ms;
       int64_t cap = std::min(J.A.n, J.B.n);
-      J.out_rows = arena_alloc<uint8_t>(ctx, cap * 40);
+      J.out_feat = arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
       J.out_uid = arena_alloc<uint32_t>(ctx, cap);
-      if (!J.out_rows || !J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (!J.out_feat || !J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (st) {
         st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
@@ -730,7 +762,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     for (size_t qi = 0; qi < nq; qi++)
       if (stepped[qi]) acc_g[qi] = v[qi];
   }
-  return run_exclusion(ctx, plans, st);
+  return run_exclusion(ctx, plans, st, tm);
 }
 
 // Global host counts for authority (ReferenceOrder.java:176-216) across url-hash
@@ -815,7 +847,12 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     Plan& P = plans[(size_t)qi];
     RankQ& R = rq[(size_t)qi];
     std::memset(&R, 0, sizeof(R));
-    R.rows = P.cont.rows;
+    R.feat = P.cont.feat;
+    R.uid = P.cont.uid;
+    R.ekhi = P.cont.uid ? nullptr : P.cont.khi;
+    R.eklo = P.cont.uid ? nullptr : P.cont.klo;
+    R.dkhi = ctx->dkhi;
+    R.dklo = ctx->dklo;
     R.removed = P.removed;
     R.n = P.empty ? 0 : P.cont.n;
     R.nchunks = ceil_div(R.n, CHUNK);
@@ -940,7 +977,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base) || upload(ctx, d_cq, chunk_q)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
+  hipEvent_t sp = span_open(ctx, tm);
   if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  span_close(ctx, tm, sp);
   if (W > 1 && any_auth) {
     int rc2 = exchange_host_counts(ctx, nq, nslots, slot_base, d_hkeys, d_hcnt, d_ss);
     if (rc2) return rc2;
@@ -948,7 +987,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (W > 1) {
     if (int rc = coll_allgather(ctx, d_ss, d_all, sizeof(ShardSum) * nq)) return rc;
   }
+  sp = span_open(ctx, tm);
   if (launch_combine(d_q, nq, d_all, W, d_norm, ctx->stream)) return ctx->fail(YRWI_E_HIP, "combine launch");
+  span_close(ctx, tm, sp);
   if (tm) { tm->tn = ctx->event(); hipEventRecord(tm->tn, ctx->stream); }
 
   if (h_scores_all) {  // yrwi_normalize_score
@@ -975,8 +1016,10 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   int32_t* d_redo = arena_alloc<int32_t>(ctx, std::max<int64_t>(chunks, 1));
   if (!d_zero || !d_redo) return ctx->fail(YRWI_E_NOMEM, "arena");
   HIPCHK(ctx, hipMemsetAsync(d_zero, 0, 2 * sizeof(int32_t), ctx->stream));
+  sp = span_open(ctx, tm);
   if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
+  span_close(ctx, tm, sp);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
   std::vector<const Cand*> fptr((size_t)nq);
@@ -1019,8 +1062,10 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     int32_t* d_oc = arena_alloc<int32_t>(ctx, ngr);
     if (!d_gb || !d_gn || !d_gk || !d_out || !d_oc) return ctx->fail(YRWI_E_NOMEM, "arena");
     if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn) || upload(ctx, d_gk, gk)) return YRWI_E_HIP;
+    hipEvent_t sq = span_open(ctx, tm);
     if (launch_topq(d_gb, d_gn, d_gk, ngr, cur, curc, in_stride, keff, d_out, d_oc, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "top-k launch");
+    span_close(ctx, tm, sq);
     for (int qi : part) {
       fptr[(size_t)qi] = d_out + lbase[(size_t)qi] * keff;
       fcnt[(size_t)qi] = d_oc + lbase[(size_t)qi];
@@ -1059,15 +1104,19 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
   std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
   if (W == 1) {
+    sp = span_open(ctx, tm);
     if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, 0, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "emit launch");
+    span_close(ctx, tm, sp);
     if (any_dd) {
       yrwi_hit* d_stack = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
       int32_t* d_scnt = arena_alloc<int32_t>(ctx, nq);
       if (!d_stack || !d_scnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+      sp = span_open(ctx, tm);
       if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_stack, d_scnt, 2, ctx->stream) ||
           launch_pull(d_q, nq, d_stack, d_scnt, kint, 1, kmax, d_hits, d_nout, ctx->stream))
         return ctx->fail(YRWI_E_HIP, "doubledom launch");
+      span_close(ctx, tm, sp);
     }
   } else {
     yrwi_hit* d_mine = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kint);
@@ -1080,13 +1129,17 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     int32_t* d_scnt = arena_alloc<int32_t>(ctx, nq);
     if (!d_mine || !d_mcnt || !d_allh || !d_alln || !d_slot || !d_dup || !d_stack || !d_scnt)
       return ctx->fail(YRWI_E_NOMEM, "arena");
+    sp = span_open(ctx, tm);
     if (launch_emit(d_q, nq, d_fptr, d_fcnt, kint, d_mine, d_mcnt, 1, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "emit launch");
+    span_close(ctx, tm, sp);
     if (int rc = coll_allgather(ctx, d_mine, d_allh, sizeof(yrwi_hit) * (size_t)nq * kint)) return rc;
     if (int rc = coll_allgather(ctx, d_mcnt, d_alln, sizeof(int32_t) * (size_t)nq)) return rc;
+    sp = span_open(ctx, tm);
     if (launch_gmerge(d_q, d_allh, d_alln, W, nq, kint, d_slot, d_dup, d_stack, d_scnt, ctx->stream) ||
         launch_pull(d_q, nq, d_stack, d_scnt, kint, 0, kmax, d_hits, d_nout, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "shard merge launch");
+    span_close(ctx, tm, sp);
     hD.resize((size_t)nq);
     HIPCHK(ctx, hipMemcpy2DAsync(hD.data(), sizeof(int32_t), reinterpret_cast<const uint8_t*>(d_norm) + offsetof(NormState, D),
                                  sizeof(NormState), sizeof(int32_t), (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
@@ -1158,8 +1211,9 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
     if (rc) return rc;
     if (st) st->postings_in += all[(size_t)i].postings_in;
   }
-  // J1/J2 on global list sizes (one exchange of the batch's term sizes when sharded)
-  if (begin_pass(L)) return YRWI_E_HIP;
+  // J1/J2 on global list sizes (one exchange of the batch's term sizes when sharded,
+  // through this lane's arena and staging)
+  if (L->world > 1 && begin_pass(L)) return YRWI_E_HIP;
   if (int rc = plan_batch(L, all)) return rc;
   const int64_t budget = scratch_budget(L);
   for (int g0 = 0; g0 < nq;) {
@@ -1197,6 +1251,8 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
       }
       for (auto& ev : tm.kcompact)
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_compact_ns += (int64_t)(ms * 1e6);
+      for (auto& ev : tm.spans)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_kernels_ns += (int64_t)(ms * 1e6);
       if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
       if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
     }
@@ -1271,6 +1327,7 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->t_probe_ns += p.t_probe_ns;
       st->bytes_compact += p.bytes_compact;
       st->t_compact_ns += p.t_compact_ns;
+      st->t_kernels_ns += p.t_kernels_ns;
       st->t_norm_ns += p.t_norm_ns;
       st->t_score_ns += p.t_score_ns;
       st->n_join_launches += p.n_join_launches;
@@ -1408,7 +1465,15 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
     return 0;
   }
   std::vector<uint8_t> rows((size_t)P.cont.n * 40), rem;
-  HIPCHK(ctx, hipMemcpyAsync(rows.data(), P.cont.rows, rows.size(), hipMemcpyDeviceToHost, ctx->stream));
+  const uint8_t* src = P.cont.rows;  // a single include list is returned as it is stored (:355-370)
+  if (!src) {  // a joined container: its rows as toRowEntry re-encodes them (J6)
+    uint8_t* d_rows = arena_alloc<uint8_t>(L, P.cont.n * 40);
+    if (!d_rows) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (launch_feat_rows(P.cont.feat, P.cont.uid, ctx->dkhi, ctx->dklo, P.cont.n, plans[0].now_ms, d_rows, L->stream))
+      return ctx->fail(YRWI_E_HIP, "row launch");
+    src = d_rows;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(rows.data(), src, rows.size(), hipMemcpyDeviceToHost, ctx->stream));
   if (P.removed) {
     rem.resize((size_t)P.cont.n);
     HIPCHK(ctx, hipMemcpyAsync(rem.data(), P.removed, rem.size(), hipMemcpyDeviceToHost, ctx->stream));
@@ -1451,7 +1516,10 @@ extern "C" int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_
   std::vector<Plan> plans(1);
   Plan& P = plans[0];
   P.empty = false;
-  P.cont = DList{khi, klo, rows, m};
+  uint64_t* feat = arena_alloc<uint64_t>(L, m * FEAT_WORDS);
+  if (!feat) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (launch_features(rows, m, feat, ctx->stream)) return ctx->fail(YRWI_E_HIP, "features launch");
+  P.cont = DList{khi, klo, rows, m, nullptr, feat};
   P.removed = nullptr;
   if (prof) P.prof = *prof; else yrwi_profile_default(&P.prof);
   size_t ll = language ? strnlen(language, 8) : 0;

@@ -75,7 +75,8 @@ struct ListRec {
   uint8_t* rows = nullptr;
   int64_t n = 0;
   uint32_t* uid = nullptr;  // url ids (rebuilt with the url dictionary)
-  DList dl() const { return DList{khi, klo, rows, n, uid}; }
+  uint64_t* feat = nullptr; // ranking records (built with the url dictionary)
+  DList dl() const { return DList{khi, klo, rows, n, uid, feat}; }
 };
 
 // bump allocator over device chunks
@@ -200,6 +201,8 @@ struct Lane {
   Stage stage;
   Stage out_stage;           // pinned landing buffer for results
   int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
+  const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
+  const uint8_t* dklo = nullptr;
   Arena arena{(size_t)256 << 20};
   std::string err;
   std::vector<hipEvent_t> evpool;
@@ -306,6 +309,10 @@ struct CtxBase {
   bool uid_dirty = true;
   uint32_t* uid_all = nullptr;
   size_t uid_cap = 0;
+  uint64_t* dkhi = nullptr;  // key of every url id (72-bit Base64 key: hi 64 bits, low byte)
+  uint8_t* dklo = nullptr;
+  size_t dict_cap = 0;
+  int64_t nurls = 0;
   std::string err;
   int64_t npostings = 0;
 

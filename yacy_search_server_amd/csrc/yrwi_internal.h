@@ -37,10 +37,24 @@ constexpr int64_t DAY_MS = 86400000LL;
 struct DList {
   const uint64_t* khi;
   const uint8_t* klo;
-  const uint8_t* rows;  // 40-byte WordReferenceRow
+  const uint8_t* rows;  // 40-byte WordReferenceRow (index lists; joined containers have none)
   int64_t n;
   const uint32_t* uid;
+  const uint64_t* feat;  // FEAT_WORDS words per posting: the ranking record (FeatRec below)
 };
+
+// The ranking record of a posting, 32 bytes (4 little-endian words), built from
+// its WordReferenceRow (WordReferenceRow.java:49-72) by k_features and carried
+// through every join: the joins gather 32 B of the accumulated side and 16 B of
+// the joined side instead of 40-byte rows, and the ranking kernels stream it.
+//   w0 = t | w << 16 | p << 32 | u << 48 | c << 56   posintext, wordsintext, phrasesintext, wordsintitle, hitcount
+//   w1 = r | o << 8 | i << 16 | x << 24 | y << 32 | m << 40 | n << 48 | d << 56
+//        posinphrase, posofphrase, worddistance, llocal, lother, urllength, urlcomps, doctype
+//   w2 = a | l << 16 | z << 32          lastModified days, language (byte 22 low), flags (byte 29 low)
+//   w3 = h | dl << 32                   ByteArray.hashCode(urlhash), domLengthEstimation key (ahpla[urlhash[11]] & 3)
+// The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.
+constexpr int FEAT_WORDS = 4;
+constexpr int FEAT_BYTES = 8 * FEAT_WORDS;
 
 // Feature rule of a join step (ReferenceContainer.joinConstructive :406-416).
 enum JoinMode : int32_t {
@@ -66,7 +80,7 @@ struct JoinQ {
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
-  uint8_t* out_rows;
+  uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
   int64_t now_ms;
   int64_t* m_out;      // number of output rows (written by the scan kernel)
 };
@@ -154,7 +168,12 @@ struct FilterQ {
 };
 
 struct RankQ {
-  const uint8_t* rows;     // container rows (sorted by url hash)
+  const uint64_t* feat;    // container ranking records (sorted by url hash), FEAT_WORDS per element
+  const uint32_t* uid;     // container url ids (keys from the url dictionary dkhi/dklo) ...
+  const uint64_t* ekhi;    // ... or, without url ids, the elements' own keys
+  const uint8_t* eklo;
+  const uint64_t* dkhi;    // url dictionary: key of every url id
+  const uint8_t* dklo;
   const uint8_t* removed;  // exclusion marks or nullptr
   int64_t n;
   int64_t chunk_base;
@@ -198,6 +217,12 @@ int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n
 // (defined in yrwi_kernels.hip; all asynchronous on `stream`)
 int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err,
                          void* stream);
+// ranking records (FeatRec) of n rows
+int launch_features(const uint8_t* rows, int64_t n, uint64_t* feat, void* stream);
+// joined container -> 40-byte rows as toRowEntry writes them (WordReferenceVars.java:301-327):
+// key of url id uid[i] from the dictionary, the record's columns, freshUntil from "now"
+int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* dkhi, const uint8_t* dklo, int64_t n,
+                     int64_t now_ms, uint8_t* rows, void* stream);
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,

@@ -190,6 +190,119 @@ __global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t
   if (e) atomicOr(err, e);
 }
 
+// ==================================================== decoded postings
+struct Feat {  // decoded WordReferenceVars fields of one posting
+  int32_t f[NF];
+  int32_t a, p, od;
+  double tf;
+  uint32_t z;     // flags (Bitfield bit j = bit j)
+  uint32_t lang;  // language cell: byte 22 | byte 23 << 8
+  uint32_t d;     // doctype
+  int32_t dl;     // DigestURL.domLengthEstimation key: ahpla[urlhash[11]] & 3
+};
+
+__device__ __forceinline__ int32_t url_hashcode(const Row& r);
+
+__device__ __forceinline__ Feat decode(const Row& r) {
+  Feat x;
+  x.f[F_HITCOUNT] = (int32_t)r.b(O_C);
+  x.f[F_LLOCAL] = (int32_t)r.b(O_X);
+  x.f[F_LOTHER] = (int32_t)r.b(O_Y);
+  x.f[F_WORDSINTEXT] = (int32_t)r.u16(O_W);
+  x.f[F_PHRASESINTEXT] = (int32_t)r.u16(O_P);
+  x.f[F_POSINTEXT] = (int32_t)r.u16(O_T);
+  x.f[F_POSINPHRASE] = (int32_t)r.b(O_R);
+  x.f[F_POSOFPHRASE] = (int32_t)r.b(O_O);
+  x.f[F_URLLENGTH] = (int32_t)r.b(O_M);
+  x.f[F_URLCOMPS] = (int32_t)r.b(O_N);
+  x.f[F_WORDSINTITLE] = (int32_t)r.b(O_U);
+  x.a = (int32_t)r.u16(O_A);
+  x.p = x.f[F_POSINTEXT];
+  x.od = (int32_t)r.b(O_I);
+  // WordReferenceRow.termFrequency (WordReferenceRow.java:355-357)
+  x.tf = (double)x.f[F_HITCOUNT] / (double)(x.f[F_WORDSINTEXT] + x.f[F_WORDSINTITLE] + 1);
+  x.z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24);
+  x.lang = r.b(O_L) | (r.b(O_L + 1) << 8);
+  x.d = r.b(O_D);
+  x.dl = ahpla(r.b(11)) & 3;
+  return x;
+}
+
+// ---- ranking records (FeatRec, yrwi_internal.h)
+struct Rec {
+  uint64_t w[FEAT_WORDS];
+};
+
+__device__ __forceinline__ Rec rec_of_row(const Row& r) {
+  Rec q;
+  q.w[0] = (uint64_t)r.u16(O_T) | (uint64_t)r.u16(O_W) << 16 | (uint64_t)r.u16(O_P) << 32 | (uint64_t)r.b(O_U) << 48 |
+           (uint64_t)r.b(O_C) << 56;
+  q.w[1] = (uint64_t)r.b(O_R) | (uint64_t)r.b(O_O) << 8 | (uint64_t)r.b(O_I) << 16 | (uint64_t)r.b(O_X) << 24 |
+           (uint64_t)r.b(O_Y) << 32 | (uint64_t)r.b(O_M) << 40 | (uint64_t)r.b(O_N) << 48 | (uint64_t)r.b(O_D) << 56;
+  const uint64_t z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | ((uint64_t)r.b(O_Z + 3) << 24);
+  q.w[2] = (uint64_t)r.u16(O_A) | (uint64_t)(r.b(O_L) | (r.b(O_L + 1) << 8)) << 16 | z << 32;
+  q.w[3] = (uint64_t)(uint32_t)url_hashcode(r) | (uint64_t)(ahpla(r.b(11)) & 3) << 32;
+  return q;
+}
+
+// record loads: every feat array starts 256-B aligned, records are 32 B
+__device__ __forceinline__ Rec load_rec(const uint64_t* f, int64_t e) {
+  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(f + e * FEAT_WORDS);
+  const ulonglong2 x = p[0], y = p[1];
+  Rec q;
+  q.w[0] = x.x;
+  q.w[1] = x.y;
+  q.w[2] = y.x;
+  q.w[3] = y.y;
+  return q;
+}
+__device__ __forceinline__ void store_rec(uint64_t* f, int64_t e, const Rec& q) {
+  ulonglong2* p = reinterpret_cast<ulonglong2*>(f + e * FEAT_WORDS);
+  p[0] = make_ulonglong2(q.w[0], q.w[1]);
+  p[1] = make_ulonglong2(q.w[2], q.w[3]);
+}
+
+__device__ __forceinline__ Feat decode_rec(const Rec& q) {
+  Feat x;
+  const uint64_t w0 = q.w[0], w1 = q.w[1], w2 = q.w[2];
+  x.f[F_HITCOUNT] = (int32_t)(w0 >> 56);
+  x.f[F_LLOCAL] = (int32_t)((w1 >> 24) & 0xFF);
+  x.f[F_LOTHER] = (int32_t)((w1 >> 32) & 0xFF);
+  x.f[F_WORDSINTEXT] = (int32_t)((w0 >> 16) & 0xFFFF);
+  x.f[F_PHRASESINTEXT] = (int32_t)((w0 >> 32) & 0xFFFF);
+  x.f[F_POSINTEXT] = (int32_t)(w0 & 0xFFFF);
+  x.f[F_POSINPHRASE] = (int32_t)(w1 & 0xFF);
+  x.f[F_POSOFPHRASE] = (int32_t)((w1 >> 8) & 0xFF);
+  x.f[F_URLLENGTH] = (int32_t)((w1 >> 40) & 0xFF);
+  x.f[F_URLCOMPS] = (int32_t)((w1 >> 48) & 0xFF);
+  x.f[F_WORDSINTITLE] = (int32_t)((w0 >> 48) & 0xFF);
+  x.a = (int32_t)(w2 & 0xFFFF);
+  x.p = x.f[F_POSINTEXT];
+  x.od = (int32_t)((w1 >> 16) & 0xFF);
+  x.tf = (double)x.f[F_HITCOUNT] / (double)(x.f[F_WORDSINTEXT] + x.f[F_WORDSINTITLE] + 1);
+  x.z = (uint32_t)(w2 >> 32);
+  x.lang = (uint32_t)((w2 >> 16) & 0xFFFF);
+  x.d = (uint32_t)(w1 >> 56);
+  x.dl = (int32_t)((q.w[3] >> 32) & 3);
+  return x;
+}
+
+// 72-bit url-hash key of container element e: its own key, or its url id's in the dictionary
+__device__ __forceinline__ void key_at(const RankQ& Q, int64_t e, uint64_t& hi, uint32_t& lo) {
+  if (Q.uid) {
+    const uint32_t u = Q.uid[e];
+    hi = Q.dkhi[u];
+    lo = Q.dklo[u];
+  } else {
+    hi = Q.ekhi[e];
+    lo = Q.eklo[e];
+  }
+}
+// url-hash chars 6..11 (the host hash, DigestURL :229-296) = the key's low 36 bits
+__device__ __forceinline__ uint64_t key_host36(uint64_t hi, uint32_t lo) {
+  return ((hi & 0xFFFFFFFull) << 8) | (lo & 0xFFu);
+}
+
 // =========================================================== join: partition
 // One thread per merge tile: the merge-path split of the tile's first and last
 // diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
@@ -231,15 +344,16 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
 }
 
 // joined worddistance (WordReferenceVars.distance :287-294 after join :465-499)
-__device__ __forceinline__ int32_t joined_distance(const uint8_t* ra, const uint8_t* rb, int mode) {
-  if (mode == JM_TEST_LARGE_B) return rb[O_I];
-  if (mode == JM_TEST_LARGE_A) return ra[O_I];
-  int pa = ((int)ra[O_T] << 8) | ra[O_T + 1], pb = ((int)rb[O_T] << 8) | rb[O_T + 1];
+// from the two postings' ranking records (posintext in word 0, stored distance in word 1)
+__device__ __forceinline__ int32_t joined_distance(const uint64_t* fa, const uint64_t* fb, int mode) {
+  if (mode == JM_TEST_LARGE_B) return (int32_t)((fb[1] >> 16) & 0xFF);
+  if (mode == JM_TEST_LARGE_A) return (int32_t)((fa[1] >> 16) & 0xFF);
+  const int pa = (int)(fa[0] & 0xFFFF), pb = (int)(fb[0] & 0xFFFF);
   if (pa > 0 && pb > 0) {
     int d = pa > pb ? pa - pb : pb - pa;
     if (d != 0) return d;
   }
-  return ra[O_I];
+  return (int32_t)((fa[1] >> 16) & 0xFF);
 }
 
 // ============================================================ join: tiles
@@ -357,9 +471,9 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
         if (mark) {
           J.removed[a0 + a_at(st)] = 1;
         } else {
-          const uint8_t* ra = J.A.rows + (a0 + a_at(st)) * YRWI_ROW_BYTES;
-          const uint8_t* rb = J.B.rows + (b0 + b_at(st)) * YRWI_ROW_BYTES;
-          if (joined_distance(ra, rb, J.mode) > J.maxd) mbits &= ~(1u << st);
+          const uint64_t* fa = J.A.feat + (a0 + a_at(st)) * FEAT_WORDS;
+          const uint64_t* fb = J.B.feat + (b0 + b_at(st)) * FEAT_WORDS;
+          if (joined_distance(fa, fb, J.mode) > J.maxd) mbits &= ~(1u << st);
         }
       }
     }
@@ -481,7 +595,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   }
   const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
   if (hit && !mark && J.maxd < 65535) {
-    if (joined_distance(J.A.rows + ia * YRWI_ROW_BYTES, J.B.rows + ib * YRWI_ROW_BYTES, J.mode) > J.maxd) hit = false;
+    if (joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) hit = false;
   }
   if (mark) {
     if (hit) J.removed[ia] = 1;
@@ -517,12 +631,14 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
 }
 
 // ============================================================ join: compact
-// Joined row: J5 (WordReferenceVars.join :465-499) + J6 (toRowEntry :301-322 ->
-// WordReferenceRow ctor :116-161).
-// J5 + J6 on loaded rows: for by-test modes `o` is already the large side's row
-__device__ __forceinline__ Row joined_row_of(Row o, const Row& B, int mode, int64_t now_ms) {
+// Joined posting: J5 (WordReferenceVars.join :465-499) + J6 (toRowEntry :301-322
+// -> WordReferenceRow ctor :116-161), on ranking records.  `o` is the record of
+// the accumulated side (by-test modes: the large side's, joined with itself: its
+// own features); b0/b1 are words 0-1 of the joined side (enumeration only).
+__device__ __forceinline__ Rec joined_rec(Rec o, uint64_t b0, uint64_t b1, int mode, int64_t now_ms) {
   if (mode == JM_ENUM) {
-    int pa = (int)o.u16(O_T), pb = (int)B.u16(O_T);
+    const uint64_t a0 = o.w[0], a1 = o.w[1];
+    const int pa = (int)(a0 & 0xFFFF), pb = (int)(b0 & 0xFFFF);
     int pos = 0, post = pa;
     bool has = false;
     if (pa > 0 && pb > 0) {
@@ -531,86 +647,34 @@ __device__ __forceinline__ Row joined_row_of(Row o, const Row& B, int mode, int6
     } else if (pa == 0) {
       post = pb;
     }
-    int oa = (int)o.b(O_O), ob = (int)B.b(O_O), r = (int)o.b(O_R), op = oa;
-    if (oa == ob) r = min(r, (int)B.b(O_R));
-    else if (oa > ob) { op = ob; r = (int)B.b(O_R); }
-    int w = max((int)o.u16(O_W), (int)B.u16(O_W));
-    int u = max((int)o.b(O_U), (int)B.b(O_U));
-    int p = max((int)o.u16(O_P), (int)B.u16(O_P));
-    int c = max((int)o.b(O_C), (int)B.b(O_C));
+    const int oa = (int)((a1 >> 8) & 0xFF), ob = (int)((b1 >> 8) & 0xFF);
+    int r = (int)(a1 & 0xFF), op = oa;
+    if (oa == ob) r = min(r, (int)(b1 & 0xFF));
+    else if (oa > ob) { op = ob; r = (int)(b1 & 0xFF); }
+    const uint64_t w = max((a0 >> 16) & 0xFFFF, (b0 >> 16) & 0xFFFF);
+    const uint64_t p = max((a0 >> 32) & 0xFFFF, (b0 >> 32) & 0xFFFF);
+    const uint64_t u = max((a0 >> 48) & 0xFF, (b0 >> 48) & 0xFF);
+    const uint64_t c = max(a0 >> 56, b0 >> 56);
     int dist = 0;
     if (has && post > 0) dist = post > pos ? post - pos : pos - post;
-    if (dist == 0) dist = (int)o.b(O_I);
-    o.set(O_T, (uint32_t)post >> 8); o.set(O_T + 1, (uint32_t)post);
-    o.set(O_O, (uint32_t)op); o.set(O_R, (uint32_t)r);
-    o.set(O_W, (uint32_t)w >> 8); o.set(O_W + 1, (uint32_t)w);
-    o.set(O_U, (uint32_t)u);
-    o.set(O_P, (uint32_t)p >> 8); o.set(O_P + 1, (uint32_t)p);
-    o.set(O_C, (uint32_t)c);
-    o.set(O_I, (uint32_t)dist);
+    if (dist == 0) dist = (int)((a1 >> 16) & 0xFF);
+    o.w[0] = (uint64_t)post | w << 16 | p << 32 | u << 48 | c << 56;
+    o.w[1] = (a1 & ~0xFFFFFFull) | (uint64_t)r | (uint64_t)op << 8 | (uint64_t)(dist & 0xFF) << 16;  // i: 1-byte cell
   }
-  // by test: the large row joined with itself -> its own features, stored distance
-  const int32_t mddlm = clamp_days((int32_t)o.u16(O_A), now_ms);
-  const int32_t mddct = micro_date_days(now_ms);
-  int32_t fresh = add32(mddlm, mul32(sub32(mddct, mddlm), 2));
-  if (fresh < 0) fresh = 0;
-  o.set(O_A, (uint32_t)mddlm >> 8); o.set(O_A + 1, (uint32_t)mddlm);
-  o.set(O_S, (uint32_t)fresh >> 8); o.set(O_S + 1, (uint32_t)fresh);
-  o.set(O_G, 0);
-  o.set(O_K, 0);
+  // lastModified re-encoded through MicroDate: future days clamp to today (J6)
+  const int32_t mddlm = clamp_days((int32_t)(o.w[2] & 0xFFFF), now_ms);
+  o.w[2] = (o.w[2] & ~0xFFFFull) | (uint64_t)(mddlm & 0xFFFF);
   return o;
-}
-
-__device__ __forceinline__ Row joined_row(const uint8_t* ra, const uint8_t* rb, int mode, int64_t now_ms) {
-  const Row a = load_row(mode == JM_TEST_LARGE_B ? rb : ra);
-  Row b{};
-  if (mode == JM_ENUM) b = load_row(rb);
-  return joined_row_of(a, b, mode, now_ms);
-}
-
-// url-hash key of a row (bytes 0..11), as k_validate computes it for the index
-__device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo) {
-  uint64_t x = 0;
-#pragma unroll
-  for (int j = 0; j < 10; j++) x = (x << 6) | (uint64_t)(ahpla(r.b(j)) & 63);
-  const uint32_t c10 = (uint32_t)ahpla(r.b(10)) & 63, c11 = (uint32_t)ahpla(r.b(11)) & 63;
-  hi = (x << 4) | (c10 >> 2);
-  lo = ((c10 & 3u) << 6) | c11;
 }
 
 // One workgroup per COMPACT_TILES consecutive tiles: the tiles' matches are
 // concatenated (LDS prefix of their counts) and spread over all 256 threads.
 // The output url id comes with the pair (written by k_join / k_probe).  Each
 // thread takes COMPACT_UNROLL matches at a time and issues all their pair and
-// row loads before combining any of them: the gathers are latency-bound, so
-// more of them in flight per thread is what moves the rows.
-// Gather loads of k_compact.  Every list and container starts 256-B aligned and
-// its allocation is rounded up to 256 B, so a row (40 B at an 8-B aligned
-// offset) lies inside the three 16-B aligned blocks starting at floor16(p):
-// three dwordx4 loads replace five dwordx2 loads, and the block past the row
-// (p % 16 == 0) is still inside the allocation.  The joined row needs only
-// bytes 16..23 and 32..39 of the B row (J5: u w p / c t r o), two loads.
-__device__ __forceinline__ Row load_row_wide(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(a & ~(uintptr_t)15);
-  const ulonglong2 x = q[0], y = q[1], z = q[2];
-  const bool odd = (a & 15) != 0;  // row starts at byte 8 of the first block
-  Row r;
-  r.w[0] = odd ? x.y : x.x;
-  r.w[1] = odd ? y.x : x.y;
-  r.w[2] = odd ? y.y : y.x;
-  r.w[3] = odd ? z.x : y.y;
-  r.w[4] = odd ? z.y : z.x;
-  return r;
-}
-__device__ __forceinline__ Row load_row_join_side(const uint8_t* p) {
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-  Row r{};
-  r.w[2] = q[2];
-  r.w[4] = q[4];
-  return r;
-}
-
+// record loads before combining any of them: the gathers are latency-bound, so
+// more of them in flight per thread is what moves the records.  Per match it
+// gathers the 32-byte record of the accumulated side (one aligned 32-B block)
+// and words 0-1 of the joined side (16 B), and writes one 32-B record + url id.
 #ifndef YRWI_COMPACT_TILES
 #define YRWI_COMPACT_TILES 4
 #endif
@@ -621,9 +685,9 @@ constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
 constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
 
 struct CompactJob {
-  const uint8_t* ar;
-  const uint8_t* br;
-  uint8_t* orows;
+  const uint64_t* af;
+  const uint64_t* bf;
+  uint64_t* ofeat;
   uint32_t* ouid;
   int64_t now_ms;
   int64_t off;
@@ -646,9 +710,9 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       if (c) {
         const JoinQ& J = jobs[find_job(tile_base, njobs, t)];
         CompactJob& X = sJ[threadIdx.x];
-        X.ar = J.A.rows;
-        X.br = J.B.rows;
-        X.orows = J.out_rows;
+        X.af = J.A.feat;
+        X.bf = J.B.feat;
+        X.ofeat = J.out_feat;
         X.ouid = J.out_uid;
         X.now_ms = J.now_ms;
         X.off = tile_off[t];
@@ -682,53 +746,90 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         uid[u] = pair_uid[pi[u]];
       }
     }
-    Row A[COMPACT_UNROLL], B[COMPACT_UNROLL];
+    Rec A[COMPACT_UNROLL];
+    ulonglong2 B[COMPACT_UNROLL];
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
+      B[u] = make_ulonglong2(0, 0);
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
-      A[u] = load_row_wide(X.mode == JM_TEST_LARGE_B ? X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES
-                                                      : X.ar + (int64_t)pr[u].x * YRWI_ROW_BYTES);
-      if (X.mode == JM_ENUM) B[u] = load_row_join_side(X.br + (int64_t)pr[u].y * YRWI_ROW_BYTES);
+      A[u] = X.mode == JM_TEST_LARGE_B ? load_rec(X.bf, pr[u].y) : load_rec(X.af, pr[u].x);
+      if (X.mode == JM_ENUM) B[u] = *reinterpret_cast<const ulonglong2*>(X.bf + (int64_t)pr[u].y * FEAT_WORDS);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
       const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
-      store_row(X.orows + o * YRWI_ROW_BYTES, joined_row_of(A[u], B[u], X.mode, X.now_ms));
+      store_rec(X.ofeat, o, joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
       X.ouid[o] = uid[u];
     }
   }
 }
 
-// ================================================================ ranking
-struct Feat {  // decoded WordReferenceVars fields of one row
-  int32_t f[NF];
-  int32_t a, p, od;
-  double tf;
-};
-
-__device__ __forceinline__ Feat decode(const Row& r) {
-  Feat x;
-  x.f[F_HITCOUNT] = (int32_t)r.b(O_C);
-  x.f[F_LLOCAL] = (int32_t)r.b(O_X);
-  x.f[F_LOTHER] = (int32_t)r.b(O_Y);
-  x.f[F_WORDSINTEXT] = (int32_t)r.u16(O_W);
-  x.f[F_PHRASESINTEXT] = (int32_t)r.u16(O_P);
-  x.f[F_POSINTEXT] = (int32_t)r.u16(O_T);
-  x.f[F_POSINPHRASE] = (int32_t)r.b(O_R);
-  x.f[F_POSOFPHRASE] = (int32_t)r.b(O_O);
-  x.f[F_URLLENGTH] = (int32_t)r.b(O_M);
-  x.f[F_URLCOMPS] = (int32_t)r.b(O_N);
-  x.f[F_WORDSINTITLE] = (int32_t)r.b(O_U);
-  x.a = (int32_t)r.u16(O_A);
-  x.p = x.f[F_POSINTEXT];
-  x.od = (int32_t)r.b(O_I);
-  // WordReferenceRow.termFrequency (WordReferenceRow.java:355-357)
-  x.tf = (double)x.f[F_HITCOUNT] / (double)(x.f[F_WORDSINTEXT] + x.f[F_WORDSINTITLE] + 1);
-  return x;
+// url-hash key -> the 12 url-hash characters (Base64Order.enhancedCoder alphabet)
+__device__ __forceinline__ uint8_t b64char(uint32_t c) {
+  return (uint8_t)(c < 26 ? 'A' + c : c < 52 ? 'a' + (c - 26) : c < 62 ? '0' + (c - 52) : c == 62 ? '-' : '_');
 }
+__device__ __forceinline__ void key_chars(uint64_t hi, uint32_t lo, uint8_t* h) {
+#pragma unroll
+  for (int j = 0; j < 10; j++) h[j] = b64char((uint32_t)(hi >> (4 + 6 * (9 - j))) & 63u);
+  h[10] = b64char((uint32_t)(((hi & 15u) << 2) | ((lo >> 6) & 3u)));
+  h[11] = b64char(lo & 63u);
+}
+
+// url-hash key of a row (bytes 0..11), as k_validate computes it for the index
+__device__ __forceinline__ void row_key(const Row& r, uint64_t& hi, uint32_t& lo) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 10; j++) x = (x << 6) | (uint64_t)(ahpla(r.b(j)) & 63);
+  const uint32_t c10 = (uint32_t)ahpla(r.b(10)) & 63, c11 = (uint32_t)ahpla(r.b(11)) & 63;
+  hi = (x << 4) | (c10 >> 2);
+  lo = ((c10 & 3u) << 6) | c11;
+}
+
+// ranking records of index rows (built with the url dictionary)
+__global__ void k_features(const uint8_t* __restrict__ rows, int64_t n, uint64_t* __restrict__ feat) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) store_rec(feat, i, rec_of_row(load_row(rows + i * YRWI_ROW_BYTES)));
+}
+
+// joined container -> the 40-byte rows toRowEntry writes (WordReferenceRow ctor
+// :116-161): url hash from the dictionary, freshUntil = lastModified + 2 (today -
+// lastModified) days, floored at 0; typeofword and reserve 0
+__global__ void k_feat_rows(const uint64_t* __restrict__ feat, const uint32_t* __restrict__ uid,
+                            const uint64_t* __restrict__ dkhi, const uint8_t* __restrict__ dklo, int64_t n,
+                            int64_t now_ms, uint8_t* __restrict__ rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Rec q = load_rec(feat, i);
+  uint8_t h[12];
+  key_chars(dkhi[uid[i]], dklo[uid[i]], h);
+  Row r{};
+  for (int j = 0; j < 12; j++) r.set(j, h[j]);
+  const uint64_t w0 = q.w[0], w1 = q.w[1], w2 = q.w[2];
+  const int32_t a = (int32_t)(w2 & 0xFFFF);
+  int32_t fresh = add32(a, mul32(sub32(micro_date_days(now_ms), a), 2));
+  if (fresh < 0) fresh = 0;
+  r.set(O_A, (uint32_t)a >> 8); r.set(O_A + 1, (uint32_t)a);
+  r.set(O_S, (uint32_t)fresh >> 8); r.set(O_S + 1, (uint32_t)fresh);
+  r.set(O_U, (uint32_t)(w0 >> 48));
+  r.set(O_W, (uint32_t)(w0 >> 24)); r.set(O_W + 1, (uint32_t)(w0 >> 16));
+  r.set(O_P, (uint32_t)(w0 >> 40)); r.set(O_P + 1, (uint32_t)(w0 >> 32));
+  r.set(O_D, (uint32_t)(w1 >> 56));
+  r.set(O_L, (uint32_t)(w2 >> 16)); r.set(O_L + 1, (uint32_t)(w2 >> 24));
+  r.set(O_X, (uint32_t)(w1 >> 24)); r.set(O_Y, (uint32_t)(w1 >> 32));
+  r.set(O_M, (uint32_t)(w1 >> 40)); r.set(O_N, (uint32_t)(w1 >> 48));
+  r.set(O_G, 0);
+  for (int j = 0; j < 4; j++) r.set(O_Z + j, (uint32_t)(w2 >> (32 + 8 * j)));
+  r.set(O_C, (uint32_t)(w0 >> 56));
+  r.set(O_T, (uint32_t)(w0 >> 8)); r.set(O_T + 1, (uint32_t)w0);
+  r.set(O_R, (uint32_t)w1); r.set(O_O, (uint32_t)(w1 >> 8)); r.set(O_I, (uint32_t)(w1 >> 16));
+  r.set(O_K, 0);
+  store_row(rows + i * YRWI_ROW_BYTES, r);
+}
+
+// ================================================================ ranking
 
 __device__ __forceinline__ uint64_t host36(const Row& r) {
   uint64_t h = 0;
@@ -809,8 +910,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     av[s] = -1;
     uint32_t po = 0;
     if (v) {
-      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
-      const Feat F = decode(r);
+      const Feat F = decode_rec(load_rec(Q.feat, e));
 #pragma unroll
       for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], F.f[f]); mx[f] = max(mx[f], F.f[f]); }
       tfmn = fmin(tfmn, F.tf);
@@ -821,7 +921,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
       if (Q.want_authority) {
-        uint64_t key = host36(r) + 1;
+        uint64_t khi;
+        uint32_t klo;
+        key_at(Q, e, khi, klo);
+        uint64_t key = key_host36(khi, klo) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
           unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
@@ -1026,9 +1129,8 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
     bool ok = e < e1 && e > first && !(Q.removed && Q.removed[e]);
     int32_t p = -1, od = 0;
     if (ok) {
-      const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
-      p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
-      od = r[O_I];
+      p = (int32_t)(Q.feat[e * FEAT_WORDS] & 0xFFFF);
+      od = (int32_t)((Q.feat[e * FEAT_WORDS + 1] >> 16) & 0xFF);
     }
     if (__all(!ok || p <= L.prun)) {
       const int32_t m = wave_max_i(ok ? od : 0);
@@ -1255,9 +1357,8 @@ __global__ void k_combine(const RankQ* __restrict__ qs, int nq, const ShardSum* 
       bool first = true;
       for (int64_t e = 0; e < Q.n; e++) {
         if (Q.removed && Q.removed[e]) continue;
-        const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
-        int32_t p = ((int32_t)r[O_T] << 8) | r[O_T + 1];
-        int32_t od = r[O_I];
+        int32_t p = (int32_t)(Q.feat[e * FEAT_WORDS] & 0xFFFF);
+        int32_t od = (int32_t)((Q.feat[e * FEAT_WORDS + 1] >> 16) & 0xFF);
         if (first) { fd.P = p; first = false; }
         else fd.piece(p, od, od);
       }
@@ -1297,8 +1398,7 @@ __device__ __forceinline__ int32_t qdiv(int32_t n, double r) {
 }
 
 // ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265), settled min/max.
-__device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const NormState& N, const RankQ& Q,
-                                            int32_t hcount) {
+__device__ __forceinline__ int64_t cardinal(const Feat& t, const NormState& N, const RankQ& Q, int32_t hcount) {
   const yrwi_profile& rk = Q.prof;
   int32_t tfterm = 0;
   if (!(N.tf_mx == N.tf_mn))
@@ -1311,7 +1411,7 @@ __device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const N
     if (hi == lo) return 0;
     return shl32(qdiv(shl32(sub32(tv, lo), 8), rc), c);
   };
-  const int dl = ahpla(r.b(11)) & 3;  // DigestURL.domLengthEstimation; << (8/20) == << 0
+  const int dl = t.dl;  // DigestURL.domLengthEstimation; << (8/20) == << 0
   const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
   int32_t s = shl32(256 - dln, rk.coeff_domlength);
   s = add32(s, inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], N.rcp[F_URLCOMPS], rk.coeff_urlcomps));
@@ -1337,7 +1437,7 @@ __device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const N
     int32_t auth = div32(shl32(hcount, 8), add32(1, N.maxdom));  // ReferenceOrder.authority :213-216
     R = add64(R, (int64_t)shl32(auth, rk.coeff_authority));
   }
-  const uint32_t z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24);
+  const uint32_t z = t.z;
   const int32_t c255 = 255;
   if (z & (1u << 28)) R = add64(R, shl32(c255, rk.coeff_appurl));
   if (z & (1u << 25)) R = add64(R, shl32(c255, rk.coeff_app_dc_title));
@@ -1350,7 +1450,7 @@ __device__ __forceinline__ int64_t cardinal(const Row& r, const Feat& t, const N
   if (z & (1u << 21)) R = add64(R, shl32(c255, rk.coeff_cathasaudio));
   if (z & (1u << 22)) R = add64(R, shl32(c255, rk.coeff_cathasvideo));
   if (z & (1u << 23)) R = add64(R, shl32(c255, rk.coeff_cathasapp));
-  if (Q.lang_ok && r.b(O_L) == Q.lang[0] && r.b(O_L + 1) == Q.lang[1]) R = add64(R, shl32(c255, rk.coeff_language));
+  if (Q.lang_ok && t.lang == ((uint32_t)Q.lang[0] | ((uint32_t)Q.lang[1] << 8))) R = add64(R, shl32(c255, rk.coeff_language));
   return R;
 }
 
@@ -1361,8 +1461,8 @@ __device__ __forceinline__ int32_t url_hashcode(const Row& r) {
   return h;
 }
 
-__device__ __forceinline__ int32_t host_count(const RankQ& Q, const Row& r) {
-  uint64_t key = host36(r) + 1;
+__device__ __forceinline__ int32_t host_count(const RankQ& Q, uint64_t host) {
+  uint64_t key = host + 1;
   uint64_t slot = mix64(key) & Q.hmask;
   while (true) {
     uint64_t k = Q.hkeys[slot];
@@ -1489,16 +1589,14 @@ __device__ __forceinline__ bool sorted_has_u64(const uint64_t* __restrict__ a, i
   return lo < n && a[lo] == x;
 }
 
-__device__ __forceinline__ bool flag_bit(const Row& r, int j) { return (r.b(O_Z + (j >> 3)) >> (j & 7)) & 1u; }
+__device__ __forceinline__ bool flag_bit(uint32_t z, int j) { return (z >> j) & 1u; }  // Bitfield.get :88-93
 
-__device__ __forceinline__ bool passes(const FilterQ& F, const Row& r);
+__device__ __forceinline__ bool passes(const FilterQ& F, const Feat& t, uint64_t host);
 
 // returns true if the posting enters the stack; counts flags into sFlag (LDS) when asked
-__device__ __forceinline__ bool admit(const FilterQ& F, const Row& r, int32_t* sFlag) {
+// (hi, lo: the posting's url-hash key)
+__device__ __forceinline__ bool admit(const FilterQ& F, const Feat& t, uint64_t hi, uint32_t lo, int32_t* sFlag) {
   if (F.nurl) {  // doublecheck: url already in SearchEvent.urlhashes
-    uint64_t hi;
-    uint32_t lo;
-    row_key(r, hi, lo);
     int64_t a = 0, b = F.nurl;
     while (a < b) {
       const int64_t m = (a + b) >> 1;
@@ -1507,43 +1605,42 @@ __device__ __forceinline__ bool admit(const FilterQ& F, const Row& r, int32_t* s
     }
     if (a < F.nurl && F.url_hi[a] == hi && (uint32_t)F.url_lo[a] == lo) return false;
   }
-  if (sFlag) {
-    const uint32_t z = (r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | (r.b(O_Z + 3) << 24));
-    for (uint32_t m = z; m; m &= m - 1) atomicAdd(&sFlag[__ffs(m) - 1], 1);
-  }
-  return passes(F, r);
+  if (sFlag)
+    for (uint32_t m = t.z; m; m &= m - 1) atomicAdd(&sFlag[__ffs(m) - 1], 1);
+  return passes(F, t, key_host36(hi, lo));
 }
 
-// the constraints after the doublecheck and the flag counts (:749-802)
-__device__ __forceinline__ bool passes(const FilterQ& F, const Row& r) {
+// the constraints after the doublecheck and the flag counts (:749-802); host =
+// the posting's host hash (url-hash chars 6..11 as 36 bits)
+__device__ __forceinline__ bool passes(const FilterQ& F, const Feat& t, uint64_t host) {
+  const uint32_t z = t.z;
   if (F.has_constraint) {
     bool ok = F.all_of ? true : false;
     for (int j = 0; j < 32; j++) {
       const bool c = (F.constraint[j >> 3] >> (j & 7)) & 1u;
       if (!c) continue;
-      if (F.all_of) { if (!flag_bit(r, j)) { ok = false; break; } }
-      else if (flag_bit(r, j)) { ok = true; break; }
+      if (F.all_of) { if (!flag_bit(z, j)) { ok = false; break; } }
+      else if (flag_bit(z, j)) { ok = true; break; }
     }
     if (!ok) return false;
   }
   if (F.contentdom > 0) {
-    const uint32_t t = r.b(O_D);
+    const uint32_t d = t.d;
     bool bad;
     if (F.strict)
-      bad = (F.contentdom == 2 && t != 'a') || (F.contentdom == 3 && t != 'm') || (F.contentdom == 1 && t != 'i') ||
-            (F.contentdom == 4 && !flag_bit(r, 23));
+      bad = (F.contentdom == 2 && d != 'a') || (F.contentdom == 3 && d != 'm') || (F.contentdom == 1 && d != 'i') ||
+            (F.contentdom == 4 && !flag_bit(z, 23));
     else
-      bad = (F.contentdom == 2 && !flag_bit(r, 21)) || (F.contentdom == 3 && !flag_bit(r, 22)) ||
-            (F.contentdom == 1 && !flag_bit(r, 20)) || (F.contentdom == 4 && !flag_bit(r, 23));
+      bad = (F.contentdom == 2 && !flag_bit(z, 21)) || (F.contentdom == 3 && !flag_bit(z, 22)) ||
+            (F.contentdom == 1 && !flag_bit(z, 20)) || (F.contentdom == 4 && !flag_bit(z, 23));
     if (bad) return false;
   }
   if (F.lang_len > 0) {  // modifier.language.equals(getLanguageString()): a 2-char string
-    if (F.lang_len != 2 || r.b(O_L) != F.lang[0] || r.b(O_L + 1) != F.lang[1]) return false;
+    if (F.lang_len != 2 || (t.lang & 0xFFu) != F.lang[0] || (t.lang >> 8) != F.lang[1]) return false;
   }
-  const uint64_t h = host36(r);
   if (!F.has_site) {
-    if (F.nsiteex && sorted_has_u64(F.siteex, F.nsiteex, h)) return false;
-  } else if (h != F.site && (!F.has_alt || h != F.altsite)) {
+    if (F.nsiteex && sorted_has_u64(F.siteex, F.nsiteex, host)) return false;
+  } else if (host != F.site && (!F.has_alt || host != F.altsite)) {
     return false;
   }
   return true;
@@ -1575,13 +1672,16 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
     a[s] = 0;
     if (z) z[s] = 0;
     if (e < Q.n && !(Q.removed && Q.removed[e])) {
-      const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
-      if (F && !admit(*F, r, flagc)) continue;
+      const Rec q = load_rec(Q.feat, e);
+      const Feat t = decode_rec(q);
+      uint64_t khi = 0;
+      uint32_t klo = 0;
+      if (F || Q.want_authority) key_at(Q, e, khi, klo);
+      if (F && !admit(*F, t, khi, klo, flagc)) continue;
       if (!SCORE) continue;
-      const Feat t = decode(r);
-      const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
-      a[s] = (uint64_t)cardinal(r, t, N, Q, hc) ^ 0x8000000000000000ull;
-      if (z) z[s] = ((uint64_t)((uint32_t)url_hashcode(r) ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+      const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
+      a[s] = (uint64_t)cardinal(t, N, Q, hc) ^ 0x8000000000000000ull;
+      if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       vm |= 1u << s;
     }
   }
@@ -1691,14 +1791,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   for (int s = 0; s < CHUNK_IPT; s++)
     if (((vm >> s) & 1u) && a[s] >= T) {
       const int64_t e = e0 + s * CHUNK_THREADS;
-      const uint8_t* r = Q.rows + e * YRWI_ROW_BYTES;
-      const uint64_t h0 = *reinterpret_cast<const uint64_t*>(r);
-      const uint32_t h1 = *reinterpret_cast<const uint32_t*>(r + 8);
-      int32_t h = 0;  // ByteArray.hashCode (ByteArray.java:80-84)
-#pragma unroll
-      for (int j = 0; j < 8; j++) h = add32(mul32(31, h), (int32_t)((h0 >> (8 * j)) & 0xFF));
-#pragma unroll
-      for (int j = 0; j < 4; j++) h = add32(mul32(31, h), (int32_t)((h1 >> (8 * j)) & 0xFF));
+      const uint32_t h = (uint32_t)Q.feat[e * FEAT_WORDS + 3];  // ByteArray.hashCode (ByteArray.java:80-84)
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       off++;
@@ -1978,9 +2071,11 @@ __global__ void k_emit(const RankQ* __restrict__ qs, int nq, const Cand* const* 
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const Cand cd = f[i];
     const uint32_t idx = ~(uint32_t)cd.k2 & 0x0FFFFFFFu;
-    const uint8_t* r = Q.rows + (int64_t)idx * YRWI_ROW_BYTES;
+    uint64_t khi;
+    uint32_t klo;
+    key_at(Q, idx, khi, klo);
     yrwi_hit h;
-    for (int j = 0; j < 12; j++) h.urlhash[j] = r[j];
+    key_chars(khi, klo, h.urlhash);
     h.tiebreak = (int32_t)((uint32_t)(cd.k2 >> 32) ^ 0x80000000u);
     h.score = (int64_t)(cd.k1 ^ 0x8000000000000000ull);
     hits[(int64_t)qi * kmax + i] = h;
@@ -2149,10 +2244,15 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
   for (int s = threadIdx.x; s < CHUNK; s += blockDim.x) {
     const int64_t e = c * CHUNK + s;
     if (e >= Q.n) break;
-    const Row r = load_row(Q.rows + e * YRWI_ROW_BYTES);
-    const Feat t = decode(r);
-    const int32_t hc = Q.want_authority ? host_count(Q, r) : 0;
-    out[e] = cardinal(r, t, N, Q, hc);
+    const Feat t = decode_rec(load_rec(Q.feat, e));
+    int32_t hc = 0;
+    if (Q.want_authority) {
+      uint64_t khi;
+      uint32_t klo;
+      key_at(Q, e, khi, klo);
+      hc = host_count(Q, key_host36(khi, klo));
+    }
+    out[e] = cardinal(t, N, Q, hc);
   }
 }
 
@@ -2241,6 +2341,20 @@ static inline int rc(hipError_t e) { return e == hipSuccess ? 0 : YRWI_E_HIP; }
 int launch_validate_rows(const uint8_t* rows, int64_t n, uint64_t* khi, uint8_t* klo, int32_t* err, void* st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_validate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), rows, n, khi, klo, err);
+  return rc(hipGetLastError());
+}
+
+int launch_features(const uint8_t* rows, int64_t n, uint64_t* feat, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_features, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), rows, n, feat);
+  return rc(hipGetLastError());
+}
+
+int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* dkhi, const uint8_t* dklo, int64_t n,
+                     int64_t now_ms, uint8_t* rows, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_feat_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), feat, uid, dkhi, dklo, n,
+                     now_ms, rows);
   return rc(hipGetLastError());
 }
 
@@ -2742,7 +2856,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_event_add(const EvDev* __restric
       int ovf = 0;
       for (int64_t i = tid; i < n; i += EV_THREADS) {
         const Row R = load_row(rows + i * YRWI_ROW_BYTES);
-        if (E.has_filter && !passes(E.f, R)) continue;
+        if (E.has_filter && !passes(E.f, decode(R), host36(R))) continue;
         uint64_t hi;
         uint32_t lo;
         row_key(R, hi, lo);
@@ -2781,12 +2895,12 @@ __global__ __launch_bounds__(EV_THREADS) void k_event_add(const EvDev* __restric
         const uint32_t fi = found ? (uint32_t)v : 0xFFFFFFFFu;
         if (!found || (uint32_t)i <= fi) {  // reaches the flag count (later duplicates hit the doublecheck)
           const uint32_t z = (R.b(O_Z) | (R.b(O_Z + 1) << 8) | (R.b(O_Z + 2) << 16) | (R.b(O_Z + 3) << 24));
-          for (uint32_t mm = z; mm; mm &= mm - 1) atomicAdd(&sFlag[__ffs(mm) - 1], 1);
+          for (uint32_t mm = z; mm; mm &= mm - 1) atomicAdd(&sFlag[__ffs(mm) - 1], 1);  // (flagcount :743-746)
         }
         if (found && (uint32_t)i == fi) {
           const Feat t = decode(R);
           const int32_t hc = Q.want_authority ? htab_count(Q.hkeys, Q.hcnt, Q.hmask, host36(R) + 1) : 0;
-          const int64_t sc = cardinal(R, t, N, Q, hc);
+          const int64_t sc = cardinal(t, N, Q, hc);
           const int slot = atomicAdd(&sMisc[1], 1);
           sK1[slot] = (uint64_t)sc ^ 0x8000000000000000ull;
           sK2[slot] = ((uint64_t)((uint32_t)url_hashcode(R) ^ 0x80000000u) << 32) | (uint64_t)(~(uint32_t)i);
