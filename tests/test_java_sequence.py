@@ -1,0 +1,62 @@
+"""The Java drop-in's call sequence, replayed through the C ABI (ctypes).
+
+java/net/yacy/kelondro/rwi/GpuTermSearch.java and
+java/net/yacy/search/ranking/GpuReferenceOrder.java cannot be compiled here (no
+JDK); this test makes exactly the libyrwi calls they make for one SearchEvent:
+
+  TermSearch  -> GpuTermSearch.joinExclude  -> yrwi_join_exclude (joined rows)
+  addRWIs     -> GpuReferenceOrder.normalizeWith -> yrwi_normalize_score (one
+                 settled score per row), then cardinal(e) = that score, fed in
+                 container order into rwiStack (WeakPriorityBlockingQueue order)
+
+and checks that the stack equals both the whole-query path (yrwi_query) and the
+oracle (SearchEvent.java:697-816, ReferenceOrder.java:70,223)."""
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from yacy_search_server_amd import RankingProfile, RWIIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+NOW = 20741 * 86400000 + 4242
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    cfg = synth.preset("small")
+    idx = synth.build_index(cfg)
+    ix = RWIIndex(0)
+    for t in range(cfg.n_terms):
+        if idx.sizes[t]:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+    yield cfg, idx, ix
+    ix.close()
+
+
+@pytest.mark.parametrize("profile", ["default", "c5", "date"])
+def test_termsearch_then_reference_order(corpus, profile):
+    cfg, idx, ix = corpus
+    prof = {"default": RankingProfile(), "c5": RankingProfile("", "date=15,domlength=15,authority=13,tf=10"),
+            "date": RankingProfile.date()}[profile]
+    whole = idx.as_dict()
+    n = 0
+    for inc, exc in synth.queries(cfg, 24, 1, 3, 1, qseed=123):
+        ih = [idx.hashes[t] for t in inc]
+        eh = [idx.hashes[t] for t in exc]
+        rows = ix.term_search(ih, eh, now_ms=NOW)                     # GpuTermSearch.joinExclude
+        assert np.array_equal(rows, orc.term_search(whole, ih, eh, 2147483647, NOW))
+        if len(rows) == 0:
+            continue
+        n += 1
+        scores = ix.normalize_score(rows, prof, "en", NOW)            # GpuReferenceOrder.normalizeWith
+        card = {bytes(r[:12]): int(s) for r, s in zip(rows, scores)}  # GpuReferenceOrder.cardinal
+        ordered = np.array([card[bytes(r[:12])] for r in rows], dtype=np.int64)  # addRWIs pollloop order
+        stack = orc.topk(rows, ordered, 100)                          # rwiStack (WeakPriorityBlockingQueue)
+        exp_scores, _ = orc.normalize_score(rows, orc.profile_from(prof), "en", NOW)
+        assert np.array_equal(scores, exp_scores)
+        assert stack == orc.search(whole, ih, eh, profile=orc.profile_from(prof), now_ms=NOW, k=100)
+        got = ix.search(ih, eh, profile=prof, now_ms=NOW, k=100)    # the whole-query path
+        assert [(h.urlhash, h.score, h.tiebreak) for h in got] == stack
+    assert n > 0
