@@ -512,7 +512,8 @@ def run_leg(R, leg, args, rank, world):
         else:
             qs = synth.queries(full, 4096, 2, 4, 0, qseed=full.seed ^ 0xC4)
         hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
-        M = R.measure(qs, hashes, RankingProfile(), len(qs), 100, args.leg_steps, 1, args.inflight, isolated=True)
+        M = R.measure(qs, hashes, RankingProfile(), len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
+                      isolated=True)
         res[leg] = _leg_line(M, leg, len(qs), world, "strong")
     elif leg == "C5":
         full = synth.preset("C5")
@@ -525,7 +526,8 @@ def run_leg(R, leg, args, rank, world):
         custom = RankingProfile()
         custom.coeff_date, custom.coeff_domlength, custom.coeff_authority, custom.coeff_termfrequency = 15, 15, 13, 10
         for name, prof in (("C5_custom", custom), ("C5_date", RankingProfile.date())):
-            M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 1, args.inflight, isolated=True)
+            M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
+                          isolated=True)
             res[name] = _leg_line(M, "C5", len(qs), world, "weak")
         R.close()
     else:

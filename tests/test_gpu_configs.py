@@ -1,0 +1,193 @@
+"""BASELINE configurations and size-edge cases through the HIP path, checked
+against the oracle (bit-exact: url hashes, order, scores, tie-breaks).
+
+  C2  the full 100M-posting index, 64 of the bench's 2-term AND queries
+  C3  the per-GPU url-hash shard (1 of 8) of the 1B corpus, 3-term AND + 1 exclude
+  C4  one batch of 4096 concurrent 2-4 term queries over that shard; 64 checked
+  C5  the custom (authority) and /date profiles on the per-GPU shard of the 5B corpus
+  J2/J3 int wrap: list sizes whose (int)(size*1000 + i) fold keys and
+      12*log2(high)*low dispatch counts wrap (ReferenceContainer.java:334-366,406-416)
+  k_probe ranges of 0, 1, 4095, 4096 and 4097 large-list ids around the
+      LDS-staging threshold (PROBE_LDS), with and without exclusion
+
+The C3 / C4 / C5 cases generate only the lists of the query terms -- exactly as
+the full corpus holds them (the generator is per term); the other
+lists cannot change a result."""
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from yacy_search_server_amd import Query, RankingProfile, RWIIndex, synth
+
+pytestmark = pytest.mark.gpu
+
+NOW = 20741 * 86400000 + 777
+
+
+def _load(idx, terms=None):
+    ix = RWIIndex(0)
+    for t in (range(len(idx.hashes)) if terms is None else terms):
+        if idx.sizes[t]:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+    return ix
+
+
+def _check(ix, idx, qs, prof=None, k=100, sample=None):
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW, k=k, profile=prof)
+             for inc, exc in qs]
+    got = ix.search_batch(batch)
+    oprof = orc.profile_from(prof) if prof is not None else None
+    for qi in (range(len(qs)) if sample is None else sample):
+        inc, exc = qs[qi]
+        d = {idx.hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
+        exp = orc.search(d, batch[qi].include, batch[qi].exclude, profile=oprof, now_ms=NOW, k=k)
+        assert [(h.urlhash, h.score, h.tiebreak) for h in got[qi]] == exp, qi
+    return got
+
+
+def test_c2_full_index_64_queries():
+    cfg = synth.preset("C2")
+    idx = synth.build_index(cfg)
+    ix = _load(idx)
+    try:
+        _check(ix, idx, synth.queries(cfg, 64, 2, 2, 0))  # the bench's first 64 queries
+    finally:
+        ix.close()
+
+
+@pytest.fixture(scope="module")
+def c3_shard():
+    full = synth.preset("C3")
+    cfg = full.shard(0, 8)
+    q3 = synth.queries(full, 32, 3, 3, 1)
+    q4 = synth.queries(full, 4096, 2, 4, 0, qseed=full.seed ^ 0xC4)
+    terms = sorted({t for inc, exc in q3 + q4 for t in inc + exc})
+    idx = synth.build_index(cfg, terms=np.array(terms))
+    ix = _load(idx, terms)
+    yield idx, q3, q4, ix
+    ix.close()
+
+
+def test_c3_shard_three_terms_one_exclude(c3_shard):
+    idx, q3, _, ix = c3_shard
+    _check(ix, idx, q3)
+
+
+def test_c4_batch_4096_queries(c3_shard):
+    idx, _, q4, ix = c3_shard
+    rng = np.random.default_rng(4)
+    _check(ix, idx, q4, sample=sorted(rng.choice(len(q4), 64, replace=False).tolist()))
+
+
+def test_c5_profiles_on_shard():
+    full = synth.preset("C5")
+    cfg = full.shard(0, 8)
+    qs = synth.queries(full, 24, 2, 4, 0)
+    terms = sorted({t for inc, exc in qs for t in inc + exc})
+    idx = synth.build_index(cfg, terms=np.array(terms))
+    ix = _load(idx, terms)
+    try:
+        custom = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+        _check(ix, idx, qs, prof=custom)
+        _check(ix, idx, qs, prof=RankingProfile.date())
+    finally:
+        ix.close()
+
+
+# ---------------------------------------------------------------- size edges
+_B64 = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_", dtype=np.uint8)
+
+
+def keyed_rows(keys, seed):
+    """Valid sorted 40-B rows with url-hash keys (key << 20 | 7) (vectorised)."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    k72 = (keys << np.uint64(20)) | np.uint64(7)
+    n = len(keys)
+    rng = np.random.default_rng(seed)
+    rows = np.zeros((n, 40), dtype=np.uint8)
+    for j in range(12):
+        sh = 6 * (11 - j)
+        rows[:, j] = _B64[((k72 >> np.uint64(sh)) & np.uint64(63)).astype(np.int64)] if sh < 64 else _B64[0]
+    rows[:, 12:14] = np.frombuffer((15000).to_bytes(2, "big"), dtype=np.uint8)
+    rows[:, 16] = rng.integers(0, 20, n)
+    w = rng.integers(20, 4000, n)
+    rows[:, 17], rows[:, 18] = (w >> 8) & 0xFF, w & 0xFF
+    rows[:, 20] = rng.integers(1, 60, n)
+    rows[:, 21] = ord("t")
+    rows[:, 22:24] = np.frombuffer(b"en", dtype=np.uint8)
+    rows[:, 24] = rng.integers(0, 30, n)
+    rows[:, 26] = rng.integers(16, 200, n)
+    rows[:, 27] = rng.integers(1, 15, n)
+    rows[:, 32] = rng.integers(0, 4, n) << 4
+    p = rng.integers(1, 3000, n)
+    rows[:, 34], rows[:, 35] = (p >> 8) & 0xFF, p & 0xFF
+    rows[:, 33] = rng.integers(1, 20, n)
+    rows[:, 36] = rng.integers(1, 40, n)
+    rows[:, 37] = rng.integers(100, 255, n)
+    rows[:, 38] = rng.integers(0, 40, n)
+    return rows
+
+
+def _run_pair(d, queries, k=100):
+    ix = RWIIndex(0)
+    try:
+        for h, r in d.items():
+            ix.add(h, r)
+        for inc, exc in queries:
+            assert np.array_equal(ix.term_search(inc, exc, 2147483647, NOW),
+                                  orc.term_search(d, inc, exc, 2147483647, NOW)), (inc, exc)
+            got = [(h.urlhash, h.score, h.tiebreak) for h in ix.search(inc, exc, now_ms=NOW, k=k)]
+            assert got == orc.search(d, inc, exc, now_ms=NOW, k=k), (inc, exc)
+    finally:
+        ix.close()
+
+
+def test_j2_fold_order_int_wrap():
+    """Sizes >= 2,147,484: (int)(size*1000 + i) wraps negative, so the two big lists
+    fold first (A then B) and the 50k list last -- not smallest first."""
+    rng = np.random.default_rng(11)
+    univ = np.arange(6_000_000)
+    a = np.sort(rng.choice(univ, 2_200_000, replace=False))
+    b = np.sort(rng.choice(univ, 2_500_000, replace=False))
+    c = np.sort(rng.choice(univ, 50_000, replace=False))
+    d = {b"WRAPlistA___": keyed_rows(a, 1), b"WRAPlistB___": keyed_rows(b, 2), b"WRAPlistC___": keyed_rows(c, 3)}
+    assert orc.fold_order([len(d[h]) for h in sorted(d)]) == [0, 1, 2]  # A, B, C: the wrapped order
+    _run_pair(d, [([b"WRAPlistA___", b"WRAPlistB___", b"WRAPlistC___"], []),
+                  ([b"WRAPlistA___", b"WRAPlistB___"], [b"WRAPlistC___"])])
+
+
+def test_j3_dispatch_int_wrap():
+    """high 8,000,000 (23 bits), low 7,900,000: 12*23*low wraps negative, so the
+    reference joins by test (self-join of the large list's rows), not by enumeration."""
+    rng = np.random.default_rng(12)
+    univ = np.arange(12_000_000)
+    a = np.sort(rng.choice(univ, 8_000_000, replace=False))
+    b = np.sort(rng.choice(univ, 7_900_000, replace=False))
+    assert orc.join_dispatch(len(a), len(b))[0]  # by test
+    d = {b"DISPlistA___": keyed_rows(a, 4), b"DISPlistB___": keyed_rows(b, 5)}
+    _run_pair(d, [([b"DISPlistA___", b"DISPlistB___"], [])], k=300)
+
+
+@pytest.mark.parametrize("R", [0, 1, 4095, 4096, 4097])
+def test_probe_range_around_lds_threshold(R, monkeypatch):
+    """One probe tile (256 small-list ids) whose large-list range holds R ids
+    (YRWI_PROBE_RATIO=1 forces probing): R <= 4096 is searched in LDS, 4097 by
+    gathers; R = 0: no small id falls inside the large list."""
+    monkeypatch.setenv("YRWI_PROBE_RATIO", "1")
+    large = np.arange(100_000, 100_000 + 20_000, dtype=np.int64) * 4
+    if R == 0:
+        small = np.arange(256, dtype=np.int64) * 4 + 1          # below the large list, no match
+    else:
+        lo = 1000
+        span = large[lo:lo + R]
+        pick = np.unique(np.concatenate([[0, R - 1], np.linspace(0, R - 1, 256).astype(np.int64)]))
+        small = np.unique(np.concatenate([span[pick], span[pick][:-1] + 1]))[:256]  # hits and misses
+        small = np.sort(small)
+        assert small[0] == span[0] and (R == 1 or small[-1] <= span[-1])
+    excl = large[1000:1000 + 4096:7]
+    d = {b"PROBsmall___": keyed_rows(small, 6), b"PROBlarge___": keyed_rows(large, 7),
+         b"PROBexcl____": keyed_rows(excl, 8)}
+    _run_pair(d, [([b"PROBsmall___", b"PROBlarge___"], []),
+                  ([b"PROBsmall___", b"PROBlarge___"], [b"PROBexcl____"]),
+                  ([b"PROBlarge___"], [b"PROBsmall___"])], k=300)

@@ -621,22 +621,32 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) +=
           step_bytes(J.algo == JA_MERGE ? J.mode : (int32_t)JM_TEST_LARGE_A, J.A.n, J.B.n);
   int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
-  for (int j = 0; j < nj; j++) jobs[(size_t)j].m_out = d_mout + j;
+  // pair runs: a job matches at most min(nA, nB) postings (both sides strictly
+  // ascending); merge tiles bound theirs by min(na, nb + 1), at most one more per tile
+  int64_t npairs = 0;
+  for (int j = 0; j < nj; j++) {
+    JoinQ& J = jobs[(size_t)j];
+    J.m_out = d_mout + j;
+    J.pair_base = npairs;
+    npairs += std::min(J.A.n, J.B.n) + (J.algo == JA_MERGE ? J.ntiles : 0);
+  }
   JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
   int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
   TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
-  uint2* d_pairs = arena_alloc<uint2>(ctx, tiles * JOIN_MAXM);
-  uint32_t* d_puid = arena_alloc<uint32_t>(ctx, tiles * JOIN_MAXM);
+  uint2* d_pairs = arena_alloc<uint2>(ctx, npairs);
+  uint32_t* d_puid = arena_alloc<uint32_t>(ctx, npairs);
+  int64_t* d_src = arena_alloc<int64_t>(ctx, tiles);
   int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
   int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
-  if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_cnt || !d_off)
+  if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_src || !d_cnt || !d_off)
     return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
-  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_cnt, d_off, false,
+  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
+                       false,
                        ctx->stream, e0, em, e1, c0, c1))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
@@ -692,7 +702,8 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
   hipEvent_t sp = span_open(ctx, tm);
-  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr, true,
+  if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, true,
                        ctx->stream, nullptr, nullptr, nullptr))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
   span_close(ctx, tm, sp);
@@ -1165,10 +1176,10 @@ static int64_t now_ns() {
 // Plan and run queries q[0, nq) on lane L; results at out (row stride kmax).
 // Every field of *st is this part's own (the caller sums parts).
 // Upper bound of the arena bytes one query takes in a pass: per fold step the
-// tile pair slots (merge: JOIN_MAXM slots of 12 B per JOIN_TILE items, ~6 B per
-// posting; probe: per PROBE_TILE small-side items, ~48 B per posting) and the
-// joined (uid, row) container (<= the smallest list, 44 B per posting), then the
-// rank phase over that container (~72 B per posting).
+// join's tile descriptors (~1 B per 64 input postings), its matched pairs (12 B
+// each, at most the smaller side) and the joined container (url id + 32-byte
+// record: 36 B per row, at most the smallest list), then the rank phase over
+// that container (exclusion marks, chunk summaries, candidates: ~48 B per row).
 static int64_t scratch_estimate(const Plan& P) {
   if (P.empty || P.seq.empty()) return 4096;
   int64_t sum = 0, nmin = INT64_MAX;
@@ -1177,7 +1188,7 @@ static int64_t scratch_estimate(const Plan& P) {
     nmin = std::min(nmin, l->n);
   }
   for (const ListRec* l : P.excl) sum += l->n;
-  return 6 * sum + (92 * (int64_t)(P.seq.size() - 1) + 80) * nmin + 65536;
+  return sum / 64 + (48 * (int64_t)(P.seq.size() - 1) + 48) * nmin + 65536;
 }
 
 // Scratch budget of one pass (YRWI_SCRATCH_GB, default 32 GiB per lane).  A

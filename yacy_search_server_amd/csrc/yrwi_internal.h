@@ -15,7 +15,7 @@ namespace yrwi {
 constexpr int JOIN_TILE = YRWI_JOIN_TILE;  // merge-path items per join workgroup
 constexpr int JOIN_THREADS = 256;
 constexpr int JOIN_IPT = JOIN_TILE / JOIN_THREADS;
-constexpr int JOIN_MAXM = JOIN_TILE / 2 + 1;  // matches per tile <= min(#A, #B + 1)
+constexpr int JOIN_MAXM = JOIN_TILE / 2 + 1;  // matches per merge tile <= min(#A, #B + 1)
 
 constexpr int CHUNK = 2048;          // container elements per rank/score workgroup
 constexpr int CHUNK_THREADS = 256;
@@ -83,6 +83,10 @@ struct JoinQ {
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
   int64_t now_ms;
   int64_t* m_out;      // number of output rows (written by the scan kernel)
+  // matched pairs of the job: [pair_base, pair_base + cap) of the step's pair
+  // arrays; every tile writes its run at tile_src[tile] (merge tiles: the prefix
+  // of their bounds min(na, nb + 1); probe tiles: PROBE_TILE per tile)
+  int64_t pair_base;
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
@@ -226,7 +230,7 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
-                     uint2* d_pairs, uint32_t* d_pair_uid,
+                     uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

@@ -307,7 +307,7 @@ __device__ __forceinline__ uint64_t key_host36(uint64_t hi, uint32_t lo) {
 // One thread per merge tile: the merge-path split of the tile's first and last
 // diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
 __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                            int64_t total_tiles, TileDesc* __restrict__ desc) {
+                            int64_t total_tiles, TileDesc* __restrict__ desc, int64_t* __restrict__ tile_src) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total_tiles) return;
   const int j = find_job(tile_base, njobs, b);
@@ -341,6 +341,7 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   D.maxd = J.maxd;
   D.pad = 0;
   desc[b] = D;
+  if (tile_src) tile_src[b] = min(D.na, D.nbl);  // matches of the tile <= min(#A, #B + lookahead); k_scan_bounds: its run
 }
 
 // joined worddistance (WordReferenceVars.distance :287-294 after join :465-499)
@@ -394,28 +395,36 @@ __device__ __forceinline__ void tile_load(const TileDesc& D, TileKeys& K) {
 __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__ jobs,
                                                       const TileDesc* __restrict__ desc, int64_t ntiles,
                                                       uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
-                                                      int32_t* __restrict__ tile_cnt, int mark) {
+                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
+                                                      int mark) {
   __shared__ uint32_t sK[JOIN_SLOTS * JOIN_THREADS];
   __shared__ int32_t sScan[4];
 
   // Tile descriptors travel through VGPRs (lane i holds dword i, read with
   // v_readlane when due): a scalar load would share lgkmcnt with LDS traffic and
   // every LDS wait of the merge would also wait for the next descriptor.
+  // lanes TILEDESC_DWORDS and +1 carry the tile's pair run (tile_src)
   const int lane = threadIdx.x & 63;
   auto desc_fetch = [&](int64_t t) -> uint32_t {
-    return (t < ntiles && lane < TILEDESC_DWORDS) ? ((const gu32c*)(desc + t))[lane] : 0u;
+    if (t >= ntiles) return 0u;
+    if (lane < TILEDESC_DWORDS) return ((const gu32c*)(desc + t))[lane];
+    if (!mark && lane < TILEDESC_DWORDS + 2) return ((const gu32c*)(tile_src + t))[lane - TILEDESC_DWORDS];
+    return 0u;
   };
-  auto desc_get = [&](uint32_t v) -> TileDesc {
+  auto desc_get = [&](uint32_t v, int64_t& src) -> TileDesc {
     TileDesc D;
     uint32_t* w = reinterpret_cast<uint32_t*>(&D);
 #pragma unroll
     for (int i = 0; i < TILEDESC_DWORDS; i++) w[i] = __builtin_amdgcn_readlane(v, i);
+    src = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, TILEDESC_DWORDS + 1) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane(v, TILEDESC_DWORDS));
     return D;
   };
   const int64_t G = gridDim.x;
   int64_t b = blockIdx.x;
   if (b >= ntiles) return;
-  TileDesc Dc = desc_get(desc_fetch(b));
+  int64_t srcc;
+  TileDesc Dc = desc_get(desc_fetch(b), srcc);
   uint32_t dnext = desc_fetch(b + G);
   TileKeys K;
   tile_load(Dc, K);
@@ -427,8 +436,9 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
     // prefetch: ids of the next tile, descriptor of the one after
     const int64_t a0 = Dc.a0, b0 = Dc.b0;
     const int jc = Dc.job, maxd = Dc.maxd;
+    const int64_t src = srcc;
     if (b + G < ntiles) {
-      Dc = desc_get(dnext);
+      Dc = desc_get(dnext, srcc);
       dnext = desc_fetch(b + 2 * G);
       tile_load(Dc, K);
     }
@@ -480,8 +490,9 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
     if (!mark) {
       int32_t tot;
       int32_t off = block_excl_sum256(__popc(mbits), sScan, &tot);
-      uint2* out = pairs + b * (int64_t)JOIN_MAXM;
-      uint32_t* outu = pair_uid + b * (int64_t)JOIN_MAXM;
+      if (threadIdx.x == 0) tile_cnt[b] = tot;
+      uint2* out = pairs + src;
+      uint32_t* outu = pair_uid + src;
       for (uint32_t m = mbits; m; m &= m - 1) {
         const int st = __ffs(m) - 1;
         const int ai = a_at(st);
@@ -489,7 +500,6 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
         outu[off] = sK[ai];
         off++;
       }
-      if (threadIdx.x == 0) tile_cnt[b] = tot;
     }
     __syncthreads();  // LDS is rewritten for the next tile
   }
@@ -551,7 +561,8 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
-                                                     int32_t* __restrict__ tile_cnt, int mark) {
+                                                     int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
+                                                     int mark) {
   __shared__ int32_t sScan[4];
 #if PROBE_LDS > 0
   __shared__ uint32_t sL[PROBE_LDS];
@@ -603,11 +614,15 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   }
   int32_t tot;
   const int32_t off = block_excl_sum256(hit ? 1 : 0, sScan, &tot);
-  if (hit) {
-    pairs[b * (int64_t)JOIN_MAXM + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
-    pair_uid[b * (int64_t)JOIN_MAXM + off] = key;
+  const int64_t src = J.pair_base + s0;  // PROBE_TILE pair slots per tile: the job's run is min(nA, nB) long
+  if (threadIdx.x == 0) {
+    tile_src[b] = src;
+    tile_cnt[b] = tot;
   }
-  if (threadIdx.x == 0) tile_cnt[b] = tot;
+  if (hit) {
+    pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
+    pair_uid[src + off] = key;
+  }
 }
 
 // ============================================================ join: scan
@@ -628,6 +643,25 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
     running += tot;
   }
   if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
+}
+
+// Merge jobs: tile_src[t] = the job's pair_base + the exclusive prefix of its
+// tiles' match bounds (k_partition), i.e. where each tile writes its pairs.
+__global__ __launch_bounds__(256) void k_scan_bounds(const JoinQ* __restrict__ jobs,
+                                                     const int64_t* __restrict__ tile_base,
+                                                     int64_t* __restrict__ tile_src) {
+  __shared__ int32_t sScan[4];
+  const JoinQ& J = jobs[blockIdx.x];
+  const int64_t base = tile_base[blockIdx.x];
+  int64_t running = J.pair_base;
+  for (int64_t t0 = 0; t0 < J.ntiles; t0 += 256) {
+    const int64_t t = t0 + threadIdx.x;
+    const int32_t c = t < J.ntiles ? (int32_t)tile_src[base + t] : 0;
+    int32_t tot;
+    const int32_t ex = block_excl_sum256(c, sScan, &tot);
+    if (t < J.ntiles) tile_src[base + t] = running + ex;
+    running += tot;
+  }
 }
 
 // ============================================================ join: compact
@@ -691,12 +725,14 @@ struct CompactJob {
   uint32_t* ouid;
   int64_t now_ms;
   int64_t off;
+  int64_t src;  // the tile's run in the pair arrays
   int32_t mode, pad;
 };
 
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
                                                  const uint32_t* __restrict__ pair_uid,
+                                                 const int64_t* __restrict__ tile_src,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
@@ -716,6 +752,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         X.ouid = J.out_uid;
         X.now_ms = J.now_ms;
         X.off = tile_off[t];
+        X.src = tile_src[t];
         X.mode = J.mode;
       }
     }
@@ -741,7 +778,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
           if (sPre[mid] <= m) lo = mid; else hi = mid - 1;
         }
         tl[u] = lo;
-        pi[u] = (t0 + lo) * (int64_t)JOIN_MAXM + (m - sPre[lo]);
+        pi[u] = sJ[lo].src + (m - sPre[lo]);
         pr[u] = pairs[pi[u]];
         uid[u] = pair_uid[pi[u]];
       }
@@ -2360,7 +2397,8 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
-                     uint2* d_pairs, uint32_t* d_pair_uid, int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark,
+                     uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
+                     int64_t* d_tile_off, bool mark,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1) {
   if (total_tiles <= 0) return 0;
@@ -2375,27 +2413,30 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     join_grid = std::max(1, cus * std::max(1, per_cu));
   }
   const int64_t probe_tiles = total_tiles - merge_tiles;
-  if (merge_tiles > 0)
+  if (merge_tiles > 0) {
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, nmerge, merge_tiles, d_desc);
+                       d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src);
+    if (!mark) hipLaunchKernelGGL(k_scan_bounds, dim3((unsigned)nmerge), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_src);
+  }
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc);
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
-                       S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_cnt, mark ? 1 : 0);
+                       S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_pair_uid, d_tile_cnt, mark ? 1 : 0);
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off);
     if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
-                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_cnt, d_tile_off);
+                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
+                       d_tile_off);
     if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
   }
   return rc(hipGetLastError());
