@@ -2,8 +2,10 @@
 
 profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
 profiles/pmc_<config>.json        per-kernel mean duration and HBM bytes per launch
-HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch: FETCH_SIZE on gfx950
-reports half of a wide coalesced stream (MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact.
+HBM bytes per dispatch = read requests leaving L2 by size (32 TCC_EA0_RDREQ_32B + 64
+TCC_EA0_RDREQ_64B + 128 TCC_EA0_RDREQ_128B) + write requests (64 TCC_EA0_WRREQ_64B + 32
+(TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B)); TCC_EA0_RDREQ_DRAM = the reads that reached DRAM
+(the rest were served by the Infinity Cache).
 """
 import csv
 import glob
@@ -53,16 +55,22 @@ def main(tag, config):
             out["kernels"][k]["calls"] = int(row["Calls"])
             out["kernels"][k]["avg_ns"] = float(row["AverageNs"])
             out["kernels"][k]["pct"] = float(row.get("Percentage", 0))
-    fetch, nf = counters(os.path.join(base, "fetch"))
-    write, nw = counters(os.path.join(base, "write"))
-    for k in set(fetch) | set(write):
+    rd, nr = counters(os.path.join(base, "rd"))
+    wr, nw = counters(os.path.join(base, "wr"))
+    for k in set(rd) | set(wr):
         d = out["kernels"].setdefault(k, {})
-        if k in fetch and nf.get(k):
-            d["fetch_kb_per_launch_raw"] = fetch[k]["FETCH_SIZE"] / nf[k]
-        if k in write and nw.get(k):
-            d["write_kb_per_launch"] = write[k]["WRITE_SIZE"] / nw[k]
-        if "fetch_kb_per_launch_raw" in d and "write_kb_per_launch" in d:
-            d["hbm_bytes_per_launch"] = (2 * d["fetch_kb_per_launch_raw"] + d["write_kb_per_launch"]) * 1024
+        if k in rd and nr.get(k):
+            c = rd[k]
+            rb = 32 * c.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) + \
+                128 * c.get("TCC_EA0_RDREQ_128B_sum", 0)
+            d["read_bytes_per_launch"] = rb / nr[k]
+            d["read_requests_dram_per_launch"] = c.get("TCC_EA0_RDREQ_DRAM_sum", 0) / nr[k]
+        if k in wr and nw.get(k):
+            c = wr[k]
+            w64 = c.get("TCC_EA0_WRREQ_64B_sum", 0)
+            d["write_bytes_per_launch"] = (64 * w64 + 32 * (c.get("TCC_EA0_WRREQ_sum", 0) - w64)) / nw[k]
+        if "read_bytes_per_launch" in d and "write_bytes_per_launch" in d:
+            d["hbm_bytes_per_launch"] = d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
     # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
     # (k_combine runs once per batch pass); index build, uploads and fills excluded
     path = ("k_partition", "k_probe_part", "k_join", "k_probe", "k_scan_tiles", "k_compact", "k_reduce",
@@ -85,7 +93,7 @@ def main(tag, config):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
         out[name + "_avg_ns"] = kd.get("avg_ns")
-    for log in ("kt.log", "fetch.log", "write.log"):
+    for log in ("kt.log", "rd.log", "wr.log"):
         p = os.path.join(base, log)
         if os.path.exists(p):
             for line in open(p):

@@ -1,11 +1,14 @@
 #!/bin/bash
 # Profile bench.py on the GPU box with rocprofv3 (run through gpurun from the repo root).
-#   pass 1: --kernel-trace --stats          -> per-kernel durations
-#   pass 2: --pmc FETCH_SIZE  (own pass)    -> HBM read bytes (x2 on gfx950, MI355X_MICROARCH.md §HBM)
-#   pass 3: --pmc WRITE_SIZE  (own pass)    -> HBM write bytes
-# Outputs under gpurun_out/prof/<tag>/ ; tools/pmc_summary.py turns them into profiles/*.
+#   pass 1: --kernel-trace --stats                              -> per-kernel durations
+#   pass 2: --pmc TCC_EA0_RDREQ_{32B,64B,128B}_sum + _DRAM_sum    -> read requests leaving L2, by size
+#   pass 3: --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum         -> write requests (64 B, the rest 32 B)
+# Each counter pass is its own run (MI355X_MICROARCH.md, HBM / rocprofv3).  Request
+# sizes are counted exactly, so no FETCH_SIZE correction is needed: on this path the
+# reads are 128-B requests (gathers and streams alike).  Outputs under
+# gpurun_out/prof/<tag>/ ; tools/pmc_summary.py turns them into profiles/*.
 set -e
-TAG=${1:-r01}
+TAG=${1:-r02}
 shift || true
 ARGS=${@:---steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 --legs none}
 ROOT=$(pwd)
@@ -13,6 +16,6 @@ OUT=$ROOT/gpurun_out/prof/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $ROOT/bench.py $ARGS > $OUT/kt.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $ROOT/bench.py $ARGS > $OUT/fetch.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $ROOT/bench.py $ARGS > $OUT/write.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_DRAM_sum --output-format csv -d $OUT/rd -o run -- python3 $ROOT/bench.py $ARGS > $OUT/rd.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/wr -o run -- python3 $ROOT/bench.py $ARGS > $OUT/wr.log 2>&1
 echo done
