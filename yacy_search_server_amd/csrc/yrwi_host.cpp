@@ -1028,7 +1028,23 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (!d_zero || !d_redo) return ctx->fail(YRWI_E_NOMEM, "arena");
   HIPCHK(ctx, hipMemsetAsync(d_zero, 0, 2 * sizeof(int32_t), ctx->stream));
   sp = span_open(ctx, tm);
-  if (launch_score(d_q, d_cq, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, ctx->stream))
+  // chunk order for k_score: every query's chunk 0, then every chunk 1, ... so that
+  // a big query's later chunks run after its threshold is set (PruneP)
+  std::vector<int32_t> order;
+  order.reserve((size_t)chunks);
+  {
+    int64_t maxc = 0;
+    for (auto& R : rq) maxc = std::max(maxc, R.nchunks);
+    for (int64_t c = 0; c < maxc; c++)
+      for (int qi = 0; qi < nq; qi++)
+        if (c < rq[(size_t)qi].nchunks) order.push_back((int32_t)(chunk_base[(size_t)qi] + c));
+  }
+  int32_t* d_order = arena_alloc<int32_t>(ctx, chunks);
+  unsigned long long* d_tq = arena_alloc<unsigned long long>(ctx, nq);
+  if (!d_order || !d_tq) return ctx->fail(YRWI_E_NOMEM, "arena");
+  if (upload(ctx, d_order, order)) return YRWI_E_HIP;
+  HIPCHK(ctx, hipMemsetAsync(d_tq, 0, sizeof(unsigned long long) * (size_t)nq, ctx->stream));
+  if (launch_score(d_q, d_cq, d_order, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
   // ---- top-k passes over groups of candidate lists until one list per query;

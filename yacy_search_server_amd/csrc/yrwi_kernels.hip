@@ -1434,47 +1434,10 @@ __device__ __forceinline__ int32_t qdiv(int32_t n, double r) {
   return n < 0 ? -q : q;
 }
 
-// ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265), settled min/max.
-__device__ __forceinline__ int64_t cardinal(const Feat& t, const NormState& N, const RankQ& Q, int32_t hcount) {
+// The long-accumulated flag and language terms of cardinal (ReferenceOrder.java:242-260)
+// added to R; Bitfield bit j is bit j of z (Bitfield.java:88-93, Tokenizer.java:51-56).
+__device__ __forceinline__ int64_t flags_lang_terms(int64_t R, uint32_t z, uint32_t lang, const RankQ& Q) {
   const yrwi_profile& rk = Q.prof;
-  int32_t tfterm = 0;
-  if (!(N.tf_mx == N.tf_mn))
-    tfterm = shl32(d2i(((t.tf - N.tf_mn) * 256.0) / (N.tf_mx - N.tf_mn)), rk.coeff_termfrequency);
-  auto inv = [](int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) -> int32_t {
-    if (hi == lo) return 0;
-    return shl32(sub32(256, qdiv(shl32(sub32(tv, lo), 8), rc)), c);
-  };
-  auto fwd = [](int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) -> int32_t {
-    if (hi == lo) return 0;
-    return shl32(qdiv(shl32(sub32(tv, lo), 8), rc), c);
-  };
-  const int dl = t.dl;  // DigestURL.domLengthEstimation; << (8/20) == << 0
-  const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
-  int32_t s = shl32(256 - dln, rk.coeff_domlength);
-  s = add32(s, inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], N.rcp[F_URLCOMPS], rk.coeff_urlcomps));
-  s = add32(s, inv(t.f[F_URLLENGTH], N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], N.rcp[F_URLLENGTH], rk.coeff_urllength));
-  s = add32(s, inv(t.f[F_POSINTEXT], N.mn[F_POSINTEXT], N.mx[F_POSINTEXT], N.rcp[F_POSINTEXT], rk.coeff_posintext));
-  s = add32(s, inv(t.f[F_POSOFPHRASE], N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], N.rcp[F_POSOFPHRASE],
-                   rk.coeff_posofphrase));
-  s = add32(s, inv(t.f[F_POSINPHRASE], N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], N.rcp[F_POSINPHRASE],
-                   rk.coeff_posinphrase));
-  s = add32(s, inv(t.od, 0, N.D, N.rcp[NF + 1], rk.coeff_worddistance));
-  s = add32(s, fwd(t.a, N.va_mn, N.va_mx, N.rcp[NF], rk.coeff_date));
-  s = add32(s, fwd(t.f[F_WORDSINTITLE], N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], N.rcp[F_WORDSINTITLE],
-                   rk.coeff_wordsintitle));
-  s = add32(s, fwd(t.f[F_WORDSINTEXT], N.mn[F_WORDSINTEXT], N.mx[F_WORDSINTEXT], N.rcp[F_WORDSINTEXT],
-                   rk.coeff_wordsintext));
-  s = add32(s, fwd(t.f[F_PHRASESINTEXT], N.mn[F_PHRASESINTEXT], N.mx[F_PHRASESINTEXT], N.rcp[F_PHRASESINTEXT],
-                   rk.coeff_phrasesintext));
-  s = add32(s, fwd(t.f[F_LLOCAL], N.mn[F_LLOCAL], N.mx[F_LLOCAL], N.rcp[F_LLOCAL], rk.coeff_llocal));
-  s = add32(s, fwd(t.f[F_LOTHER], N.mn[F_LOTHER], N.mx[F_LOTHER], N.rcp[F_LOTHER], rk.coeff_lother));
-  s = add32(s, fwd(t.f[F_HITCOUNT], N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], N.rcp[F_HITCOUNT], rk.coeff_hitcount));
-  int64_t R = add64((int64_t)s, (int64_t)tfterm);  // + tf turns the sum into a long
-  if (rk.coeff_authority > 12) {
-    int32_t auth = div32(shl32(hcount, 8), add32(1, N.maxdom));  // ReferenceOrder.authority :213-216
-    R = add64(R, (int64_t)shl32(auth, rk.coeff_authority));
-  }
-  const uint32_t z = t.z;
   const int32_t c255 = 255;
   if (z & (1u << 28)) R = add64(R, shl32(c255, rk.coeff_appurl));
   if (z & (1u << 25)) R = add64(R, shl32(c255, rk.coeff_app_dc_title));
@@ -1487,8 +1450,126 @@ __device__ __forceinline__ int64_t cardinal(const Feat& t, const NormState& N, c
   if (z & (1u << 21)) R = add64(R, shl32(c255, rk.coeff_cathasaudio));
   if (z & (1u << 22)) R = add64(R, shl32(c255, rk.coeff_cathasvideo));
   if (z & (1u << 23)) R = add64(R, shl32(c255, rk.coeff_cathasapp));
-  if (Q.lang_ok && t.lang == ((uint32_t)Q.lang[0] | ((uint32_t)Q.lang[1] << 8))) R = add64(R, shl32(c255, rk.coeff_language));
+  if (Q.lang_ok && lang == ((uint32_t)Q.lang[0] | ((uint32_t)Q.lang[1] << 8))) R = add64(R, shl32(c255, rk.coeff_language));
   return R;
+}
+
+// Normalised int terms of cardinal (ReferenceOrder.java:223-241): inv counts
+// "smaller is better" fields, fwd "larger is better"; 0 where max == min.
+__device__ __forceinline__ int32_t term_inv(int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) {
+  if (hi == lo) return 0;
+  return shl32(sub32(256, qdiv(shl32(sub32(tv, lo), 8), rc)), c);
+}
+__device__ __forceinline__ int32_t term_fwd(int32_t tv, int32_t lo, int32_t hi, double rc, int32_t c) {
+  if (hi == lo) return 0;
+  return shl32(qdiv(shl32(sub32(tv, lo), 8), rc), c);
+}
+
+// Per-query term tables (in LDS), built by every scoring workgroup:
+//  t    the nine one-byte fields' terms, CARD_TABS x 256 int32: a term depends on
+//       the field value alone, and int addition wraps associatively, so summing
+//       looked-up terms equals cardinal's running int sum;
+//  flo  the long sum of the flag terms of Bitfield bits 20-23 for each subset,
+//  fhi  the same for bits 24-29 (the flag terms are independent long additions).
+constexpr int CARD_TABS = 9;
+enum : int { CT_URLCOMPS = 0, CT_URLLENGTH, CT_POSOFPHRASE, CT_POSINPHRASE, CT_DISTANCE, CT_WORDSINTITLE,
+             CT_LLOCAL, CT_LOTHER, CT_HITCOUNT };
+struct CardTab {
+  int32_t t[CARD_TABS * 256];
+  int64_t flo[16];
+  int64_t fhi[64];
+};
+__device__ __forceinline__ void build_card_tab(CardTab* T, const NormState& N, const RankQ& Q) {
+  const yrwi_profile& rk = Q.prof;
+  for (int i = threadIdx.x; i < CARD_TABS * 256; i += blockDim.x) {
+    const int v = i & 255;
+    int32_t r;
+    switch (i >> 8) {
+      case CT_URLCOMPS:
+        r = term_inv(v, N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], N.rcp[F_URLCOMPS], rk.coeff_urlcomps);
+        break;
+      case CT_URLLENGTH:
+        r = term_inv(v, N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], N.rcp[F_URLLENGTH], rk.coeff_urllength);
+        break;
+      case CT_POSOFPHRASE:
+        r = term_inv(v, N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], N.rcp[F_POSOFPHRASE], rk.coeff_posofphrase);
+        break;
+      case CT_POSINPHRASE:
+        r = term_inv(v, N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], N.rcp[F_POSINPHRASE], rk.coeff_posinphrase);
+        break;
+      case CT_DISTANCE: r = term_inv(v, 0, N.D, N.rcp[NF + 1], rk.coeff_worddistance); break;
+      case CT_WORDSINTITLE:
+        r = term_fwd(v, N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], N.rcp[F_WORDSINTITLE], rk.coeff_wordsintitle);
+        break;
+      case CT_LLOCAL: r = term_fwd(v, N.mn[F_LLOCAL], N.mx[F_LLOCAL], N.rcp[F_LLOCAL], rk.coeff_llocal); break;
+      case CT_LOTHER: r = term_fwd(v, N.mn[F_LOTHER], N.mx[F_LOTHER], N.rcp[F_LOTHER], rk.coeff_lother); break;
+      default: r = term_fwd(v, N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], N.rcp[F_HITCOUNT], rk.coeff_hitcount); break;
+    }
+    T->t[i] = r;
+  }
+  const int i = threadIdx.x;
+  if (i < 16) T->flo[i] = flags_lang_terms(0, (uint32_t)i << 20, ~0u, Q) - flags_lang_terms(0, 0, ~0u, Q);
+  else if (i < 80) T->fhi[i - 16] = flags_lang_terms(0, (uint32_t)(i - 16) << 24, ~0u, Q) - flags_lang_terms(0, 0, ~0u, Q);
+}
+// flags_lang_terms through the tables
+__device__ __forceinline__ int64_t flags_lang_tab(int64_t R, uint32_t z, uint32_t lang, const RankQ& Q,
+                                                  const CardTab* T) {
+  const yrwi_profile& rk = Q.prof;
+  R = add64(R, T->flo[(z >> 20) & 15u]);
+  R = add64(R, T->fhi[(z >> 24) & 63u]);
+  if (z & 1u) R = add64(R, shl32(255, rk.coeff_catindexof));
+  if (Q.lang_ok && lang == ((uint32_t)Q.lang[0] | ((uint32_t)Q.lang[1] << 8))) R = add64(R, shl32(255, rk.coeff_language));
+  return R;
+}
+
+// ReferenceOrder.cardinal(WordReference) (ReferenceOrder.java:223-265), settled
+// min/max; with tab (build_card_tab) the one-byte fields' terms are looked up.
+__device__ __forceinline__ int64_t cardinal(const Feat& t, const NormState& N, const RankQ& Q, int32_t hcount,
+                                            const CardTab* tab = nullptr) {
+  const yrwi_profile& rk = Q.prof;
+  int32_t tfterm = 0;
+  if (!(N.tf_mx == N.tf_mn))
+    tfterm = shl32(d2i(((t.tf - N.tf_mn) * 256.0) / (N.tf_mx - N.tf_mn)), rk.coeff_termfrequency);
+  const int dl = t.dl;  // DigestURL.domLengthEstimation; << (8/20) == << 0
+  const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
+  int32_t s = shl32(256 - dln, rk.coeff_domlength);
+  if (tab) {
+    s = add32(s, tab->t[CT_URLCOMPS * 256 + t.f[F_URLCOMPS]]);
+    s = add32(s, tab->t[CT_URLLENGTH * 256 + t.f[F_URLLENGTH]]);
+    s = add32(s, tab->t[CT_POSOFPHRASE * 256 + t.f[F_POSOFPHRASE]]);
+    s = add32(s, tab->t[CT_POSINPHRASE * 256 + t.f[F_POSINPHRASE]]);
+    s = add32(s, tab->t[CT_DISTANCE * 256 + t.od]);
+    s = add32(s, tab->t[CT_WORDSINTITLE * 256 + t.f[F_WORDSINTITLE]]);
+    s = add32(s, tab->t[CT_LLOCAL * 256 + t.f[F_LLOCAL]]);
+    s = add32(s, tab->t[CT_LOTHER * 256 + t.f[F_LOTHER]]);
+    s = add32(s, tab->t[CT_HITCOUNT * 256 + t.f[F_HITCOUNT]]);
+  } else {
+    s = add32(s, term_inv(t.f[F_URLCOMPS], N.mn[F_URLCOMPS], N.mx[F_URLCOMPS], N.rcp[F_URLCOMPS], rk.coeff_urlcomps));
+    s = add32(s, term_inv(t.f[F_URLLENGTH], N.mn[F_URLLENGTH], N.mx[F_URLLENGTH], N.rcp[F_URLLENGTH],
+                          rk.coeff_urllength));
+    s = add32(s, term_inv(t.f[F_POSOFPHRASE], N.mn[F_POSOFPHRASE], N.mx[F_POSOFPHRASE], N.rcp[F_POSOFPHRASE],
+                          rk.coeff_posofphrase));
+    s = add32(s, term_inv(t.f[F_POSINPHRASE], N.mn[F_POSINPHRASE], N.mx[F_POSINPHRASE], N.rcp[F_POSINPHRASE],
+                          rk.coeff_posinphrase));
+    s = add32(s, term_inv(t.od, 0, N.D, N.rcp[NF + 1], rk.coeff_worddistance));
+    s = add32(s, term_fwd(t.f[F_WORDSINTITLE], N.mn[F_WORDSINTITLE], N.mx[F_WORDSINTITLE], N.rcp[F_WORDSINTITLE],
+                          rk.coeff_wordsintitle));
+    s = add32(s, term_fwd(t.f[F_LLOCAL], N.mn[F_LLOCAL], N.mx[F_LLOCAL], N.rcp[F_LLOCAL], rk.coeff_llocal));
+    s = add32(s, term_fwd(t.f[F_LOTHER], N.mn[F_LOTHER], N.mx[F_LOTHER], N.rcp[F_LOTHER], rk.coeff_lother));
+    s = add32(s, term_fwd(t.f[F_HITCOUNT], N.mn[F_HITCOUNT], N.mx[F_HITCOUNT], N.rcp[F_HITCOUNT], rk.coeff_hitcount));
+  }
+  s = add32(s, term_inv(t.f[F_POSINTEXT], N.mn[F_POSINTEXT], N.mx[F_POSINTEXT], N.rcp[F_POSINTEXT], rk.coeff_posintext));
+  s = add32(s, term_fwd(t.a, N.va_mn, N.va_mx, N.rcp[NF], rk.coeff_date));
+  s = add32(s, term_fwd(t.f[F_WORDSINTEXT], N.mn[F_WORDSINTEXT], N.mx[F_WORDSINTEXT], N.rcp[F_WORDSINTEXT],
+                        rk.coeff_wordsintext));
+  s = add32(s, term_fwd(t.f[F_PHRASESINTEXT], N.mn[F_PHRASESINTEXT], N.mx[F_PHRASESINTEXT], N.rcp[F_PHRASESINTEXT],
+                        rk.coeff_phrasesintext));
+  int64_t R = add64((int64_t)s, (int64_t)tfterm);  // + tf turns the sum into a long
+  if (rk.coeff_authority > 12) {
+    int32_t auth = div32(shl32(hcount, 8), add32(1, N.maxdom));  // ReferenceOrder.authority :213-216
+    R = add64(R, (int64_t)shl32(auth, rk.coeff_authority));
+  }
+  return tab ? flags_lang_tab(R, t.z, t.lang, Q, tab) : flags_lang_terms(R, t.z, t.lang, Q);
 }
 
 __device__ __forceinline__ int32_t url_hashcode(const Row& r) {
@@ -1555,7 +1636,8 @@ __device__ __forceinline__ int32_t block_excl_sum(int32_t v, int32_t* sh, int32_
 // returns the number written, *distinct = survivors before the cut at k
 template <int NT>
 __device__ __forceinline__ int32_t dedupe_take(const uint64_t* k1, const uint64_t* k2, int N, int32_t k, Cand* out,
-                                               int32_t* sScan, int32_t* distinct) {
+                                               int32_t* sScan, int32_t* distinct,
+                                               unsigned long long* publish = nullptr) {
   const int ipt = (N + NT - 1) / NT;  // <= 32
   const int i0 = threadIdx.x * ipt;
   int32_t keep = 0;
@@ -1572,6 +1654,7 @@ __device__ __forceinline__ int32_t dedupe_take(const uint64_t* k1, const uint64_
   for (int s = 0; s < ipt; s++) {
     if (bits & (1u << s)) {
       if (off < k) { out[off].k1 = k1[i0 + s]; out[off].k2 = k2[i0 + s]; }
+      if (off == k - 1 && publish) atomicMax(publish, (unsigned long long)k1[i0 + s]);  // the k-th distinct class
       off++;
     }
   }
@@ -1696,11 +1779,86 @@ constexpr int SCORE_SMALL = 256;
 constexpr int SCORE_CAP = YRWI_SCORE_CAP;  // early-exit bound of k_score's radix select (0: exact kq-th key)
 static_assert(SCORE_CAP <= SCORE_SMALL, "the selected prefix must fit k_score's LDS");
 
+// ---- per-query score threshold (k_score)
+// A chunk that finds k distinct (score, hashCode) classes publishes the score of
+// its k-th, s_c: at least k distinct classes of the query score >= s_c, so the
+// query's k-th class does too, and no posting scoring below s_c can be among its
+// top-k.  Later chunks of the query drop such postings before selection; with a
+// cheap exact upper bound of a posting's score they skip its cardinal altogether.
+//   bound = the int-summed terms' maxima (each normalised term <= 256 << c) except
+//           domlength and date, computed exactly, + tf and authority maxima + the
+//           exact flag / language terms
+// valid while the int sum of terms 1-14 cannot wrap (PruneP.ok; else only the
+// computed scores are compared with the threshold).
+struct PruneP {
+  int64_t hi32, lo32;  // sums of the bounded int terms' maxima / minima
+  int64_t rest;        // tf and authority maxima (long-accumulated)
+  int32_t ok;
+};
+
+__device__ __forceinline__ PruneP prune_params(const NormState& N, const RankQ& Q) {
+  const yrwi_profile& rk = Q.prof;
+  PruneP P{0, 0, 0, 1};
+  auto term = [&](bool zero, int32_t c, int64_t vlo, int64_t vhi) {
+    if (zero) return;
+    const int64_t m = (int64_t)1 << (c & 31);
+    const int64_t h = vhi * m, l = vlo * m;
+    if (h >= ((int64_t)1 << 31) || l < -((int64_t)1 << 31)) P.ok = 0;  // the term itself could wrap
+    P.hi32 += h;
+    P.lo32 += l;
+  };
+  const int32_t* mn = N.mn;
+  const int32_t* mx = N.mx;
+  term(mx[F_URLCOMPS] == mn[F_URLCOMPS], rk.coeff_urlcomps, 0, 256);
+  term(mx[F_URLLENGTH] == mn[F_URLLENGTH], rk.coeff_urllength, 0, 256);
+  term(mx[F_POSINTEXT] == mn[F_POSINTEXT], rk.coeff_posintext, 0, 256);
+  term(mx[F_POSOFPHRASE] == mn[F_POSOFPHRASE], rk.coeff_posofphrase, 0, 256);
+  term(mx[F_POSINPHRASE] == mn[F_POSINPHRASE], rk.coeff_posinphrase, 0, 256);
+  term(N.D == 0, rk.coeff_worddistance, 256 - 255 * 256, 256);  // stored distance up to 255 over D >= 1
+  term(mx[F_WORDSINTITLE] == mn[F_WORDSINTITLE], rk.coeff_wordsintitle, 0, 256);
+  term(mx[F_WORDSINTEXT] == mn[F_WORDSINTEXT], rk.coeff_wordsintext, 0, 256);
+  term(mx[F_PHRASESINTEXT] == mn[F_PHRASESINTEXT], rk.coeff_phrasesintext, 0, 256);
+  term(mx[F_LLOCAL] == mn[F_LLOCAL], rk.coeff_llocal, 0, 256);
+  term(mx[F_LOTHER] == mn[F_LOTHER], rk.coeff_lother, 0, 256);
+  term(mx[F_HITCOUNT] == mn[F_HITCOUNT], rk.coeff_hitcount, 0, 256);
+  if (!(N.tf_mx == N.tf_mn)) {
+    const int64_t h = (int64_t)256 << (rk.coeff_termfrequency & 31);
+    if (h >= ((int64_t)1 << 31)) P.ok = 0;
+    P.rest += h;
+  }
+  if (rk.coeff_authority > 12) {
+    const int64_t h = (int64_t)255 << (rk.coeff_authority & 31);
+    if (h >= ((int64_t)1 << 31)) P.ok = 0;
+    P.rest += h;
+  }
+  return P;
+}
+
+// Upper bound of cardinal for a posting's record: domlength and date exactly
+// (a posting's own date may lie above the clone-clamped maximum), the other
+// int terms at their maxima, tf / authority maxima, flags and language exactly.
+// *valid = 0 when the int sum of terms 1-14 could wrap for this posting (every
+// partial sum lies in [exact + lo32, exact + hi32] since each term's range holds 0).
+__device__ __forceinline__ int64_t score_bound(const Rec& q, const NormState& N, const RankQ& Q, const PruneP& P,
+                                               bool* valid, const CardTab* tab = nullptr) {
+  const yrwi_profile& rk = Q.prof;
+  const int dl = (int)((q.w[3] >> 32) & 3);
+  const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
+  int64_t ex = (int64_t)shl32(256 - dln, rk.coeff_domlength);
+  if (N.va_mx != N.va_mn)
+    ex += (int64_t)shl32(qdiv(shl32(sub32((int32_t)(q.w[2] & 0xFFFF), N.va_mn), 8), N.rcp[NF]), rk.coeff_date);
+  *valid = P.ok && ex + P.hi32 < ((int64_t)1 << 31) && ex + P.lo32 >= -((int64_t)1 << 31);
+  const uint32_t z = (uint32_t)(q.w[2] >> 32), lang = (uint32_t)((q.w[2] >> 16) & 0xFFFF);
+  return tab ? flags_lang_tab(ex + P.hi32 + P.rest, z, lang, Q, tab) : flags_lang_terms(ex + P.hi32 + P.rest, z, lang, Q);
+}
+
 // score keys of one chunk: a[s] = score ^ 2^63 of element e0 + s*CHUNK_THREADS,
-// bit s of the result set when that element is live and admitted
+// bit s of the result set when that element is live and admitted (and, with a
+// threshold T, its key >= T)
 template <bool SCORE = true>
 __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState& N, int64_t e0, int32_t* flagc,
-                                                uint64_t* a, uint64_t* z) {
+                                                uint64_t* a, uint64_t* z, uint64_t T = 0,
+                                                const PruneP* P = nullptr, const CardTab* tab = nullptr) {
   const FilterQ* F = Q.filt;
   uint32_t vm = 0;
 #pragma unroll
@@ -1710,20 +1868,47 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
     if (z) z[s] = 0;
     if (e < Q.n && !(Q.removed && Q.removed[e])) {
       const Rec q = load_rec(Q.feat, e);
-      const Feat t = decode_rec(q);
       uint64_t khi = 0;
       uint32_t klo = 0;
-      if (F || Q.want_authority) key_at(Q, e, khi, klo);
-      if (F && !admit(*F, t, khi, klo, flagc)) continue;
+      if (F) {
+        key_at(Q, e, khi, klo);
+        if (!admit(*F, decode_rec(q), khi, klo, flagc)) continue;
+      }
       if (!SCORE) continue;
+      // below the query's threshold by an exact upper bound: no cardinal needed
+      if (T && P && P->ok) {
+        bool valid;
+        const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
+        if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
+      }
+      if (!F && Q.want_authority) key_at(Q, e, khi, klo);
+      const Feat t = decode_rec(q);
       const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
-      a[s] = (uint64_t)cardinal(t, N, Q, hc) ^ 0x8000000000000000ull;
+#ifdef YRWI_EXP_NOSCORE  // timing experiment only (inexact): loads without cardinal
+      a[s] = (q.w[0] ^ q.w[1] ^ q.w[2] ^ (uint64_t)hc) | 0x8000000000000000ull;
+#else
+      a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
+#endif
+      if (a[s] < T) {
+        a[s] = 0;
+        continue;
+      }
       if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       vm |= 1u << s;
     }
   }
   return vm;
 }
+
+#ifdef YRWI_PHASE_CLOCK  // timing experiment only: per-block wall-clock stamps of k_score (thread 0)
+constexpr int PH_MAXB = 16384;
+__device__ unsigned long long g_ts[PH_MAXB * 8];
+__device__ unsigned long long g_phase[16];
+#define PHASE(i) \
+  if (threadIdx.x == 0 && blockIdx.x < PH_MAXB) g_ts[blockIdx.x * 8 + 1 + (i)] = wall_clock64();
+#else
+#define PHASE(i)
+#endif
 
 // MSB-first radix select over the live keys: the largest T with at least kq live keys >= T.
 // With cap > 0 the select stops at the first digit whose bin takes the count of
@@ -1768,24 +1953,38 @@ __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t 
   return prefix;
 }
 
+
+// Chunks run in `order` (every query's first chunks before anybody's later ones),
+// so a big query's later chunks find its threshold (Tq, see PruneP) established.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
                                                         const int32_t* __restrict__ chunk_q,
+                                                        const int32_t* __restrict__ order,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
                                                         int32_t* __restrict__ cand_cnt, int32_t kc,
-                                                        int32_t* __restrict__ redo, int32_t* __restrict__ nredo) {
+                                                        int32_t* __restrict__ redo, int32_t* __restrict__ nredo,
+                                                        unsigned long long* __restrict__ Tq) {
   __shared__ uint64_t s1[SCORE_SMALL];
   __shared__ uint64_t s2[SCORE_SMALL];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sHist[256];
   __shared__ int32_t sSel[3];
   __shared__ uint64_t sRed[8];
-  __shared__ NormState sN;
   __shared__ int32_t sFlag[32];
+  __shared__ PruneP sP;
+  __shared__ uint64_t sT;
+  __shared__ CardTab sCard;
   const int tid = threadIdx.x;
-  const int64_t b = blockIdx.x;
+#ifdef YRWI_PHASE_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x < PH_MAXB) g_ts[blockIdx.x * 8] = wall_clock64();
+#endif
+  const int64_t b = order[blockIdx.x];
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
-  if (tid == 0) sN = norm[qi];
+  const NormState& N = norm[qi];  // per-query constants: scalar loads
+  if (tid == 0) {
+    sT = __hip_atomic_load(Tq + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sP = prune_params(N, Q);
+  }
   if (tid < 32) sFlag[tid] = 0;
   __syncthreads();
   const FilterQ* F = Q.filt;
@@ -1799,22 +1998,33 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const int32_t kq = Q.k < kc ? Q.k : kc;
   if (kq > SCORE_SMALL) {  // large k (doubledom stacks): only the flag counts here
     if (flagc) {
-      (void)score_elems<false>(Q, sN, e0, flagc, a, nullptr);
+      (void)score_elems<false>(Q, N, e0, flagc, a, nullptr);
       __syncthreads();
       if (tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
     }
     if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
     return;
   }
-  const uint32_t vm = score_elems(Q, sN, e0, flagc, a, nullptr);
+  build_card_tab(&sCard, N, Q);
+  __syncthreads();
+  const PruneP P = sP;
+  const uint64_t T0 = sT;
+  PHASE(5)
+  const uint32_t vm = score_elems(Q, N, e0, flagc, a, nullptr, T0, &P, &sCard);
   int32_t nv;
   (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
+  PHASE(0)
+#ifdef YRWI_EXP_NOSEL  // timing experiment only (inexact): scoring without selection
+  if (tid == 0) cand_cnt[b] = 0;
+  return;
+#endif
   if (flagc && tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
   if (kq <= 0 || nv == 0) {
     if (tid == 0) cand_cnt[b] = 0;
     return;
   }
   const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed, SCORE_CAP) : 0;
+  PHASE(1)
   int32_t mine = 0;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) mine += (((vm >> s) & 1u) && a[s] >= T) ? 1 : 0;
@@ -1833,13 +2043,18 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       off++;
     }
-  const int P = pow2_at_least(nsel);
-  for (int i = nsel + tid; i < P; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
+  const int NP = pow2_at_least(nsel);
+  for (int i = nsel + tid; i < NP; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
   __syncthreads();
-  bitonic_desc<CHUNK_THREADS>(s1, s2, P);
+  PHASE(2)
+#ifndef YRWI_EXP_NOSORT  // timing experiment only (inexact)
+  bitonic_desc<CHUNK_THREADS>(s1, s2, NP);
+#endif
+  PHASE(3)
   int32_t distinct;
   Cand* out = cand + b * (int64_t)kc;
-  const int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, P, kq, out, sScan, &distinct);
+  const int32_t n = dedupe_take<CHUNK_THREADS>(s1, s2, NP, kq, out, sScan, &distinct, Tq + qi);
+  PHASE(4)
   if (distinct < kq && nsel < nv) {  // the TreeSet dedupe consumed part of the prefix
     if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
     return;
@@ -1860,20 +2075,21 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score_full(const RankQ* __res
   __shared__ int32_t sHist[256];
   __shared__ int32_t sSel[3];
   __shared__ uint64_t sRed[8];
-  __shared__ NormState sN;
+  __shared__ CardTab sCard;
   const int tid = threadIdx.x;
   const int32_t nr = *nredo;
   for (int32_t ri = blockIdx.x; ri < nr; ri += gridDim.x) {
     const int64_t b = redo[ri];
     const int qi = chunk_q[b];
     const RankQ& Q = qs[qi];
+    const NormState& N = norm[qi];
     __syncthreads();  // LDS of the previous chunk
-    if (tid == 0) sN = norm[qi];
+    build_card_tab(&sCard, N, Q);
     __syncthreads();
     const int64_t c = b - Q.chunk_base;
     const int64_t e0 = c * CHUNK + tid;
     uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
-    const uint32_t vm = score_elems(Q, sN, e0, nullptr, a, z);  // flags were counted by k_score
+    const uint32_t vm = score_elems(Q, N, e0, nullptr, a, z, 0, nullptr, &sCard);  // flags were counted by k_score
     const int32_t kq = Q.k < kc ? Q.k : kc;
     int32_t nv;
     (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);
@@ -2491,15 +2707,49 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
   return rc(hipGetLastError());
 }
 
-int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, int32_t nq, int64_t total_chunks,
+int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, int32_t* d_redo,
-                 int32_t* d_nredo, void* st) {
+                 int32_t* d_nredo, unsigned long long* d_tq, void* st) {
   if (total_chunks <= 0) return 0;
-  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                     d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo);
+  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_order,
+                     d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
   const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
   hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
                      d_cand_cnt, kc, d_redo, d_nredo);
+#ifdef YRWI_PHASE_CLOCK
+  {
+    static std::vector<unsigned long long> h;
+    const int nb = (int)std::min<int64_t>(total_chunks, PH_MAXB);
+    h.assign((size_t)nb * 8, 0);
+    hipStreamSynchronize(S(st));
+    hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_ts), h.size() * 8);
+    // stamps: 0 start, 6 prologue, 1 score, 2 threshold, 3 scatter, 4 sort, 5 take (0: block left earlier)
+    const int ord[7] = {0, 6, 1, 2, 3, 4, 5};
+    double dur[7] = {0}, cnt[7] = {0}, life = 0;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int b = 0; b < nb; b++) {
+      const unsigned long long* x = &h[(size_t)b * 8];
+      unsigned long long prev = x[0], last = x[0];
+      t0 = std::min(t0, x[0]);
+      for (int j = 1; j < 7; j++) {
+        const unsigned long long v = x[ord[j]];
+        if (!v || v < prev) break;
+        dur[j] += (double)(v - prev);
+        cnt[j] += 1;
+        prev = last = v;
+      }
+      t1 = std::max(t1, last);
+      life += (double)(last - x[0]);
+    }
+    fprintf(stderr, "PHASE span %.1f us, mean block life %.2f us, mean concurrency %.0f; per block us (n):", (t1 - t0) / 100.0,
+            life / nb / 100.0, life / (double)(t1 - t0));
+    const char* nm[7] = {"", "pro", "score", "thr", "scat", "sort", "take"};
+    for (int j = 1; j < 7; j++) fprintf(stderr, " %s %.2f (%.0f)", nm[j], cnt[j] ? dur[j] / cnt[j] / 100.0 : 0.0, cnt[j]);
+    fprintf(stderr, "\n");
+    std::vector<unsigned long long> z(h.size(), 0);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_ts), z.data(), z.size() * 8);
+  }
+#endif
   return rc(hipGetLastError());
 }
 
