@@ -1855,51 +1855,6 @@ __device__ __forceinline__ int64_t score_bound(const Rec& q, const NormState& N,
 // score keys of one chunk: a[s] = score ^ 2^63 of element e0 + s*CHUNK_THREADS,
 // bit s of the result set when that element is live and admitted (and, with a
 // threshold T, its key >= T)
-template <bool SCORE = true>
-__device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState& N, int64_t e0, int32_t* flagc,
-                                                uint64_t* a, uint64_t* z, uint64_t T = 0,
-                                                const PruneP* P = nullptr, const CardTab* tab = nullptr) {
-  const FilterQ* F = Q.filt;
-  uint32_t vm = 0;
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {
-    const int64_t e = e0 + s * CHUNK_THREADS;
-    a[s] = 0;
-    if (z) z[s] = 0;
-    if (e < Q.n && !(Q.removed && Q.removed[e])) {
-      const Rec q = load_rec(Q.feat, e);
-      uint64_t khi = 0;
-      uint32_t klo = 0;
-      if (F) {
-        key_at(Q, e, khi, klo);
-        if (!admit(*F, decode_rec(q), khi, klo, flagc)) continue;
-      }
-      if (!SCORE) continue;
-      // below the query's threshold by an exact upper bound: no cardinal needed
-      if (T && P && P->ok) {
-        bool valid;
-        const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
-        if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
-      }
-      if (!F && Q.want_authority) key_at(Q, e, khi, klo);
-      const Feat t = decode_rec(q);
-      const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
-#ifdef YRWI_EXP_NOSCORE  // timing experiment only (inexact): loads without cardinal
-      a[s] = (q.w[0] ^ q.w[1] ^ q.w[2] ^ (uint64_t)hc) | 0x8000000000000000ull;
-#else
-      a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
-#endif
-      if (a[s] < T) {
-        a[s] = 0;
-        continue;
-      }
-      if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
-      vm |= 1u << s;
-    }
-  }
-  return vm;
-}
-
 #ifdef YRWI_PHASE_CLOCK  // timing experiment only: per-block wall-clock stamps of k_score (thread 0)
 constexpr int PH_MAXB = 16384;
 __device__ unsigned long long g_ts[PH_MAXB * 8];
@@ -1909,6 +1864,93 @@ __device__ unsigned long long g_phase[16];
 #else
 #define PHASE(i)
 #endif
+
+// score keys of one chunk: a[s] = score ^ 2^63 of the chunk's element
+// s*CHUNK_THREADS + tid (with idx: of element idx[s*CHUNK_THREADS + tid], the
+// first cnt entries of a compacted list), bit s of the result set when that
+// element is live and admitted (and, with a threshold T, its key >= T)
+template <bool SCORE = true>
+__device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState& N, int64_t c, int32_t* flagc,
+                                                uint64_t* a, uint64_t* z, uint64_t T = 0,
+                                                const PruneP* P = nullptr, const CardTab* tab = nullptr,
+                                                const int16_t* idx = nullptr, int32_t cnt = 0) {
+  const FilterQ* F = Q.filt;
+  uint32_t vm = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int i = s * CHUNK_THREADS + (int)threadIdx.x;
+    a[s] = 0;
+    if (z) z[s] = 0;
+    int64_t e;
+    if (idx) {
+      if (i >= cnt) continue;
+      e = c * CHUNK + idx[i];
+    } else {
+      e = c * CHUNK + i;
+      if (e >= Q.n || (Q.removed && Q.removed[e])) continue;
+    }
+    const Rec q = load_rec(Q.feat, e);
+    uint64_t khi = 0;
+    uint32_t klo = 0;
+    if (F) {
+      key_at(Q, e, khi, klo);
+      if (!admit(*F, decode_rec(q), khi, klo, flagc)) continue;
+    }
+    if (!SCORE) continue;
+    // below the query's threshold by an exact upper bound: no cardinal needed
+    if (T && P && P->ok) {
+      bool valid;
+      const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
+      if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
+    }
+    if (!F && Q.want_authority) key_at(Q, e, khi, klo);
+    const Feat t = decode_rec(q);
+    const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
+#ifdef YRWI_EXP_NOSCORE  // timing experiment only (inexact): loads without cardinal
+    a[s] = (q.w[0] ^ q.w[1] ^ q.w[2] ^ (uint64_t)hc) | 0x8000000000000000ull;
+#else
+    a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
+#endif
+    if (a[s] < T) {
+      a[s] = 0;
+      continue;
+    }
+    if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+    vm |= 1u << s;
+  }
+  return vm;
+}
+
+// With the query's threshold T known (and no filters): the chunk's live elements
+// whose exact upper bound (score_bound, from words 2-3 of the record) reaches T,
+// compacted into idx (chunk-local, element order); returns their count.  cardinal
+// then runs on dense waves of survivors instead of on every wave for a few lanes.
+__device__ __forceinline__ int32_t prune_chunk(const RankQ& Q, const NormState& N, int64_t c, uint64_t T,
+                                               const PruneP& P, const CardTab* tab, int16_t* idx, int32_t* sScan) {
+  uint32_t keep = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int i = (int)threadIdx.x * CHUNK_IPT + s;  // thread-consecutive: idx comes out in element order
+    const int64_t e = c * CHUNK + i;
+    if (e >= Q.n || (Q.removed && Q.removed[e])) continue;
+    const ulonglong2 w23 = reinterpret_cast<const ulonglong2*>(Q.feat + e * FEAT_WORDS)[1];
+    Rec q;
+    q.w[0] = q.w[1] = 0;
+    q.w[2] = w23.x;
+    q.w[3] = w23.y;
+    bool valid;
+    const int64_t ub = score_bound(q, N, Q, P, &valid, tab);
+    if (!(valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T)) keep |= 1u << s;
+  }
+  int32_t tot;
+  int32_t o = block_excl_sum<CHUNK_THREADS>(__popc(keep), sScan, &tot);
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++)
+    if ((keep >> s) & 1u) idx[o++] = (int16_t)((int)threadIdx.x * CHUNK_IPT + s);
+  __syncthreads();
+  return tot;
+}
+
 
 // MSB-first radix select over the live keys: the largest T with at least kq live keys >= T.
 // With cap > 0 the select stops at the first digit whose bin takes the count of
@@ -1973,6 +2015,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ PruneP sP;
   __shared__ uint64_t sT;
   __shared__ CardTab sCard;
+  __shared__ int16_t sIdx[CHUNK];  // prune_chunk's survivors (chunk-local)
   const int tid = threadIdx.x;
 #ifdef YRWI_PHASE_CLOCK
   if (threadIdx.x == 0 && blockIdx.x < PH_MAXB) g_ts[blockIdx.x * 8] = wall_clock64();
@@ -1993,12 +2036,11 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   // strided element map (neighbouring lanes read neighbouring rows); the
   // candidate key carries the container index.  The hashCode (tie-break) is only
   // computed for the selected prefix.
-  const int64_t e0 = c * CHUNK + tid;
   uint64_t a[CHUNK_IPT];
   const int32_t kq = Q.k < kc ? Q.k : kc;
   if (kq > SCORE_SMALL) {  // large k (doubledom stacks): only the flag counts here
     if (flagc) {
-      (void)score_elems<false>(Q, N, e0, flagc, a, nullptr);
+      (void)score_elems<false>(Q, N, c, flagc, a, nullptr);
       __syncthreads();
       if (tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
     }
@@ -2010,7 +2052,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const PruneP P = sP;
   const uint64_t T0 = sT;
   PHASE(5)
-  const uint32_t vm = score_elems(Q, N, e0, flagc, a, nullptr, T0, &P, &sCard);
+  const bool comp = T0 && P.ok && !F;
+  const int32_t nc = comp ? prune_chunk(Q, N, c, T0, P, &sCard, sIdx, sScan) : 0;
+  const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, &sCard, sIdx, nc)
+                           : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, &sCard);
   int32_t nv;
   (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   PHASE(0)
@@ -2037,7 +2082,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++)
     if (((vm >> s) & 1u) && a[s] >= T) {
-      const int64_t e = e0 + s * CHUNK_THREADS;
+      const int i = s * CHUNK_THREADS + tid;
+      const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
       const uint32_t h = (uint32_t)Q.feat[e * FEAT_WORDS + 3];  // ByteArray.hashCode (ByteArray.java:80-84)
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
@@ -2087,9 +2133,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score_full(const RankQ* __res
     build_card_tab(&sCard, N, Q);
     __syncthreads();
     const int64_t c = b - Q.chunk_base;
-    const int64_t e0 = c * CHUNK + tid;
     uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
-    const uint32_t vm = score_elems(Q, N, e0, nullptr, a, z, 0, nullptr, &sCard);  // flags were counted by k_score
+    const uint32_t vm = score_elems(Q, N, c, nullptr, a, z, 0, nullptr, &sCard);  // flags were counted by k_score
     const int32_t kq = Q.k < kc ? Q.k : kc;
     int32_t nv;
     (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);
@@ -2746,6 +2791,11 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_or
     const char* nm[7] = {"", "pro", "score", "thr", "scat", "sort", "take"};
     for (int j = 1; j < 7; j++) fprintf(stderr, " %s %.2f (%.0f)", nm[j], cnt[j] ? dur[j] / cnt[j] / 100.0 : 0.0, cnt[j]);
     fprintf(stderr, "\n");
+    unsigned long long g[16];
+    hipMemcpyFromSymbol(g, HIP_SYMBOL(g_phase), sizeof(g));
+    fprintf(stderr, "PRUNE elems %llu survive %llu waves %llu all-pruned %llu\n", g[0], g[1], g[2], g[3]);
+    for (auto& x : g) x = 0;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_phase), g, sizeof(g));
     std::vector<unsigned long long> z(h.size(), 0);
     hipMemcpyToSymbol(HIP_SYMBOL(g_ts), z.data(), z.size() * 8);
   }
