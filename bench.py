@@ -238,19 +238,26 @@ class Runner:
             for f in fields:
                 agg[f] += getattr(st, f)
 
+        trace = os.environ.get("YRWI_BENCH_TRACE")  # per-batch completion times to stderr
+
         def run_steps(n):
             d = state["depth"]
             pending = []
+            tl = [time.perf_counter()]
             for i in range(n):
                 b = bufs[i % d]
                 if len(pending) == d:
                     t, bst = pending.pop(0)
                     ix.wait(t)
                     collect(bst)
+                    tl.append(time.perf_counter())
                 pending.append((ix.submit_raw(arr, nq, k, b[0], b[1], b[2]), b[2]))
             for t, bst in pending:
                 ix.wait(t)
                 collect(bst)
+                tl.append(time.perf_counter())
+            if trace:
+                log("batch done at ms: " + " ".join(f"{(x - tl[0]) * 1e3:.2f}" for x in tl[1:]))
 
         run_steps(warmup)
         for f in agg:
