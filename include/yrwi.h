@@ -234,7 +234,7 @@ int yrwi_score_nodes(yrwi_ctx* ctx, const yrwi_node* nodes, int64_t n, const yrw
 typedef struct yrwi_event yrwi_event;
 /* k: stack bound (<= YRWI_MAX_K; the results kept); filter: constraints, its
  * urlhashes seed the doublecheck set (NULL: unconstrained; its flagcount and
- * skip_double_dom are not used -- see yrwi_event_result); max_postings: the
+ * skip_double_dom are not used -- see yrwi_event_result, yrwi_event_pull); max_postings: the
  * most postings the event will receive (sizes the url and host tables). */
 int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms, int32_t k,
                     const yrwi_filter* filter, int64_t max_postings, yrwi_event** out);
@@ -262,6 +262,18 @@ typedef struct yrwi_event_info {
 /* The stack in rwiStack order (best first), up to maxn entries. */
 int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
                       yrwi_event_info* info);
+/* SearchEvent.pullOneRWI(skip_double_dom) (SearchEvent.java:1297-1394) repeated
+ * up to maxn times, stopping where it returns null: each pull polls the event's
+ * rwiStack (the entry leaves it, so later arrivals fill the bound again); with
+ * skip_double_dom, an entry whose host was already returned goes to that host's
+ * doubleDomCache queue, and after 10 such polls (or an empty stack) the best head
+ * of those queues is returned (a host whose queue empties leaves the cache).  The
+ * cache persists across calls and arrivals.  Equal heads of different hosts go
+ * by ReverseElement order, then the earliest queued (the reference walks a
+ * ConcurrentHashMap).  Every url is taken to have metadata (the fulltext lookup
+ * at :1309,1327,1392 is not on the RWI path). */
+int yrwi_event_pull(yrwi_ctx* ctx, yrwi_event* ev, int32_t skip_double_dom, yrwi_hit* out, int32_t maxn,
+                    int32_t* nout);
 void yrwi_event_close(yrwi_ctx* ctx, yrwi_event* ev);
 
 /* ---- index abstracts and the secondary search ---- */

@@ -228,6 +228,22 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventResult(JNIEn
   return res;
 }
 
+/* pullOneRWI(skipDoubleDom) up to maxn times (SearchEvent.java:1297-1394): the
+ * entries leave the event's rwiStack; yrwi_hit records in pull order */
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventPull(JNIEnv* env, jclass c, jlong ctx, jlong ev,
+                                                                        jboolean skipDoubleDom, jint maxn) {
+  yrwi_hit* hits = (yrwi_hit*)malloc(sizeof(yrwi_hit) * (size_t)(maxn > 0 ? maxn : 1));
+  int32_t n = 0;
+  int rc = yrwi_event_pull((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, skipDoubleDom ? 1 : 0, hits, maxn, &n);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewByteArray(env, (jsize)(n * (jint)sizeof(yrwi_hit)));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * (jint)sizeof(yrwi_hit)), (const jbyte*)hits);
+  }
+  free(hits);
+  return res;
+}
+
 JNIEXPORT void JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventClose(JNIEnv* env, jclass c, jlong ctx, jlong ev) {
   yrwi_event_close((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev);
 }

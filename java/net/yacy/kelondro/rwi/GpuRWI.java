@@ -88,6 +88,13 @@ public final class GpuRWI implements AutoCloseable {
         return eventResult(this.ctx, event, maxn);
     }
 
+    /** SearchEvent.pullOneRWI(skipDoubleDom) up to maxn times (SearchEvent.java:1297-1394):
+     *  yrwi_hit records (12-byte url hash, int hashCode, long score) in pull order;
+     *  the entries leave the event's rwiStack, the doubleDomCache stays with the event. */
+    public byte[] pullRWI(final long event, final boolean skipDoubleDom, final int maxn) {
+        return eventPull(this.ctx, event, skipDoubleDom, maxn);
+    }
+
     public void eventClose(final long event) {
         eventClose(this.ctx, event);
     }
@@ -158,6 +165,7 @@ public final class GpuRWI implements AutoCloseable {
                                          long maxPostings);
     private static native int eventAdd(long ctx, long event, byte[] rows, int n, boolean local);
     private static native byte[] eventResult(long ctx, long event, int maxn);
+    private static native byte[] eventPull(long ctx, long event, boolean skipDoubleDom, int maxn);
     private static native void eventClose(long ctx, long event);
     private static native byte[] indexAbstracts(long ctx, byte[] words, int nwords, long capacity);
     private static native long[] scoreNodes(long ctx, byte[] nodes, int n, int[] profile32, String language,

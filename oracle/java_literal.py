@@ -1110,6 +1110,60 @@ class SearchEventRWI:
     def stack(self) -> List[Tuple[bytes, int]]:
         return [(h, w) for (w, _, h) in self.q.items]
 
+    def pull(self, n: int, skip_double_dom: bool) -> List[Tuple[bytes, int]]:
+        """pullOneRWI(skipDoubleDom) (SearchEvent.java:1297-1394) up to n times,
+        stopping at the first null; polled entries leave rwiStack and the
+        doubleDomCache persists between calls (arrivals may come in between).
+        The metadata lookup (:1309,1327,1392) is outside the RWI path: every url
+        is taken to have metadata."""
+        if not hasattr(self, "dd"):
+            self.dd: Dict[bytes, ReverseQueue] = {}   # doubleDomCache (:426)
+            self.dd_seq: Dict[bytes, int] = {}        # url -> when it was queued
+            self.dd_next = 0
+        out: List[Tuple[bytes, int]] = []
+        while len(out) < n:
+            e = self._pull_one(skip_double_dom)
+            if e is None:
+                break
+            out.append(e)
+        return out
+
+    def _pull_one(self, skip: bool) -> Optional[Tuple[bytes, int]]:
+        c = 0
+        while len(self.q.items) > 0 and c < 10:        # pollloop (:1305)
+            c += 1
+            w, _, u = self.q.items.pop(0)               # rwiStack.poll()
+            if not skip:
+                return (u, w)
+            host = u[6:12]                              # hosthash (:1318)
+            m = self.dd.get(host)
+            if m is None:                               # first appearance: an empty queue marks the host
+                self.dd[host] = ReverseQueue(MAX_RESULTS_RWI)
+                return (u, w)
+            m.put(w, u)                                 # second appearance (:1335,1338)
+            self.dd_seq[u] = self.dd_next
+            self.dd_next += 1
+        if not self.dd:                                 # :1343
+            return None
+        # best head over all host queues (:1349-1368): the largest weight; the
+        # reference breaks ties by its ConcurrentHashMap walk, here by the
+        # queue order (weight, hashCode) and then the earliest queued entry
+        best = None
+        for host, m in self.dd.items():
+            if not m.items:
+                continue
+            hw, hh, hu = m.items[0]
+            key = (-hw, -hh, self.dd_seq[hu])
+            if best is None or key < best[0]:
+                best = (key, host)
+        if best is None:
+            return None
+        m = self.dd[best[1]]
+        w, _, u = m.items.pop(0)                        # m.poll() (:1377)
+        if not m.items:                                 # sizeAvailable() == 0 (:1378-1383)
+            del self.dd[best[1]]
+        return (u, w)
+
 
 def search(index: Dict[bytes, List[bytes]], include: Iterable[bytes], exclude: Iterable[bytes],
            profile: RankingProfile, language: str = "en", max_distance: int = 2147483647,

@@ -230,3 +230,67 @@ def test_event_errors():
                     ev.add_rwis(big[s:s + 5000])
     finally:
         ix.close()
+
+
+# ---------------------------------------------------------------- doubledom pull
+def test_oracle_pull_matches_settled_restatement():
+    """Stateful pullOneRWI over one settled stack, in pieces, equals the
+    one-shot restatement pull_double_dom (and a plain poll without skipDoubleDom)."""
+    _, idx = _pool()
+    rng = np.random.default_rng(5)
+    ref = jl.SearchEventRWI(jl.RankingProfile(), "en", NOW, maxsize=400)
+    for rows, local in _arrivals(idx, rng, 8, big=True):
+        ref.add_rwis(_rows(rows), local)
+    st = ref.stack()
+    exp = jl.pull_double_dom(st, len(st))
+    got = []
+    for n in (1, 9, 10, 11, 50, 1000):
+        got += ref.pull(n, True)
+    assert got == exp
+    ref2 = jl.SearchEventRWI(jl.RankingProfile(), "en", NOW, maxsize=400)
+    ref2.q.items = [(w, jl.bytearray_hashcode(h), h) for h, w in st]
+    assert ref2.pull(10_000, False) == st
+
+
+def _pull_script(ix, arrivals, steps, k, profile_fields=None):
+    """arrivals interleaved with pulls (n, skipDoubleDom) on the GPU event and the
+    oracle's SearchEventRWI; every pull and the final stack compared."""
+    lp = jl.RankingProfile()
+    gp = RankingProfile()
+    for f, v in (profile_fields or {}).items():
+        setattr(lp, f, v)
+        setattr(gp, f, v)
+    ref = jl.SearchEventRWI(lp, "en", NOW, maxsize=k)
+    total = sum(len(r) for r, _ in arrivals)
+    with ix.event(gp, "en", NOW, k=k, max_postings=total + 16) as ev:
+        for (rows, local), (n, skip) in zip(arrivals, steps):
+            ref.add_rwis(_rows(rows), local)
+            ev.add_rwis(rows, local)
+            got = [(h.urlhash, h.score) for h in ev.pull(n, skip)]
+            assert got == ref.pull(n, skip), (n, skip)
+        hits, info = ev.results()
+        assert [(h.urlhash, h.score) for h in hits] == ref.stack()
+        assert info.stack_size == len(ref.stack())
+        rest = [(h.urlhash, h.score) for h in ev.pull(k + 1, True)]
+        assert rest == ref.pull(k + 1, True)
+        assert ev.pull(5, True) == [] and ref.pull(5, True) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_event_pull_double_dom(seed):
+    """pullOneRWI(skipDoubleDom) on a live event: arrivals between pulls refill the
+    bounded stack, the doubleDomCache carries over, hosts whose queue empties are
+    new again (SearchEvent.java:1297-1394)."""
+    from yacy_search_server_amd import RWIIndex
+    _, idx = _pool()
+    rng = np.random.default_rng(40 + seed)
+    order = np.argsort(-idx.sizes)
+    arr = _arrivals(idx, rng, 9, local_term=int(order[seed]), big=True)
+    steps = [(int(rng.integers(0, 40)), bool(rng.random() < 0.8)) for _ in arr]
+    ix = RWIIndex(0)
+    try:
+        _pull_script(ix, arr, steps, k=300)
+        _pull_script(ix, arr, [(n, True) for n, _ in steps], k=3000, profile_fields={"coeff_authority": 14})
+    finally:
+        ix.close()

@@ -5,14 +5,28 @@
 // the event's ReferenceOrder, doublecheck set, flag counts and rwiStack carry
 // over between arrivals.  All of that state lives in device memory; k_event_add
 // (yrwi_kernels.hip) applies a batch of arrivals, one workgroup per event.
+#include <map>
+
 #include "yrwi_host.h"
 
 using namespace yrwi;
+
+// One doubleDomCache queue entry (SearchEvent.java:1319-1339): a polled stack entry
+// and when it was queued (the tie-break between equal heads of different hosts).
+struct DDEntry {
+  yrwi_hit h;
+  uint64_t seq;
+};
 
 struct yrwi_event {
   EvDev h{};         // host copy of the device descriptor
   void* mem = nullptr;
   int32_t k = 0;
+  // SearchEvent.doubleDomCache: host hash (url-hash chars 6..11) -> that host's
+  // queued entries in ReverseElement order; a host with an empty queue has had
+  // one entry returned and none queued since
+  std::map<uint64_t, std::vector<DDEntry>> dd;
+  uint64_t dd_next = 0;
 };
 
 namespace {
@@ -218,6 +232,105 @@ extern "C" int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, i
     info->max_distance = (S.hasA && S.P > 0) ? std::abs(S.P - S.A) : 0;
     info->err = S.err;
     info->stack_size = S.nstack;
+  }
+  return 0;
+}
+
+namespace {
+
+uint64_t host6(const yrwi_hit& h) {
+  uint64_t v = 0;
+  for (int j = 6; j < 12; j++) v = v << 8 | h.urlhash[j];
+  return v;
+}
+// ReverseElement.compareTo (WeakPriorityBlockingQueue.java:414-425): weight, then hashCode
+int rev_cmp(const yrwi_hit& a, const yrwi_hit& b) {
+  if (std::memcmp(a.urlhash, b.urlhash, 12) == 0) return 0;
+  if (a.score != b.score) return a.score > b.score ? -1 : 1;
+  if (a.tiebreak != b.tiebreak) return a.tiebreak > b.tiebreak ? -1 : 1;
+  return 0;
+}
+// WeakPriorityBlockingQueue.put (:119-134) into a host queue bounded by max_results_rwi
+void dd_put(std::vector<DDEntry>& q, const DDEntry& e) {
+  size_t lo = 0;
+  while (lo < q.size() && rev_cmp(q[lo].h, e.h) < 0) lo++;
+  if (lo < q.size() && rev_cmp(q[lo].h, e.h) == 0) return;  // the TreeSet holds an equal element
+  for (const DDEntry& x : q)
+    if (rev_cmp(x.h, e.h) == 0) return;
+  q.insert(q.begin() + (std::ptrdiff_t)lo, e);
+  if ((int32_t)q.size() > YRWI_MAX_K) q.pop_back();
+}
+
+}  // namespace
+
+extern "C" int yrwi_event_pull(yrwi_ctx* ctx, yrwi_event* ev, int32_t skip_double_dom, yrwi_hit* out, int32_t maxn,
+                               int32_t* nout) {
+  if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out) || !nout) return YRWI_E_ARG;
+  *nout = 0;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  EvState S;
+  HIPCHK(ctx, hipMemcpyAsync(&S, ev->h.st, sizeof(S), hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  if (S.err) return ctx->fail(S.err, "event tables overflowed earlier");
+  std::vector<yrwi_hit> stk((size_t)S.nstack);
+  if (S.nstack > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(stk.data(), ev->h.stack + (int64_t)S.cur * ev->k, sizeof(yrwi_hit) * stk.size(),
+                               hipMemcpyDeviceToHost, L->stream));
+    HIPCHK(ctx, lane_sync(L));
+  }
+  // pullOneRWI(skipDoubleDom) (SearchEvent.java:1297-1394), maxn times or until null
+  size_t p = 0;  // entries polled from rwiStack
+  int32_t n = 0;
+  while (n < maxn) {
+    bool got = false;
+    for (int c = 0; p < stk.size() && c < 10; c++) {  // pollloop (:1305)
+      const yrwi_hit& rwi = stk[p++];
+      if (!skip_double_dom) {
+        out[n++] = rwi;
+        got = true;
+        break;
+      }
+      auto it = ev->dd.find(host6(rwi));
+      if (it == ev->dd.end()) {  // first appearance of the host (:1320-1332)
+        ev->dd.emplace(host6(rwi), std::vector<DDEntry>());
+        out[n++] = rwi;
+        got = true;
+        break;
+      }
+      dd_put(it->second, DDEntry{rwi, ev->dd_next++});  // second appearance (:1335,1338)
+    }
+    if (got) continue;
+    if (ev->dd.empty()) break;  // :1343
+    // best head over the host queues (:1349-1368): largest weight; equal heads by
+    // queue order, then the earliest queued (the reference walks a ConcurrentHashMap)
+    auto best = ev->dd.end();
+    for (auto it = ev->dd.begin(); it != ev->dd.end(); ++it) {
+      if (it->second.empty()) continue;
+      if (best == ev->dd.end()) { best = it; continue; }
+      const DDEntry& a = it->second.front();
+      const DDEntry& b = best->second.front();
+      const int c = rev_cmp(a.h, b.h);
+      if (c < 0 || (c == 0 && a.seq < b.seq)) best = it;
+    }
+    if (best == ev->dd.end()) break;
+    out[n++] = best->second.front().h;  // m.poll() (:1377)
+    best->second.erase(best->second.begin());
+    if (best->second.empty()) ev->dd.erase(best);  // sizeAvailable() == 0 (:1378-1383)
+  }
+  *nout = n;
+  // the polled entries leave the device stack: the rest moves to the other half
+  if (p > 0) {
+    const int32_t rest = S.nstack - (int32_t)p, nc = 1 - S.cur;
+    if (rest > 0)
+      HIPCHK(ctx, hipMemcpyAsync(ev->h.stack + (int64_t)nc * ev->k, ev->h.stack + (int64_t)S.cur * ev->k + (int64_t)p,
+                                 sizeof(yrwi_hit) * (size_t)rest, hipMemcpyDeviceToDevice, L->stream));
+    const int32_t v[2] = {rest, nc};
+    static_assert(offsetof(EvState, cur) == offsetof(EvState, nstack) + 4, "nstack, cur adjacent");
+    HIPCHK(ctx, hipMemcpyAsync(reinterpret_cast<uint8_t*>(ev->h.st) + offsetof(EvState, nstack), v, sizeof(v),
+                               hipMemcpyHostToDevice, L->stream));
+    HIPCHK(ctx, lane_sync(L));
   }
   return 0;
 }

@@ -171,6 +171,15 @@ class SearchEvent:
                                                          ctypes.byref(info)))
         return [Hit(bytes(out[i].urlhash), out[i].score, out[i].tiebreak) for i in range(n.value)], info
 
+    def pull(self, n: int, skip_double_dom: bool = True) -> List["Hit"]:
+        """SearchEvent.pullOneRWI(skipDoubleDom) up to n times (SearchEvent.java:1297-1394):
+        the entries leave the stack; the doubleDomCache persists across calls."""
+        out = (_lib.CHit * max(1, n))()
+        got = ctypes.c_int32()
+        _check(self._ix._h, _lib.lib().yrwi_event_pull(self._ix._h, self._e, 1 if skip_double_dom else 0, out, n,
+                                                       ctypes.byref(got)))
+        return [Hit(bytes(out[i].urlhash), out[i].score, out[i].tiebreak) for i in range(got.value)]
+
     def close(self):
         if self._e and self._ix._h:
             _lib.lib().yrwi_event_close(self._ix._h, self._e)
