@@ -146,10 +146,20 @@ const char* yrwi_last_error(yrwi_ctx* ctx);
  * sorts (duplicate url hashes: the first occurrence wins, RowSet.mergeEnum). */
 int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted);
 int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n);
-/* Builds the url dictionary (url hash -> order-preserving 32-bit url id, the
- * join key in HBM) now instead of at the next query; the index is immutable
- * for queries until the next put_list / load_heaps. */
+/* Brings the url dictionary (url hash -> order-preserving 32-bit url id, the
+ * join key in HBM) up to date now instead of at the next query.  The first
+ * build sorts every key; later put_list / removal / load_heaps changes are
+ * merged in incrementally (IndexCell.add, IndexCell.java:289): only the changed
+ * lists' keys are sorted, keys new to the dictionary shift the ids after them
+ * (the other lists' ids are remapped in one pass, not re-sorted), and keys of
+ * removed postings stay until a full rebuild (when the changed lists hold over
+ * a quarter of the postings, or removed ones over half; YRWI_DICT_FULL=1
+ * forces it). */
 int yrwi_build_url_ids(yrwi_ctx* ctx);
+/* Diagnostic: brings the ids up to date, then *bad = postings whose id does not
+ * name their url hash or does not ascend within its list, plus dictionary
+ * entries out of order (0 when consistent); *nurls = dictionary size (may be NULL). */
+int yrwi_check_url_ids(yrwi_ctx* ctx, int64_t* bad, int64_t* nurls);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
 
 /* ---- YaCy on-disk index ---- */

@@ -5,10 +5,17 @@
 // preserve Base64Order (the 72-bit key order), so a list sorted by url hash is
 // sorted by url id and every merge / probe / exclusion decision is unchanged,
 // while the join kernels stream and compare 4-byte ids instead of 9-byte keys
-// (DESIGN.md §3).  The dictionary is rebuilt on the device before the first
-// query after any list changed: all keys are radix-sorted (klo, then stably
-// khi) with their posting positions, equal neighbours share a rank, and the
-// ranks are scattered back to each list's uid slice.
+// (DESIGN.md §3).  Built in full the first time (and when much of the index
+// changed): all keys are radix-sorted (klo, then stably khi) with their posting
+// positions, equal neighbours share a rank, and the ranks are scattered back to
+// each list's uid slice.  After that, the lists added or replaced since the last
+// query are merged in incrementally (IndexCell.add keeps adding postings,
+// IndexCell.java:289): only their keys are sorted; keys new to the dictionary get
+// their insertion points, every old id u moves to u + (new keys at or before it),
+// the other lists' ids are shifted by that prefix count (none at all when no key
+// is new), and the changed lists look their ids up.  Removed postings leave
+// their keys in the dictionary -- an id without postings changes no join --
+// until the next full rebuild.
 
 #include <hipcub/hipcub.hpp>
 
@@ -71,6 +78,121 @@ __global__ void k_dict_keys(const uint32_t* __restrict__ flag, const uint32_t* _
 
 unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// 72-bit key order: (hi, lo) lexicographic
+__device__ __forceinline__ bool key_less(uint64_t ah, uint8_t al, uint64_t bh, uint8_t bl) {
+  return ah < bh || (ah == bh && al < bl);
+}
+__device__ __forceinline__ int64_t dict_lower_bound(const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl,
+                                                    int64_t n, uint64_t h, uint8_t l) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key_less(dh[mid], dl[mid], h, l)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// distinct sorted keys: key j (a run start) -> slot rank1[j] - 1
+__global__ void k_cand_compact(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rank1,
+                               const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
+                               const uint32_t* __restrict__ pos, int64_t n, uint64_t* __restrict__ ch,
+                               uint8_t* __restrict__ cl) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || !flag[j]) return;
+  ch[rank1[j] - 1u] = kh[j];
+  cl[rank1[j] - 1u] = kl[pos[j]];
+}
+
+// candidate key -> insertion point in the dictionary, and whether it is new
+__global__ void k_dict_lookup(const uint64_t* __restrict__ ch, const uint8_t* __restrict__ cl, int64_t nc,
+                              const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl, int64_t nd,
+                              uint32_t* __restrict__ ins, uint32_t* __restrict__ isnew) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const int64_t p = dict_lower_bound(dh, dl, nd, ch[c], cl[c]);
+  ins[c] = (uint32_t)p;
+  isnew[c] = (p < nd && dh[p] == ch[c] && dl[p] == cl[c]) ? 0u : 1u;
+}
+
+// the new keys in order, their insertion points counted per old id
+__global__ void k_new_compact(const uint32_t* __restrict__ isnew, const uint32_t* __restrict__ rnew,
+                              const uint64_t* __restrict__ ch, const uint8_t* __restrict__ cl,
+                              const uint32_t* __restrict__ ins, int64_t nc, uint64_t* __restrict__ nh,
+                              uint8_t* __restrict__ nl, uint32_t* __restrict__ nins, uint32_t* __restrict__ hist) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc || !isnew[c]) return;
+  const uint32_t j = rnew[c] - 1u;
+  nh[j] = ch[c];
+  nl[j] = cl[c];
+  nins[j] = ins[c];
+  atomicAdd(&hist[ins[c]], 1u);
+}
+
+// old id u -> u + delta[u] (delta: new keys inserted at or before u)
+__global__ void k_dict_move_old(const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl,
+                                const uint32_t* __restrict__ delta, int64_t nd, uint64_t* __restrict__ dh2,
+                                uint8_t* __restrict__ dl2) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nd) return;
+  dh2[u + delta[u]] = dh[u];
+  dl2[u + delta[u]] = dl[u];
+}
+// new key j lands after ins[j] old keys and j new ones
+__global__ void k_dict_put_new(const uint64_t* __restrict__ nh, const uint8_t* __restrict__ nl,
+                               const uint32_t* __restrict__ nins, int64_t nn, uint64_t* __restrict__ dh2,
+                               uint8_t* __restrict__ dl2) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nn) return;
+  dh2[nins[j] + j] = nh[j];
+  dl2[nins[j] + j] = nl[j];
+}
+
+struct UidSeg {
+  uint32_t* uid;
+  const uint64_t* khi;
+  const uint8_t* klo;
+};
+__device__ __forceinline__ int seg_of(const int64_t* __restrict__ off, int nseg, int64_t i) {
+  int lo = 0, hi = nseg - 1;  // last segment with off <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+// unchanged lists: ids shift by the new keys before them
+__global__ void k_uid_remap(const UidSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
+                            const uint32_t* __restrict__ delta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = seg_of(off, nseg, i);
+  uint32_t* u = segs[s].uid + (i - off[s]);
+  *u += delta[*u];
+}
+// changed lists: ids looked up in the (updated) dictionary
+__global__ void k_uid_assign(const UidSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
+                             const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl, int64_t nd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = seg_of(off, nseg, i);
+  const int64_t j = i - off[s];
+  segs[s].uid[j] = (uint32_t)dict_lower_bound(dh, dl, nd, segs[s].khi[j], segs[s].klo[j]);
+}
+// consistency: every posting's id names its key, ids ascend within a list, the dictionary ascends
+__global__ void k_uid_check(const UidSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
+                            const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl, int64_t nd,
+                            unsigned long long* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nd && i > 0 && !key_less(dh[i - 1], dl[i - 1], dh[i], dl[i])) atomicAdd(bad, 1ull);
+  if (i >= n) return;
+  const int s = seg_of(off, nseg, i);
+  const int64_t j = i - off[s];
+  const uint32_t u = segs[s].uid[j];
+  bool ok = (int64_t)u < nd && dh[u] == segs[s].khi[j] && dl[u] == segs[s].klo[j];
+  if (ok && j > 0) ok = segs[s].uid[j - 1] < u;
+  if (!ok) atomicAdd(bad, 1ull);
+}
+
 struct DevBuf {
   void* p = nullptr;
   ~DevBuf() {
@@ -85,55 +207,40 @@ struct DevBuf {
 
 }  // namespace
 
-int ensure_url_ids(CtxBase* ctx) {
-  if (!ctx->uid_dirty) return 0;
-  hipStream_t st = ctx->stream;
-  std::vector<ListRec*> lists;
+namespace {
+
+// keys of the postings of `lists`, sorted (klo, then stably khi), with run flags
+// and ranks: sorted key j = (kh[j], kl[pos[j]]), rank1[j] = 1 + its distinct rank
+struct SortedKeys {
+  DevBuf bsegs, boff, bkh, bkh2, bkl, bkl2, bpos, bpos2, bflag, brank, btmp;
+  uint64_t* kh = nullptr;
+  uint8_t* kl = nullptr;
+  uint32_t *pos = nullptr, *flag = nullptr, *rank1 = nullptr;
   int64_t n = 0;
-  for (auto& kv : ctx->lists) {
-    lists.push_back(&kv.second);
-    n += kv.second.n;
-  }
-  if (n > (int64_t)INT32_MAX) return ctx->fail(YRWI_E_LIMIT, "more than 2^31 postings in one context");
-  if (n > 0 && (size_t)n > ctx->uid_cap) {
-    if (ctx->uid_all) hipFree(ctx->uid_all);
-    ctx->uid_all = nullptr;
-    ctx->uid_cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&ctx->uid_all), (size_t)n * 4) != hipSuccess)
-      return ctx->fail(YRWI_E_NOMEM, "url id allocation");
-    ctx->uid_cap = (size_t)n;
-  }
-  if (n == 0) {
-    ctx->uid_dirty = false;
-    return 0;
-  }
-  // ranking records of lists that have none yet (new or replaced lists)
-  for (ListRec* L : lists) {
-    if (L->feat || L->n == 0) continue;
-    L->feat = reinterpret_cast<uint64_t*>(ctx->index_mem.alloc((size_t)L->n * FEAT_BYTES));
-    if (!L->feat) return ctx->fail(YRWI_E_NOMEM, "ranking record allocation");
-    if (launch_features(L->rows, L->n, L->feat, st)) return ctx->fail(YRWI_E_HIP, "features launch");
-  }
+  uint32_t ndistinct = 0;
+};
+
+int sort_keys(CtxBase* ctx, const std::vector<ListRec*>& lists, SortedKeys& K) {
+  hipStream_t st = ctx->stream;
   std::vector<DictSeg> segs;
   std::vector<int64_t> off;
-  int64_t o = 0;
+  int64_t n = 0;
   for (ListRec* L : lists) {
     segs.push_back({L->khi, L->klo});
-    off.push_back(o);
-    L->uid = ctx->uid_all + o;
-    o += L->n;
+    off.push_back(n);
+    n += L->n;
   }
-  DevBuf bsegs, boff, bkh, bkh2, bkl, bkl2, bpos, bpos2, bflag, brank, btmp;
-  DictSeg* d_segs = bsegs.get<DictSeg>(segs.size());
-  int64_t* d_off = boff.get<int64_t>(off.size());
-  uint64_t* kh = bkh.get<uint64_t>((size_t)n);
-  uint64_t* kh2 = bkh2.get<uint64_t>((size_t)n);
-  uint8_t* kl = bkl.get<uint8_t>((size_t)n);
-  uint8_t* kl2 = bkl2.get<uint8_t>((size_t)n);
-  uint32_t* pos = bpos.get<uint32_t>((size_t)n);
-  uint32_t* pos2 = bpos2.get<uint32_t>((size_t)n);
-  uint32_t* flag = bflag.get<uint32_t>((size_t)n);
-  uint32_t* rank1 = brank.get<uint32_t>((size_t)n);
+  K.n = n;
+  DictSeg* d_segs = K.bsegs.get<DictSeg>(segs.size());
+  int64_t* d_off = K.boff.get<int64_t>(off.size());
+  uint64_t* kh = K.bkh.get<uint64_t>((size_t)n);
+  uint64_t* kh2 = K.bkh2.get<uint64_t>((size_t)n);
+  uint8_t* kl = K.bkl.get<uint8_t>((size_t)n);
+  uint8_t* kl2 = K.bkl2.get<uint8_t>((size_t)n);
+  uint32_t* pos = K.bpos.get<uint32_t>((size_t)n);
+  uint32_t* pos2 = K.bpos2.get<uint32_t>((size_t)n);
+  uint32_t* flag = K.bflag.get<uint32_t>((size_t)n);
+  uint32_t* rank1 = K.brank.get<uint32_t>((size_t)n);
   if (!d_segs || !d_off || !kh || !kh2 || !kl || !kl2 || !pos || !pos2 || !flag || !rank1)
     return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
   HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(DictSeg), hipMemcpyHostToDevice, st));
@@ -145,7 +252,7 @@ int ensure_url_ids(CtxBase* ctx) {
   HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, kh2, kh, pos2, pos, ni, 0, 64, st));
   HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, t3, flag, rank1, ni, st));
   size_t tb = std::max(t1, std::max(t2, t3));
-  void* tmp = btmp.get<uint8_t>(tb);
+  void* tmp = K.btmp.get<uint8_t>(tb);
   if (!tmp) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
   // (klo) then, stably, (khi): sorted by the 72-bit key; pos = posting index
   HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t1, kl, kl2, pos, pos2, ni, 0, 8, st));
@@ -153,11 +260,44 @@ int ensure_url_ids(CtxBase* ctx) {
   HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t2, kh2, kh, pos2, pos, ni, 0, 64, st));
   hipLaunchKernelGGL(k_dict_flags, dim3(nb(n)), dim3(256), 0, st, kh, pos, kl, n, flag);
   HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp, t3, flag, rank1, ni, st));
-  hipLaunchKernelGGL(k_dict_scatter, dim3(nb(n)), dim3(256), 0, st, rank1, pos, n, ctx->uid_all);
-  uint32_t nurls = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&nurls, rank1 + (n - 1), 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&K.ndistinct, rank1 + (n - 1), 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  K.kh = kh;
+  K.kl = kl;
+  K.pos = pos;
+  K.flag = flag;
+  K.rank1 = rank1;
+  return 0;
+}
+
+void publish_dict(CtxBase* ctx) {
+  for (Lane* L : ctx->lanes) {  // no batch is in flight while the dictionary changes
+    L->dkhi = ctx->dkhi;
+    L->dklo = ctx->dklo;
+  }
+}
+
+int full_rebuild(CtxBase* ctx, const std::vector<ListRec*>& lists, int64_t n) {
+  hipStream_t st = ctx->stream;
+  if (n > 0 && (size_t)n > ctx->uid_cap) {
+    if (ctx->uid_all) hipFree(ctx->uid_all);
+    ctx->uid_all = nullptr;
+    ctx->uid_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->uid_all), (size_t)n * 4) != hipSuccess)
+      return ctx->fail(YRWI_E_NOMEM, "url id allocation");
+    ctx->uid_cap = (size_t)n;
+  }
+  int64_t o = 0;
+  for (ListRec* L : lists) {
+    L->uid = ctx->uid_all + o;
+    o += L->n;
+  }
+  SortedKeys K;
+  if (int rc = sort_keys(ctx, lists, K)) return rc;
+  hipLaunchKernelGGL(k_dict_scatter, dim3(nb(n)), dim3(256), 0, st, K.rank1, K.pos, n, ctx->uid_all);
+  const uint32_t nurls = K.ndistinct;
   if ((size_t)nurls > ctx->dict_cap) {
+    HIPCHK(ctx, hipStreamSynchronize(st));
     if (ctx->dkhi) hipFree(ctx->dkhi);
     if (ctx->dklo) hipFree(ctx->dklo);
     ctx->dkhi = nullptr;
@@ -169,14 +309,204 @@ int ensure_url_ids(CtxBase* ctx) {
     ctx->dict_cap = nurls;
   }
   ctx->nurls = nurls;
-  for (Lane* L : ctx->lanes) {  // no batch is in flight while the dictionary is rebuilt
-    L->dkhi = ctx->dkhi;
-    L->dklo = ctx->dklo;
-  }
-  hipLaunchKernelGGL(k_dict_keys, dim3(nb(n)), dim3(256), 0, st, flag, rank1, kh, kl, pos, n, ctx->dkhi, ctx->dklo);
+  publish_dict(ctx);
+  hipLaunchKernelGGL(k_dict_keys, dim3(nb(n)), dim3(256), 0, st, K.flag, K.rank1, K.kh, K.kl, K.pos, n, ctx->dkhi,
+                     ctx->dklo);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipStreamSynchronize(st));  // scratch is freed on return
+  ctx->dict_valid = true;
+  ctx->dict_churn = 0;
+  return 0;
+}
+
+std::vector<UidSeg> uid_segs(const std::vector<ListRec*>& lists, std::vector<int64_t>* off, int64_t* n) {
+  std::vector<UidSeg> v;
+  *n = 0;
+  for (ListRec* L : lists) {
+    if (L->n == 0) continue;
+    v.push_back({L->uid, L->khi, L->klo});
+    off->push_back(*n);
+    *n += L->n;
+  }
+  return v;
+}
+
+// the lists of ctx->dict_pending (`changed`) merged into a valid dictionary
+int incremental(CtxBase* ctx, const std::vector<ListRec*>& changed, const std::vector<ListRec*>& others) {
+  hipStream_t st = ctx->stream;
+  SortedKeys K;
+  if (int rc = sort_keys(ctx, changed, K)) return rc;
+  const int64_t nc = K.ndistinct, nd = ctx->nurls;
+  DevBuf bch, bcl, bins, bisnew, brnew, btmp;
+  uint64_t* ch = bch.get<uint64_t>((size_t)nc);
+  uint8_t* cl = bcl.get<uint8_t>((size_t)nc);
+  uint32_t* ins = bins.get<uint32_t>((size_t)nc);
+  uint32_t* isnew = bisnew.get<uint32_t>((size_t)nc);
+  uint32_t* rnew = brnew.get<uint32_t>((size_t)nc);
+  if (!ch || !cl || !ins || !isnew || !rnew) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+  hipLaunchKernelGGL(k_cand_compact, dim3(nb(K.n)), dim3(256), 0, st, K.flag, K.rank1, K.kh, K.kl, K.pos, K.n, ch, cl);
+  hipLaunchKernelGGL(k_dict_lookup, dim3(nb(nc)), dim3(256), 0, st, ch, cl, nc, ctx->dkhi, ctx->dklo, nd, ins, isnew);
+  size_t t1 = 0;
+  HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, t1, isnew, rnew, (int)nc, st));
+  void* tmp = btmp.get<uint8_t>(std::max<size_t>(t1, 1));
+  if (!tmp) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+  HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp, t1, isnew, rnew, (int)nc, st));
+  uint32_t nn = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&nn, rnew + (nc - 1), 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (nd + (int64_t)nn > (int64_t)UINT32_MAX) return ctx->fail(YRWI_E_LIMIT, "more than 2^32 urls in one context");
+  if (nn > 0) {
+    DevBuf bnh, bnl, bnins, bhist, bdelta, btmp2;
+    uint64_t* nh = bnh.get<uint64_t>(nn);
+    uint8_t* nl = bnl.get<uint8_t>(nn);
+    uint32_t* nins = bnins.get<uint32_t>(nn);
+    uint32_t* hist = bhist.get<uint32_t>((size_t)nd + 1);
+    uint32_t* delta = bdelta.get<uint32_t>((size_t)nd + 1);
+    if (!nh || !nl || !nins || !hist || !delta) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+    HIPCHK(ctx, hipMemsetAsync(hist, 0, ((size_t)nd + 1) * 4, st));
+    hipLaunchKernelGGL(k_new_compact, dim3(nb(nc)), dim3(256), 0, st, isnew, rnew, ch, cl, ins, nc, nh, nl, nins, hist);
+    size_t t2 = 0;
+    HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, t2, hist, delta, (int)nd + 1, st));
+    void* tmp2 = btmp2.get<uint8_t>(std::max<size_t>(t2, 1));
+    if (!tmp2) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+    HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp2, t2, hist, delta, (int)nd + 1, st));
+    // the grown dictionary (new arrays: old ids move)
+    const int64_t nd2 = nd + nn;
+    const size_t cap2 = std::max<size_t>((size_t)nd2, ctx->dict_cap);
+    uint64_t* dh2 = nullptr;
+    uint8_t* dl2 = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&dh2), cap2 * 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dl2), cap2) != hipSuccess) {
+      if (dh2) hipFree(dh2);
+      return ctx->fail(YRWI_E_NOMEM, "url dictionary allocation");
+    }
+    hipLaunchKernelGGL(k_dict_move_old, dim3(nb(nd)), dim3(256), 0, st, ctx->dkhi, ctx->dklo, delta, nd, dh2, dl2);
+    hipLaunchKernelGGL(k_dict_put_new, dim3(nb(nn)), dim3(256), 0, st, nh, nl, nins, (int64_t)nn, dh2, dl2);
+    // every unchanged list's ids shift by the new keys before them
+    std::vector<int64_t> off;
+    int64_t no = 0;
+    std::vector<UidSeg> segs = uid_segs(others, &off, &no);
+    DevBuf bsegs, boff;
+    if (no > 0) {
+      UidSeg* d_segs = bsegs.get<UidSeg>(segs.size());
+      int64_t* d_off = boff.get<int64_t>(off.size());
+      if (!d_segs || !d_off) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+      HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(UidSeg), hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_uid_remap, dim3(nb(no)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), no, delta);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    hipFree(ctx->dkhi);
+    hipFree(ctx->dklo);
+    ctx->dkhi = dh2;
+    ctx->dklo = dl2;
+    ctx->dict_cap = cap2;
+    ctx->nurls = nd2;
+    publish_dict(ctx);
+  }
+  // the changed lists' ids, looked up in the dictionary
+  for (ListRec* L : changed) {
+    L->uid = reinterpret_cast<uint32_t*>(ctx->index_mem.alloc((size_t)L->n * 4));
+    if (!L->uid) return ctx->fail(YRWI_E_NOMEM, "url id allocation");
+  }
+  std::vector<int64_t> off;
+  int64_t np = 0;
+  std::vector<UidSeg> segs = uid_segs(changed, &off, &np);
+  DevBuf bsegs, boff;
+  UidSeg* d_segs = bsegs.get<UidSeg>(segs.size());
+  int64_t* d_off = boff.get<int64_t>(off.size());
+  if (!d_segs || !d_off) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+  HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(UidSeg), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_uid_assign, dim3(nb(np)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), np, ctx->dkhi,
+                     ctx->dklo, ctx->nurls);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // namespace
+
+void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
+  ctx->uid_dirty = true;
+  ctx->dict_churn += old_n;
+  if (added) ctx->dict_pending.insert(term);
+  else ctx->dict_pending.erase(term);
+}
+
+int ensure_url_ids(CtxBase* ctx) {
+  if (!ctx->uid_dirty) return 0;
+  hipStream_t st = ctx->stream;
+  std::vector<ListRec*> lists, changed, others;
+  int64_t n = 0, nchanged = 0;
+  for (auto& kv : ctx->lists) {
+    if (kv.second.n == 0) continue;
+    lists.push_back(&kv.second);
+    n += kv.second.n;
+    if (ctx->dict_pending.count(kv.first)) {
+      changed.push_back(&kv.second);
+      nchanged += kv.second.n;
+    } else {
+      others.push_back(&kv.second);
+    }
+  }
+  if (n > (int64_t)INT32_MAX) return ctx->fail(YRWI_E_LIMIT, "more than 2^31 postings in one context");
+  // ranking records of lists that have none yet (new or replaced lists)
+  for (ListRec* L : lists) {
+    if (L->feat) continue;
+    L->feat = reinterpret_cast<uint64_t*>(ctx->index_mem.alloc((size_t)L->n * FEAT_BYTES));
+    if (!L->feat) return ctx->fail(YRWI_E_NOMEM, "ranking record allocation");
+    if (launch_features(L->rows, L->n, L->feat, st)) return ctx->fail(YRWI_E_HIP, "features launch");
+  }
+  int rc = 0;
+  if (n == 0) {
+    ctx->dict_valid = false;
+  } else {
+    // a full rebuild when there is no dictionary yet, when the changed lists hold a
+    // large share of the postings, or when removed postings' keys pile up
+    const char* e = getenv("YRWI_DICT_FULL");
+    const bool full = !ctx->dict_valid || ctx->nurls == 0 || (e && atoi(e)) || 4 * nchanged > n ||
+                      2 * ctx->dict_churn > n;
+    rc = full ? full_rebuild(ctx, lists, n) : (changed.empty() ? 0 : incremental(ctx, changed, others));
+  }
+  if (rc) {
+    ctx->dict_valid = false;  // the next call rebuilds in full
+    return rc;
+  }
+  ctx->dict_pending.clear();
   ctx->uid_dirty = false;
+  return 0;
+}
+
+int check_url_ids(CtxBase* ctx, int64_t* bad) {
+  *bad = 0;
+  if (int rc = ensure_url_ids(ctx)) return rc;
+  hipStream_t st = ctx->stream;
+  std::vector<ListRec*> lists;
+  for (auto& kv : ctx->lists)
+    if (kv.second.n) lists.push_back(&kv.second);
+  std::vector<int64_t> off;
+  int64_t n = 0;
+  std::vector<UidSeg> segs = uid_segs(lists, &off, &n);
+  const int64_t m = std::max<int64_t>(n, ctx->nurls);
+  if (m == 0) return 0;
+  DevBuf bsegs, boff, bbad;
+  UidSeg* d_segs = bsegs.get<UidSeg>(std::max<size_t>(segs.size(), 1));
+  int64_t* d_off = boff.get<int64_t>(std::max<size_t>(off.size(), 1));
+  unsigned long long* d_bad = bbad.get<unsigned long long>(1);
+  if (!d_segs || !d_off || !d_bad) return ctx->fail(YRWI_E_NOMEM, "check scratch");
+  if (!segs.empty()) {
+    HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(UidSeg), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(ctx, hipMemsetAsync(d_bad, 0, 8, st));
+  hipLaunchKernelGGL(k_uid_check, dim3(nb(m)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), n, ctx->dkhi,
+                     ctx->dklo, ctx->nurls, d_bad);
+  unsigned long long hb = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&hb, d_bad, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *bad = (int64_t)hb;
   return 0;
 }
 

@@ -252,7 +252,11 @@ extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_
   drain(ctx);  // in-flight batches read the list table
   if (n == 0) {
     auto it = ctx->lists.find(tk);
-    if (it != ctx->lists.end()) { ctx->npostings -= it->second.n; ctx->lists.erase(it); ctx->uid_dirty = true; }
+    if (it != ctx->lists.end()) {
+      index_changed(ctx, tk, it->second.n, false);
+      ctx->npostings -= it->second.n;
+      ctx->lists.erase(it);
+    }
     return 0;
   }
   std::vector<uint8_t> tmp;
@@ -290,11 +294,21 @@ extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_
   if (herr & 2) return ctx->fail(YRWI_E_NULL_LANGUAGE, "row with empty language cell (reference NPE)");
   if (herr & 4) return ctx->fail(YRWI_E_UNSORTED, "rows are not strictly ascending by url hash");
   auto it = ctx->lists.find(tk);
-  if (it != ctx->lists.end()) ctx->npostings -= it->second.n;
+  const int64_t old_n = it != ctx->lists.end() ? it->second.n : 0;
+  ctx->npostings -= old_n;
   ctx->lists[tk] = L;
   ctx->npostings += n;
-  ctx->uid_dirty = true;
+  index_changed(ctx, tk, old_n, true);
   return 0;
+}
+
+extern "C" int yrwi_check_url_ids(yrwi_ctx* ctx, int64_t* bad, int64_t* nurls) {
+  if (!ctx || !bad) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  const int rc = check_url_ids(ctx, bad);
+  if (nurls) *nurls = ctx->nurls;
+  return rc;
 }
 
 extern "C" int yrwi_build_url_ids(yrwi_ctx* ctx) {

@@ -13,6 +13,7 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
@@ -313,6 +314,12 @@ struct CtxBase {
   uint8_t* dklo = nullptr;
   size_t dict_cap = 0;
   int64_t nurls = 0;
+  // incremental maintenance (yrwi_dict.hip): lists added or replaced since the
+  // dictionary was last brought up to date; keys of removed postings stay in it
+  // (an id without postings changes no join) until the next full rebuild
+  std::unordered_set<KeyT, KeyHash> dict_pending;
+  bool dict_valid = false;   // every list outside dict_pending has url ids in the dictionary
+  int64_t dict_churn = 0;    // postings removed or replaced since the last full rebuild
   std::string err;
   int64_t npostings = 0;
 
@@ -408,6 +415,10 @@ struct Xfer {
 };
 // (re)build the url dictionary and every list's url ids if the index changed
 int ensure_url_ids(CtxBase* ctx);
+// the list of `term` was added / replaced (added = true) or removed: url ids are due
+void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added);
+// brings the url ids up to date, then counts inconsistencies (0: every id names its key)
+int check_url_ids(CtxBase* ctx, int64_t* bad);
 
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op);    // in place; sum or max

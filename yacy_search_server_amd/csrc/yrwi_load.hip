@@ -384,10 +384,11 @@ extern "C" int yrwi_load_heaps(yrwi_ctx* ctx, const char* const* paths, int32_t 
     R.klo = acc.klo;
     R.rows = acc.rows;
     R.n = acc.n;
-    if (has_ram) ctx->npostings -= it->second.n;
+    const int64_t old_n = has_ram ? it->second.n : 0;
+    ctx->npostings -= old_n;
     ctx->lists[T.first] = R;
     ctx->npostings += R.n;
-    ctx->uid_dirty = true;
+    index_changed(ctx, T.first, old_n, true);
     S.terms++;
     S.postings += R.n;
   }

@@ -263,8 +263,15 @@ class RWIIndex:
         return st
 
     def build_url_ids(self) -> None:
-        """Build the url dictionary now (else the next query does)."""
+        """Bring the url dictionary up to date now (else the next query does)."""
         _check(self._h, _lib.lib().yrwi_build_url_ids(self._h))
+
+    def check_url_ids(self) -> Tuple[int, int]:
+        """(inconsistent postings / dictionary entries, dictionary size) after bringing
+        the url ids up to date (diagnostic; 0 inconsistencies expected)."""
+        bad, nurls = ctypes.c_int64(), ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_check_url_ids(self._h, ctypes.byref(bad), ctypes.byref(nurls)))
+        return bad.value, nurls.value
 
     def get_size(self, term: bytes) -> int:
         n = ctypes.c_int64()
