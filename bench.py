@@ -102,14 +102,31 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cgroup_cpus():
+    """CPUs' worth of time the cgroup grants this job (cpu.max quota / period), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores():
     """(threads used, affinity cores, why): every core of this process's affinity,
-    capped by the host-thread share the machine gives this job (OMP_NUM_THREADS /
-    MAX_JOBS, set to the per-GPU share on the GPU boxes)."""
+    capped by what the job may actually use -- the cgroup CPU quota (cpu.max) and
+    the host-thread share the machine gives this job (OMP_NUM_THREADS / MAX_JOBS,
+    the per-GPU share on the GPU boxes).  More threads than the quota only
+    time-slice the same CPUs."""
     aff = len(os.sched_getaffinity(0))
-    share = [int(os.environ[v]) for v in ("OMP_NUM_THREADS", "MAX_JOBS") if os.environ.get(v, "").isdigit()]
-    if share and min(share) < aff:
-        return min(share), aff, f"host-thread share of this job (OMP_NUM_THREADS={min(share)}) of {aff} affinity cores"
+    caps = [(int(os.environ[v]), f"{v}={os.environ[v]}") for v in ("OMP_NUM_THREADS", "MAX_JOBS")
+            if os.environ.get(v, "").isdigit()]
+    q = cgroup_cpus()
+    if q is not None:
+        caps.append((q, f"cgroup cpu.max quota of {q} CPUs"))
+    caps = [c for c in caps if c[0] < aff]
+    if caps:
+        n, why = min(caps)
+        return n, aff, f"{why} of {aff} affinity cores"
     return aff, aff, "all affinity cores"
 
 
@@ -427,6 +444,7 @@ def run(args, rank, world, local):
         cpu = cpu_baseline(idx, qs, NOW_MS, args.k, args.cpu_budget, nthr, prof, args.config)
         cpu["cores_why"] = why
         cpu["affinity_cores"] = aff
+        cpu["cgroup_cpus"] = cgroup_cpus()
         cpu1 = cpu_baseline(idx, qs, NOW_MS, args.k, args.cpu_budget / 2, 1, prof, args.config)
     R.close()
     shard_postings = len(idx.rows)
@@ -474,6 +492,7 @@ def run(args, rank, world, local):
                             "n": len(lat)} if lat else None),
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
+            "realloc_events_timed": timed["n_realloc"],  # device-wide allocations inside the timed steps
             "inflight": args.inflight,
             # per batch, from the library's own HIP events (isolated pass): join+probe kernels,
             # normalisation (reduce..combine), scoring (score..emit), all kernels; host = call to results

@@ -112,7 +112,8 @@ typedef struct yrwi_stats {
   int64_t bytes_join;    /* sum K over the merge-path join jobs (the k_join launches timed in t_join_ns) */
   int64_t t_join_ns;     /* device time of the k_join launches (HIP events on the context stream) */
   int64_t t_norm_ns, t_score_ns, t_total_ns;
-  int32_t n_join_launches, n_enum_steps, n_test_steps, reserved;
+  int32_t n_join_launches, n_enum_steps, n_test_steps;
+  int32_t n_realloc;     /* device-wide allocation events (scratch or pinned staging growth) during the call */
   int64_t bytes_probe;   /* sum K over the skewed (probe) join jobs, timed in t_probe_ns */
   int64_t t_probe_ns;    /* device time of the k_probe launches */
   int64_t bytes_compact; /* bytes k_compact moves: per joined row 12 B pair + url id read, the 32-B ranking

@@ -61,7 +61,7 @@ class CStats(ctypes.Structure):
                 ("bytes_join", ctypes.c_int64), ("t_join_ns", ctypes.c_int64), ("t_norm_ns", ctypes.c_int64),
                 ("t_score_ns", ctypes.c_int64), ("t_total_ns", ctypes.c_int64),
                 ("n_join_launches", ctypes.c_int32), ("n_enum_steps", ctypes.c_int32),
-                ("n_test_steps", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("n_test_steps", ctypes.c_int32), ("n_realloc", ctypes.c_int32),
                 ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64),
                 ("bytes_compact", ctypes.c_int64), ("t_compact_ns", ctypes.c_int64),
                 ("t_kernels_ns", ctypes.c_int64)]

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <chrono>
 #include <condition_variable>
@@ -80,6 +81,11 @@ struct ListRec {
   DList dl() const { return DList{khi, klo, rows, n, uid, feat}; }
 };
 
+// device-wide allocation events (hipMalloc / hipFree / hipHostMalloc / hipHostFree
+// on the query path: each one synchronises the whole device, so two lanes stop
+// overlapping while it runs); reported per batch in yrwi_stats.n_realloc
+inline std::atomic<int64_t> g_realloc{0};
+
 // bump allocator over device chunks
 struct Arena {
   std::vector<std::pair<uint8_t*, size_t>> chunks;
@@ -94,6 +100,7 @@ struct Arena {
     }
     if (cur >= chunks.size()) {
       size_t sz = std::max(std::max(bytes, min_chunk), capacity());  // geometric: few hipMallocs
+      g_realloc++;
       void* p = nullptr;
       if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
       chunks.push_back({(uint8_t*)p, sz});
@@ -108,6 +115,7 @@ struct Arena {
   // only call when no kernel uses arena memory any more
   void reset() {
     if (chunks.size() > 1) {
+      g_realloc++;
       size_t need = total_used + (1 << 20);
       for (auto& c : chunks) hipFree(c.first);
       chunks.clear();
@@ -122,6 +130,7 @@ struct Arena {
   // one chunk of at least `bytes` (no allocation in use: call between passes)
   void reserve(size_t bytes) {
     if (capacity() >= bytes && chunks.size() <= 1) return;
+    g_realloc++;
     for (auto& c : chunks) hipFree(c.first);
     chunks.clear();
     void* p = nullptr;
@@ -361,6 +370,7 @@ inline hipError_t lane_sync(Lane* L) {
 // pinned buffer of at least `bytes` (contents dropped on growth); nullptr on failure
 inline uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
   if (bytes > S->cap) {
+    g_realloc++;
     if (drain && lane_sync(ctx) != hipSuccess) return nullptr;
     if (S->p) hipHostFree(S->p);
     S->p = nullptr;
@@ -381,6 +391,7 @@ inline int upload(Lane* ctx, T* dst, const std::vector<T>& v) {
   Stage& S = ctx->stage;
   size_t off = (S.used + 255) & ~(size_t)255;
   if (off + bytes > S.cap) {
+    g_realloc++;
     // copies still read the old buffer: drain them, then grow
     HIPCHK(ctx, lane_sync(ctx));
     if (S.p) HIPCHK(ctx, hipHostFree(S.p));

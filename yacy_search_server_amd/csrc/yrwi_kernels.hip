@@ -920,7 +920,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ double sD[8];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sFirst[4];
-  __shared__ uint32_t sPO[CHUNK];  // element order: valid << 31 | od << 16 | p
+  // element order: valid << 31 | od << 16 | p; one pad word per 32 so that the
+  // thread-consecutive reads (stride CHUNK_IPT words) spread over the banks
+  __shared__ uint32_t sPO[CHUNK + CHUNK / 32];
   __shared__ uint32_t sSegP[CHUNK_THREADS * CHUNK_IPT];
   __shared__ uint32_t sSegM[CHUNK_THREADS * CHUNK_IPT];
   __shared__ uint32_t sSegL[CHUNK_THREADS * CHUNK_IPT];
@@ -974,7 +976,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
         }
       }
     }
-    sPO[eo] = po;
+    sPO[eo + (eo >> 5)] = po;
   }
   // first valid element of the chunk (element order)
   int32_t firstIdx;
@@ -1003,7 +1005,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int eo = (int)threadIdx.x * CHUNK_IPT + s;
-    const uint32_t po = sPO[eo];
+    const uint32_t po = sPO[eo + (eo >> 5)];
     P[s] = (int32_t)(po & 0xFFFFu);
     OD[s] = (int32_t)((po >> 16) & 0xFFu);
     rest[s] = (po >> 31) && eo != firstIdx;
