@@ -622,14 +622,19 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
   if (!owner.empty()) owner.swap(ow);
 }
 
+static int64_t now_ns();
+
 // One fold step's join jobs: layout, launch, joined sizes back to the plans.
 static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>& jobs, std::vector<int>& owner,
                          yrwi_stats* st, Timing* tm) {
   std::vector<int64_t> tile_base;
   int nmerge;
   int64_t merge_tiles, tiles;
+  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
+  const int64_t h0 = hprof ? now_ns() : 0;
   layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
   const int nj = (int)jobs.size();
+  const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
     for (const JoinQ& J : jobs)  // a probe job reads at most the galloping bound, whatever the reference dispatch
       (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) +=
@@ -655,7 +660,9 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
   if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_src || !d_cnt || !d_off)
     return ctx->fail(YRWI_E_NOMEM, "arena");
+  const int64_t h2 = hprof ? now_ns() : 0;
   if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  const int64_t h3 = hprof ? now_ns() : 0;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
@@ -669,9 +676,15 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     tm->spans.push_back({sp, c1});
   }
   if (st) st->n_join_launches++;
+  const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
   HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  const int64_t h5 = hprof ? now_ns() : 0;
   HIPCHK(ctx, lane_sync(ctx));
+  if (hprof)
+    fprintf(stderr, "[yrwi join] jobs %d layout %.3f alloc %.3f upload %.3f launch %.3f d2h %.3f sync %.3f ms\n", nj,
+            (h1 - h0) / 1e6, (h2 - h1) / 1e6, (h3 - h2) / 1e6, (h4 - h3) / 1e6, (h5 - h4) / 1e6,
+            (now_ns() - h5) / 1e6);
   if (st)  // k_compact per joined row: pair + id read, the records it gathers (32 B, + 16 B of the joined
            // side for enumeration steps), record + id written
     for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 96 : 80);
@@ -864,6 +877,10 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
                           int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
   const int nq = (int)plans.size();
   const int W = exchange ? ctx->world : 1;
+  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
+  int64_t hq[8] = {0};
+  auto mark = [&](int i) { if (hprof) hq[i] = now_ns(); };
+  mark(0);
   std::vector<RankQ> rq((size_t)nq);
   std::vector<int64_t> chunk_base((size_t)nq), slot_base((size_t)nq + 1);
   int64_t chunks = 0, nslots = 0;
@@ -1000,7 +1017,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++) chunk_q[(size_t)(chunk_base[(size_t)qi] + c)] = qi;
   int32_t* d_cq = arena_alloc<int32_t>(ctx, chunks);
   if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
+  mark(1);
   if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base) || upload(ctx, d_cq, chunk_q)) return YRWI_E_HIP;
+  mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
@@ -1029,6 +1048,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     return 0;
   }
 
+  mark(3);
   // ---- score + per-chunk top-k
   int32_t keff = 1;
   for (auto& R : rq) keff = std::max(keff, R.k);
@@ -1044,14 +1064,18 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   sp = span_open(ctx, tm);
   // chunk order for k_score: every query's chunk 0, then every chunk 1, ... so that
   // a big query's later chunks run after its threshold is set (PruneP)
-  std::vector<int32_t> order;
-  order.reserve((size_t)chunks);
+  std::vector<int32_t> order((size_t)chunks);
   {
+    // counting sort by chunk index c (stable in query order): O(chunks + max chunks)
     int64_t maxc = 0;
     for (auto& R : rq) maxc = std::max(maxc, R.nchunks);
-    for (int64_t c = 0; c < maxc; c++)
-      for (int qi = 0; qi < nq; qi++)
-        if (c < rq[(size_t)qi].nchunks) order.push_back((int32_t)(chunk_base[(size_t)qi] + c));
+    std::vector<int64_t> at((size_t)maxc + 1, 0);
+    for (auto& R : rq)
+      for (int64_t c = 0; c < R.nchunks; c++) at[(size_t)c + 1]++;
+    for (int64_t c = 0; c < maxc; c++) at[(size_t)c + 1] += at[(size_t)c];
+    for (int qi = 0; qi < nq; qi++)
+      for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++)
+        order[(size_t)at[(size_t)c]++] = (int32_t)(chunk_base[(size_t)qi] + c);
   }
   int32_t* d_order = arena_alloc<int32_t>(ctx, chunks);
   unsigned long long* d_tq = arena_alloc<unsigned long long>(ctx, nq);
@@ -1061,6 +1085,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (launch_score(d_q, d_cq, d_order, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq, ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
+  mark(4);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
   std::vector<const Cand*> fptr((size_t)nq);
@@ -1144,6 +1169,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));
   }
   if (!d_fptr || !d_fcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
+  mark(5);
   if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
   std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
   if (W == 1) {
@@ -1188,7 +1214,13 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
                                  sizeof(NormState), sizeof(int32_t), (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
   }
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
+  mark(6);
   HIPCHK(ctx, lane_sync(ctx));
+  mark(7);
+  if (hprof)
+    fprintf(stderr, "[yrwi rank] setup %.3f upload %.3f norm %.3f score %.3f topq %.3f emit %.3f sync %.3f ms\n",
+            (hq[1] - hq[0]) / 1e6, (hq[2] - hq[1]) / 1e6, (hq[3] - hq[2]) / 1e6, (hq[4] - hq[3]) / 1e6,
+            (hq[5] - hq[4]) / 1e6, (hq[6] - hq[5]) / 1e6, (hq[7] - hq[6]) / 1e6);
   for (int32_t D : hD)
     if (D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
   if (!direct) {
@@ -1249,6 +1281,8 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
                            yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
   const int64_t r0 = g_realloc.load();
+  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;  // per-batch host breakdown to stderr
+  int64_t tp = 0, tj = 0, tr = 0, w0 = L->wait_ns, wj = 0;
   std::vector<Plan> all((size_t)nq);
   for (int i = 0; i < nq; i++) {
     int rc = plan_query(ix, L, q[i], &all[(size_t)i]);
@@ -1259,6 +1293,7 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   // through this lane's arena and staging)
   if (L->world > 1 && begin_pass(L)) return YRWI_E_HIP;
   if (int rc = plan_batch(L, all)) return rc;
+  tp = now_ns() - t0;
   const int64_t budget = scratch_budget(L);
   for (int g0 = 0; g0 < nq;) {
     int g1 = g0;
@@ -1278,14 +1313,19 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
       tm.t0 = L->event();
       hipEventRecord(tm.t0, L->stream);
     }
+    const int64_t tj0 = now_ns(), wj0 = L->wait_ns;
     int rc = run_join_phase(L, plans, st, tmp);
     if (rc) return rc;
+    tj += now_ns() - tj0;
+    wj += L->wait_ns - wj0;
+    const int64_t tr0 = now_ns();
     if (tmp) {
       tm.tj = L->event();
       hipEventRecord(tm.tj, L->stream);
     }
     rc = run_rank_phase(L, plans, kmax, out + (size_t)g0 * kmax, nout + g0, nullptr, st, tmp);
     if (rc) return rc;
+    tr += now_ns() - tr0;
     if (st) {
       if (g1 < nq) HIPCHK(L, lane_sync(L));  // the pass's events must be complete before they are reused
       float ms = 0;
@@ -1316,6 +1356,11 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   if (st) {
     st->t_total_ns = now_ns() - t0;
     st->n_realloc = (int32_t)(g_realloc.load() - r0);
+  }
+  if (hprof) {
+    const int64_t wall = now_ns() - t0, wait = L->wait_ns - w0;
+    fprintf(stderr, "[yrwi host] nq %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms\n", nq,
+            wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6);
   }
   return 0;
 }

@@ -231,6 +231,7 @@ struct Lane {
   // another lane's thread is sizing this lane's arena (see share_arena_size)
   bool active = false, reserving = false;
   int rc = 0;
+  int64_t wait_ns = 0;  // host time spent waiting for this lane's device work (lane_sync)
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -364,7 +365,11 @@ inline hipError_t lane_sync(Lane* L) {
   if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
     return hipErrorOutOfMemory;
   hipError_t e = hipEventRecord(L->sync_ev, L->stream);
-  return e != hipSuccess ? e : hipEventSynchronize(L->sync_ev);
+  if (e != hipSuccess) return e;
+  const auto t0 = std::chrono::steady_clock::now();
+  e = hipEventSynchronize(L->sync_ev);
+  L->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  return e;
 }
 
 // pinned buffer of at least `bytes` (contents dropped on growth); nullptr on failure
