@@ -14,3 +14,14 @@ with open(sys.argv[1], "w") as o:
     for r in rows:
         o.write("%-50s %6s %10.1f us\n" % (r["Name"].split("(")[0][:50], r["Calls"], float(r["AverageNs"]) / 1e3))
 PY
+if [ -n "$KTRACE" ]; then  # per-dispatch durations of the kernels whose name contains $KTRACE
+python3 - "$R/gpurun_out/${TAG}_ktrace.txt" "$KTRACE" <<'PY'
+import csv, glob, sys
+f = glob.glob("/tmp/kst/**/*kernel_trace.csv", recursive=True)[0]
+rows = [r for r in csv.DictReader(open(f)) if sys.argv[2] in r["Kernel_Name"]]
+with open(sys.argv[1], "w") as o:
+    for r in rows:
+        o.write("%s %d %.1f\n" % (r["Kernel_Name"].split("(")[0], int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0),
+                                   (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+PY
+fi

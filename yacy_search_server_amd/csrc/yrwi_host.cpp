@@ -1082,7 +1082,12 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   if (!d_order || !d_tq) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_order, order)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_tq, 0, sizeof(unsigned long long) * (size_t)nq, ctx->stream));
-  if (launch_score(d_q, d_cq, d_order, nq, chunks, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq, ctx->stream))
+  // (a separate launch of every query's first chunk, so that all later chunks
+  // start with a threshold, measured 39 + 86 us against 99 us for one launch:
+  // the seed launch is one round of full-length blocks)
+  const int64_t seed = 0;
+  if (launch_score(d_q, d_cq, d_order, nq, chunks, seed, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq,
+                   ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
   mark(4);

@@ -1925,14 +1925,14 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
 
 // With the query's threshold T known (and no filters): the chunk's live elements
 // whose exact upper bound (score_bound, from words 2-3 of the record) reaches T,
-// compacted into idx (chunk-local, element order); returns their count.  cardinal
+// compacted into idx (chunk-local indices); returns their count.  cardinal
 // then runs on dense waves of survivors instead of on every wave for a few lanes.
 __device__ __forceinline__ int32_t prune_chunk(const RankQ& Q, const NormState& N, int64_t c, uint64_t T,
                                                const PruneP& P, const CardTab* tab, int16_t* idx, int32_t* sScan) {
   uint32_t keep = 0;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    const int i = (int)threadIdx.x * CHUNK_IPT + s;  // thread-consecutive: idx comes out in element order
+    const int i = s * CHUNK_THREADS + (int)threadIdx.x;  // coalesced; the order of idx does not matter
     const int64_t e = c * CHUNK + i;
     if (e >= Q.n || (Q.removed && Q.removed[e])) continue;
     const ulonglong2 w23 = reinterpret_cast<const ulonglong2*>(Q.feat + e * FEAT_WORDS)[1];
@@ -1948,7 +1948,7 @@ __device__ __forceinline__ int32_t prune_chunk(const RankQ& Q, const NormState& 
   int32_t o = block_excl_sum<CHUNK_THREADS>(__popc(keep), sScan, &tot);
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++)
-    if ((keep >> s) & 1u) idx[o++] = (int16_t)((int)threadIdx.x * CHUNK_IPT + s);
+    if ((keep >> s) & 1u) idx[o++] = (int16_t)(s * CHUNK_THREADS + (int)threadIdx.x);
   __syncthreads();
   return tot;
 }
@@ -2755,11 +2755,17 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 }
 
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
-                 const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc, int32_t* d_redo,
-                 int32_t* d_nredo, unsigned long long* d_tq, void* st) {
+                 int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
+                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* st) {
   if (total_chunks <= 0) return 0;
-  hipLaunchKernelGGL(k_score, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_order,
-                     d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+  // seed_chunks (0 < seed < total): the first chunks of `order` run as a launch of
+  // their own, so every later chunk starts with its query's threshold set
+  const int64_t s0 = (seed_chunks > 0 && seed_chunks < total_chunks) ? seed_chunks : total_chunks;
+  hipLaunchKernelGGL(k_score, dim3((unsigned)s0), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_order, d_norm,
+                     d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+  if (s0 < total_chunks)
+    hipLaunchKernelGGL(k_score, dim3((unsigned)(total_chunks - s0)), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
+                       d_order + s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
   const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
   hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
                      d_cand_cnt, kc, d_redo, d_nredo);
