@@ -2059,7 +2059,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, &sCard, sIdx, nc)
                            : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, &sCard);
   int32_t nv;
-  (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
+  int32_t voff = block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   PHASE(0)
 #ifdef YRWI_EXP_NOSEL  // timing experiment only (inexact): scoring without selection
   if (tid == 0) cand_cnt[b] = 0;
@@ -2068,6 +2068,24 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   if (flagc && tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
   if (kq <= 0 || nv == 0) {
     if (tid == 0) cand_cnt[b] = 0;
+    return;
+  }
+  if (nv <= kq && Q.nchunks > 1) {
+    // nothing to cut: every live candidate goes to k_topq as it is (k_topq sorts
+    // and dedupes the union of a query's lists; only a single-chunk query's list
+    // is final and must leave here sorted and deduped)
+    Cand* out = cand + b * (int64_t)kc;
+#pragma unroll
+    for (int s = 0; s < CHUNK_IPT; s++)
+      if ((vm >> s) & 1u) {
+        const int i = s * CHUNK_THREADS + tid;
+        const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
+        const uint32_t h = (uint32_t)Q.feat[e * FEAT_WORDS + 3];  // ByteArray.hashCode (ByteArray.java:80-84)
+        out[voff].k1 = a[s];
+        out[voff].k2 = ((uint64_t)(h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+        voff++;
+      }
+    if (tid == 0) cand_cnt[b] = nv;
     return;
   }
   const uint64_t T = nv > kq ? score_threshold(a, vm, kq, sHist, sSel, sRed, SCORE_CAP) : 0;
@@ -2170,7 +2188,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score_full(const RankQ* __res
 }
 
 // Top-k of a group of candidate lists (gn[g] <= 64 lists from list gbase[g];
-// each list sorted, deduped, <= its stride kc entries; k = gk[g]; the host sizes
+// each list <= its stride kc entries, in any order and not necessarily deduped --
+// the union is selected, sorted and deduped here; k = gk[g]; the host sizes
 // groups to <= CAP candidates), in rounds.  The group's candidates are staged in
 // LDS; a round takes the r = k - emitted largest remaining candidates by the full
 // 128-bit key (k1, k2) -- exact, keys are unique -- found by MSB-first radix
