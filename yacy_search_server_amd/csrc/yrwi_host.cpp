@@ -1064,7 +1064,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   sp = span_open(ctx, tm);
   // chunk order for k_score: every query's chunk 0, then every chunk 1, ... so that
   // a big query's later chunks run after its threshold is set (PruneP)
-  std::vector<int32_t> order((size_t)chunks);
+  std::vector<int32_t> order((size_t)chunks * 2);  // (chunk, query) pairs
   {
     // counting sort by chunk index c (stable in query order): O(chunks + max chunks)
     int64_t maxc = 0;
@@ -1074,10 +1074,13 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       for (int64_t c = 0; c < R.nchunks; c++) at[(size_t)c + 1]++;
     for (int64_t c = 0; c < maxc; c++) at[(size_t)c + 1] += at[(size_t)c];
     for (int qi = 0; qi < nq; qi++)
-      for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++)
-        order[(size_t)at[(size_t)c]++] = (int32_t)(chunk_base[(size_t)qi] + c);
+      for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++) {
+        const size_t o = (size_t)at[(size_t)c]++;
+        order[2 * o] = (int32_t)(chunk_base[(size_t)qi] + c);
+        order[2 * o + 1] = qi;
+      }
   }
-  int32_t* d_order = arena_alloc<int32_t>(ctx, chunks);
+  int32_t* d_order = arena_alloc<int32_t>(ctx, 2 * chunks);
   unsigned long long* d_tq = arena_alloc<unsigned long long>(ctx, nq);
   if (!d_order || !d_tq) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_order, order)) return YRWI_E_HIP;

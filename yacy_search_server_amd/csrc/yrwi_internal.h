@@ -240,7 +240,7 @@ int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* 
                   ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
-// chunks in d_order; d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip
+// chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
                  int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* stream);

@@ -923,9 +923,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   // element order: valid << 31 | od << 16 | p; one pad word per 32 so that the
   // thread-consecutive reads (stride CHUNK_IPT words) spread over the banks
   __shared__ uint32_t sPO[CHUNK + CHUNK / 32];
-  __shared__ uint32_t sSegP[CHUNK_THREADS * CHUNK_IPT];
-  __shared__ uint32_t sSegM[CHUNK_THREADS * CHUNK_IPT];
-  __shared__ uint32_t sSegL[CHUNK_THREADS * CHUNK_IPT];
+  __shared__ uint32_t sSegP[SEGC];  // the first SEGC fold segments (more: the summary overflows)
+  __shared__ uint32_t sSegM[SEGC];
+  __shared__ uint32_t sSegL[SEGC];
   __shared__ int32_t sFirstInfo[3];
 
   const int64_t b = blockIdx.x;
@@ -1044,15 +1044,21 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   }
   int32_t nsegTot;
   int32_t segOff = block_excl_sum256(nrec, sScan, &nsegTot);
-  // assemble segments in LDS (capacity CHUNK: every element could be a record)
+  // the first SEGC segments in LDS (a chunk with more keeps none: its summary
+  // overflows and k_shard_fin rewalks it)
+  int32_t segM = 0, segL = 0;  // this thread's share of M_rest / L_rest (max over every segment)
   {
     int32_t o = segOff;
 #pragma unroll
     for (int s = 0; s < CHUNK_IPT; s++) {
       if (isrec[s]) {
-        sSegP[o] = (uint32_t)P[s];
-        sSegM[o] = (uint32_t)recM[s];
-        sSegL[o] = recL[s];
+        if (o < SEGC) {
+          sSegP[o] = (uint32_t)P[s];
+          sSegM[o] = (uint32_t)recM[s];
+          sSegL[o] = recL[s];
+        }
+        segM = max(segM, recM[s]);
+        segL = max(segL, (int32_t)recL[s]);
         o++;
       }
     }
@@ -1060,20 +1066,26 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __syncthreads();
   // the continuation piece (elements before this thread's first record) belongs to segment segOff-1
   if (segOff > 0 && (accM > 0 || accL > 0)) {
-    atomicMax(&sSegM[segOff - 1], (uint32_t)accM);
-    if (accL > 0) atomicMax(&sSegL[segOff - 1], accL);
+    if (segOff - 1 < SEGC) {
+      atomicMax(&sSegM[segOff - 1], (uint32_t)accM);
+      if (accL > 0) atomicMax(&sSegL[segOff - 1], accL);
+    }
+    segM = max(segM, accM);
+    segL = max(segL, (int32_t)accL);
   }
   __syncthreads();
 
   // block reductions of the min/max fields
-  const int NI = 2 * NF + 4;
-  int32_t vals[2 * NF + 4];
+  const int NI = 2 * NF + 6;
+  int32_t vals[2 * NF + 6];
 #pragma unroll
   for (int f = 0; f < NF; f++) { vals[f] = wave_min_i(mn[f]); vals[NF + f] = wave_max_i(mx[f]); }
   vals[2 * NF + 0] = wave_min_i(vamn);
   vals[2 * NF + 1] = wave_max_i(vamx);
   vals[2 * NF + 2] = wave_max_i(pmax);
   vals[2 * NF + 3] = wave_sum_i(nval);
+  vals[2 * NF + 4] = wave_max_i(segM);
+  vals[2 * NF + 5] = wave_max_i(segL);
   tfmn = wave_min_d(tfmn);
   tfmx = wave_max_d(tfmx);
   if (lane == 0) {
@@ -1113,9 +1125,12 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       S.first = -1;
       S.p_first = S.od_first = S.a_first = 0;
     }
-    int32_t Mr = 0;
-    uint32_t Lkey = 0;
-    for (int i = 0; i < nsegTot; i++) { Mr = max(Mr, (int32_t)sSegM[i]); Lkey = max(Lkey, sSegL[i]); }
+    int32_t Mr = 0, Lk = 0;
+    for (int w = 0; w < 4; w++) {
+      Mr = max(Mr, sI[w * NI + 2 * NF + 4]);
+      Lk = max(Lk, sI[w * NI + 2 * NF + 5]);
+    }
+    const uint32_t Lkey = (uint32_t)Lk;
     S.M_rest = Mr;
     S.L_rest = (int32_t)(Lkey & 0xFFu);
     S.nseg = nsegTot;
@@ -2022,8 +2037,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
 #ifdef YRWI_PHASE_CLOCK
   if (threadIdx.x == 0 && blockIdx.x < PH_MAXB) g_ts[blockIdx.x * 8] = wall_clock64();
 #endif
-  const int64_t b = order[blockIdx.x];
-  const int qi = chunk_q[b];
+  const int2 ob = reinterpret_cast<const int2*>(order)[blockIdx.x];  // (chunk, its query): one load
+  const int64_t b = ob.x;
+  const int qi = ob.y;
   const RankQ& Q = qs[qi];
   const NormState& N = norm[qi];  // per-query constants: scalar loads
   if (tid == 0) {
@@ -2784,7 +2800,7 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_or
                      d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
   if (s0 < total_chunks)
     hipLaunchKernelGGL(k_score, dim3((unsigned)(total_chunks - s0)), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                       d_order + s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+                       d_order + 2 * s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
   const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
   hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
                      d_cand_cnt, kc, d_redo, d_nredo);
