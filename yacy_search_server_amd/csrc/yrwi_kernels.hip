@@ -908,6 +908,23 @@ __device__ __forceinline__ double wave_min_d(double v) {
 
 constexpr int32_t BIG = 0x7FFFFFFF;
 
+// Two 16-bit fields per word: min / max of both halves at once (v_pk_min_u16 /
+// v_pk_max_u16); every int field of a record fits 16 bits.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+constexpr int NP2 = (NF + 1) / 2;  // packed field pairs
+
+// termFrequency c / d (WordReferenceRow.java:355-357) as an exact fraction: c <= 255,
+// 1 <= d < 2^17, so c1 * d2 < 2^25 compares two of them without rounding, and the
+// double of the extreme fraction is the extreme double (division rounds monotonically)
+__device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int32_t d2) { return c1 * d2 < c2 * d1; }
+
+
 // One workgroup per CHUNK container elements.  Rows are read coalesced
 // (element s*256 + tid of the chunk), which is all the order-independent parts
 // need (min/max, tf, host counts); the order-dependent fold of posintext /
@@ -917,7 +934,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
   __shared__ int32_t sI[4 * (2 * NF + 8)];
-  __shared__ double sD[8];
   __shared__ int32_t sScan[4];
   __shared__ int32_t sFirst[4];
   // element order: valid << 31 | od << 16 | p; one pad word per 32 so that the
@@ -935,11 +951,11 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 
   // ---- coalesced pass: order-independent summaries
-  int32_t mn[NF], mx[NF];
+  uint32_t pmn[NP2], pmx[NP2];  // fields 2j | 2j+1 << 16
 #pragma unroll
-  for (int f = 0; f < NF; f++) { mn[f] = BIG; mx[f] = -1; }
+  for (int j = 0; j < NP2; j++) { pmn[j] = 0xFFFFFFFFu; pmx[j] = 0u; }
   int32_t pmax = -1, nval = 0, myfirst = BIG;
-  double tfmn = 1e300, tfmx = -1e300;
+  int32_t tcn = -1, tdn = 1, tcx = -1, tdx = 1;  // tf min / max as fractions (-1: none yet)
   int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
@@ -949,11 +965,27 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     av[s] = -1;
     uint32_t po = 0;
     if (v) {
+#ifdef YRWI_EXP_REDUCE_NOLOAD  // timing experiment only (inexact): synthetic records, no loads
+      Rec qx;
+      qx.w[0] = 0x0102030405060708ull * (uint64_t)(e | 1);
+      qx.w[1] = qx.w[0] ^ 0x1111111111111111ull;
+      qx.w[2] = qx.w[0] >> 7;
+      qx.w[3] = 0;
+      const Feat F = decode_rec(qx);
+#else
       const Feat F = decode_rec(load_rec(Q.feat, e));
+#endif
 #pragma unroll
-      for (int f = 0; f < NF; f++) { mn[f] = min(mn[f], F.f[f]); mx[f] = max(mx[f], F.f[f]); }
-      tfmn = fmin(tfmn, F.tf);
-      tfmx = fmax(tfmx, F.tf);
+      for (int j = 0; j < NP2; j++) {
+        const uint32_t w = (uint32_t)F.f[2 * j] | (2 * j + 1 < NF ? (uint32_t)F.f[2 * j + 1] << 16 : 0u);
+        pmn[j] = pk_min16(pmn[j], w);
+        pmx[j] = pk_max16(pmx[j], w);
+      }
+      {
+        const int32_t tc = F.f[F_HITCOUNT], td = F.f[F_WORDSINTEXT] + F.f[F_WORDSINTITLE] + 1;
+        if (tcn < 0 || frac_lt(tc, td, tcn, tdn)) { tcn = tc; tdn = td; }
+        if (tcx < 0 || frac_lt(tcx, tdx, tc, td)) { tcx = tc; tdx = td; }
+      }
       pmax = max(pmax, F.p);
       nval++;
       myfirst = min(myfirst, eo);
@@ -1075,47 +1107,88 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   }
   __syncthreads();
 
-  // block reductions of the min/max fields
-  const int NI = 2 * NF + 6;
-  int32_t vals[2 * NF + 6];
+  // block reductions: packed min/max pairs, the int summaries, the tf fractions
+  constexpr int NI = 2 * NP2 + 6 + 4;
+  int32_t vals[NI];
 #pragma unroll
-  for (int f = 0; f < NF; f++) { vals[f] = wave_min_i(mn[f]); vals[NF + f] = wave_max_i(mx[f]); }
-  vals[2 * NF + 0] = wave_min_i(vamn);
-  vals[2 * NF + 1] = wave_max_i(vamx);
-  vals[2 * NF + 2] = wave_max_i(pmax);
-  vals[2 * NF + 3] = wave_sum_i(nval);
-  vals[2 * NF + 4] = wave_max_i(segM);
-  vals[2 * NF + 5] = wave_max_i(segL);
-  tfmn = wave_min_d(tfmn);
-  tfmx = wave_max_d(tfmx);
+  for (int j = 0; j < NP2; j++) {
+    uint32_t x = pmn[j], y = pmx[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      x = pk_min16(x, (uint32_t)__shfl_xor((int)x, o, 64));
+      y = pk_max16(y, (uint32_t)__shfl_xor((int)y, o, 64));
+    }
+    vals[j] = (int32_t)x;
+    vals[NP2 + j] = (int32_t)y;
+  }
+  vals[2 * NP2 + 0] = wave_min_i(vamn);
+  vals[2 * NP2 + 1] = wave_max_i(vamx);
+  vals[2 * NP2 + 2] = wave_max_i(pmax);
+  vals[2 * NP2 + 3] = wave_sum_i(nval);
+  vals[2 * NP2 + 4] = wave_max_i(segM);
+  vals[2 * NP2 + 5] = wave_max_i(segL);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t c1 = __shfl_xor(tcn, o, 64), d1 = __shfl_xor(tdn, o, 64);
+    const int32_t c2 = __shfl_xor(tcx, o, 64), d2 = __shfl_xor(tdx, o, 64);
+    if (c1 >= 0 && (tcn < 0 || frac_lt(c1, d1, tcn, tdn))) { tcn = c1; tdn = d1; }
+    if (c2 >= 0 && (tcx < 0 || frac_lt(tcx, tdx, c2, d2))) { tcx = c2; tdx = d2; }
+  }
+  vals[2 * NP2 + 6] = tcn;
+  vals[2 * NP2 + 7] = tdn;
+  vals[2 * NP2 + 8] = tcx;
+  vals[2 * NP2 + 9] = tdx;
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < NI; i++) sI[wv * NI + i] = vals[i];
-    sD[wv] = tfmn;
-    sD[4 + wv] = tfmx;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    ChunkSum& S = out[b];
-    for (int f = 0; f < NF; f++) {
-      int32_t a = BIG, z = -1;
-      for (int w = 0; w < 4; w++) { a = min(a, sI[w * NI + f]); z = max(z, sI[w * NI + NF + f]); }
-      S.mn[f] = a;
-      S.mx[f] = z;
-    }
-    int32_t a = BIG, z = -1, pm = -1, nv = 0;
+  // the four waves combined in parallel, one summary field per thread
+  ChunkSum& S = out[b];
+  const int t = (int)threadIdx.x;
+  int32_t nvb = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) nvb += sI[w * NI + 2 * NP2 + 3];
+  if (t < NP2) {  // field pair t: min
+    uint32_t x = 0xFFFFFFFFu;
+    for (int w = 0; w < 4; w++) x = pk_min16(x, (uint32_t)sI[w * NI + t]);
+    S.mn[2 * t] = nvb ? (int32_t)(x & 0xFFFFu) : BIG;
+    if (2 * t + 1 < NF) S.mn[2 * t + 1] = nvb ? (int32_t)(x >> 16) : BIG;
+  } else if (t < 2 * NP2) {  // field pair t - NP2: max
+    const int j = t - NP2;
+    uint32_t y = 0u;
+    for (int w = 0; w < 4; w++) y = pk_max16(y, (uint32_t)sI[w * NI + NP2 + j]);
+    S.mx[2 * j] = nvb ? (int32_t)(y & 0xFFFFu) : -1;
+    if (2 * j + 1 < NF) S.mx[2 * j + 1] = nvb ? (int32_t)(y >> 16) : -1;
+  } else if (t == 2 * NP2) {
+    int32_t a = BIG, z = -1, pm = -1, Mr = 0, Lk = 0;
     for (int w = 0; w < 4; w++) {
-      a = min(a, sI[w * NI + 2 * NF]);
-      z = max(z, sI[w * NI + 2 * NF + 1]);
-      pm = max(pm, sI[w * NI + 2 * NF + 2]);
-      nv += sI[w * NI + 2 * NF + 3];
+      a = min(a, sI[w * NI + 2 * NP2]);
+      z = max(z, sI[w * NI + 2 * NP2 + 1]);
+      pm = max(pm, sI[w * NI + 2 * NP2 + 2]);
+      Mr = max(Mr, sI[w * NI + 2 * NP2 + 4]);
+      Lk = max(Lk, sI[w * NI + 2 * NP2 + 5]);
     }
     S.va_mn_rest = a;
     S.va_mx_rest = z;
     S.pmax = pm;
-    S.nvalid = nv;
-    S.tf_mn = fmin(fmin(sD[0], sD[1]), fmin(sD[2], sD[3]));
-    S.tf_mx = fmax(fmax(sD[4], sD[5]), fmax(sD[6], sD[7]));
+    S.nvalid = nvb;
+    S.M_rest = Mr;
+    S.L_rest = (int32_t)((uint32_t)Lk & 0xFFu);
+    S.nseg = nsegTot;
+    S.overflow = nsegTot > SEGC ? 1 : 0;
+  } else if (t == 2 * NP2 + 1) {
+    int32_t cn = -1, dn = 1, cx = -1, dx = 1;
+    for (int w = 0; w < 4; w++) {
+      const int32_t c1 = sI[w * NI + 2 * NP2 + 6], d1 = sI[w * NI + 2 * NP2 + 7];
+      const int32_t c2 = sI[w * NI + 2 * NP2 + 8], d2 = sI[w * NI + 2 * NP2 + 9];
+      if (c1 >= 0 && (cn < 0 || frac_lt(c1, d1, cn, dn))) { cn = c1; dn = d1; }
+      if (c2 >= 0 && (cx < 0 || frac_lt(cx, dx, c2, d2))) { cx = c2; dx = d2; }
+    }
+    // the same double WordReferenceRow.termFrequency computes (decode_rec)
+    S.tf_mn = cn >= 0 ? (double)cn / (double)dn : 1e300;
+    S.tf_mx = cx >= 0 ? (double)cx / (double)dx : -1e300;
+  } else if (t == 2 * NP2 + 2) {
     if (firstIdx != BIG) {
       S.first = (int32_t)(c * CHUNK + firstIdx);
       S.p_first = sFirstInfo[0];
@@ -1125,19 +1198,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       S.first = -1;
       S.p_first = S.od_first = S.a_first = 0;
     }
-    int32_t Mr = 0, Lk = 0;
-    for (int w = 0; w < 4; w++) {
-      Mr = max(Mr, sI[w * NI + 2 * NF + 4]);
-      Lk = max(Lk, sI[w * NI + 2 * NF + 5]);
-    }
-    const uint32_t Lkey = (uint32_t)Lk;
-    S.M_rest = Mr;
-    S.L_rest = (int32_t)(Lkey & 0xFFu);
-    S.nseg = nsegTot;
-    S.overflow = nsegTot > SEGC ? 1 : 0;
-    if (nsegTot <= SEGC)
-      for (int i = 0; i < nsegTot; i++)
-        S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
+  } else if (t >= 64 && t < 64 + SEGC) {
+    const int i = t - 64;
+    if (nsegTot <= SEGC && i < nsegTot) S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
   }
 }
 
