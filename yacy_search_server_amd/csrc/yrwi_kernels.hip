@@ -1143,23 +1143,36 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     for (int i = 0; i < NI; i++) sI[wv * NI + i] = vals[i];
   }
   __syncthreads();
-  // the four waves combined in parallel, one summary field per thread
+  // the four waves combined in parallel, one summary field per thread.  A query
+  // of one chunk gets its shard summary here too (the chunk's summary is the
+  // shard's; its fold pieces are the chunk's segments) unless the segments
+  // overflowed -- k_shard_fin skips it then (one = true).
   ChunkSum& S = out[b];
   const int t = (int)threadIdx.x;
   int32_t nvb = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) nvb += sI[w * NI + 2 * NP2 + 3];
+  const bool one = Q.nchunks == 1 && nsegTot <= SEGC;
+  ShardSum& SS = shard[qi];
   if (t < NP2) {  // field pair t: min
     uint32_t x = 0xFFFFFFFFu;
     for (int w = 0; w < 4; w++) x = pk_min16(x, (uint32_t)sI[w * NI + t]);
     S.mn[2 * t] = nvb ? (int32_t)(x & 0xFFFFu) : BIG;
     if (2 * t + 1 < NF) S.mn[2 * t + 1] = nvb ? (int32_t)(x >> 16) : BIG;
+    if (one) {
+      SS.mn[2 * t] = S.mn[2 * t];
+      if (2 * t + 1 < NF) SS.mn[2 * t + 1] = S.mn[2 * t + 1];
+    }
   } else if (t < 2 * NP2) {  // field pair t - NP2: max
     const int j = t - NP2;
     uint32_t y = 0u;
     for (int w = 0; w < 4; w++) y = pk_max16(y, (uint32_t)sI[w * NI + NP2 + j]);
     S.mx[2 * j] = nvb ? (int32_t)(y & 0xFFFFu) : -1;
     if (2 * j + 1 < NF) S.mx[2 * j + 1] = nvb ? (int32_t)(y >> 16) : -1;
+    if (one) {
+      SS.mx[2 * j] = S.mx[2 * j];
+      if (2 * j + 1 < NF) SS.mx[2 * j + 1] = S.mx[2 * j + 1];
+    }
   } else if (t == 2 * NP2) {
     int32_t a = BIG, z = -1, pm = -1, Mr = 0, Lk = 0;
     for (int w = 0; w < 4; w++) {
@@ -1177,6 +1190,13 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     S.L_rest = (int32_t)((uint32_t)Lk & 0xFFu);
     S.nseg = nsegTot;
     S.overflow = nsegTot > SEGC ? 1 : 0;
+    if (one) {
+      SS.nvalid = nvb;
+      SS.va_mn_rest = a;
+      SS.va_mx_rest = z;
+      SS.nseg = nvb ? nsegTot : 0;
+      SS.overflow = 0;
+    }
   } else if (t == 2 * NP2 + 1) {
     int32_t cn = -1, dn = 1, cx = -1, dx = 1;
     for (int w = 0; w < 4; w++) {
@@ -1188,6 +1208,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     // the same double WordReferenceRow.termFrequency computes (decode_rec)
     S.tf_mn = cn >= 0 ? (double)cn / (double)dn : 1e300;
     S.tf_mx = cx >= 0 ? (double)cx / (double)dx : -1e300;
+    if (one) {
+      SS.tf_mn = S.tf_mn;
+      SS.tf_mx = S.tf_mx;
+    }
   } else if (t == 2 * NP2 + 2) {
     if (firstIdx != BIG) {
       S.first = (int32_t)(c * CHUNK + firstIdx);
@@ -1198,9 +1222,18 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       S.first = -1;
       S.p_first = S.od_first = S.a_first = 0;
     }
+    if (one) {
+      SS.has_first = nvb > 0;
+      SS.p_first = S.p_first;
+      SS.od_first = S.od_first;
+      SS.a_first = S.a_first;
+    }
   } else if (t >= 64 && t < 64 + SEGC) {
     const int i = t - 64;
-    if (nsegTot <= SEGC && i < nsegTot) S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
+    if (nsegTot <= SEGC && i < nsegTot) {
+      S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
+      if (one && nvb) SS.seg[i] = S.seg[i];
+    }
   }
 }
 
@@ -1297,6 +1330,7 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
   const ChunkSum* C = cs + chunk_base[qi];
   const int64_t nc = Q.nchunks;
   ShardSum& S = out[qi];
+  if (nc == 1 && !C[0].overflow) return;  // k_reduce wrote this one (one chunk, no overflow)
 
   // ---- min / max / counts / first chunk, one pass.  virtualAge over the shard's
   // rest = chunk rests + first elements of every chunk but the shard's first: each
