@@ -169,19 +169,27 @@ def test_j3_dispatch_int_wrap():
     _run_pair(d, [([b"DISPlistA___", b"DISPlistB___"], [])], k=300)
 
 
-@pytest.mark.parametrize("R", [0, 1, 4095, 4096, 4097])
+@pytest.mark.parametrize("R", [0, 1, 4095, 4096, 4097, 40_000, 131_072, 131_200, 600_000, 4_200_000])
 def test_probe_range_around_lds_threshold(R, monkeypatch):
     """One probe tile (256 small-list ids) whose large-list range holds R ids
-    (YRWI_PROBE_RATIO=1 forces probing): R <= 4096 is searched in LDS, 4097 by
-    gathers; R = 0: no small id falls inside the large list."""
+    (YRWI_PROBE_RATIO=1 forces probing): R <= 4096 is searched in LDS; longer
+    ranges search the list's line heads in LDS -- level 1 (every 32nd id) up to
+    4096 heads (R ~ 131k), level 2 (every 1024th) up to ~4.19 M ids -- and the
+    4.2 M range falls back to the global binary search.  Keys sit on, just
+    after and just before line-head positions (32 / 1024 ids); R = 0: no small
+    id falls inside the large list."""
     monkeypatch.setenv("YRWI_PROBE_RATIO", "1")
-    large = np.arange(100_000, 100_000 + 20_000, dtype=np.int64) * 4
+    lo = 1000
+    large = np.arange(100_000, 100_000 + max(20_000, lo + R + 2000), dtype=np.int64) * 4
     if R == 0:
         small = np.arange(256, dtype=np.int64) * 4 + 1          # below the large list, no match
     else:
-        lo = 1000
         span = large[lo:lo + R]
-        pick = np.unique(np.concatenate([[0, R - 1], np.linspace(0, R - 1, 256).astype(np.int64)]))
+        pos = lo + np.arange(R)
+        edge = np.flatnonzero((pos % 1024 <= 1) | (pos % 1024 == 1023) | (pos % 32 <= 1) | (pos % 32 == 31))
+        pick = np.unique(np.concatenate([[0, R - 1], np.linspace(0, R - 1, 64).astype(np.int64),
+                                         edge[np.linspace(0, len(edge) - 1, 60).astype(np.int64)] if len(edge) else []]))
+        pick = pick.astype(np.int64)
         small = np.unique(np.concatenate([span[pick], span[pick][:-1] + 1]))[:256]  # hits and misses
         small = np.sort(small)
         assert small[0] == span[0] and (R == 1 or small[-1] <= span[-1])

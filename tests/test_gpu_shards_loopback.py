@@ -215,3 +215,37 @@ def test_loopback_exclude_term_absent_from_a_shard():
         exp = orc.search(whole, i, e, now_ms=NOW, k=100)
         for r in range(world):
             assert [(h.urlhash, h.score, h.tiebreak) for h in res[r][qi]] == exp, (r, qi)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_async_batches_in_flight(world):
+    """Sharded contexts run two lanes: several submitted batches per rank are in
+    flight at once, each lane with its own group, and the batch parts enqueue
+    their collectives in submission order (CollTurn).  Batches of different
+    sizes and shapes (3-4 terms: fold-step size exchanges; authority profile:
+    host-count exchange; an empty batch) must all come back bit-exact."""
+    full = synth.preset("small")
+    whole_ix = synth.build_index(full)
+    whole, H = whole_ix.as_dict(), whole_ix.hashes
+    c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+    sets = [synth.queries(full, n, 1, 4, 1, qseed=90 + i) if n else [] for i, n in enumerate([12, 5, 0, 20, 9, 3])]
+
+    def prof(i, j):
+        return c5 if (i + j) % 3 == 0 else None
+
+    def fn(r, ix):
+        pend = [ix.submit([Query([H[t] for t in inc], [H[t] for t in exc], now_ms=NOW, k=100, profile=prof(i, j))
+                           for j, (inc, exc) in enumerate(qs)]) for i, qs in enumerate(sets)]
+        return [p.result() for p in pend]
+
+    parts = [synth.build_index(full.shard(r, world)).as_dict() for r in range(world)]
+    res = _run_parts(parts, world, fn)
+    for i, qs in enumerate(sets):
+        exp = [orc.search(whole, [H[t] for t in inc], [H[t] for t in exc],
+                          profile=(orc.profile_from(prof(i, j)) if prof(i, j) else None), now_ms=NOW, k=100)
+               for j, (inc, exc) in enumerate(qs)]
+        for r in range(world):
+            got = res[r][i]
+            assert len(got) == len(qs), (r, i)
+            for j, g in enumerate(got):
+                assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp[j], (r, i, j)

@@ -110,7 +110,31 @@ static int loop_round(Lane* L, const void* send, size_t bytes, const std::vector
   return rc;
 }
 
+void turn_acquire(Lane* L) {
+  if (!L->turn || L->seq < 0 || L->turn_held) return;
+  std::unique_lock<std::mutex> lk(L->turn->mu);
+  L->turn->cv.wait(lk, [L] { return L->turn->next == L->seq; });
+  L->turn_held = true;
+}
+
+void turn_release(Lane* L) {
+  if (!L->turn || L->seq < 0 || L->world <= 1) {  // one context: no collectives to order
+    L->seq = -1;
+    return;
+  }
+  {
+    std::unique_lock<std::mutex> lk(L->turn->mu);
+    // a part that never held the turn still passes it, in order
+    L->turn->cv.wait(lk, [L] { return L->turn->next == L->seq; });
+    L->turn->next = L->seq + 1;
+  }
+  L->turn->cv.notify_all();
+  L->seq = -1;
+  L->turn_held = false;
+}
+
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
+  if (L->world > 1) turn_acquire(L);
   if (L->world <= 1) {
     if (hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, L->stream) != hipSuccess)
       return L->fail(YRWI_E_HIP, "copy");
@@ -135,6 +159,7 @@ int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
 
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op) {
   if (L->world <= 1 || n == 0) return 0;
+  turn_acquire(L);
   if (!L->loop) {
     if (ncclAllReduce(buf, buf, n, ncclInt32, max_op ? ncclMax : ncclSum, L->comm, L->stream) != ncclSuccess)
       return L->fail(YRWI_E_RCCL, "allreduce");
@@ -148,6 +173,7 @@ int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op) {
 }
 
 int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) {
+  turn_acquire(L);
   if (!L->loop) {
     if (ncclGroupStart() != ncclSuccess) return L->fail(YRWI_E_RCCL, "group");
     for (const Xfer& x : sends)

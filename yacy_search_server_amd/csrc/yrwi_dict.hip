@@ -64,6 +64,42 @@ __global__ void k_dict_scatter(const uint32_t* __restrict__ rank1, const uint32_
   if (j < n) uid[pos[j]] = rank1[j] - 1u;
 }
 
+// the ids of the concatenated lists -> uid_all, whose list slices start on 128-B
+// lines: one workgroup per PAD_CHUNK ids of one list (host-built descriptors)
+constexpr int PAD_CHUNK = 4096;
+struct PadChunk {
+  int64_t src, dst;
+  int32_t n, pad;
+};
+__global__ __launch_bounds__(256) void k_pad_copy(const PadChunk* __restrict__ ch, const uint32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ dst) {
+  const PadChunk c = ch[blockIdx.x];
+  for (int x = threadIdx.x; x < c.n; x += 256) dst[c.dst + x] = src[c.src + x];
+}
+
+// Line heads of every list (DList::head): level 1 = the first id of each 32-id
+// line, level 2 = every 32nd level-1 head.  k_probe searches the heads of a
+// probe tile's range in LDS and then reads one leaf line per key.
+struct HeadSeg {
+  const uint32_t* uid;
+  uint32_t* head;
+  int64_t n;
+};
+__global__ void k_heads(const HeadSeg* __restrict__ segs, const int64_t* __restrict__ hoff, int nseg, int64_t nh) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nh) return;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (hoff[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const HeadSeg S = segs[lo];
+  const int64_t g = i - hoff[lo];
+  const int64_t c1 = head1_cap(S.n);
+  if (g < head1_n(S.n)) S.head[g] = S.uid[g << 5];
+  else if (g >= c1 && g - c1 < head2_n(S.n)) S.head[g] = S.uid[(g - c1) << 10];
+}
+
 // the key of every url id: the first posting of each run of equal keys
 __global__ void k_dict_keys(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rank1,
                             const uint64_t* __restrict__ kh, const uint8_t* __restrict__ kl,
@@ -205,6 +241,27 @@ struct DevBuf {
   }
 };
 
+__global__ void k_heads_check(const HeadSeg* __restrict__ segs, const int64_t* __restrict__ hoff, int nseg,
+                              int64_t nh, unsigned long long* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nh) return;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (hoff[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const HeadSeg S = segs[lo];
+  const int64_t g = i - hoff[lo];
+  const int64_t c1 = head1_cap(S.n);
+  if (S.head == nullptr) {
+    if (g == 0) atomicAdd(bad, 1ull);
+  } else if (g < head1_n(S.n)) {
+    if (S.head[g] != S.uid[g << 5]) atomicAdd(bad, 1ull);
+  } else if (g >= c1 && g - c1 < head2_n(S.n)) {
+    if (S.head[g] != S.uid[(g - c1) << 10]) atomicAdd(bad, 1ull);
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -218,6 +275,8 @@ struct SortedKeys {
   uint32_t *pos = nullptr, *flag = nullptr, *rank1 = nullptr;
   int64_t n = 0;
   uint32_t ndistinct = 0;
+  int nseg = 0;
+  const int64_t* d_off = nullptr;  // first posting of every list (concatenation order)
 };
 
 int sort_keys(CtxBase* ctx, const std::vector<ListRec*>& lists, SortedKeys& K) {
@@ -231,6 +290,7 @@ int sort_keys(CtxBase* ctx, const std::vector<ListRec*>& lists, SortedKeys& K) {
     n += L->n;
   }
   K.n = n;
+  K.nseg = (int)segs.size();
   DictSeg* d_segs = K.bsegs.get<DictSeg>(segs.size());
   int64_t* d_off = K.boff.get<int64_t>(off.size());
   uint64_t* kh = K.bkh.get<uint64_t>((size_t)n);
@@ -262,6 +322,7 @@ int sort_keys(CtxBase* ctx, const std::vector<ListRec*>& lists, SortedKeys& K) {
   HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp, t3, flag, rank1, ni, st));
   HIPCHK(ctx, hipMemcpyAsync(&K.ndistinct, rank1 + (n - 1), 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  K.d_off = d_off;
   K.kh = kh;
   K.kl = kl;
   K.pos = pos;
@@ -279,22 +340,39 @@ void publish_dict(CtxBase* ctx) {
 
 int full_rebuild(CtxBase* ctx, const std::vector<ListRec*>& lists, int64_t n) {
   hipStream_t st = ctx->stream;
-  if (n > 0 && (size_t)n > ctx->uid_cap) {
+  std::vector<int64_t> poff;
+  int64_t np = 0;
+  for (ListRec* L : lists) {
+    poff.push_back(np);
+    np += (L->n + 31) & ~(int64_t)31;  // slices start on 128-B lines
+  }
+  if (np > 0 && (size_t)np > ctx->uid_cap) {
     if (ctx->uid_all) hipFree(ctx->uid_all);
     ctx->uid_all = nullptr;
     ctx->uid_cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&ctx->uid_all), (size_t)n * 4) != hipSuccess)
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->uid_all), (size_t)np * 4) != hipSuccess)
       return ctx->fail(YRWI_E_NOMEM, "url id allocation");
-    ctx->uid_cap = (size_t)n;
+    ctx->uid_cap = (size_t)np;
   }
-  int64_t o = 0;
-  for (ListRec* L : lists) {
-    L->uid = ctx->uid_all + o;
-    o += L->n;
-  }
+  for (size_t s = 0; s < lists.size(); s++) lists[s]->uid = ctx->uid_all + poff[s];
   SortedKeys K;
   if (int rc = sort_keys(ctx, lists, K)) return rc;
-  hipLaunchKernelGGL(k_dict_scatter, dim3(nb(n)), dim3(256), 0, st, K.rank1, K.pos, n, ctx->uid_all);
+  // ids in concatenation order, then copied into the line-aligned slices
+  std::vector<PadChunk> chunks;
+  int64_t o = 0;
+  for (size_t s = 0; s < lists.size(); s++) {
+    for (int64_t x = 0; x < lists[s]->n; x += PAD_CHUNK)
+      chunks.push_back({o + x, poff[s] + x, (int32_t)std::min<int64_t>(PAD_CHUNK, lists[s]->n - x), 0});
+    o += lists[s]->n;
+  }
+  DevBuf btmp, bch;
+  uint32_t* d_tmp = btmp.get<uint32_t>((size_t)n);
+  PadChunk* d_ch = bch.get<PadChunk>(chunks.size());
+  if (!d_tmp || !d_ch) return ctx->fail(YRWI_E_NOMEM, "url dictionary scratch");
+  HIPCHK(ctx, hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(PadChunk), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_dict_scatter, dim3(nb(n)), dim3(256), 0, st, K.rank1, K.pos, n, d_tmp);
+  if (!chunks.empty())
+    hipLaunchKernelGGL(k_pad_copy, dim3((unsigned)chunks.size()), dim3(256), 0, st, d_ch, d_tmp, ctx->uid_all);
   const uint32_t nurls = K.ndistinct;
   if ((size_t)nurls > ctx->dict_cap) {
     HIPCHK(ctx, hipStreamSynchronize(st));
@@ -426,6 +504,42 @@ int incremental(CtxBase* ctx, const std::vector<ListRec*>& changed, const std::v
   return 0;
 }
 
+// every list's line heads, after its url ids changed (all of them shift on an
+// incremental update that adds keys): one pass of n/32 + n/1024 id reads
+int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
+  hipStream_t st = ctx->stream;
+  std::vector<HeadSeg> segs;
+  std::vector<int64_t> hoff;
+  int64_t nh = 0;
+  for (ListRec* L : lists) {
+    hoff.push_back(nh);
+    nh += heads_cap(L->n);
+  }
+  if (nh == 0) return 0;
+  if ((size_t)nh > ctx->head_cap) {
+    if (ctx->head_all) hipFree(ctx->head_all);
+    ctx->head_all = nullptr;
+    ctx->head_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->head_all), (size_t)nh * 4) != hipSuccess)
+      return ctx->fail(YRWI_E_NOMEM, "line head allocation");
+    ctx->head_cap = (size_t)nh;
+  }
+  for (size_t s = 0; s < lists.size(); s++) {
+    lists[s]->head = ctx->head_all + hoff[s];
+    segs.push_back({lists[s]->uid, lists[s]->head, lists[s]->n});
+  }
+  DevBuf bsegs, boff;
+  HeadSeg* d_segs = bsegs.get<HeadSeg>(segs.size());
+  int64_t* d_off = boff.get<int64_t>(hoff.size());
+  if (!d_segs || !d_off) return ctx->fail(YRWI_E_NOMEM, "line head scratch");
+  HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(HeadSeg), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_off, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_heads, dim3(nb(nh)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), nh);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));  // scratch is freed on return
+  return 0;
+}
+
 }  // namespace
 
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
@@ -474,6 +588,10 @@ int ensure_url_ids(CtxBase* ctx) {
     ctx->dict_valid = false;  // the next call rebuilds in full
     return rc;
   }
+  if ((rc = build_heads(ctx, lists))) {
+    ctx->dict_valid = false;
+    return rc;
+  }
   ctx->dict_pending.clear();
   ctx->uid_dirty = false;
   return 0;
@@ -503,6 +621,24 @@ int check_url_ids(CtxBase* ctx, int64_t* bad) {
   HIPCHK(ctx, hipMemsetAsync(d_bad, 0, 8, st));
   hipLaunchKernelGGL(k_uid_check, dim3(nb(m)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), n, ctx->dkhi,
                      ctx->dklo, ctx->nurls, d_bad);
+  // every list's line heads name the ids they copy (k_probe relies on them)
+  std::vector<HeadSeg> hsegs;
+  std::vector<int64_t> hoff;
+  int64_t nh = 0;
+  for (ListRec* L : lists) {
+    hsegs.push_back({L->uid, L->head, L->n});
+    hoff.push_back(nh);
+    nh += heads_cap(L->n);
+  }
+  DevBuf bh, bho;
+  if (nh > 0) {
+    HeadSeg* d_h = bh.get<HeadSeg>(hsegs.size());
+    int64_t* d_ho = bho.get<int64_t>(hoff.size());
+    if (!d_h || !d_ho) return ctx->fail(YRWI_E_NOMEM, "check scratch");
+    HIPCHK(ctx, hipMemcpyAsync(d_h, hsegs.data(), hsegs.size() * sizeof(HeadSeg), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_ho, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_heads_check, dim3(nb(nh)), dim3(256), 0, st, d_h, d_ho, (int)hsegs.size(), nh, d_bad);
+  }
   unsigned long long hb = 0;
   HIPCHK(ctx, hipMemcpyAsync(&hb, d_bad, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));

@@ -162,10 +162,10 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   ctx->device = device;
   ctx->rank = rank;
   ctx->world = world;
-  // Sharded contexts default to one lane: collectives of concurrently running
-  // communicators on the same GPUs are not ordered against each other.
+  // Two lanes, sharded or not: the collectives of the lanes' batch parts are
+  // enqueued in one total order on every rank (CollTurn, yrwi_host.h).
   const char* e = getenv("YRWI_LANES");
-  const int nl = e ? std::max(1, std::min(8, atoi(e))) : (world > 1 ? 1 : 2);
+  const int nl = e ? std::max(1, std::min(8, atoi(e))) : 2;
   for (int l = 0; l < nl; l++) {
     Lane* L = new Lane();
     L->device = device;
@@ -182,6 +182,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
       return YRWI_E_HIP;
     }
     L->hostreg = &ctx->hostreg;
+    L->turn = &ctx->turn;
     L->start_worker();
   }
   ctx->stream = ctx->lanes[0]->stream;
@@ -235,6 +236,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   close_lanes(ctx);
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
+  if (ctx->head_all) hipFree(ctx->head_all);
   if (ctx->dkhi) hipFree(ctx->dkhi);
   if (ctx->dklo) hipFree(ctx->dklo);
   delete ctx;
@@ -1212,6 +1214,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     span_close(ctx, tm, sp);
     if (int rc = coll_allgather(ctx, d_mine, d_allh, sizeof(yrwi_hit) * (size_t)nq * kint)) return rc;
     if (int rc = coll_allgather(ctx, d_mcnt, d_alln, sizeof(int32_t) * (size_t)nq)) return rc;
+    if (ctx->release_after_final) turn_release(ctx);  // the next batch part's collectives may follow now
     sp = span_open(ctx, tm);
     if (launch_gmerge(d_q, d_allh, d_alln, W, nq, kint, d_slot, d_dup, d_stack, d_scnt, ctx->stream) ||
         launch_pull(d_q, nq, d_stack, d_scnt, kint, 0, kmax, d_hits, d_nout, ctx->stream))
@@ -1281,6 +1284,8 @@ static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q,
                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   L->enter();
   const int rc = run_batch_part_(ix, L, q, nq, kmax, out, nout, st);
+  turn_release(L);  // error paths, parts without collectives: the turn still passes in order
+  L->release_after_final = false;
   L->leave();
   return rc;
 }
@@ -1313,6 +1318,7 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
       g1++;
     }
     std::vector<Plan> plans(std::make_move_iterator(all.begin() + g0), std::make_move_iterator(all.begin() + g1));
+    L->release_after_final = g1 >= nq;
     if (begin_pass(L)) return YRWI_E_HIP;
     // HIP events (per-kernel timing) only when the caller asked for statistics
     Timing tm;
@@ -1401,6 +1407,9 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   std::vector<yrwi_stats> pst((size_t)nl);
   for (auto& p : pst) std::memset(&p, 0, sizeof(p));
   auto cut = [&](int l) { return (int32_t)((int64_t)nq * l / nl); };
+  const int64_t seq0 = ctx->coll_seq;  // collective order of the parts (CollTurn)
+  ctx->coll_seq += nl;
+  for (int l = 0; l < nl; l++) ctx->lanes[(size_t)l]->seq = seq0 + l;
   auto part = [=, &pst](int l) {
     Lane* L = ctx->lanes[(size_t)l];
     L->rc = run_batch_part(ctx, L, q + cut(l), cut(l + 1) - cut(l), kmax, out + (size_t)cut(l) * kmax, nout + cut(l),
@@ -1453,9 +1462,11 @@ extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, 
   Lane* L = ctx->lanes[(size_t)(t % (int64_t)ctx->lanes.size())];
   L->wait();  // the lane's previous batch (its status is already recorded)
   ctx->next_ticket++;
+  L->seq = ctx->coll_seq++;  // collective order (CollTurn): submission order, the same on every rank
   L->submit([=] {
     if (st) std::memset(st, 0, sizeof(*st));
     const int rc = nq == 0 ? 0 : run_batch_part(ctx, L, q, nq, kmax, out, nout, st);
+    turn_release(L);  // nq == 0: nothing ran, the turn passes all the same
     {
       std::lock_guard<std::mutex> lk(ctx->st_mu);
       ctx->status[t] = {rc, rc ? L->err : std::string()};

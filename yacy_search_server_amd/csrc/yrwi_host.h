@@ -78,7 +78,8 @@ struct ListRec {
   int64_t n = 0;
   uint32_t* uid = nullptr;  // url ids (rebuilt with the url dictionary)
   uint64_t* feat = nullptr; // ranking records (built with the url dictionary)
-  DList dl() const { return DList{khi, klo, rows, n, uid, feat}; }
+  uint32_t* head = nullptr; // line heads of uid (DList::head; rebuilt with the url ids)
+  DList dl() const { return DList{khi, klo, rows, n, uid, feat, head}; }
 };
 
 // device-wide allocation events (hipMalloc / hipFree / hipHostMalloc / hipHostFree
@@ -197,6 +198,21 @@ struct HostRegistry {
 
 struct LoopGroup;  // in-process shard group (yrwi_coll.cpp)
 
+// Order of the collectives of concurrently running batch parts (sharded
+// contexts).  Every batch part gets a sequence number in
+// submission order -- the same on every rank, since the ranks submit the same
+// batches -- and may enqueue its collectives only once the part before it has
+// enqueued its last one (CollTurn::next == its number).  So every rank enqueues
+// all collectives in one total order, (part, step), whatever the timing of its
+// lane threads: no rank can wait inside one communicator's collective for a
+// peer that is blocked behind another's, even when both lanes' streams land on
+// one hardware queue.
+struct CollTurn {
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t next = 0;
+};
+
 // One execution lane: a HIP stream with its own scratch arena, pinned staging,
 // events and (sharded) communicator.  A batch is split over the lanes and each
 // lane runs its part from its own host thread, so one lane's host planning and
@@ -232,6 +248,12 @@ struct Lane {
   bool active = false, reserving = false;
   int rc = 0;
   int64_t wait_ns = 0;  // host time spent waiting for this lane's device work (lane_sync)
+  // collective order (CollTurn): the running part's sequence number (-1: none,
+  // unordered), whether it holds the turn, and whether its last pass passes the
+  // turn on right after its final collective
+  CollTurn* turn = nullptr;
+  int64_t seq = -1;
+  bool turn_held = false, release_after_final = false;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -311,6 +333,9 @@ struct CtxBase {
   HostRegistry hostreg;
   // asynchronous batches: ticket t runs on lane t % lanes; finished status by ticket
   int64_t next_ticket = 0;
+  // collective order of batch parts (sequence numbers handed out by the caller's thread)
+  CollTurn turn;
+  int64_t coll_seq = 0;
   std::mutex st_mu;
   std::unordered_map<int64_t, std::pair<int, std::string>> status;
   std::unordered_map<KeyT, ListRec, KeyHash> lists;
@@ -318,8 +343,10 @@ struct CtxBase {
   // url dictionary (yrwi_dict.hip): every list's uid array is a slice of uid_all;
   // rebuilt before the next query after any list changed
   bool uid_dirty = true;
-  uint32_t* uid_all = nullptr;
+  uint32_t* uid_all = nullptr;   // list slices start on 128-B lines (32 ids)
   size_t uid_cap = 0;
+  uint32_t* head_all = nullptr;  // every list's line heads (DList::head)
+  size_t head_cap = 0;
   uint64_t* dkhi = nullptr;  // key of every url id (72-bit Base64 key: hi 64 bits, low byte)
   uint8_t* dklo = nullptr;
   size_t dict_cap = 0;
@@ -436,6 +463,8 @@ void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added);
 // brings the url ids up to date, then counts inconsistencies (0: every id names its key)
 int check_url_ids(CtxBase* ctx, int64_t* bad);
 
+void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)
+void turn_release(Lane* L);  // pass the turn to the next part (waits for L's turn first); idempotent
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op);    // in place; sum or max
 int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs);  // grouped send/recv

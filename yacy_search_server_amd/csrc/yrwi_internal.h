@@ -41,7 +41,16 @@ struct DList {
   int64_t n;
   const uint32_t* uid;
   const uint64_t* feat;  // FEAT_WORDS words per posting: the ranking record (FeatRec below)
+  // line heads of an index list (yrwi_dict.hip, k_heads), nullptr for joined
+  // containers: head[g] = uid[32 g] (the first id of every 128-B line of uid),
+  // then, at head + head1_cap(n), head[32 g] again every 32nd: uid[1024 g]
+  const uint32_t* head;
 };
+// the two head levels of a list of n postings (each level padded to 32 entries)
+__host__ __device__ constexpr int64_t head1_n(int64_t n) { return (n + 31) >> 5; }
+__host__ __device__ constexpr int64_t head1_cap(int64_t n) { return (head1_n(n) + 31) & ~(int64_t)31; }
+__host__ __device__ constexpr int64_t head2_n(int64_t n) { return (n + 1023) >> 10; }
+__host__ __device__ constexpr int64_t heads_cap(int64_t n) { return head1_cap(n) + ((head2_n(n) + 31) & ~(int64_t)31); }
 
 // The ranking record of a posting, 32 bytes (4 little-endian words), built from
 // its WordReferenceRow (WordReferenceRow.java:49-72) by k_features and carried

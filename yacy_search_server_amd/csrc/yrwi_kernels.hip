@@ -526,6 +526,71 @@ __device__ __forceinline__ int64_t lower_bound_uid(const uint32_t* __restrict__ 
   return lo;
 }
 
+// lower bound of `key` in an index list with line heads: binary search over the
+// level-2 heads (n/1024 ids, shared by every search of the list: L2 hits), then
+// one line of level-1 heads and one leaf line
+__device__ __forceinline__ int64_t lower_bound_list(const DList& L, uint32_t key) {
+  const uint32_t* __restrict__ h2 = L.head + head1_cap(L.n);
+  const int64_t n2 = head2_n(L.n);
+  const int64_t a = lower_bound_uid(h2, 0, n2, key);  // first level-2 head >= key
+  int64_t wl = a > 0 ? ((a - 1) << 10) + 1 : 0, wr = a < n2 ? (a << 10) : L.n;
+  const int64_t f0 = (wl + 31) >> 5, f1 = (wr + 31) >> 5;
+  const int64_t c = lower_bound_uid(L.head, f0, f1, key);
+  if (c > f0) wl = ((c - 1) << 5) + 1;
+  if (c < f1) wr = c << 5;
+  return lower_bound_uid(L.uid, wl, wr, key);
+}
+
+#if PROBE_LDS > 0
+// A probe tile whose large-list range [lo, hi) is longer than PROBE_LDS ids:
+// the level-1 line heads of the range (first id of every 32-id line, DList::head)
+// -- or, past PROBE_LDS of those, the level-2 heads (every 1024th id) -- are
+// staged in LDS with one coalesced read, each key finds the first head >= it
+// there, and the lower bound lies between that head and the one before: one
+// line of level-1 heads (level 2 only) and one 128-B leaf line of ids per key,
+// instead of a global binary search of log2(range) dependent loads.  Returns
+// false (nothing read, no barrier) when the list has no heads or the range
+// needs more than two levels; the decision is uniform over the workgroup.
+// `kp` = the thread's small-list key (nullptr: no key).
+__device__ __forceinline__ bool probe_heads(const DList& Lg, int64_t lo, int64_t hi, uint32_t* __restrict__ sL,
+                                            uint32_t& key, const uint32_t* kp, int64_t* jl, bool* hit) {
+  if (Lg.head == nullptr) return false;
+  int sh = 5;
+  const uint32_t* __restrict__ hd = Lg.head;
+  int64_t g0 = (lo + 31) >> 5, g1 = (hi + 31) >> 5;  // heads at positions in [lo, hi)
+  if (g1 - g0 > PROBE_LDS) {
+    sh = 10;
+    hd = Lg.head + head1_cap(Lg.n);
+    g0 = (lo + 1023) >> 10;
+    g1 = (hi + 1023) >> 10;
+    if (g1 - g0 > PROBE_LDS) return false;
+  }
+  const int H = (int)(g1 - g0);
+  for (int x = threadIdx.x; x < H; x += PROBE_TILE) sL[x] = hd[g0 + x];
+  if (kp) key = *kp;
+  __syncthreads();
+  if (!kp) return true;
+  int a = 0, b = H;  // first staged head >= key
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (sL[mid] < key) a = mid + 1; else b = mid;
+  }
+  // the lower bound is in (position of head a-1, position of head a], within [lo, hi]
+  int64_t wl = a > 0 ? ((g0 + a - 1) << sh) + 1 : lo;
+  int64_t wr = a < H ? ((g0 + a) << sh) : hi;
+  if (sh == 10) {  // narrow to one leaf line with the <= 32 level-1 heads inside [wl, wr)
+    const int64_t f0 = (wl + 31) >> 5, f1 = (wr + 31) >> 5;
+    const int64_t c = lower_bound_uid(Lg.head, f0, f1, key);
+    if (c > f0) wl = ((c - 1) << 5) + 1;
+    if (c < f1) wr = c << 5;
+  }
+  const int64_t p = lower_bound_uid(Lg.uid, wl, wr, key);
+  *jl = p;
+  *hit = p < hi && Lg.uid[p] == key;
+  return true;
+}
+#endif
+
 __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
                              int64_t tile0, int64_t ntiles, ProbeDesc* __restrict__ pdesc) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -537,6 +602,15 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const int64_t s0 = (tile0 + t - tile_base[j]) * PROBE_TILE;
   const int64_t s1 = s0 + PROBE_TILE < Sm.n ? s0 + PROBE_TILE : Sm.n;
   const uint32_t k0 = Sm.uid[s0], k1 = Sm.uid[s1 - 1];
+  ProbeDesc D;
+  D.job = j;
+  D.pad = 0;
+  if (Lg.head) {  // index list: through its line heads (level 2, one level-1 line, one leaf line)
+    D.lo = lower_bound_list(Lg, k0);
+    D.hi = lower_bound_list(Lg, k1 + 1u);  // ids < 2^32 - 1: k1 + 1 does not wrap
+    pdesc[t] = D;
+    return;
+  }
   // lower bound of the first id, upper bound of the last
   int64_t lo0 = 0, hi0 = Lg.n, lo1 = 0, hi1 = Lg.n;
   while (lo0 < hi0 || lo1 < hi1) {
@@ -549,11 +623,8 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
       if (Lg.uid[mid] <= k1) lo1 = mid + 1; else hi1 = mid;
     }
   }
-  ProbeDesc D;
   D.lo = lo0;
   D.hi = lo1;
-  D.job = j;
-  D.pad = 0;
   pdesc[t] = D;
 }
 
@@ -596,6 +667,8 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
       jl = D.lo + lo;
       hit = lo < (int)R && sL[lo] == key;
     }
+  } else if (probe_heads(Lg, D.lo, D.hi, sL, key, i < Sm.n ? Sm.uid + i : nullptr, &jl, &hit)) {
+    // long range of an index list: its line heads searched in LDS, one leaf line per key
   } else
 #endif
   if (i < Sm.n) {

@@ -413,11 +413,8 @@ class RWIIndex:
         return self.search_batch([Query(include, exclude, max_distance, k, profile, language, now_ms, filter)],
                                  stats=stats)[0]
 
-    def search_batch(self, queries: Sequence[Query], stats: Optional[CStats] = None,
-                     kmax: Optional[int] = None) -> List[List[Hit]]:
+    def _marshal(self, queries: Sequence[Query], kmax: Optional[int]):
         nq = len(queries)
-        if nq == 0:
-            return []
         kmax = kmax or max(1, min(MAX_RESULTS_RWI, max(q.k for q in queries)))
         arr = (CQuery * nq)()
         keep = []
@@ -442,13 +439,32 @@ class RWIIndex:
                 arr[i].filter = ctypes.pointer(q.filter.c)
         hits = (CHit * (nq * kmax))()
         nout = (ctypes.c_int32 * nq)()
+        return arr, keep, hits, nout, kmax
+
+    @staticmethod
+    def _unmarshal(nq: int, kmax: int, hits, nout) -> List[List[Hit]]:
+        return [[Hit(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score, hits[i * kmax + j].tiebreak)
+                 for j in range(nout[i])] for i in range(nq)]
+
+    def search_batch(self, queries: Sequence[Query], stats: Optional[CStats] = None,
+                     kmax: Optional[int] = None) -> List[List[Hit]]:
+        nq = len(queries)
+        if nq == 0:
+            return []
+        arr, keep, hits, nout, kmax = self._marshal(queries, kmax)
         st = stats if stats is not None else CStats()
         _check(self._h, _lib.lib().yrwi_query_batch(self._h, arr, nq, kmax, hits, nout, ctypes.byref(st)))
-        res = []
-        for i in range(nq):
-            res.append([Hit(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score, hits[i * kmax + j].tiebreak)
-                        for j in range(nout[i])])
-        return res
+        return self._unmarshal(nq, kmax, hits, nout)
+
+    def submit(self, queries: Sequence[Query], kmax: Optional[int] = None) -> "PendingBatch":
+        """Start a batch asynchronously (yrwi_query_batch_submit); .result() waits for it.
+        Batches run on the context's lanes in submission order (ticket t on lane t % lanes)."""
+        nq = len(queries)
+        arr, keep, hits, nout, kmax = self._marshal(queries, kmax) if nq else ((CQuery * 1)(), [], (CHit * 1)(),
+                                                                               (ctypes.c_int32 * 1)(), 1)
+        st = CStats()
+        ticket = self.submit_raw(arr, nq, kmax, hits, nout, st)
+        return PendingBatch(self, ticket, nq, kmax, (arr, keep, hits, nout, st))
 
     def search_batch_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> None:
         """Zero-marshalling batch call for benchmarks (pre-built ctypes arrays)."""
@@ -472,6 +488,18 @@ class RWIIndex:
         arr = (ctype * max(1, n)).from_address(p.value)
         self._pinned = getattr(self, "_pinned", []) + [p.value]
         return arr
+
+
+class PendingBatch:
+    """A submitted batch: its ctypes buffers stay alive until result() collects it."""
+
+    def __init__(self, index: RWIIndex, ticket: int, nq: int, kmax: int, bufs):
+        self.index, self.ticket, self.nq, self.kmax, self._bufs = index, ticket, nq, kmax, bufs
+
+    def result(self) -> List[List[Hit]]:
+        self.index.wait(self.ticket)
+        _, _, hits, nout, _ = self._bufs
+        return RWIIndex._unmarshal(self.nq, self.kmax, hits, nout)
 
 
 def unique_id() -> bytes:
