@@ -46,8 +46,8 @@ def log(*a):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--k", type=int, default=100)
@@ -64,7 +64,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency", type=int, default=100, help="single-query latency samples")
-    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (throughput mode)")
+    ap.add_argument("--inflight", type=int, default=4, help="batches in flight (throughput mode; the library runs 4 lanes)")
     ap.add_argument("--dry-run", action="store_true", help="ranks + rendezvous only (gloo, no GPU): launcher test")
     return ap.parse_args(argv)
 
