@@ -58,6 +58,40 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_joinExclude(JNIEn
   return res;  /* null on error (caller: yrwi_last_error) */
 }
 
+/* joinExclude into a direct ByteBuffer the caller owns and reuses (no JNI array copy
+ * of the joined container): returns m (rows written, 40 bytes each) or the (negative)
+ * error code -- YRWI_E_ARG when the container holds more rows than capacity / 40. */
+JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_joinExcludeInto(JNIEnv* env, jclass c, jlong ctx,
+                                                                         jbyteArray incl, jint nincl,
+                                                                         jbyteArray excl, jint nexcl, jint maxd,
+                                                                         jlong now, jobject out) {
+  uint8_t* dst = (uint8_t*)(*env)->GetDirectBufferAddress(env, out);
+  const jlong capb = (*env)->GetDirectBufferCapacity(env, out);
+  if (dst == NULL || capb < 0) return YRWI_E_ARG;
+  jbyte* ib = (*env)->GetByteArrayElements(env, incl, NULL);
+  jbyte* eb = (*env)->GetByteArrayElements(env, excl, NULL);
+  int64_t m = 0;
+  int rc = yrwi_join_exclude((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)ib, nincl, (const uint8_t*)eb, nexcl, maxd, now,
+                             dst, capb / 40, &m);
+  (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
+  (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
+  return rc == 0 ? (jlong)m : (jlong)rc;
+}
+
+/* yrwi_stats -> long[]: postings_in, joined, bytes_alg, bytes_join, t_join_ns, t_norm_ns,
+ * t_score_ns, t_total_ns, n_join_launches, n_enum_steps, n_test_steps, n_realloc,
+ * bytes_probe, t_probe_ns, bytes_compact, t_compact_ns, t_kernels_ns (17 values) */
+#define YRWI_JNI_NSTATS 17
+static void stats_out(JNIEnv* env, jlongArray a, const yrwi_stats* st) {
+  if (a == NULL) return;
+  const jlong v[YRWI_JNI_NSTATS] = {st->postings_in, st->joined, st->bytes_alg, st->bytes_join, st->t_join_ns,
+                                    st->t_norm_ns, st->t_score_ns, st->t_total_ns, st->n_join_launches,
+                                    st->n_enum_steps, st->n_test_steps, st->n_realloc, st->bytes_probe,
+                                    st->t_probe_ns, st->bytes_compact, st->t_compact_ns, st->t_kernels_ns};
+  jsize n = (*env)->GetArrayLength(env, a);
+  (*env)->SetLongArrayRegion(env, a, 0, n < YRWI_JNI_NSTATS ? n : YRWI_JNI_NSTATS, v);
+}
+
 JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_normalizeScore(JNIEnv* env, jclass c, jlong ctx,
                                                                              jbyteArray rows, jint m, jintArray prof,
                                                                              jstring lang, jlong now) {
@@ -77,7 +111,7 @@ JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_normalizeScore(JN
 JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_query(JNIEnv* env, jclass c, jlong ctx,
                                                                     jbyteArray incl, jint nincl, jbyteArray excl,
                                                                     jint nexcl, jint maxd, jint k, jintArray prof,
-                                                                    jstring lang, jlong now) {
+                                                                    jstring lang, jlong now, jlongArray stats) {
   yrwi_profile p;
   to_profile(env, prof, &p);
   yrwi_query_desc q;
@@ -91,12 +125,15 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_query(JNIEnv* env
   strncpy(q.language, l, sizeof(q.language) - 1);
   yrwi_hit* hits = (yrwi_hit*)malloc(sizeof(yrwi_hit) * (size_t)(k > 0 ? k : 1));
   int32_t n = 0;
-  int rc = yrwi_query((yrwi_ctx*)(intptr_t)ctx, &q, hits, &n, NULL);
+  yrwi_stats st;
+  memset(&st, 0, sizeof(st));
+  int rc = yrwi_query((yrwi_ctx*)(intptr_t)ctx, &q, hits, &n, stats ? &st : NULL);
   (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
   (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
   (*env)->ReleaseStringUTFChars(env, lang, l);
   jbyteArray res = NULL;
   if (rc == 0) {
+    stats_out(env, stats, &st);
     res = (*env)->NewByteArray(env, (jsize)(n * (jint)sizeof(yrwi_hit)));
     (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * (jint)sizeof(yrwi_hit)), (const jbyte*)hits);
   }

@@ -36,6 +36,17 @@ public final class GpuRWI implements AutoCloseable {
                            maxDistance, nowMillis);
     }
 
+    /** joinExclude into a caller-owned direct buffer (ByteBuffer.allocateDirect, reused
+     *  across queries): no copy of the joined container through a Java array.  Returns
+     *  the number of 40-byte rows written; throws when the container does not fit. */
+    public long joinExcludeInto(final byte[][] include, final byte[][] exclude, final int maxDistance,
+                                final long nowMillis, final java.nio.ByteBuffer out) {
+        final long m = joinExcludeInto(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
+                                       maxDistance, nowMillis, out);
+        if (m < 0) check((int) m);
+        return m;
+    }
+
     /** ReferenceOrder.normalizeWith + cardinal with settled min/max: one score per row. */
     public long[] normalizeScore(final byte[] rows, final int m, final int[] profile32, final String language,
                                  final long nowMillis) {
@@ -47,7 +58,15 @@ public final class GpuRWI implements AutoCloseable {
     public byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
                         final int[] profile32, final String language, final long nowMillis) {
         return query(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length, maxDistance, k,
-                     profile32, language, nowMillis);
+                     profile32, language, nowMillis, null);
+    }
+
+    /** query(...) with the call's yrwi_stats (17 longs, order in yrwi_jni.c stats_out):
+     *  postings in, joined rows, algorithmic bytes, per-phase device times, launches. */
+    public byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+                        final int[] profile32, final String language, final long nowMillis, final long[] stats) {
+        return query(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length, maxDistance, k,
+                     profile32, language, nowMillis, stats);
     }
 
     /** IndexCell's BLOB heaps (text.index.*.blob) into the GPU index; lists already
@@ -152,8 +171,10 @@ public final class GpuRWI implements AutoCloseable {
                                              int maxDistance, long nowMillis);
     private static native long[] normalizeScore(long ctx, byte[] rows, int m, int[] profile32, String language,
                                                 long nowMillis);
+    private static native long joinExcludeInto(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl,
+                                               int maxDistance, long nowMillis, java.nio.ByteBuffer out);
     private static native byte[] query(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl, int maxDistance,
-                                       int k, int[] profile32, String language, long nowMillis);
+                                       int k, int[] profile32, String language, long nowMillis, long[] stats);
     private static native long[] loadHeaps(long ctx, String[] paths, int byName);
     private static native byte[] queryFiltered(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl,
                                                int maxDistance, int k, int[] profile32, String language,

@@ -60,3 +60,36 @@ def test_termsearch_then_reference_order(corpus, profile):
         got = ix.search(ih, eh, profile=prof, now_ms=NOW, k=100)    # the whole-query path
         assert [(h.urlhash, h.score, h.tiebreak) for h in got] == stack
     assert n > 0
+
+
+def test_join_into_direct_buffer_and_query_stats(corpus):
+    """GpuRWI.joinExcludeInto: the joined rows land in a caller-owned buffer of
+    capacity/40 rows (JNI: a direct ByteBuffer); a buffer one row short is
+    refused with YRWI_E_ARG.  GpuRWI.query(..., long[] stats): the call's
+    yrwi_stats (joined rows = the container TermSearch returns)."""
+    import ctypes
+    from yacy_search_server_amd import _lib
+    from yacy_search_server_amd._lib import CStats
+    cfg, idx, ix = corpus
+    lib = _lib.lib()
+    done = 0
+    for inc, exc in synth.queries(cfg, 12, 2, 3, 1, qseed=321):
+        ih = b"".join(idx.hashes[t] for t in inc)
+        eh = b"".join(idx.hashes[t] for t in exc)
+        rows = ix.term_search([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW)
+        m = len(rows)
+        if m == 0:
+            continue
+        buf = np.zeros((m, 40), dtype=np.uint8)
+        got = ctypes.c_int64()
+        assert lib.yrwi_join_exclude(ix._h, ih, len(inc), eh, len(exc), 2147483647, NOW, buf.ctypes.data, m,
+                                     ctypes.byref(got)) == 0
+        assert got.value == m and np.array_equal(buf, rows)
+        assert lib.yrwi_join_exclude(ix._h, ih, len(inc), eh, len(exc), 2147483647, NOW, buf.ctypes.data, m - 1,
+                                     ctypes.byref(got)) == -1  # YRWI_E_ARG
+        st = CStats()
+        ix.search([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW, k=100, stats=st)
+        assert st.postings_in == sum(int(idx.sizes[t]) for t in inc + exc)
+        assert st.joined >= m and st.t_total_ns > 0
+        done += 1
+    assert done > 0
