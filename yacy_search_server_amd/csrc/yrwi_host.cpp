@@ -691,11 +691,20 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
             (h1 - h0) / 1e6, (h2 - h1) / 1e6, (h3 - h2) / 1e6, (h4 - h3) / 1e6, (h5 - h4) / 1e6,
             (now_ns() - h5) / 1e6);
   if (st)  // k_compact per joined row: pair + id read, the records it gathers (32 B, + 16 B of the joined
-           // side for enumeration steps), record + id written
-    for (int j = 0; j < nj; j++) st->bytes_compact += mh[(size_t)j] * (jobs[(size_t)j].mode == JM_ENUM ? 96 : 80);
+           // side for enumeration steps, + the deferred rows' sources and records), record + id written;
+           // deferred output: A's sources read, sources + id written
+    for (int j = 0; j < nj; j++) {
+      const JoinQ& J = jobs[(size_t)j];
+      const int64_t atw = J.A.tup ? J.A.tw : 0;
+      st->bytes_compact += mh[(size_t)j] * (J.out_tup ? 12 + 4 * atw + 4 + 4 * (int64_t)J.out_tw
+                                                      : (J.mode == JM_ENUM ? 96 : 80) + 4 * atw +
+                                                            (atw > 1 ? 24 * (atw - 1) : 0));
+    }
   for (int j = 0; j < nj; j++) {
     Plan& P = plans[(size_t)owner[(size_t)j]];
-    P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], jobs[(size_t)j].out_uid, jobs[(size_t)j].out_feat};
+    const JoinQ& J = jobs[(size_t)j];
+    P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
+                   J.out_tup ? J.out_tw : 0};
   }
   return 0;
 }
@@ -761,9 +770,12 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     const Plan& P = plans[qi];
     return !P.empty && P.seq.size() > s + 1 && acc_g[qi] > 0;
   };
+  static const bool defer = !(getenv("YRWI_NO_DEFER") && atoi(getenv("YRWI_NO_DEFER")));
   for (size_t s = 0;; s++) {
     std::vector<JoinQ> jobs;
     std::vector<int> owner;
+    std::vector<FoldSrc> fold;
+    std::vector<int> fold_job;
     bool any = false, more = false;  // some query steps now / after this step (global decisions)
     for (size_t qi = 0; qi < nq; qi++) {
       if (!steps(qi, s)) continue;
@@ -781,10 +793,30 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.mode = dispatch_mode(acc_g[qi], P.seq_ng[s + 1]);
       J.maxd = P.maxd;
       J.now_ms = P.now_ms;
+      P.step_mode[s] = J.mode;
       int64_t cap = std::min(J.A.n, J.B.n);
-      J.out_feat = arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
       J.out_uid = arena_alloc<uint32_t>(ctx, cap);
-      if (!J.out_feat || !J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
+      // A step before the fold's last keeps its rows deferred (the rows of lists
+      // 0..s+1 they join, no records): the next step joins on url ids alone, and
+      // only the last step gathers and folds the records of the rows that survive.
+      // A maxDistance filter needs every step's joined features: materialised.
+      const bool last = P.seq.size() == s + 2;
+      if (!last && defer && P.maxd >= 65535) {
+        J.out_tw = (int32_t)s + 2;
+        J.out_tup = arena_alloc<int32_t>(ctx, cap * J.out_tw);
+        if (!J.out_tup) return ctx->fail(YRWI_E_NOMEM, "arena");
+      } else {
+        J.out_feat = arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
+        if (!J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
+        if (J.A.tup) {
+          FoldSrc F{};
+          for (int l = 0; l < J.A.tw; l++) F.feat[l] = P.seq[(size_t)l]->feat;
+          for (size_t t = 0; t < s; t++) F.mode[t] = P.step_mode[t];
+          fold.push_back(F);
+          fold_job.push_back((int)jobs.size());
+        }
+      }
+      if (!J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (st) {
         st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
@@ -793,6 +825,12 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       owner.push_back((int)qi);
     }
     if (!any) break;
+    if (!fold.empty()) {  // the fold programs of the jobs whose A is deferred
+      FoldSrc* d_fold = arena_alloc<FoldSrc>(ctx, (int64_t)fold.size());
+      if (!d_fold) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (upload(ctx, d_fold, fold)) return YRWI_E_HIP;
+      for (size_t f = 0; f < fold.size(); f++) jobs[(size_t)fold_job[f]].fold = d_fold + f;
+    }
     if (!jobs.empty())
       if (int rc = run_join_jobs(ctx, plans, jobs, owner, st, tm)) return rc;
     if (!more) break;

@@ -166,8 +166,9 @@ struct Plan {
   int64_t now_ms = 0;
   int64_t postings_in = 0;
   const yrwi_filter* filter = nullptr;  // addRWIs constraints (nullptr: none)
-  // runtime container
+  // runtime container (a deferred one between the steps of a multi-term fold)
   DList cont{nullptr, nullptr, nullptr, 0};
+  int32_t step_mode[YRWI_MAX_TERMS] = {0};  // JoinMode of every fold step taken
   uint8_t* removed = nullptr;
 };
 

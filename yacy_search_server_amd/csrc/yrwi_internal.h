@@ -45,6 +45,10 @@ struct DList {
   // containers: head[g] = uid[32 g] (the first id of every 128-B line of uid),
   // then, at head + head1_cap(n), head[32 g] again every 32nd: uid[1024 g]
   const uint32_t* head;
+  // deferred container of a multi-term fold (not its last step): no records, the
+  // rows of the fold's lists 0..tw-1 it joins, tw per row (tup[row * tw + list])
+  const int32_t* tup;
+  int32_t tw;
 };
 // the two head levels of a list of n postings (each level padded to 32 entries)
 __host__ __device__ constexpr int64_t head1_n(int64_t n) { return (n + 31) >> 5; }
@@ -79,6 +83,14 @@ enum JoinMode : int32_t {
 enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1 };
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
 
+// The lists of a multi-term fold and the join mode of each step, for the last
+// step's k_compact: it folds the deferred rows' records (J5/J6 step by step,
+// exactly as materialising every step would) before joining the last list.
+struct FoldSrc {
+  const uint64_t* feat[YRWI_MAX_TERMS];  // ranking records of the fold's lists, in fold order
+  int32_t mode[YRWI_MAX_TERMS];          // JoinMode of step s (lists 0..s with list s+1)
+};
+
 struct JoinQ {
   DList A, B;
   int64_t tile_base;   // first global tile of this job
@@ -92,6 +104,11 @@ struct JoinQ {
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
   int64_t now_ms;
   int64_t* m_out;      // number of output rows (written by the scan kernel)
+  // deferred output (out_tw > 0: a step before the fold's last): out_tw source rows
+  // per joined row instead of a record; fold: the lists / modes when A is deferred
+  int32_t* out_tup;
+  int32_t out_tw;
+  const FoldSrc* fold;
   // matched pairs of the job: [pair_base, pair_base + cap) of the step's pair
   // arrays; every tile writes its run at tile_src[tile] (merge tiles: the prefix
   // of their bounds min(na, nb + 1); probe tiles: PROBE_TILE per tile)

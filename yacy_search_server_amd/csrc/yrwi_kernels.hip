@@ -799,8 +799,28 @@ struct CompactJob {
   int64_t now_ms;
   int64_t off;
   int64_t src;  // the tile's run in the pair arrays
-  int32_t mode, pad;
+  int32_t mode;
+  int32_t atw;           // A deferred: its rows' source width (0: A has records)
+  const int32_t* atup;
+  int32_t* otup;         // deferred output (otw > 0)
+  const FoldSrc* fold;   // A deferred, this the last step: the fold's lists and modes
+  int32_t otw, pad;
 };
+
+// the record of a deferred row (sources r[0..tw-1] in the fold's lists): J5/J6
+// folded step by step, as every step's k_compact would have materialised it
+__device__ __forceinline__ Rec fold_deferred(const FoldSrc& F, const int32_t* __restrict__ r, int tw, int64_t now_ms) {
+  Rec acc = load_rec(F.feat[0], r[0]);
+  for (int s = 0; s + 1 < tw; s++) {
+    const int32_t m = F.mode[s];
+    const int64_t e = r[s + 1];
+    ulonglong2 b = make_ulonglong2(0, 0);
+    if (m == JM_TEST_LARGE_B) acc = load_rec(F.feat[s + 1], e);  // self-join of the larger side
+    else if (m == JM_ENUM) b = *reinterpret_cast<const ulonglong2*>(F.feat[s + 1] + e * FEAT_WORDS);
+    acc = joined_rec(acc, b.x, b.y, m, now_ms);
+  }
+  return acc;
+}
 
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
@@ -827,6 +847,11 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         X.off = tile_off[t];
         X.src = tile_src[t];
         X.mode = J.mode;
+        X.atw = J.A.tup ? J.A.tw : 0;
+        X.atup = J.A.tup;
+        X.otup = J.out_tup;
+        X.otw = J.out_tup ? J.out_tw : 0;
+        X.fold = J.fold;
       }
     }
     const int32_t inc = wave_incl_sum(c);
@@ -856,6 +881,25 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         uid[u] = pair_uid[pi[u]];
       }
     }
+    // deferred rows: a step before the fold's last writes the joined row's sources
+    // (A's sources + the B row) instead of gathering any record
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      if (tl[u] < 0) continue;
+      const CompactJob& X = sJ[tl[u]];
+      if (X.otw == 0) continue;
+      const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
+      int32_t* dst = X.otup + o * X.otw;
+      if (X.atw) {
+        const int32_t* srcr = X.atup + (int64_t)pr[u].x * X.atw;
+        for (int j = 0; j < X.atw; j++) dst[j] = srcr[j];
+      } else {
+        dst[0] = (int32_t)pr[u].x;
+      }
+      dst[X.otw - 1] = (int32_t)pr[u].y;
+      X.ouid[o] = uid[u];
+      tl[u] = -1;
+    }
     Rec A[COMPACT_UNROLL];
     ulonglong2 B[COMPACT_UNROLL];
 #pragma unroll
@@ -863,7 +907,9 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       B[u] = make_ulonglong2(0, 0);
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
-      A[u] = X.mode == JM_TEST_LARGE_B ? load_rec(X.bf, pr[u].y) : load_rec(X.af, pr[u].x);
+      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+      else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
+      else A[u] = load_rec(X.af, pr[u].x);
       if (X.mode == JM_ENUM) B[u] = *reinterpret_cast<const ulonglong2*>(X.bf + (int64_t)pr[u].y * FEAT_WORDS);
     }
 #pragma unroll
