@@ -162,13 +162,14 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   ctx->device = device;
   ctx->rank = rank;
   ctx->world = world;
-  // Four lanes, sharded or not (C2: 0.79-0.81 ms per batch with four in flight
-  // against 1.0-1.25 with two: a lane's host planning and its mid-batch wait for
-  // the joined sizes leave the device idle unless enough other batches queue
-  // work).  The collectives of the lanes' batch parts are enqueued in one total
-  // order on every rank (CollTurn, yrwi_host.h).
+  // Eight lanes, sharded or not (C2, 400-step runs on one box: 0.76-0.80 ms per
+  // batch with eight in flight, 0.80-0.86 with four, 1.0-1.25 with two: a lane's
+  // host planning and its mid-batch wait for the joined sizes leave the device
+  // idle unless enough other batches queue work).  The collectives of the lanes'
+  // batch parts are enqueued in one total order on every rank (CollTurn,
+  // yrwi_host.h).  Scratch: 128 GiB over all lanes (scratch_budget).
   const char* e = getenv("YRWI_LANES");
-  const int nl = e ? std::max(1, std::min(8, atoi(e))) : 4;
+  const int nl = e ? std::max(1, std::min(8, atoi(e))) : 8;
   for (int l = 0; l < nl; l++) {
     Lane* L = new Lane();
     L->device = device;
@@ -186,6 +187,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
     }
     L->hostreg = &ctx->hostreg;
     L->turn = &ctx->turn;
+    L->nlanes = nl;
     L->start_worker();
   }
   ctx->stream = ctx->lanes[0]->stream;
@@ -1313,8 +1315,8 @@ static int64_t scratch_estimate(const Plan& P) {
 // the estimate depends on the local shard), so they keep one pass per batch.
 static int64_t scratch_budget(const Lane* L) {
   if (L->world > 1) return INT64_MAX;
-  const char* e = getenv("YRWI_SCRATCH_GB");
-  const double gb = e ? atof(e) : 32.0;
+  const char* e = getenv("YRWI_SCRATCH_GB");  // per lane; default 128 GiB shared by the lanes
+  const double gb = e ? atof(e) : 128.0 / (double)std::max(1, L->nlanes);
   return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
 }
 

@@ -221,6 +221,7 @@ struct CollTurn {
 // of the two lanes share the device).
 struct Lane {
   int device = 0, rank = 0, world = 1;
+  int nlanes = 1;  // lanes of the context (scratch budget share)
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   LoopGroup* loop = nullptr;  // test transport instead of comm (yrwi_coll.cpp)
