@@ -162,6 +162,12 @@ int yrwi_build_url_ids(yrwi_ctx* ctx);
  * entries out of order (0 when consistent); *nurls = dictionary size (may be NULL). */
 int yrwi_check_url_ids(yrwi_ctx* ctx, int64_t* bad, int64_t* nurls);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
+/* Diagnostic of the node's shared-memory size exchange (no GPU needed): rank
+ * `rank` of `world` processes / threads sharing group id `id` runs `nparts`
+ * batch parts of `ncalls` exchanges each, vectors of n values (rank + part +
+ * call + i), and checks every sum.  0 when all sums are right; YRWI_E_RCCL on a
+ * wrong sum or a peer that never arrives; 1 when the mailbox is unavailable. */
+int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, int64_t nparts, int32_t ncalls, int64_t n);
 
 /* ---- YaCy on-disk index ---- */
 /* Loads BLOB heap files of the RWI (records [int32 reclen][12-byte term hash]

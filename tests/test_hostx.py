@@ -1,0 +1,41 @@
+"""The node's shared-memory size exchange (yrwi_coll.cpp) across
+separate processes, as the ranks of `bench.py --gpus N` use it: no GPU needed.
+Every rank runs the same batch parts and exchanges; the sums must be exact, with
+more parts than mailbox slots (slots are reused) and ranks started at
+different times."""
+import multiprocessing as mp
+import os
+
+import pytest
+
+
+def _rank(uid, world, rank, nparts, ncalls, n, delay, q):
+    import time
+    time.sleep(delay)
+    from yacy_search_server_amd import _lib
+    q.put((rank, _lib.lib().yrwi_hostx_selftest(uid, world, rank, nparts, ncalls, n)))
+
+
+@pytest.mark.parametrize("world,nparts,ncalls,n", [(2, 40, 3, 1000), (4, 20, 8, 4096), (8, 12, 2, 17)])
+def test_hostx_processes(world, nparts, ncalls, n):
+    uid = b"YRWI-HOSTX-TEST" + os.urandom(113)
+    before = {f for f in os.listdir("/dev/shm") if f.startswith("yrwi-hx-")}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(uid, world, r, nparts, ncalls, n, 0.05 * ((r * 7) % world), q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {r: 0 for r in range(world)}, res
+    after = {f for f in os.listdir("/dev/shm") if f.startswith("yrwi-hx-")}
+    assert after <= before  # rank 0 unlinked the mailbox
+
+
+def test_hostx_oversized_vector_not_handled():
+    """Vectors longer than the mailbox's slots fall back to the device all-gather."""
+    from yacy_search_server_amd import _lib
+    uid = b"YRWI-HOSTX-TEST" + os.urandom(113)
+    assert _lib.lib().yrwi_hostx_selftest(uid, 1, 0, 1, 1, 10) == 1  # world 1: no mailbox

@@ -138,6 +138,8 @@ SIGNATURES = {
     "yrwi_event_result": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(CHit), ctypes.c_int32,
                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CEventInfo)]),
     "yrwi_check_url_ids": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_hostx_selftest": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.c_int64]),
     "yrwi_event_pull": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, ctypes.POINTER(CHit), ctypes.c_int32,
                                        ctypes.POINTER(ctypes.c_int32)]),
     "yrwi_event_close": (None, [_VP, _VP]),

@@ -12,6 +12,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -132,6 +139,161 @@ void turn_release(Lane* L) {
   L->seq = -1;
   L->turn_held = false;
 }
+
+// ---------------------------------------------------------------- host exchange
+// The batch's global list sizes (J1/J2/J3 planning) are host data: the ranks of
+// one node sum them through a shared-memory mailbox instead of a device
+// collective.  A mailbox exchange waits only for the same batch part on the
+// other ranks, never for a device queue, so it needs no collective turn: the
+// parts' planning and joins overlap freely and the turn (CollTurn) is held only
+// around the rank phase's device collectives.  One exchange = one key (part
+// sequence number * HX_CALLS + call index, identical on every rank); a slot is
+// claimed by the first rank to reach its key, written by every rank, read by
+// every rank and freed by the last reader.  Longer vectors, unordered callers
+// and a missing mailbox fall back to the device all-gather.
+namespace {
+constexpr int HX_SLOTS = 64, HX_MAXN = 4096, HX_CALLS = 8, HX_MAXW = 16;
+struct HxEntry {
+  int64_t n;
+  int64_t v[HX_MAXN];
+};
+struct HxSlot {
+  std::atomic<int64_t> owner;  // key + 1 of the exchange using the slot, 0: free
+  std::atomic<int32_t> nwritten, nread;
+  char pad[48];
+};
+}  // namespace
+
+struct HostX {
+  void* base = nullptr;
+  size_t bytes = 0;
+  int world = 0, rank = 0;
+  std::string name;
+  HxSlot* slot(int i) const { return reinterpret_cast<HxSlot*>(static_cast<char*>(base) + (size_t)i * sizeof(HxSlot)); }
+  HxEntry* entry(int i, int r) const {
+    char* e0 = static_cast<char*>(base) + (size_t)HX_SLOTS * sizeof(HxSlot);
+    return reinterpret_cast<HxEntry*>(e0 + ((size_t)i * world + r) * sizeof(HxEntry));
+  }
+};
+
+HostX* hostx_open(const uint8_t id[128], int world, int rank) {
+  if (world < 2 || world > HX_MAXW || getenv("YRWI_NO_HOSTX")) return nullptr;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the group id: the segment's name
+  for (int i = 0; i < 128; i++) h = (h ^ id[i]) * 1099511628211ull;
+  char nm[64];
+  snprintf(nm, sizeof(nm), "/yrwi-hx-%016llx-%d", (unsigned long long)h, world);
+  const size_t bytes = (size_t)HX_SLOTS * sizeof(HxSlot) + (size_t)HX_SLOTS * world * sizeof(HxEntry);
+  const int fd = shm_open(nm, O_CREAT | O_RDWR, 0600);  // zero-filled when new: every slot free
+  if (fd < 0) return nullptr;
+  if (ftruncate(fd, (off_t)bytes) != 0) {
+    close(fd);
+    return nullptr;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return nullptr;
+  HostX* x = new HostX();
+  x->base = p;
+  x->bytes = bytes;
+  x->world = world;
+  x->rank = rank;
+  x->name = nm;
+  return x;
+}
+
+void hostx_close(HostX* x, bool unlink_name) {
+  if (!x) return;
+  munmap(x->base, x->bytes);
+  if (unlink_name) shm_unlink(x->name.c_str());
+  delete x;
+}
+
+void hostx_unlink(HostX* x) {
+  if (x) shm_unlink(x->name.c_str());
+}
+
+// spin, then yield; false after `limit` (a peer that never arrives: fail, do not hang)
+template <class F>
+static bool hx_wait(F ready, double limit_s = 300.0) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int64_t i = 0;; i++) {
+    if (ready()) return true;
+    if (i < 2000) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    sched_yield();
+    if ((i & 1023) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+      return false;
+  }
+}
+
+// 1: not handled here (caller falls back to the device all-gather); <0: error
+int hostx_allsum(Lane* L, std::vector<int64_t>& v) {
+  HostX* x = L->hostx;
+  if (!x || L->seq < 0 || L->xcall >= HX_CALLS || v.size() > (size_t)HX_MAXN) return 1;
+  const int64_t key = L->seq * HX_CALLS + L->xcall++;
+  const int si = (int)(key % HX_SLOTS);
+  HxSlot* S = x->slot(si);
+  // claim (or join) the slot for this key
+  if (!hx_wait([&] {
+        int64_t cur = S->owner.load(std::memory_order_acquire);
+        if (cur == key + 1) return true;
+        if (cur != 0) return false;
+        return S->owner.compare_exchange_strong(cur, key + 1, std::memory_order_acq_rel) || cur == key + 1;
+      }))
+    return L->fail(YRWI_E_RCCL, "host exchange: slot never freed");
+  HxEntry* me = x->entry(si, x->rank);
+  me->n = (int64_t)v.size();
+  std::memcpy(me->v, v.data(), v.size() * sizeof(int64_t));
+  S->nwritten.fetch_add(1, std::memory_order_acq_rel);
+  if (!hx_wait([&] { return S->nwritten.load(std::memory_order_acquire) == x->world; }))
+    return L->fail(YRWI_E_RCCL, "host exchange: a rank never arrived");
+  std::vector<int64_t> sum(v.size(), 0);
+  for (int r = 0; r < x->world; r++) {
+    const HxEntry* e = x->entry(si, r);
+    if (e->n != (int64_t)v.size()) return L->fail(YRWI_E_RCCL, "host exchange: size mismatch");
+    for (size_t i = 0; i < v.size(); i++) sum[i] += e->v[i];
+  }
+  v.swap(sum);
+  if (S->nread.fetch_add(1, std::memory_order_acq_rel) + 1 == x->world) {  // the last reader frees the slot
+    S->nwritten.store(0, std::memory_order_relaxed);
+    S->nread.store(0, std::memory_order_relaxed);
+    S->owner.store(0, std::memory_order_release);
+  }
+  return 0;
+}
+
+}  // namespace yrwi
+
+extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, int64_t nparts, int32_t ncalls,
+                                   int64_t n) {
+  using namespace yrwi;
+  HostX* x = hostx_open(id, world, rank);
+  if (!x) return 1;
+  Lane L;  // host-side state only: no stream, no worker thread
+  L.world = world;
+  L.rank = rank;
+  L.hostx = x;
+  int rc = 0;
+  for (int64_t p = 0; p < nparts && rc == 0; p++) {
+    L.seq = p;
+    L.xcall = 0;
+    for (int32_t c = 0; c < ncalls && rc == 0; c++) {
+      std::vector<int64_t> v((size_t)n);
+      for (int64_t i = 0; i < n; i++) v[(size_t)i] = rank + p + c + i;
+      const int r = hostx_allsum(&L, v);
+      if (r != 0) { rc = r < 0 ? r : YRWI_E_RCCL; break; }
+      for (int64_t i = 0; i < n; i++)
+        if (v[(size_t)i] != (int64_t)world * (p + c + i) + (int64_t)world * (world - 1) / 2) { rc = YRWI_E_RCCL; break; }
+    }
+  }
+  hostx_close(x, rank == 0);
+  return rc;
+}
+
+namespace yrwi {
 
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
   if (L->world > 1) turn_acquire(L);

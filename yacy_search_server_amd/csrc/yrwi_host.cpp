@@ -202,6 +202,10 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
   int rc = open_common(device, rank, world, out);
   if (rc) return rc;
   yrwi_ctx* ctx = *out;
+  if (world > 1) {  // list-size exchanges through host shared memory (the ranks of one node)
+    ctx->hostx = hostx_open(nccl_id, world, rank);
+    for (Lane* L : ctx->lanes) L->hostx = ctx->hostx;
+  }
   if (world > 1 && std::memcmp(nccl_id, LOOP_TAG, sizeof(LOOP_TAG)) == 0) {
     // in-process loopback group (tests: several shards on one GPU), one per lane
     bool ok = true;
@@ -223,6 +227,7 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
     ncclComm_t c0 = nullptr;
     bool ok = ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
     if (ok) ctx->lanes[0]->comm = c0;
+    if (ok && rank == 0) hostx_unlink(ctx->hostx);  // every rank has it mapped (opened before the collective init)
     // one communicator per lane: lanes issue their collectives independently
     for (size_t l = 1; ok && l < ctx->lanes.size(); l++)
       ok = ncclCommSplit(c0, 0, rank, &ctx->lanes[l]->comm, nullptr) == ncclSuccess;
@@ -239,6 +244,8 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   close_lanes(ctx);
+  hostx_close(ctx->hostx, ctx->rank == 0);
+  ctx->hostx = nullptr;
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
   if (ctx->head_all) hipFree(ctx->head_all);
@@ -485,6 +492,8 @@ static void plan_finish(Plan* P, const int64_t* ng_inc, const int64_t* ng_exc) {
 // the same length, in the same sequence of calls); identity on one context.
 static int allsum_host(Lane* L, std::vector<int64_t>& v) {
   if (L->world <= 1 || v.empty()) return 0;
+  const int hx = hostx_allsum(L, v);  // the node's shared-memory mailbox (no device collective, no turn)
+  if (hx <= 0) return hx;
   const size_t n = v.size();
   int64_t* d_v = arena_alloc<int64_t>(L, (int64_t)n);
   int64_t* d_all = arena_alloc<int64_t>(L, (int64_t)n * L->world);
@@ -1452,7 +1461,10 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   auto cut = [&](int l) { return (int32_t)((int64_t)nq * l / nl); };
   const int64_t seq0 = ctx->coll_seq;  // collective order of the parts (CollTurn)
   ctx->coll_seq += nl;
-  for (int l = 0; l < nl; l++) ctx->lanes[(size_t)l]->seq = seq0 + l;
+  for (int l = 0; l < nl; l++) {
+    ctx->lanes[(size_t)l]->seq = seq0 + l;
+    ctx->lanes[(size_t)l]->xcall = 0;
+  }
   auto part = [=, &pst](int l) {
     Lane* L = ctx->lanes[(size_t)l];
     L->rc = run_batch_part(ctx, L, q + cut(l), cut(l + 1) - cut(l), kmax, out + (size_t)cut(l) * kmax, nout + cut(l),
@@ -1506,6 +1518,7 @@ extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, 
   L->wait();  // the lane's previous batch (its status is already recorded)
   ctx->next_ticket++;
   L->seq = ctx->coll_seq++;  // collective order (CollTurn): submission order, the same on every rank
+  L->xcall = 0;
   L->submit([=] {
     if (st) std::memset(st, 0, sizeof(*st));
     const int rc = nq == 0 ? 0 : run_batch_part(ctx, L, q, nq, kmax, out, nout, st);

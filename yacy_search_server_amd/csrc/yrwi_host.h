@@ -198,6 +198,7 @@ struct HostRegistry {
 };
 
 struct LoopGroup;  // in-process shard group (yrwi_coll.cpp)
+struct HostX;      // shared-memory mailbox of the node's ranks (yrwi_coll.cpp)
 
 // Order of the collectives of concurrently running batch parts (sharded
 // contexts).  Every batch part gets a sequence number in
@@ -255,6 +256,8 @@ struct Lane {
   // turn on right after its final collective
   CollTurn* turn = nullptr;
   int64_t seq = -1;
+  HostX* hostx = nullptr;  // host exchange of the batch part's list sizes (shared by the lanes)
+  int32_t xcall = 0;       // exchanges made by the running part
   bool turn_held = false, release_after_final = false;
 
   int fail(int code, const std::string& m) {
@@ -338,6 +341,7 @@ struct CtxBase {
   // collective order of batch parts (sequence numbers handed out by the caller's thread)
   CollTurn turn;
   int64_t coll_seq = 0;
+  HostX* hostx = nullptr;
   std::mutex st_mu;
   std::unordered_map<int64_t, std::pair<int, std::string>> status;
   std::unordered_map<KeyT, ListRec, KeyHash> lists;
@@ -465,6 +469,10 @@ void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added);
 // brings the url ids up to date, then counts inconsistencies (0: every id names its key)
 int check_url_ids(CtxBase* ctx, int64_t* bad);
 
+HostX* hostx_open(const uint8_t id[128], int world, int rank);  // nullptr: not available (device fallback)
+void hostx_close(HostX* x, bool unlink_name);
+void hostx_unlink(HostX* x);
+int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)
 void turn_release(Lane* L);  // pass the turn to the next part (waits for L's turn first); idempotent
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
