@@ -395,12 +395,22 @@ inline T* arena_alloc(Lane* ctx, int64_t count) {
 // Wait for this lane's work so far: an event, not a stream sync, so lanes that
 // share one stream do not wait for work the other lane enqueues later.
 inline hipError_t lane_sync(Lane* L) {
-  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
+  // YRWI_BLOCKING_SYNC=1: the lane thread sleeps in the wait instead of spinning
+  static const bool blocking = getenv("YRWI_BLOCKING_SYNC") && atoi(getenv("YRWI_BLOCKING_SYNC"));
+  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming |
+                                                              (blocking ? hipEventBlockingSync : 0)) != hipSuccess)
     return hipErrorOutOfMemory;
   hipError_t e = hipEventRecord(L->sync_ev, L->stream);
   if (e != hipSuccess) return e;
   const auto t0 = std::chrono::steady_clock::now();
-  e = hipEventSynchronize(L->sync_ev);
+  // YRWI_SYNC_POLL_US > 0: poll the event, sleeping that long between polls (the
+  // lanes' waits would otherwise spin one host core each against the job's quota)
+  static const int poll_us = getenv("YRWI_SYNC_POLL_US") ? atoi(getenv("YRWI_SYNC_POLL_US")) : 0;
+  if (poll_us > 0 && !blocking) {
+    while ((e = hipEventQuery(L->sync_ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
+  } else {
+    e = hipEventSynchronize(L->sync_ev);
+  }
   L->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   return e;
 }
