@@ -169,16 +169,19 @@ def test_j3_dispatch_int_wrap():
     _run_pair(d, [([b"DISPlistA___", b"DISPlistB___"], [])], k=300)
 
 
+@pytest.mark.parametrize("bm", [0, 64])
 @pytest.mark.parametrize("R", [0, 1, 4095, 4096, 4097, 40_000, 131_072, 131_200, 600_000, 4_200_000])
-def test_probe_range_around_lds_threshold(R, monkeypatch):
+def test_probe_range_around_lds_threshold(R, bm, monkeypatch):
     """One probe tile (256 small-list ids) whose large-list range holds R ids
     (YRWI_PROBE_RATIO=1 forces probing): R <= 4096 is searched in LDS; longer
     ranges search the list's line heads in LDS -- level 1 (every 32nd id) up to
     4096 heads (R ~ 131k), level 2 (every 1024th) up to ~4.19 M ids -- and the
     4.2 M range falls back to the global binary search.  Keys sit on, just
     after and just before line-head positions (32 / 1024 ids); R = 0: no small
-    id falls inside the large list."""
+    id falls inside the large list.  bm = 64: the large list gets a url-id
+    bitmap and every range is probed through it instead (bm = 0: no bitmaps)."""
     monkeypatch.setenv("YRWI_PROBE_RATIO", "1")
+    monkeypatch.setenv("YRWI_BM_DIV", str(bm))
     lo = 1000
     large = np.arange(100_000, 100_000 + max(20_000, lo + R + 2000), dtype=np.int64) * 4
     if R == 0:

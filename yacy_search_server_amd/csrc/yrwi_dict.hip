@@ -241,6 +241,46 @@ struct DevBuf {
   }
 };
 
+// url-id bitmaps of the large lists (DList::bm): per posting, its id's bit, and
+// the list position of the first posting of every 64-id word (the word's rank)
+struct BmSeg {
+  const uint32_t* uid;
+  uint64_t* bm;
+  int64_t n;
+};
+__global__ void k_bitmap_set(const BmSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const BmSeg S = segs[lo];
+  const int64_t j = i - off[lo];
+  const uint32_t u = S.uid[j];
+  const uint64_t w = u >> 6;
+  atomicOr(reinterpret_cast<unsigned long long*>(S.bm + 2 * w), 1ull << (u & 63u));
+  if (j == 0 || (S.uid[j - 1] >> 6) != w) S.bm[2 * w + 1] = (uint64_t)j;
+}
+
+// bitmap lists: every posting's bit is set and its word's rank + the bits below give its position
+__global__ void k_bitmap_check(const BmSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
+                               unsigned long long* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const BmSeg S = segs[lo];
+  const int64_t j = i - off[lo];
+  const uint32_t u = S.uid[j];
+  const uint64_t bits = S.bm[2 * (u >> 6)], bit = 1ull << (u & 63u);
+  if (!(bits & bit) || (int64_t)S.bm[2 * (u >> 6) + 1] + __popcll(bits & (bit - 1ull)) != j) atomicAdd(bad, 1ull);
+}
+
 __global__ void k_heads_check(const HeadSeg* __restrict__ segs, const int64_t* __restrict__ hoff, int nseg,
                               int64_t nh, unsigned long long* __restrict__ bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -540,6 +580,57 @@ int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   return 0;
 }
 
+// Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 64) of the url
+// ids (and 4096 postings): nurls/4 bytes each, so at most 16x the list's own ids
+// (at 1/64 density); total capped by YRWI_BM_GB (default 8).  YRWI_BM_DIV=0: none.
+int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
+  hipStream_t st = ctx->stream;
+  for (ListRec* L : lists) L->bm = nullptr;
+  const char* e = getenv("YRWI_BM_DIV");
+  const int64_t div = e ? atoll(e) : 64;
+  const char* g = getenv("YRWI_BM_GB");
+  const int64_t cap_bytes = (int64_t)((g ? atof(g) : 8.0) * (double)(1ll << 30));
+  if (div <= 0 || ctx->nurls <= 0) return 0;
+  const int64_t words = (ctx->nurls + 63) / 64;
+  const int64_t per = 2 * words;  // uint64 per bitmap
+  const int64_t thr = std::max<int64_t>(4096, ctx->nurls / div);
+  std::vector<ListRec*> big;
+  for (ListRec* L : lists)
+    if (L->n >= thr) big.push_back(L);
+  std::sort(big.begin(), big.end(), [](const ListRec* a, const ListRec* b) { return a->n > b->n; });
+  while (!big.empty() && (int64_t)big.size() * per * 8 > cap_bytes) big.pop_back();  // the largest lists first
+  if (big.empty()) return 0;
+  const size_t need = (size_t)big.size() * (size_t)per;
+  if (need > ctx->bm_cap) {
+    if (ctx->bm_all) hipFree(ctx->bm_all);
+    ctx->bm_all = nullptr;
+    ctx->bm_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->bm_all), need * 8) != hipSuccess)
+      return 0;  // no bitmaps: the joins search the lists instead
+    ctx->bm_cap = need;
+  }
+  HIPCHK(ctx, hipMemsetAsync(ctx->bm_all, 0, need * 8, st));
+  std::vector<BmSeg> segs;
+  std::vector<int64_t> off;
+  int64_t n = 0;
+  for (size_t k = 0; k < big.size(); k++) {
+    big[k]->bm = ctx->bm_all + (size_t)k * (size_t)per;
+    segs.push_back({big[k]->uid, big[k]->bm, big[k]->n});
+    off.push_back(n);
+    n += big[k]->n;
+  }
+  DevBuf bsegs, boff;
+  BmSeg* d_segs = bsegs.get<BmSeg>(segs.size());
+  int64_t* d_off = boff.get<int64_t>(off.size());
+  if (!d_segs || !d_off) return ctx->fail(YRWI_E_NOMEM, "bitmap scratch");
+  HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(BmSeg), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_bitmap_set, dim3(nb(n)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), n);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
 }  // namespace
 
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
@@ -588,7 +679,7 @@ int ensure_url_ids(CtxBase* ctx) {
     ctx->dict_valid = false;  // the next call rebuilds in full
     return rc;
   }
-  if ((rc = build_heads(ctx, lists))) {
+  if ((rc = build_heads(ctx, lists)) || (rc = build_bitmaps(ctx, lists))) {
     ctx->dict_valid = false;
     return rc;
   }
@@ -638,6 +729,24 @@ int check_url_ids(CtxBase* ctx, int64_t* bad) {
     HIPCHK(ctx, hipMemcpyAsync(d_h, hsegs.data(), hsegs.size() * sizeof(HeadSeg), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemcpyAsync(d_ho, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_heads_check, dim3(nb(nh)), dim3(256), 0, st, d_h, d_ho, (int)hsegs.size(), nh, d_bad);
+  }
+  std::vector<BmSeg> vbs;
+  std::vector<int64_t> vbo;
+  int64_t nbm = 0;
+  for (ListRec* L : lists)
+    if (L->bm) {
+      vbs.push_back({L->uid, L->bm, L->n});
+      vbo.push_back(nbm);
+      nbm += L->n;
+    }
+  DevBuf bb, bbo;
+  if (nbm > 0) {
+    BmSeg* d_b = bb.get<BmSeg>(vbs.size());
+    int64_t* d_bo = bbo.get<int64_t>(vbo.size());
+    if (!d_b || !d_bo) return ctx->fail(YRWI_E_NOMEM, "check scratch");
+    HIPCHK(ctx, hipMemcpyAsync(d_b, vbs.data(), vbs.size() * sizeof(BmSeg), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_bo, vbo.data(), vbo.size() * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_bitmap_check, dim3(nb(nbm)), dim3(256), 0, st, d_b, d_bo, (int)vbs.size(), nbm, d_bad);
   }
   unsigned long long hb = 0;
   HIPCHK(ctx, hipMemcpyAsync(&hb, d_bad, 8, hipMemcpyDeviceToHost, st));

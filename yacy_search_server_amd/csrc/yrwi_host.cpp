@@ -249,6 +249,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
   if (ctx->head_all) hipFree(ctx->head_all);
+  if (ctx->bm_all) hipFree(ctx->bm_all);
   if (ctx->dkhi) hipFree(ctx->dkhi);
   if (ctx->dklo) hipFree(ctx->dklo);
   delete ctx;
@@ -602,9 +603,13 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
   for (size_t i = 0; i < jobs.size(); i++) {
     JoinQ& J = jobs[i];
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
-    J.algo = (nl > probe_ratio * ns) ? JA_PROBE : JA_MERGE;  // skewed sizes: probe the large list
     J.small_is_A = J.A.n <= J.B.n;
-    J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, PROBE_TILE);
+    // skewed sizes: probe the large list; a large list with a url-id bitmap is
+    // probed at any ratio (the small side's ids stream, the bitmap stays in L2)
+    const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
+    J.algo = (bm || nl > probe_ratio * ns) ? JA_PROBE : JA_MERGE;
+    J.ptile = bm ? BM_TILE : PROBE_TILE;
+    J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
     order[i] = i;
   }
   // Within each algorithm, jobs that share their larger list run back to back:

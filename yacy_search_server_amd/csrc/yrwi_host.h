@@ -79,7 +79,8 @@ struct ListRec {
   uint32_t* uid = nullptr;  // url ids (rebuilt with the url dictionary)
   uint64_t* feat = nullptr; // ranking records (built with the url dictionary)
   uint32_t* head = nullptr; // line heads of uid (DList::head; rebuilt with the url ids)
-  DList dl() const { return DList{khi, klo, rows, n, uid, feat, head}; }
+  uint64_t* bm = nullptr;   // url-id bitmap (DList::bm; large lists only, rebuilt with the url ids)
+  DList dl() const { return DList{khi, klo, rows, n, uid, feat, head, nullptr, 0, bm}; }
 };
 
 // device-wide allocation events (hipMalloc / hipFree / hipHostMalloc / hipHostFree
@@ -353,6 +354,8 @@ struct CtxBase {
   size_t uid_cap = 0;
   uint32_t* head_all = nullptr;  // every list's line heads (DList::head)
   size_t head_cap = 0;
+  uint64_t* bm_all = nullptr;    // the bitmaps of the large lists (DList::bm)
+  size_t bm_cap = 0;
   uint64_t* dkhi = nullptr;  // key of every url id (72-bit Base64 key: hi 64 bits, low byte)
   uint8_t* dklo = nullptr;
   size_t dict_cap = 0;

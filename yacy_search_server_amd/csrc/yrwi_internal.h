@@ -49,6 +49,11 @@ struct DList {
   // rows of the fold's lists 0..tw-1 it joins, tw per row (tup[row * tw + list])
   const int32_t* tup;
   int32_t tw;
+  // url-id bitmap of a large index list (nullptr: none), 16 B per 64 ids: word
+  // 2w = bits of ids 64w..64w+63, word 2w+1 = the list position of the first id
+  // of word 2w (rank): membership and position of an id in one 16-B load.
+  // k_probe looks the smaller side's ids up in it instead of searching the list.
+  const uint64_t* bm;
 };
 // the two head levels of a list of n postings (each level padded to 32 entries)
 __host__ __device__ constexpr int64_t head1_n(int64_t n) { return (n + 31) >> 5; }
@@ -82,6 +87,7 @@ enum JoinMode : int32_t {
 // for skewed ones (the galloping bound of BASELINE.md §4).
 enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1 };
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
+constexpr int BM_TILE = 2048;    // small-list elements per bitmap-probe workgroup (8 per thread)
 
 // The lists of a multi-term fold and the join mode of each step, for the last
 // step's k_compact: it folds the deferred rows' records (J5/J6 step by step,
@@ -99,6 +105,8 @@ struct JoinQ {
   int32_t maxd;
   int32_t algo;        // JoinAlgo
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
+  int32_t ptile;       // JA_PROBE: small-list elements per tile (PROBE_TILE, BM_TILE with a bitmap)
+  int32_t pad_;
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
@@ -111,7 +119,7 @@ struct JoinQ {
   const FoldSrc* fold;
   // matched pairs of the job: [pair_base, pair_base + cap) of the step's pair
   // arrays; every tile writes its run at tile_src[tile] (merge tiles: the prefix
-  // of their bounds min(na, nb + 1); probe tiles: PROBE_TILE per tile)
+  // of their bounds min(na, nb + 1); probe tiles: ptile per tile)
   int64_t pair_base;
 };
 

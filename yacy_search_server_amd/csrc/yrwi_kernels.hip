@@ -599,12 +599,17 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const JoinQ& J = jobs[j];
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
-  const int64_t s0 = (tile0 + t - tile_base[j]) * PROBE_TILE;
-  const int64_t s1 = s0 + PROBE_TILE < Sm.n ? s0 + PROBE_TILE : Sm.n;
-  const uint32_t k0 = Sm.uid[s0], k1 = Sm.uid[s1 - 1];
+  const int64_t s0 = (tile0 + t - tile_base[j]) * J.ptile;
+  const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
+  if (Lg.bm) {  // bitmap probe: no range needed
+    D.lo = D.hi = 0;
+    pdesc[t] = D;
+    return;
+  }
+  const uint32_t k0 = Sm.uid[s0], k1 = Sm.uid[s1 - 1];
   if (Lg.head) {  // index list: through its line heads (level 2, one level-1 line, one leaf line)
     D.lo = lower_bound_list(Lg, k0);
     D.hi = lower_bound_list(Lg, k1 + 1u);  // ids < 2^32 - 1: k1 + 1 does not wrap
@@ -644,14 +649,73 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const JoinQ& J = jobs[D.job];
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
+  if (Lg.bm) {
+    // url-id bitmap of the large list: one 16-B load per key gives membership and,
+    // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
+    // small-list ids per tile, 8 consecutive ones per thread (hits stay in order).
+    constexpr int KPT = BM_TILE / PROBE_TILE;
+    const int64_t s0 = (b - tile_base[D.job]) * BM_TILE;
+    const int64_t i0 = s0 + (int64_t)threadIdx.x * KPT;
+    uint32_t keys[KPT];
+    if (i0 + KPT <= Sm.n) {
+      const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
+      const uint4 u0 = q[0], u1 = q[1];
+      keys[0] = u0.x; keys[1] = u0.y; keys[2] = u0.z; keys[3] = u0.w;
+      keys[4] = u1.x; keys[5] = u1.y; keys[6] = u1.z; keys[7] = u1.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < KPT; k++) keys[k] = i0 + k < Sm.n ? Sm.uid[i0 + k] : 0u;
+    }
+    uint32_t hm = 0;
+    int64_t jls[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      jls[k] = 0;
+      if (i0 + k >= Sm.n) continue;
+      const ulonglong2 E = reinterpret_cast<const ulonglong2*>(Lg.bm)[keys[k] >> 6];
+      const uint64_t bit = 1ull << (keys[k] & 63u);
+      if (E.x & bit) {
+        hm |= 1u << k;
+        jls[k] = (int64_t)E.y + __popcll(E.x & (bit - 1ull));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      if (!((hm >> k) & 1u)) continue;
+      const int64_t ia = J.small_is_A ? i0 + k : jls[k], ib = J.small_is_A ? jls[k] : i0 + k;
+      if (mark) {
+        J.removed[ia] = 1;
+      } else if (J.maxd < 65535 &&
+                 joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) {
+        hm &= ~(1u << k);
+      }
+    }
+    if (mark) return;
+    int32_t tot;
+    int32_t off = block_excl_sum256(__popc(hm), sScan, &tot);
+    const int64_t src = J.pair_base + s0;  // BM_TILE pair slots per tile
+    if (threadIdx.x == 0) {
+      tile_src[b] = src;
+      tile_cnt[b] = tot;
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      if (!((hm >> k) & 1u)) continue;
+      const int64_t ia = J.small_is_A ? i0 + k : jls[k], ib = J.small_is_A ? jls[k] : i0 + k;
+      pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
+      pair_uid[src + off] = keys[k];
+      off++;
+    }
+    return;
+  }
   const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
   const int64_t i = s0 + threadIdx.x;
   bool hit = false;
   int64_t jl = 0;
   uint32_t key = 0;
 #if PROBE_LDS > 0
-  const int64_t R = D.hi - D.lo;  // workgroup-uniform
-  if (R <= PROBE_LDS) {
+  if (D.hi - D.lo <= PROBE_LDS) {  // workgroup-uniform
+    const int64_t R = D.hi - D.lo;
     // short range: read it once, coalesced, and search in LDS -- 4 B per range
     // id instead of the two or three sector gathers per key of the lower levels
     const uint32_t* __restrict__ g = Lg.uid + D.lo;
