@@ -208,7 +208,9 @@ int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_
  * host thread) while the caller prepares the next one.  q, the profiles it
  * points to, out, nout and st must stay valid until yrwi_query_batch_wait(ticket)
  * returns; every ticket must be waited for exactly once.  Lists must not be
- * changed while batches are in flight (put_list waits for them). */
+ * changed while batches are in flight (put_list waits for them).  Sharded
+ * contexts: every rank submits the same batches in the same order (the batches'
+ * device collectives are enqueued in submission order). */
 int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                             yrwi_hit* out, int32_t* nout, yrwi_stats* st, int64_t* ticket);
 int yrwi_query_batch_wait(yrwi_ctx* ctx, int64_t ticket);
