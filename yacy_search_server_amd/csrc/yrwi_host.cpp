@@ -347,7 +347,9 @@ extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostin
   if (nterms) *nterms = (int64_t)ctx->lists.size();
   if (npostings) *npostings = ctx->npostings;
   if (device_bytes) {
-    size_t b = ctx->index_mem.capacity();
+    // index memory, url ids, line heads, bitmaps, url dictionary, lane scratch
+    size_t b = ctx->index_mem.capacity() + ctx->uid_cap * 4 + ctx->head_cap * 4 + ctx->bm_cap * 8 +
+               ctx->dict_cap * 9;
     for (Lane* L : ctx->lanes) b += L->arena.capacity();
     *device_bytes = (int64_t)b;
   }
