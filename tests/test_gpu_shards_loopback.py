@@ -249,3 +249,36 @@ def test_loopback_async_batches_in_flight(world):
             assert len(got) == len(qs), (r, i)
             for j, g in enumerate(got):
                 assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp[j], (r, i, j)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_many_batches_in_flight(world):
+    """Stress of the sharded lanes: 40 submitted batches per rank (more than the
+    lanes and the mailbox's slot window, so lanes and slots are reused while
+    other batches still run), sizes 1-30 queries with 1-4 include terms, one
+    exclude term in every third batch, the authority profile in every fifth.
+    Every batch must come back bit-exact and nothing may hang."""
+    full = synth.preset("tiny")
+    whole_ix = synth.build_index(full)
+    whole, H = whole_ix.as_dict(), whole_ix.hashes
+    c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+    rng = np.random.default_rng(7)
+    sets = [synth.queries(full, int(rng.integers(1, 31)), 1, 4, 1 if i % 3 == 0 else 0, qseed=500 + i)
+            for i in range(40)]
+
+    def prof(i):
+        return c5 if i % 5 == 0 else None
+
+    def fn(r, ix):
+        pend = [ix.submit([Query([H[t] for t in inc], [H[t] for t in exc], now_ms=NOW, k=50, profile=prof(i))
+                           for inc, exc in qs]) for i, qs in enumerate(sets)]
+        return [p.result() for p in pend]
+
+    parts = [synth.build_index(full.shard(r, world)).as_dict() for r in range(world)]
+    res = _run_parts(parts, world, fn)
+    for i, qs in enumerate(sets):
+        exp = [orc.search(whole, [H[t] for t in inc], [H[t] for t in exc],
+                          profile=(orc.profile_from(prof(i)) if prof(i) else None), now_ms=NOW, k=50)
+               for inc, exc in qs]
+        for r in range(world):
+            assert [[(h.urlhash, h.score, h.tiebreak) for h in g] for g in res[r][i]] == exp, (r, i)
