@@ -228,9 +228,18 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
     bool ok = ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
     if (ok) ctx->lanes[0]->comm = c0;
     if (ok && rank == 0) hostx_unlink(ctx->hostx);  // every rank has it mapped (opened before the collective init)
-    // one communicator per lane: lanes issue their collectives independently
-    for (size_t l = 1; ok && l < ctx->lanes.size(); l++)
-      ok = ncclCommSplit(c0, 0, rank, &ctx->lanes[l]->comm, nullptr) == ncclSuccess;
+    // one communicator per lane: lanes issue their collectives independently.  If
+    // the split fails (the same way on every rank), the lanes share c0 -- still
+    // safe: the collective turn lets one batch part at a time enqueue, in one
+    // total order on every rank (close_lanes destroys c0 once).
+    bool split = ok;
+    for (size_t l = 1; split && l < ctx->lanes.size(); l++)
+      split = ncclCommSplit(c0, 0, rank, &ctx->lanes[l]->comm, nullptr) == ncclSuccess;
+    if (ok && !split)
+      for (size_t l = 1; l < ctx->lanes.size(); l++) {
+        if (ctx->lanes[l]->comm && ctx->lanes[l]->comm != c0) ncclCommDestroy(ctx->lanes[l]->comm);
+        ctx->lanes[l]->comm = c0;
+      }
     if (!ok) {
       yrwi_close(ctx);
       *out = nullptr;
