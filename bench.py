@@ -412,6 +412,11 @@ def run(args, rank, world, local):
     iso, timed = M["iso"], M["timed"]
     pmc = load_pmc(args.config) if world == 1 and args.shard_of == 1 else None
     roof = roofline_path(iso, pmc, None)
+    # the same bytes over the timed region's time per batch (batches in flight overlap)
+    if timed.get("bytes_alg") and ms_per_step > 0:
+        ach = timed["bytes_alg"] / args.steps / (ms_per_step * 1e-3) / 1e9  # this rank's bytes: per GPU
+        roof["throughput_mode"] = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                                   "per": "GPU", "time": "ms_per_step (timed region, batches in flight)"}
     kern = roofline_kernels(iso, pmc)
 
     # single-query latency (host call -> top-k in host memory)
