@@ -59,7 +59,9 @@ def parse_args(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--shard-of", type=int, default=1,
                     help="(1 GPU) run the rank-0 url-hash shard of a W-GPU corpus: the per-GPU slice of C3/C5")
-    ap.add_argument("--legs", default="C3,C4,C5", help="extra BASELINE configs after the headline, or 'none'")
+    ap.add_argument("--legs", default="auto",
+                    help="extra BASELINE configs after the headline ('C3,C4,C5'), or 'none'; "
+                         "auto: C3,C4,C5 on one GPU, none for N > 1 (the scaling runs time the headline only)")
     ap.add_argument("--leg-steps", type=int, default=20)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -465,6 +467,8 @@ def run(args, rank, world, local):
     del idx
 
     legs = {}
+    if args.legs == "auto":
+        args.legs = "C3,C4,C5" if world == 1 else "none"
     if args.legs and args.legs != "none" and args.shard_of == 1:
         for leg in [x.strip() for x in args.legs.split(",") if x.strip()]:
             try:
