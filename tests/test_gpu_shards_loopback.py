@@ -251,13 +251,18 @@ def test_loopback_async_batches_in_flight(world):
                 assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp[j], (r, i, j)
 
 
+@pytest.mark.parametrize("hostx", [1, 0])
 @pytest.mark.parametrize("world", [2, 8])
-def test_loopback_many_batches_in_flight(world):
+def test_loopback_many_batches_in_flight(world, hostx, monkeypatch):
     """Stress of the sharded lanes: 40 submitted batches per rank (more than the
     lanes and the mailbox's slot window, so lanes and slots are reused while
     other batches still run), sizes 1-30 queries with 1-4 include terms, one
     exclude term in every third batch, the authority profile in every fifth.
-    Every batch must come back bit-exact and nothing may hang."""
+    hostx = 0: no shared-memory mailbox, the planning sizes go through the device
+    all-gather under the collective turn.  Every batch must come back bit-exact
+    and nothing may hang."""
+    if not hostx:
+        monkeypatch.setenv("YRWI_NO_HOSTX", "1")
     full = synth.preset("tiny")
     whole_ix = synth.build_index(full)
     whole, H = whole_ix.as_dict(), whole_ix.hashes
