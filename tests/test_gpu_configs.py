@@ -1,14 +1,14 @@
 """BASELINE configurations and size-edge cases through the HIP path, checked
 against the oracle (bit-exact: url hashes, order, scores, tie-breaks).
 
-  C2  the full 100M-posting index, 64 of the bench's 2-term AND queries
+  C2  the full 100M-posting index, all 1000 of the bench's 2-term AND queries
   C3  the per-GPU url-hash shard (1 of 8) of the 1B corpus, 3-term AND + 1 exclude
   C4  one batch of 4096 concurrent 2-4 term queries over that shard; 64 checked
   C5  the custom (authority) and /date profiles on the per-GPU shard of the 5B corpus
   J2/J3 int wrap: list sizes whose (int)(size*1000 + i) fold keys and
       12*log2(high)*low dispatch counts wrap (ReferenceContainer.java:334-366,406-416)
-  k_probe ranges of 0, 1, 4095, 4096 and 4097 large-list ids around the
-      LDS-staging threshold (PROBE_LDS), with and without exclusion
+  k_probe ranges around the LDS-staging threshold (PROBE_LDS) and the line-head
+      levels, with and without exclusion, with and without url-id bitmaps
 
 The C3 / C4 / C5 cases generate only the lists of the query terms -- exactly as
 the full corpus holds them (the generator is per term); the other
@@ -46,12 +46,12 @@ def _check(ix, idx, qs, prof=None, k=100, sample=None):
     return got
 
 
-def test_c2_full_index_64_queries():
+def test_c2_full_index_all_bench_queries():
     cfg = synth.preset("C2")
     idx = synth.build_index(cfg)
     ix = _load(idx)
     try:
-        _check(ix, idx, synth.queries(cfg, 64, 2, 2, 0))  # the bench's first 64 queries
+        _check(ix, idx, synth.queries(cfg, 1000, 2, 2, 0))  # the bench's batch, every query
     finally:
         ix.close()
 
