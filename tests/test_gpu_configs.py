@@ -4,7 +4,7 @@ against the oracle (bit-exact: url hashes, order, scores, tie-breaks).
   C2  the full 100M-posting index, all 1000 of the bench's 2-term AND queries
   C3  the per-GPU url-hash shard (1 of 8) of the 1B corpus, 1000 3-term AND + 1 exclude
   C4  one batch of 4096 concurrent 2-4 term queries over that shard; every 4th (1024) checked
-  C5  the custom (authority) and /date profiles on the per-GPU shard of the 5B corpus
+  C5  the custom (authority) and /date profiles on the per-GPU shard of the 5B corpus (100 queries each)
   J2/J3 int wrap: list sizes whose (int)(size*1000 + i) fold keys and
       12*log2(high)*low dispatch counts wrap (ReferenceContainer.java:334-366,406-416)
   k_probe ranges around the LDS-staging threshold (PROBE_LDS) and the line-head
@@ -82,7 +82,7 @@ def test_c4_batch_4096_queries(c3_shard):
 def test_c5_profiles_on_shard():
     full = synth.preset("C5")
     cfg = full.shard(0, 8)
-    qs = synth.queries(full, 24, 2, 4, 0)
+    qs = synth.queries(full, 100, 2, 4, 0)
     terms = sorted({t for inc, exc in qs for t in inc + exc})
     idx = synth.build_index(cfg, terms=np.array(terms))
     ix = _load(idx, terms)
