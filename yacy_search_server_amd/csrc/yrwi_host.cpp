@@ -169,7 +169,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   // batch parts are enqueued in one total order on every rank (CollTurn,
   // yrwi_host.h).  Scratch: 128 GiB over all lanes (scratch_budget).
   const char* e = getenv("YRWI_LANES");
-  const int nl = e ? std::max(1, std::min(8, atoi(e))) : 8;
+  const int nl = e ? std::max(1, std::min(16, atoi(e))) : 8;
   for (int l = 0; l < nl; l++) {
     Lane* L = new Lane();
     L->device = device;
