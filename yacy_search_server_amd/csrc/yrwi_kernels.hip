@@ -1156,6 +1156,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 #pragma unroll
   for (int j = 0; j < NP2; j++) { pmn[j] = 0xFFFFFFFFu; pmx[j] = 0u; }
   int32_t pmax = -1, nval = 0, myfirst = BIG;
+  int32_t hmax = 0;  // largest host count this thread saw (one atomicMax per wave below)
   int32_t tcn = -1, tdn = 1, tcx = -1, tdx = 1;  // tf min / max as fractions (-1: none yet)
   int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
 #pragma unroll
@@ -1202,7 +1203,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
           unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
           if (prev == 0ull || prev == key) {
             uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
-            atomicMax(&shard[qi].maxdom, (int32_t)cnt);
+            hmax = max(hmax, (int32_t)cnt);  // the last increment of every host sees its final count
             break;
           }
           slot = (slot + 1) & Q.hmask;
@@ -1210,6 +1211,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       }
     }
     sPO[eo + (eo >> 5)] = po;
+  }
+  if (Q.want_authority) {  // block-uniform: one atomicMax per wave instead of one per posting
+    const int32_t wm = wave_max_i(hmax);
+    if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
   }
   // first valid element of the chunk (element order)
   int32_t firstIdx;
