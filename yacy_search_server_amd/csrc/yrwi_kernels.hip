@@ -2316,6 +2316,9 @@ __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t 
 }
 
 
+#ifndef YRWI_CARD_TAB_MIN
+#define YRWI_CARD_TAB_MIN 512
+#endif
 // Chunks run in `order` (every query's first chunks before anybody's later ones),
 // so a big query's later chunks find its threshold (Tq, see PruneP) established.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
@@ -2368,15 +2371,19 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
     return;
   }
-  build_card_tab(&sCard, N, Q);
+  // the one-byte fields' term tables pay off only for a chunk with many postings
+  // (2304 entries per workgroup); a short chunk computes its few cardinals directly
+  const int64_t nel = Q.n - c * CHUNK < CHUNK ? Q.n - c * CHUNK : CHUNK;
+  const CardTab* tab = nel > YRWI_CARD_TAB_MIN ? &sCard : nullptr;  // workgroup-uniform
+  if (tab) build_card_tab(&sCard, N, Q);
   __syncthreads();
   const PruneP P = sP;
   const uint64_t T0 = sT;
   PHASE(5)
   const bool comp = T0 && P.ok && !F;
-  const int32_t nc = comp ? prune_chunk(Q, N, c, T0, P, &sCard, sIdx, sScan) : 0;
-  const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, &sCard, sIdx, nc)
-                           : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, &sCard);
+  const int32_t nc = comp ? prune_chunk(Q, N, c, T0, P, tab, sIdx, sScan) : 0;
+  const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, tab, sIdx, nc)
+                           : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, tab);
   int32_t nv;
   int32_t voff = block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   PHASE(0)
