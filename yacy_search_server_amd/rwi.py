@@ -474,7 +474,8 @@ class RWIIndex:
     def submit_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> int:
         """Start a batch; the ctypes buffers must stay alive until wait(ticket)."""
         t = ctypes.c_int64()
-        _check(self._h, _lib.lib().yrwi_query_batch_submit(self._h, cq, nq, kmax, hits, nout, ctypes.byref(st),
+        _check(self._h, _lib.lib().yrwi_query_batch_submit(self._h, cq, nq, kmax, hits, nout,
+                                                           ctypes.byref(st) if st is not None else None,
                                                            ctypes.byref(t)))
         return t.value
 
