@@ -148,6 +148,7 @@ static void close_lanes(yrwi_ctx* ctx) {
     for (auto e : L->evpool) hipEventDestroy(e);
     if (L->stage.p) hipHostFree(L->stage.p);
     if (L->out_stage.p) hipHostFree(L->out_stage.p);
+    if (L->down_stage.p) hipHostFree(L->down_stage.p);
     if (L->sync_ev) hipEventDestroy(L->sync_ev);
     if (L->stream && L->own_stream) hipStreamDestroy(L->stream);
     delete L;
@@ -710,9 +711,13 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (st) st->n_join_launches++;
   const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
-  HIPCHK(ctx, hipMemcpyAsync(mh.data(), d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  // joined sizes through pinned memory (a pageable readback is staged by the runtime)
+  uint8_t* land = stage_reserve(ctx, &ctx->down_stage, (size_t)nj * sizeof(int64_t), true);
+  if (!land) return YRWI_E_HIP;
+  HIPCHK(ctx, hipMemcpyAsync(land, d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   const int64_t h5 = hprof ? now_ns() : 0;
   HIPCHK(ctx, lane_sync(ctx));
+  std::memcpy(mh.data(), land, (size_t)nj * sizeof(int64_t));
   if (hprof)
     fprintf(stderr, "[yrwi join] jobs %d layout %.3f alloc %.3f upload %.3f launch %.3f d2h %.3f sync %.3f ms\n", nj,
             (h1 - h0) / 1e6, (h2 - h1) / 1e6, (h3 - h2) / 1e6, (h4 - h3) / 1e6, (h5 - h4) / 1e6,

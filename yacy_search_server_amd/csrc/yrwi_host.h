@@ -230,6 +230,7 @@ struct Lane {
   hipEvent_t coll_ev[2] = {nullptr, nullptr};
   Stage stage;
   Stage out_stage;           // pinned landing buffer for results
+  Stage down_stage;          // pinned landing buffer for small per-step readbacks (joined sizes)
   int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
   const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
   const uint8_t* dklo = nullptr;
