@@ -87,7 +87,10 @@ enum JoinMode : int32_t {
 // for skewed ones (the galloping bound of BASELINE.md §4).
 enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1 };
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
-constexpr int BM_TILE = 2048;    // small-list elements per bitmap-probe workgroup (8 per thread)
+#ifndef YRWI_BM_TILE
+#define YRWI_BM_TILE 1024
+#endif
+constexpr int BM_TILE = YRWI_BM_TILE;  // small-list elements per bitmap-probe workgroup (4 per thread; 2048: probe 168 -> 198 us on C2, 4096: 243)
 
 // The lists of a multi-term fold and the join mode of each step, for the last
 // step's k_compact: it folds the deferred rows' records (J5/J6 step by step,

@@ -672,14 +672,17 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
     // small-list ids per tile, 8 consecutive ones per thread (hits stay in order).
     constexpr int KPT = BM_TILE / PROBE_TILE;
+    static_assert(KPT % 4 == 0 && KPT <= 32, "bitmap tile: whole uint4 loads, one hit bit per key");
     const int64_t s0 = (b - tile_base[D.job]) * BM_TILE;
     const int64_t i0 = s0 + (int64_t)threadIdx.x * KPT;
     uint32_t keys[KPT];
     if (i0 + KPT <= Sm.n) {
       const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
-      const uint4 u0 = q[0], u1 = q[1];
-      keys[0] = u0.x; keys[1] = u0.y; keys[2] = u0.z; keys[3] = u0.w;
-      keys[4] = u1.x; keys[5] = u1.y; keys[6] = u1.z; keys[7] = u1.w;
+#pragma unroll
+      for (int v = 0; v < KPT / 4; v++) {
+        const uint4 u = q[v];
+        keys[4 * v] = u.x; keys[4 * v + 1] = u.y; keys[4 * v + 2] = u.z; keys[4 * v + 3] = u.w;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < KPT; k++) keys[k] = i0 + k < Sm.n ? Sm.uid[i0 + k] : 0u;
