@@ -3,4 +3,4 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 900 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
-bash tools/kstats.sh r02o
+bash tools/kstats.sh final
