@@ -672,16 +672,25 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
     // small-list ids per tile, 8 consecutive ones per thread (hits stay in order).
     constexpr int KPT = BM_TILE / PROBE_TILE;
-    static_assert(KPT % 4 == 0 && KPT <= 32, "bitmap tile: whole uint4 loads, one hit bit per key");
+    static_assert(KPT % 2 == 0 && KPT <= 32, "bitmap tile: whole uint2 / uint4 loads, one hit bit per key");
     const int64_t s0 = (b - tile_base[D.job]) * BM_TILE;
     const int64_t i0 = s0 + (int64_t)threadIdx.x * KPT;
     uint32_t keys[KPT];
     if (i0 + KPT <= Sm.n) {
-      const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
+      if constexpr (KPT % 4 == 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
 #pragma unroll
-      for (int v = 0; v < KPT / 4; v++) {
-        const uint4 u = q[v];
-        keys[4 * v] = u.x; keys[4 * v + 1] = u.y; keys[4 * v + 2] = u.z; keys[4 * v + 3] = u.w;
+        for (int v = 0; v < KPT / 4; v++) {
+          const uint4 u = q[v];
+          keys[4 * v] = u.x; keys[4 * v + 1] = u.y; keys[4 * v + 2] = u.z; keys[4 * v + 3] = u.w;
+        }
+      } else {
+        const uint2* q = reinterpret_cast<const uint2*>(Sm.uid + i0);
+#pragma unroll
+        for (int v = 0; v < KPT / 2; v++) {
+          const uint2 u = q[v];
+          keys[2 * v] = u.x; keys[2 * v + 1] = u.y;
+        }
       }
     } else {
 #pragma unroll
