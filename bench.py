@@ -113,6 +113,19 @@ def cgroup_cpus():
         return None
 
 
+def cgroup_cpu_stat():
+    """The job's cgroup CPU accounting (usage / throttling counters), or None."""
+    try:
+        out = {}
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                out[k] = int(v)
+        return out
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores():
     """(threads used, affinity cores, why): every core of this process's affinity,
     capped by what the job may actually use -- the cgroup CPU quota (cpu.max) and
@@ -230,6 +243,7 @@ class Runner:
         (one batch in flight) whose library statistics give the per-kernel times."""
         import ctypes
         import torch
+        from yacy_search_server_amd import _lib
         from yacy_search_server_amd._lib import CHit, CQuery, CStats
         ix = self.ix
         arr = (CQuery * nq)()
@@ -291,14 +305,23 @@ class Runner:
             agg[f] = 0
         self.barrier()
         torch.cuda.synchronize()
+        gap = float(os.environ.get("YRWI_BENCH_GAP_MS", "0"))  # diagnosis: idle time before the timed region
+        if gap > 0:
+            time.sleep(gap / 1e3)
+        r0 = _lib.lib().yrwi_realloc_events()
+        cs0 = cgroup_cpu_stat()
         t0 = time.perf_counter()
         run_steps(steps, stats=timed_stats)
         torch.cuda.synchronize()  # every batch was waited for; this brackets the device too
         self.barrier()
         dt = time.perf_counter() - t0
+        realloc_timed = int(_lib.lib().yrwi_realloc_events() - r0)  # process-wide, no HIP events needed
+        cs1 = cgroup_cpu_stat()
+        throttle = {k: cs1[k] - cs0[k] for k in cs0 if k in cs1} if cs0 and cs1 else None
         if not timed_stats:
             for f in agg:
                 agg[f] = per_batch[f] * steps if f != "n_realloc" else 0
+        agg["n_realloc"] = realloc_timed
         total_post = float(agg["postings_in"])
         if self.dist is not None:
             tt = torch.tensor([dt, total_post], dtype=torch.float64, device="cuda")
@@ -326,6 +349,7 @@ class Runner:
             iso["batches"] = 1
             iso["isolated_runs_t_kernels_us"] = [round(r["t_kernels_ns"] / 1e3, 1) for r in runs]
         timed["stats_in_timed_region"] = timed_stats
+        timed["cgroup_cpu_stat"] = throttle
         return {"dt": dt, "steps": steps, "total_post": total_post, "timed": timed, "iso": iso, "bufs": bufs,
                 "arr": arr, "keep": keep}
 
@@ -530,9 +554,10 @@ def run(args, rank, world, local):
                             "n": len(lat)} if lat else None),
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
-            # device-wide allocations inside the timed steps (counted only when the timed
-            # region collects statistics, YRWI_BENCH_STATS=1; the warm-up grows every arena)
-            "realloc_events_timed": timed["n_realloc"] if timed["stats_in_timed_region"] else None,
+            # device-wide allocation events (scratch / pinned staging growth) inside the timed steps
+            "realloc_events_timed": timed["n_realloc"],
+            # the job's CPU-quota accounting over the timed region (cgroup cpu.stat deltas)
+            "cgroup_cpu_stat_timed": timed.get("cgroup_cpu_stat"),
             "timed_region": ("batches submitted with per-batch statistics (YRWI_BENCH_STATS=1)"
                              if timed["stats_in_timed_region"] else
                              "batches submitted without statistics (no HIP events: the production call); "

@@ -162,6 +162,11 @@ int yrwi_build_url_ids(yrwi_ctx* ctx);
  * entries out of order (0 when consistent); *nurls = dictionary size (may be NULL). */
 int yrwi_check_url_ids(yrwi_ctx* ctx, int64_t* bad, int64_t* nurls);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
+/* Device-wide allocation events of the process so far (scratch arena growth,
+ * pinned staging growth: each one stalls every lane of the device while it
+ * runs).  A caller counts them around a timed region without per-batch
+ * statistics; steady-state batches make none. */
+int64_t yrwi_realloc_events(void);
 /* Diagnostic of the node's shared-memory size exchange (no GPU needed): rank
  * `rank` of `world` processes / threads sharing group id `id` runs `nparts`
  * batch parts of `ncalls` exchanges each, vectors of n values (rank + part +

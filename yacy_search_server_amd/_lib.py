@@ -117,6 +117,7 @@ SIGNATURES = {
     "yrwi_list_size": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "yrwi_index_stats": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_realloc_events": (ctypes.c_int64, []),
     "yrwi_query": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.POINTER(CHit),
                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CStats)]),
     "yrwi_query_batch": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.c_int32, ctypes.c_int32,

@@ -125,7 +125,7 @@ void turn_acquire(Lane* L) {
 }
 
 void turn_release(Lane* L) {
-  if (!L->turn || L->seq < 0 || L->world <= 1) {  // one context: no collectives to order
+  if (!L->turn || L->seq < 0 || !L->sharded) {  // one context: no collectives to order
     L->seq = -1;
     return;
   }
@@ -164,14 +164,23 @@ struct HxSlot {
 };
 }  // namespace
 
+// segment header: ranks that mapped it (the last of `world` unlinks the name)
+struct HxHead {
+  std::atomic<int32_t> attached;
+  char pad[60];
+};
+
 struct HostX {
   void* base = nullptr;
   size_t bytes = 0;
   int world = 0, rank = 0;
   std::string name;
-  HxSlot* slot(int i) const { return reinterpret_cast<HxSlot*>(static_cast<char*>(base) + (size_t)i * sizeof(HxSlot)); }
+  HxHead* head() const { return static_cast<HxHead*>(base); }
+  HxSlot* slot(int i) const {
+    return reinterpret_cast<HxSlot*>(static_cast<char*>(base) + sizeof(HxHead) + (size_t)i * sizeof(HxSlot));
+  }
   HxEntry* entry(int i, int r) const {
-    char* e0 = static_cast<char*>(base) + (size_t)HX_SLOTS * sizeof(HxSlot);
+    char* e0 = static_cast<char*>(base) + sizeof(HxHead) + (size_t)HX_SLOTS * sizeof(HxSlot);
     return reinterpret_cast<HxEntry*>(e0 + ((size_t)i * world + r) * sizeof(HxEntry));
   }
 };
@@ -182,7 +191,8 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank) {
   for (int i = 0; i < 128; i++) h = (h ^ id[i]) * 1099511628211ull;
   char nm[64];
   snprintf(nm, sizeof(nm), "/yrwi-hx-%016llx-%d", (unsigned long long)h, world);
-  const size_t bytes = (size_t)HX_SLOTS * sizeof(HxSlot) + (size_t)HX_SLOTS * world * sizeof(HxEntry);
+  const size_t bytes =
+      sizeof(HxHead) + (size_t)HX_SLOTS * sizeof(HxSlot) + (size_t)HX_SLOTS * world * sizeof(HxEntry);
   const int fd = shm_open(nm, O_CREAT | O_RDWR, 0600);  // zero-filled when new: every slot free
   if (fd < 0) return nullptr;
   if (ftruncate(fd, (off_t)bytes) != 0) {
@@ -198,8 +208,14 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank) {
   x->world = world;
   x->rank = rank;
   x->name = nm;
+  // every rank of the group maps the segment before its first exchange (at
+  // open); the last one to do so removes the name, so nothing is left in
+  // /dev/shm whatever way the processes end
+  if (x->head()->attached.fetch_add(1, std::memory_order_acq_rel) + 1 == world) shm_unlink(nm);
   return x;
 }
+
+int hostx_attached(const HostX* x) { return x ? x->head()->attached.load(std::memory_order_acquire) : 0; }
 
 void hostx_close(HostX* x, bool unlink_name) {
   if (!x) return;
@@ -208,13 +224,11 @@ void hostx_close(HostX* x, bool unlink_name) {
   delete x;
 }
 
-void hostx_unlink(HostX* x) {
-  if (x) shm_unlink(x->name.c_str());
-}
-
-// spin, then yield; false after `limit` (a peer that never arrives: fail, do not hang)
+// spin, then yield; false after YRWI_HOSTX_TIMEOUT_S (default 60 s: a peer that
+// never arrives fails the batch instead of hanging it)
 template <class F>
-static bool hx_wait(F ready, double limit_s = 300.0) {
+static bool hx_wait(F ready) {
+  static const double limit_s = getenv("YRWI_HOSTX_TIMEOUT_S") ? atof(getenv("YRWI_HOSTX_TIMEOUT_S")) : 60.0;
   const auto t0 = std::chrono::steady_clock::now();
   for (int64_t i = 0;; i++) {
     if (ready()) return true;
@@ -296,8 +310,8 @@ extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, i
 namespace yrwi {
 
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
-  if (L->world > 1) turn_acquire(L);
-  if (L->world <= 1) {
+  if (L->sharded) turn_acquire(L);
+  if (!L->sharded) {
     if (hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, L->stream) != hipSuccess)
       return L->fail(YRWI_E_HIP, "copy");
     return 0;
@@ -320,7 +334,7 @@ int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
 }
 
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op) {
-  if (L->world <= 1 || n == 0) return 0;
+  if (!L->sharded || n == 0) return 0;
   turn_acquire(L);
   if (!L->loop) {
     if (ncclAllReduce(buf, buf, n, ncclInt32, max_op ? ncclMax : ncclSum, L->comm, L->stream) != ncclSuccess)

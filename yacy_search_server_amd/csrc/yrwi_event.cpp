@@ -121,8 +121,7 @@ extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const ch
     sl.push_back((uint8_t)key.lo);
   }
   std::vector<EvDev> hv{h};
-  if (upload(L, reinterpret_cast<uint64_t*>(base + o_sx), siteex) || upload(L, d_dev, hv) ||
-      upload(L, reinterpret_cast<uint64_t*>(base + o_sh), sh) || upload(L, base + o_sl, sl))
+  if (upload(L, reinterpret_cast<uint64_t*>(base + o_sx), siteex, d_dev, hv, reinterpret_cast<uint64_t*>(base + o_sh), sh, base + o_sl, sl))
     return fail(YRWI_E_HIP, "event upload");
   if (launch_event_seed(d_dev, reinterpret_cast<uint64_t*>(base + o_sh), base + o_sl, (int64_t)sh.size(), s))
     return fail(YRWI_E_HIP, "event seed launch");
@@ -189,7 +188,7 @@ extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
   }
   hipStream_t s = L->stream;
   if (total) HIPCHK(ctx, hipMemcpyAsync(d_rows, stg, (size_t)total * YRWI_ROW_BYTES, hipMemcpyHostToDevice, s));
-  if (upload(L, d_ev, hev) || upload(L, d_jobs, jobs) || upload(L, d_jb, jb)) return ctx->take(L, YRWI_E_HIP);
+  if (upload(L, d_ev, hev, d_jobs, jobs, d_jb, jb)) return ctx->take(L, YRWI_E_HIP);
   if (launch_event_add(d_ev, d_jobs, d_jb, (int32_t)evs.size(), d_status, s))
     return ctx->fail(YRWI_E_HIP, "event_add launch");
   std::vector<int32_t> st((size_t)narr);

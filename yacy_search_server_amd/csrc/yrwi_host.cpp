@@ -156,6 +156,24 @@ static void close_lanes(yrwi_ctx* ctx) {
   ctx->lanes.clear();
 }
 
+// What a lane's first batch would otherwise set up inside the caller's first
+// timed batches: its wait event, the pinned staging buffers (uploads, joined-size
+// readbacks, result landing), the first scratch chunk and the stream's hardware
+// queue (a first operation on it).  Runs on the lane's own thread at open.
+static int warm_lane(Lane* L) {
+  if (hipSetDevice(L->device) != hipSuccess) return L->fail(YRWI_E_HIP, "hipSetDevice");
+  constexpr size_t kStage = (size_t)4 << 20;
+  if (!stage_reserve(L, &L->stage, kStage, false) || !stage_reserve(L, &L->down_stage, kStage, false) ||
+      !stage_reserve(L, &L->out_stage, kStage, false))
+    return YRWI_E_HIP;
+  uint8_t* p = L->arena.alloc(256);
+  if (!p) return L->fail(YRWI_E_NOMEM, "scratch");
+  HIPCHK(L, hipMemsetAsync(p, 0, 256, L->stream));
+  HIPCHK(L, lane_sync(L));
+  L->arena.reset();
+  return 0;
+}
+
 static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   *out = nullptr;
   if (hipSetDevice(device) != hipSuccess) return YRWI_E_HIP;
@@ -188,8 +206,20 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
     }
     L->hostreg = &ctx->hostreg;
     L->turn = &ctx->turn;
+    L->scratch_hint = &ctx->scratch_hint;
     L->nlanes = nl;
     L->start_worker();
+  }
+  for (Lane* L : ctx->lanes) L->submit([L] { L->rc = warm_lane(L); });
+  int wrc = 0;
+  for (Lane* L : ctx->lanes) {
+    L->wait();
+    if (L->rc && !wrc) wrc = L->rc;
+  }
+  if (wrc) {
+    close_lanes(ctx);
+    delete ctx;
+    return wrc;
   }
   ctx->stream = ctx->lanes[0]->stream;
   *out = ctx;
@@ -203,11 +233,17 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
   int rc = open_common(device, rank, world, out);
   if (rc) return rc;
   yrwi_ctx* ctx = *out;
+  const bool loop = world > 1 && std::memcmp(nccl_id, LOOP_TAG, sizeof(LOOP_TAG)) == 0;
+  // YRWI_COLL_SELF=1: a world-1 context runs the sharded protocol over a real
+  // 1-rank communicator (tests: RCCL on a one-GPU box; Lane::sharded)
+  const char* cs = getenv("YRWI_COLL_SELF");
+  ctx->sharded = world > 1 || (cs && atoi(cs));
+  for (Lane* L : ctx->lanes) L->sharded = ctx->sharded;
   if (world > 1) {  // list-size exchanges through host shared memory (the ranks of one node)
     ctx->hostx = hostx_open(nccl_id, world, rank);
     for (Lane* L : ctx->lanes) L->hostx = ctx->hostx;
   }
-  if (world > 1 && std::memcmp(nccl_id, LOOP_TAG, sizeof(LOOP_TAG)) == 0) {
+  if (loop) {
     // in-process loopback group (tests: several shards on one GPU), one per lane
     bool ok = true;
     for (size_t l = 0; ok && l < ctx->lanes.size(); l++) {
@@ -222,13 +258,31 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
       *out = nullptr;
       return YRWI_E_ARG;
     }
-  } else if (world > 1) {
+  } else if (ctx->sharded) {
     ncclUniqueId u;
     std::memcpy(&u, nccl_id, 128);
     ncclComm_t c0 = nullptr;
     bool ok = ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
     if (ok) ctx->lanes[0]->comm = c0;
-    if (ok && rank == 0) hostx_unlink(ctx->hostx);  // every rank has it mapped (opened before the collective init)
+    // the mailbox only works if every rank mapped the same segment (one node, one
+    // /dev/shm): every rank opened it before the init above, so after it each
+    // rank sees world attachments or not; all ranks agree (min over the ranks)
+    // and drop the mailbox together if any one saw fewer (device all-gather then)
+    if (ok && world > 1) {
+      int32_t* d_flag = nullptr;
+      int32_t flag = hostx_attached(ctx->hostx) == world ? 1 : 0;
+      ok = hipMalloc(&d_flag, 4) == hipSuccess;
+      ok = ok && hipMemcpy(d_flag, &flag, 4, hipMemcpyHostToDevice) == hipSuccess;
+      ok = ok && ncclAllReduce(d_flag, d_flag, 1, ncclInt32, ncclMin, c0, ctx->stream) == ncclSuccess;
+      ok = ok && hipMemcpyAsync(&flag, d_flag, 4, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
+      ok = ok && hipStreamSynchronize(ctx->stream) == hipSuccess;
+      if (d_flag) hipFree(d_flag);
+      if (ok && !flag && ctx->hostx) {
+        hostx_close(ctx->hostx, false);
+        ctx->hostx = nullptr;
+        for (Lane* L : ctx->lanes) L->hostx = nullptr;
+      }
+    }
     // one communicator per lane: lanes issue their collectives independently.  If
     // the split fails (the same way on every rank), the lanes share c0 -- still
     // safe: the collective turn lets one batch part at a time enqueue, in one
@@ -254,7 +308,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   close_lanes(ctx);
-  hostx_close(ctx->hostx, ctx->rank == 0);
+  hostx_close(ctx->hostx, false);  // unlinked once every rank mapped it (hostx_open)
   ctx->hostx = nullptr;
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
@@ -351,6 +405,8 @@ extern "C" int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n)
   *n = it == ctx->lists.end() ? 0 : it->second.n;
   return 0;
 }
+
+extern "C" int64_t yrwi_realloc_events(void) { return g_realloc.load(); }
 
 extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes) {
   if (!ctx) return YRWI_E_ARG;
@@ -504,7 +560,7 @@ static void plan_finish(Plan* P, const int64_t* ng_inc, const int64_t* ng_exc) {
 // Element-wise sum of v over the url-hash shards (every rank passes vectors of
 // the same length, in the same sequence of calls); identity on one context.
 static int allsum_host(Lane* L, std::vector<int64_t>& v) {
-  if (L->world <= 1 || v.empty()) return 0;
+  if (!L->sharded || v.empty()) return 0;
   const int hx = hostx_allsum(L, v);  // the node's shared-memory mailbox (no device collective, no turn)
   if (hx <= 0) return hx;
   const size_t n = v.size();
@@ -527,7 +583,7 @@ static int allsum_host(Lane* L, std::vector<int64_t>& v) {
 // plan_finish for a batch: global term sizes from one exchange of the local
 // sizes of the batch's distinct terms (sharded), or the local sizes (one context).
 static int plan_batch(Lane* L, std::vector<Plan>& plans) {
-  if (L->world <= 1) {  // one context: its own sizes are the global ones
+  if (!L->sharded) {  // one context: its own sizes are the global ones
     for (Plan& P : plans) {
       int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
       for (int i = 0; i < P.ninc; i++) gi[i] = P.linc[i] ? P.linc[i]->n : 0;
@@ -672,7 +728,12 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     for (const JoinQ& J : jobs)  // a probe job reads at most the galloping bound, whatever the reference dispatch
       (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) +=
           step_bytes(J.algo == JA_MERGE ? J.mode : (int32_t)JM_TEST_LARGE_A, J.A.n, J.B.n);
-  int64_t* d_mout = arena_alloc<int64_t>(ctx, nj);
+  // joined sizes land in pinned host memory: k_scan_tiles writes them through its
+  // device address (no copy engine), the host reads them after the step's sync
+  uint8_t* land = stage_reserve(ctx, &ctx->down_stage, (size_t)nj * sizeof(int64_t), true);
+  if (!land) return YRWI_E_HIP;
+  int64_t* d_mout = nullptr;
+  HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_mout), land, 0));
   // pair runs: a job matches at most min(nA, nB) postings (both sides strictly
   // ascending); merge tiles bound theirs by min(na, nb + 1), at most one more per tile
   int64_t npairs = 0;
@@ -691,10 +752,10 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   int64_t* d_src = arena_alloc<int64_t>(ctx, tiles);
   int32_t* d_cnt = arena_alloc<int32_t>(ctx, tiles);
   int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
-  if (!d_mout || !d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_src || !d_cnt || !d_off)
+  if (!d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_src || !d_cnt || !d_off)
     return ctx->fail(YRWI_E_NOMEM, "arena");
   const int64_t h2 = hprof ? now_ns() : 0;
-  if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
   const int64_t h3 = hprof ? now_ns() : 0;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
@@ -711,10 +772,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (st) st->n_join_launches++;
   const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
-  // joined sizes through pinned memory (a pageable readback is staged by the runtime)
-  uint8_t* land = stage_reserve(ctx, &ctx->down_stage, (size_t)nj * sizeof(int64_t), true);
-  if (!land) return YRWI_E_HIP;
-  HIPCHK(ctx, hipMemcpyAsync(land, d_mout, nj * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   const int64_t h5 = hprof ? now_ns() : 0;
   HIPCHK(ctx, lane_sync(ctx));
   std::memcpy(mh.data(), land, (size_t)nj * sizeof(int64_t));
@@ -773,7 +830,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
   if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
-  if (upload(ctx, d_jobs, jobs) || upload(ctx, d_tb, tile_base)) return YRWI_E_HIP;
+  if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
                        nullptr, true,
@@ -952,6 +1009,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
                           int32_t* h_nout, int64_t* h_scores_all, yrwi_stats* st, Timing* tm, bool exchange = true) {
   const int nq = (int)plans.size();
   const int W = exchange ? ctx->world : 1;
+  const bool shx = exchange && ctx->sharded;  // the url-hash-shard protocol
   static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
   int64_t hq[8] = {0};
   auto mark = [&](int i) { if (hprof) hq[i] = now_ns(); };
@@ -983,7 +1041,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.now_ms = P.now_ms;
     R.k = P.k;
     R.want_authority = P.prof.coeff_authority > 12 && R.n > 0;
-    R.idx_tag = W > 1 ? (uint32_t)ctx->rank << 28 : 0u;
+    R.idx_tag = shx ? (uint32_t)ctx->rank << 28 : 0u;
     R.doubledom = P.filter && P.filter->skip_double_dom ? 1 : 0;
     R.kout = P.k;
     if (R.doubledom) R.k = YRWI_MAX_K;  // pullOneRWI draws from the whole rwiStack (max_results_rwi)
@@ -1064,13 +1122,13 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       G.flagcount = plans[(size_t)qi].filter->flagcount ? d_flag + (int64_t)f * 32 : nullptr;
       rq[(size_t)qi].filt = d_fq + f;
     }
-    if (upload(ctx, d_fq, fq) || upload(ctx, d_sx, sx) || upload(ctx, d_uh, uh) || upload(ctx, d_ul, ul))
+    if (upload(ctx, d_fq, fq, d_sx, sx, d_uh, uh, d_ul, ul))
       return YRWI_E_HIP;
   }
   // flag counters back to the callers' filters (summed over the shards)
   auto flagcounts_out = [&]() -> int {
     if (!d_flag) return 0;
-    if (W > 1)
+    if (shx)
       if (int rc = coll_allreduce_i32(ctx, d_flag, (size_t)nf * 32, false)) return rc;
     std::vector<int32_t> h((size_t)nf * 32);
     HIPCHK(ctx, hipMemcpyAsync(h.data(), d_flag, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -1084,7 +1142,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   int64_t* d_cb = arena_alloc<int64_t>(ctx, nq);
   ChunkSum* d_cs = arena_alloc<ChunkSum>(ctx, chunks);
   ShardSum* d_ss = arena_alloc<ShardSum>(ctx, nq);
-  ShardSum* d_all = W > 1 ? arena_alloc<ShardSum>(ctx, (int64_t)nq * W) : d_ss;
+  ShardSum* d_all = shx ? arena_alloc<ShardSum>(ctx, (int64_t)nq * W) : d_ss;
   NormState* d_norm = arena_alloc<NormState>(ctx, nq);
   if (!d_q || !d_cb || !d_cs || !d_ss || !d_all || !d_norm) return ctx->fail(YRWI_E_NOMEM, "arena");
   std::vector<int32_t> chunk_q((size_t)chunks);
@@ -1093,17 +1151,17 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   int32_t* d_cq = arena_alloc<int32_t>(ctx, chunks);
   if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
   mark(1);
-  if (upload(ctx, d_q, rq) || upload(ctx, d_cb, chunk_base) || upload(ctx, d_cq, chunk_q)) return YRWI_E_HIP;
+  if (upload(ctx, d_q, rq, d_cb, chunk_base, d_cq, chunk_q)) return YRWI_E_HIP;
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
-  if (W > 1 && any_auth) {
+  if (shx && any_auth) {
     int rc2 = exchange_host_counts(ctx, nq, nslots, slot_base, d_hkeys, d_hcnt, d_ss);
     if (rc2) return rc2;
   }
-  if (W > 1) {
+  if (shx) {
     if (int rc = coll_allgather(ctx, d_ss, d_all, sizeof(ShardSum) * nq)) return rc;
   }
   sp = span_open(ctx, tm);
@@ -1210,7 +1268,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     Cand* d_out = arena_alloc<Cand>(ctx, ngr * keff);
     int32_t* d_oc = arena_alloc<int32_t>(ctx, ngr);
     if (!d_gb || !d_gn || !d_gk || !d_out || !d_oc) return ctx->fail(YRWI_E_NOMEM, "arena");
-    if (upload(ctx, d_gb, gb) || upload(ctx, d_gn, gn) || upload(ctx, d_gk, gk)) return YRWI_E_HIP;
+    if (upload(ctx, d_gb, gb, d_gn, gn, d_gk, gk)) return YRWI_E_HIP;
     hipEvent_t sq = span_open(ctx, tm);
     if (launch_topq(d_gb, d_gn, d_gk, ngr, cur, curc, in_stride, keff, d_out, d_oc, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "top-k launch");
@@ -1253,9 +1311,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   }
   if (!d_fptr || !d_fcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
   mark(5);
-  if (upload(ctx, d_fptr, fptr) || upload(ctx, d_fcnt, fcnt)) return YRWI_E_HIP;
+  if (upload(ctx, d_fptr, fptr, d_fcnt, fcnt)) return YRWI_E_HIP;
   std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
-  if (W == 1) {
+  if (!shx) {
     sp = span_open(ctx, tm);
     if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, 0, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "emit launch");
@@ -1344,7 +1402,7 @@ static int64_t scratch_estimate(const Plan& P) {
 // sharded contexts never split (every rank must issue the same collectives, and
 // the estimate depends on the local shard), so they keep one pass per batch.
 static int64_t scratch_budget(const Lane* L) {
-  if (L->world > 1) return INT64_MAX;
+  if (L->sharded) return INT64_MAX;
   const char* e = getenv("YRWI_SCRATCH_GB");  // per lane; default 128 GiB shared by the lanes
   const double gb = e ? atof(e) : 128.0 / (double)std::max(1, L->nlanes);
   return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
@@ -1366,7 +1424,7 @@ static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q,
 static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                            yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
-  const int64_t r0 = g_realloc.load();
+  const int64_t r0 = t_realloc;
   static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;  // per-batch host breakdown to stderr
   int64_t tp = 0, tj = 0, tr = 0, w0 = L->wait_ns, wj = 0;
   std::vector<Plan> all((size_t)nq);
@@ -1377,7 +1435,7 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   }
   // J1/J2 on global list sizes (one exchange of the batch's term sizes when sharded,
   // through this lane's arena and staging)
-  if (L->world > 1 && begin_pass(L)) return YRWI_E_HIP;
+  if (L->sharded && begin_pass(L)) return YRWI_E_HIP;
   if (int rc = plan_batch(L, all)) return rc;
   tp = now_ns() - t0;
   const int64_t budget = scratch_budget(L);
@@ -1435,6 +1493,11 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   if (L->arena.chunks.size() > 1) {
     HIPCHK(L, lane_sync(L));
     L->arena.reset();
+    // busy lanes take this size at their next pass (begin_pass)
+    size_t h = L->scratch_hint ? L->scratch_hint->load() : 0;
+    while (L->scratch_hint && h < L->arena.capacity() &&
+           !L->scratch_hint->compare_exchange_weak(h, L->arena.capacity())) {
+    }
     // the lanes share one workload: idle lanes take the same size now, so their
     // first batch does not pay for growing (single-lane sharded contexts: none)
     for (Lane* o : ix->lanes)
@@ -1442,12 +1505,12 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   }
   if (st) {
     st->t_total_ns = now_ns() - t0;
-    st->n_realloc = (int32_t)(g_realloc.load() - r0);
+    st->n_realloc = (int32_t)(t_realloc - r0);
   }
   if (hprof) {
     const int64_t wall = now_ns() - t0, wait = L->wait_ns - w0;
-    fprintf(stderr, "[yrwi host] nq %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms\n", nq,
-            wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6);
+    fprintf(stderr, "[yrwi host] nq %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms, scratch %.1f MB\n",
+            nq, wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6, L->arena.capacity() / 1e6);
   }
   return 0;
 }

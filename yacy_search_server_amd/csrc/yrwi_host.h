@@ -87,6 +87,17 @@ struct ListRec {
 // on the query path: each one synchronises the whole device, so two lanes stop
 // overlapping while it runs); reported per batch in yrwi_stats.n_realloc
 inline std::atomic<int64_t> g_realloc{0};
+inline thread_local int64_t t_realloc = 0;  // the calling thread's events (per-batch statistics)
+// one device-wide allocation event; YRWI_REALLOC_LOG=1 prints each (kind, bytes, time)
+inline void note_realloc(const char* what, size_t bytes) {
+  g_realloc++;
+  t_realloc++;
+  static const bool log = getenv("YRWI_REALLOC_LOG") != nullptr;
+  if (log)
+    fprintf(stderr, "[yrwi realloc] %s %.1f MB at %.3f ms\n", what, bytes / 1e6,
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+                    .count() / 1e3);
+}
 
 // bump allocator over device chunks
 struct Arena {
@@ -102,7 +113,7 @@ struct Arena {
     }
     if (cur >= chunks.size()) {
       size_t sz = std::max(std::max(bytes, min_chunk), capacity());  // geometric: few hipMallocs
-      g_realloc++;
+      note_realloc("arena grow", sz);
       void* p = nullptr;
       if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
       chunks.push_back({(uint8_t*)p, sz});
@@ -117,7 +128,7 @@ struct Arena {
   // only call when no kernel uses arena memory any more
   void reset() {
     if (chunks.size() > 1) {
-      g_realloc++;
+      note_realloc("arena consolidate", total_used);
       size_t need = total_used + (1 << 20);
       for (auto& c : chunks) hipFree(c.first);
       chunks.clear();
@@ -132,7 +143,7 @@ struct Arena {
   // one chunk of at least `bytes` (no allocation in use: call between passes)
   void reserve(size_t bytes) {
     if (capacity() >= bytes && chunks.size() <= 1) return;
-    g_realloc++;
+    note_realloc("arena reserve", bytes);
     for (auto& c : chunks) hipFree(c.first);
     chunks.clear();
     void* p = nullptr;
@@ -223,6 +234,11 @@ struct CollTurn {
 // of the two lanes share the device).
 struct Lane {
   int device = 0, rank = 0, world = 1;
+  // the url-hash-shard protocol runs (global-size planning, collectives, shard
+  // merge): world > 1, or a world-1 context over a real 1-rank RCCL communicator
+  // (YRWI_COLL_SELF=1 at yrwi_open_shard: every RCCL call of the sharded path
+  // runs with production counts, types and streams on one GPU)
+  bool sharded = false;
   int nlanes = 1;  // lanes of the context (scratch budget share)
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
@@ -253,6 +269,10 @@ struct Lane {
   bool active = false, reserving = false;
   int rc = 0;
   int64_t wait_ns = 0;  // host time spent waiting for this lane's device work (lane_sync)
+  // scratch high-water mark of the context's lanes (bytes): a lane whose arena is
+  // smaller takes that size at the start of its next pass instead of growing
+  // inside it (one allocation, before any of the pass's kernels)
+  std::atomic<size_t>* scratch_hint = nullptr;
   // collective order (CollTurn): the running part's sequence number (-1: none,
   // unordered), whether it holds the turn, and whether its last pass passes the
   // turn on right after its final collective
@@ -335,6 +355,7 @@ struct Lane {
 
 struct CtxBase {
   int device = 0, rank = 0, world = 1;
+  bool sharded = false;  // Lane::sharded
   hipStream_t stream = nullptr;  // == lanes[0]->stream (index uploads)
   std::vector<Lane*> lanes;
   HostRegistry hostreg;
@@ -344,6 +365,7 @@ struct CtxBase {
   CollTurn turn;
   int64_t coll_seq = 0;
   HostX* hostx = nullptr;
+  std::atomic<size_t> scratch_hint{0};  // Lane::scratch_hint
   std::mutex st_mu;
   std::unordered_map<int64_t, std::pair<int, std::string>> status;
   std::unordered_map<KeyT, ListRec, KeyHash> lists;
@@ -422,7 +444,7 @@ inline hipError_t lane_sync(Lane* L) {
 // pinned buffer of at least `bytes` (contents dropped on growth); nullptr on failure
 inline uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
   if (bytes > S->cap) {
-    g_realloc++;
+    note_realloc("pinned stage", bytes);
     if (drain && lane_sync(ctx) != hipSuccess) return nullptr;
     if (S->p) hipHostFree(S->p);
     S->p = nullptr;
@@ -436,32 +458,78 @@ inline uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
   return S->p;
 }
 
-template <class T>
-inline int upload(Lane* ctx, T* dst, const std::vector<T>& v) {
-  if (v.empty()) return 0;
-  const size_t bytes = v.size() * sizeof(T);
+// Host -> device uploads of per-batch descriptors.  The bytes are staged in the
+// lane's pinned buffer and pulled by ONE copy kernel per call (k_copy_in reads
+// the pinned pages through their device address) on the lane's stream: no DMA
+// engine on the query path.  SDMA copies measured 1.3-1.5 ms per C2 batch over
+// the driver's 20-step run against 0.8 with HSA_ENABLE_SDMA=0 (the copy engines'
+// queues stall the lanes' first batches: profiles/r03a_sdma.txt).
+struct UpEnt {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+
+inline int upload_list(Lane* ctx, const UpEnt* e, int n) {
   Stage& S = ctx->stage;
-  size_t off = (S.used + 255) & ~(size_t)255;
-  if (off + bytes > S.cap) {
-    g_realloc++;
-    // copies still read the old buffer: drain them, then grow
+  size_t need = S.used;
+  for (int i = 0; i < n; i++) need = ((need + 255) & ~(size_t)255) + e[i].bytes;
+  if (need > S.cap) {
+    note_realloc("pinned upload stage", need);
+    // copy kernels still read the old buffer: drain them, then grow
     HIPCHK(ctx, lane_sync(ctx));
     if (S.p) HIPCHK(ctx, hipHostFree(S.p));
     S.p = nullptr;
-    S.cap = std::max<size_t>(std::max<size_t>(2 * S.cap, bytes + 256), (size_t)4 << 20);
+    S.cap = std::max<size_t>(std::max<size_t>(2 * S.cap, need - S.used + 256 * (size_t)n), (size_t)4 << 20);
     HIPCHK(ctx, hipHostMalloc(reinterpret_cast<void**>(&S.p), S.cap, hipHostMallocDefault));
-    off = 0;
+    S.used = 0;
   }
-  std::memcpy(S.p + off, v.data(), bytes);
-  HIPCHK(ctx, hipMemcpyAsync(dst, S.p + off, bytes, hipMemcpyHostToDevice, ctx->stream));
-  S.used = off + bytes;
+  uint8_t* d_base = nullptr;
+  HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_base), S.p, 0));
+  CopyIn c{};
+  for (int i = 0; i < n; i++) {
+    if (e[i].bytes == 0) continue;
+    const size_t off = (S.used + 255) & ~(size_t)255;
+    std::memcpy(S.p + off, e[i].src, e[i].bytes);
+    S.used = off + e[i].bytes;
+    if (c.n == COPY_IN_MAX) {
+      if (launch_copy_in(c, ctx->stream)) return ctx->fail(YRWI_E_HIP, "copy-in launch");
+      c = CopyIn{};
+    }
+    c.src[c.n] = d_base + off;
+    c.dst[c.n] = static_cast<uint8_t*>(e[i].dst);
+    c.bytes[c.n] = e[i].bytes;
+    c.n++;
+  }
+  if (c.n && launch_copy_in(c, ctx->stream)) return ctx->fail(YRWI_E_HIP, "copy-in launch");
   return 0;
+}
+
+inline void up_collect(UpEnt*, int&) {}
+template <class T, class... R>
+inline void up_collect(UpEnt* e, int& n, T* dst, const std::vector<T>& v, R&&... rest) {
+  e[n++] = UpEnt{dst, v.data(), v.size() * sizeof(T)};
+  up_collect(e, n, std::forward<R>(rest)...);
+}
+
+// upload(ctx, d_a, va, d_b, vb, ...): every (device destination, host vector)
+// pair in one copy kernel
+template <class T, class... R>
+inline int upload(Lane* ctx, T* dst, const std::vector<T>& v, R&&... rest) {
+  UpEnt e[1 + sizeof...(R) / 2];
+  int n = 0;
+  up_collect(e, n, dst, v, std::forward<R>(rest)...);
+  return upload_list(ctx, e, n);
 }
 
 // start of a device pass: nothing is in flight any more, scratch can be reused
 inline int begin_pass(Lane* ctx) {
   HIPCHK(ctx, lane_sync(ctx));
   ctx->arena.reset();
+  if (ctx->scratch_hint) {
+    const size_t h = ctx->scratch_hint->load();
+    if (ctx->arena.capacity() < h) ctx->arena.reserve(h);
+  }
   ctx->stage.used = 0;
   ctx->evnext = 0;
   const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
@@ -485,7 +553,7 @@ int check_url_ids(CtxBase* ctx, int64_t* bad);
 
 HostX* hostx_open(const uint8_t id[128], int world, int rank);  // nullptr: not available (device fallback)
 void hostx_close(HostX* x, bool unlink_name);
-void hostx_unlink(HostX* x);
+int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)
 void turn_release(Lane* L);  // pass the turn to the next part (waits for L's turn first); idempotent

@@ -248,6 +248,16 @@ struct HostMsg {
 };
 
 // ---------------------------------------------------------------- launchers
+// host -> device copies of up to COPY_IN_MAX staged ranges in one launch: src =
+// device address of pinned host memory, dst = device memory (yrwi_host.h upload)
+constexpr int COPY_IN_MAX = 8;
+struct CopyIn {
+  const uint8_t* src[COPY_IN_MAX];
+  uint8_t* dst[COPY_IN_MAX];
+  uint64_t bytes[COPY_IN_MAX];
+  int32_t n;
+};
+int launch_copy_in(const CopyIn& c, void* stream);
 int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* stream);
 int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
                      int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* stream);

@@ -154,6 +154,42 @@ __device__ __forceinline__ int32_t block_excl_max256(int32_t v, int32_t* sh /*4*
   return max(off, prev);
 }
 
+// ============================================================ uploads
+// One launch copies every staged range of an upload (yrwi_host.h upload_list):
+// COPY_IN_BLOCK bytes per workgroup, 16 B per thread per step, read from pinned
+// host memory through its device address.  Ranges start 256-B aligned on both
+// sides (stage offsets, arena allocations); a range's tail is copied bytewise.
+constexpr int COPY_IN_BLOCK = 16384;
+__global__ __launch_bounds__(256) void k_copy_in(CopyIn c) {
+  uint32_t b = blockIdx.x;
+  int e = 0;
+  for (; e < c.n; e++) {
+    const uint32_t nb = (uint32_t)((c.bytes[e] + COPY_IN_BLOCK - 1) / COPY_IN_BLOCK);
+    if (b < nb) break;
+    b -= nb;
+  }
+  if (e >= c.n) return;
+  const uint8_t* __restrict__ src = c.src[e];
+  uint8_t* __restrict__ dst = c.dst[e];
+  const uint64_t n = c.bytes[e];
+  const uint64_t end = min<uint64_t>(n, (uint64_t)(b + 1) * COPY_IN_BLOCK);
+  for (uint64_t o = (uint64_t)b * COPY_IN_BLOCK + threadIdx.x * 16u; o < end; o += 256 * 16) {
+    if (o + 16 <= end) {
+      *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+    } else {
+      for (uint64_t x = o; x < end; x++) dst[x] = src[x];
+    }
+  }
+}
+
+int launch_copy_in(const CopyIn& c, void* stream) {
+  uint32_t blocks = 0;
+  for (int e = 0; e < c.n; e++) blocks += (uint32_t)((c.bytes[e] + COPY_IN_BLOCK - 1) / COPY_IN_BLOCK);
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(k_copy_in, dim3(blocks), dim3(256), 0, (hipStream_t)stream, c);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ====================================================== put_list validation
 // err bits: 1 = malformed hash, 2 = empty language cell, 4 = not strictly ascending
 __global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t* __restrict__ khi,
@@ -1179,16 +1215,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     av[s] = -1;
     uint32_t po = 0;
     if (v) {
-#ifdef YRWI_EXP_REDUCE_NOLOAD  // timing experiment only (inexact): synthetic records, no loads
-      Rec qx;
-      qx.w[0] = 0x0102030405060708ull * (uint64_t)(e | 1);
-      qx.w[1] = qx.w[0] ^ 0x1111111111111111ull;
-      qx.w[2] = qx.w[0] >> 7;
-      qx.w[3] = 0;
-      const Feat F = decode_rec(qx);
-#else
       const Feat F = decode_rec(load_rec(Q.feat, e));
-#endif
 #pragma unroll
       for (int j = 0; j < NP2; j++) {
         const uint32_t w = (uint32_t)F.f[2 * j] | (2 * j + 1 < NF ? (uint32_t)F.f[2 * j + 1] << 16 : 0u);
@@ -2238,11 +2265,7 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
     if (!F && Q.want_authority) key_at(Q, e, khi, klo);
     const Feat t = decode_rec(q);
     const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
-#ifdef YRWI_EXP_NOSCORE  // timing experiment only (inexact): loads without cardinal
-    a[s] = (q.w[0] ^ q.w[1] ^ q.w[2] ^ (uint64_t)hc) | 0x8000000000000000ull;
-#else
     a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
-#endif
     if (a[s] < T) {
       a[s] = 0;
       continue;
@@ -2399,10 +2422,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   int32_t nv;
   int32_t voff = block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   PHASE(0)
-#ifdef YRWI_EXP_NOSEL  // timing experiment only (inexact): scoring without selection
-  if (tid == 0) cand_cnt[b] = 0;
-  return;
-#endif
   if (flagc && tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
   if (kq <= 0 || nv == 0) {
     if (tid == 0) cand_cnt[b] = 0;
@@ -2451,9 +2470,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   for (int i = nsel + tid; i < NP; i += CHUNK_THREADS) { s1[i] = 0; s2[i] = 0; }
   __syncthreads();
   PHASE(2)
-#ifndef YRWI_EXP_NOSORT  // timing experiment only (inexact)
   bitonic_desc<CHUNK_THREADS>(s1, s2, NP);
-#endif
   PHASE(3)
   int32_t distinct;
   Cand* out = cand + b * (int64_t)kc;
