@@ -9,6 +9,7 @@ by tests/test_multi_gloo.py)."""
 import os
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -73,3 +74,52 @@ def test_sharded_query_on_one_gpu(world):
     for rank, status, info in res:
         assert status == "ok", (rank, info)
         assert info == [], (rank, info)
+
+
+def test_rccl_self_world1(monkeypatch):
+    """The sharded protocol over a REAL 1-rank RCCL communicator on this GPU
+    (YRWI_COLL_SELF=1, yrwi_open_shard with world 1): global-size planning goes
+    through the device all-gather (no host mailbox at world 1), then the ShardSum
+    all-gather, the authority host-count exchange (grouped ncclSend / ncclRecv to
+    self and the max all-reduce), the flag-count all-reduce and the top-k
+    all-gather + shard merge -- every RCCL call site of yrwi_coll.cpp with the
+    production counts, types and streams.  Bit-exact against the oracle."""
+    monkeypatch.setenv("YRWI_COLL_SELF", "1")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import java_literal as jl
+    import oracle as orc
+    from yacy_search_server_amd import Query, QueryFilter, RankingProfile, RWIIndex, synth, unique_id
+    full = synth.preset("small")
+    idx = synth.build_index(full)
+    ix = RWIIndex(0, shard=(0, 1, unique_id()))
+    try:
+        for t in range(full.n_terms):
+            if idx.sizes[t]:
+                ix.add(idx.hashes[t], idx.list_rows(t))
+        maps = open("/proc/self/maps").read()
+        assert "librccl" in maps, "RCCL is not mapped into the process"
+        qs = synth.queries(full, 40, 1, 4, 1, qseed=43)
+        c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")  # authority -> send/recv to self
+        batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW, k=100,
+                       profile=(c5 if i % 2 else None)) for i, (inc, exc) in enumerate(qs)]
+        # two batches in flight on different lanes: the collective turn orders their RCCL calls
+        p1 = ix.submit(batch[:20])
+        p2 = ix.submit(batch[20:])
+        got = p1.result() + p2.result()
+        whole = idx.as_dict()
+        for qi, (q, g) in enumerate(zip(batch, got)):
+            prof = orc.profile_from(q.profile) if q.profile is not None else None
+            exp = orc.search(whole, q.include, q.exclude, profile=prof, now_ms=NOW, k=100)
+            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, qi
+        # flag counts: the all-reduce of the counters
+        big = [int(t) for t in np.argsort(-idx.sizes)[:2]]
+        lit = {h: [bytes(x) for x in rows] for h, rows in whole.items()}
+        for kw in (dict(constraint=b"\0\0\x10\x01"), dict(skip_double_dom=True)):
+            q = Query([idx.hashes[t] for t in big], [], now_ms=NOW, k=50, filter=QueryFilter(**kw))
+            (g,) = ix.search_batch([q])
+            lf = jl.QueryFilter(**kw)
+            e = jl.search(lit, q.include, q.exclude, jl.RankingProfile(), "en", now_ms=NOW, k=50, filt=lf)
+            assert [(h.urlhash, h.score) for h in g] == e, kw
+            assert q.filter.flagcount == lf.flagcount, kw
+    finally:
+        ix.close()
