@@ -54,6 +54,8 @@ def parse_args(argv=None):
     ap.add_argument("--terms", type=int, default=2, help="include terms per query (minimum)")
     ap.add_argument("--max-terms", type=int, default=0, help="include terms per query (maximum; default --terms)")
     ap.add_argument("--exclude", type=int, default=0, help="exclude terms per query")
+    ap.add_argument("--qseed", type=lambda x: int(x, 0), default=None,
+                    help="query stream seed (default: the config's; C4 uses seed ^ 0xC4)")
     ap.add_argument("--profile", default="default", choices=["default", "custom", "date"],
                     help="custom = C5's date=15,domlength=15,authority=13,tf=10; date = the /date modifier")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
@@ -63,6 +65,8 @@ def parse_args(argv=None):
                     help="extra BASELINE configs after the headline ('C3,C4,C5'), or 'none'; "
                          "auto: C3,C4,C5 on one GPU, none for N > 1 (the scaling runs time the headline only)")
     ap.add_argument("--leg-steps", type=int, default=20)
+    ap.add_argument("--leg-check", type=int, default=16, help="queries of each leg's timed batch checked against the oracle")
+    ap.add_argument("--leg-latency", type=int, default=50, help="single-query latency samples per leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency", type=int, default=100, help="single-query latency samples")
@@ -354,64 +358,131 @@ class Runner:
                 "arr": arr, "keep": keep}
 
 
-def roofline_path(iso, pmc, head_of_pmc):
-    """Path-level roofline: B = sum K + 12 sum
-    n_excl + 23 t m_out algorithmic bytes per batch over the batch's kernel time
-    (HIP events around every group of launches, t_kernels_ns)."""
-    nb = max(1, iso["batches"])
-    t = iso["t_kernels_ns"] / nb * 1e-9
-    b = iso["bytes_alg"] / nb
-    ach = b / t / 1e9 if t > 0 else 0.0
-    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-         "kernel": "query path (k_partition .. k_emit, every kernel of one batch)",
-         "bytes_per_batch_alg": int(b), "kernel_us_per_batch": round(t * 1e6, 1),
-         "measured": "HIP events around every group of back-to-back launches of the batch (t_kernels_ns), "
-                     "isolated pass with one batch in flight (median of five batches)"}
-    if iso.get("isolated_runs_t_kernels_us"):
-        r["isolated_batches_kernel_us"] = iso["isolated_runs_t_kernels_us"]
-    if ach > HBM_PEAK_GBS:
-        # the §8(d) model charges 12 B per key and the reference's binary-search reads for
-        # by-test steps; the 4-B url ids, line heads and deferred multi-term folds read less,
-        # so the model's rate passes the HBM peak: no fraction of peak is claimed from it
-        r["frac_alg"] = r["frac"]
-        r["frac"] = None
-        r["note"] = ("algorithmic bytes (SURVEY §8(d)) per kernel second exceed the HBM peak: the layout moves "
-                     "fewer bytes than the model charges (4-B url ids instead of 12-B keys, line-head probes, "
-                     "deferred multi-term folds); the physical rate is in the rocprof PMC profiles")
-    if pmc and pmc.get("path_hbm_bytes_per_batch"):
-        r["traffic"] = pmc["path_hbm_bytes_per_batch"]
-        r["traffic_source"] = f"{pmc['_file']} (rocprofv3 --pmc passes: TCC_EA0_RDREQ_32B/64B/128B and WRREQ/WRREQ_64B by request size, the L2 fabric requests FETCH_SIZE / WRITE_SIZE derive from; tag {pmc.get('tag')}, " \
-                              f"commit {pmc.get('head', head_of_pmc)})"
-    return r
+def check_and_latency(R, M, qs, hashes, idx, prof, k, nchk, nlat, label):
+    """Outside the timed region: (a) the isolated pass's results (bufs[0], the last
+    batch run) of `nchk` queries spread over the batch against the oracle (checker
+    only, oracle/yrwi_oracle.cpp); (b) host-call -> top-k-in-host-memory latency of
+    `nlat` single queries of the same set."""
+    import ctypes
+    import numpy as np
+    from yacy_search_server_amd._lib import CHit, CStats
+    nq = len(qs)
+    parity = None
+    if nchk > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc
+        oprof = orc.profile_from(prof)
+        hits, nout = M["bufs"][0][0], M["bufs"][0][1]
+        picks = sorted({i * nq // min(nchk, nq) for i in range(min(nchk, nq))})
+        bad = []
+        for qi in picks:
+            inc, exc = qs[qi]
+            d = {hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
+            exp = orc.search(d, [hashes[t] for t in inc], [hashes[t] for t in exc], profile=oprof,
+                             now_ms=NOW_MS, k=k)
+            got = [(bytes(hits[qi * k + j].urlhash), hits[qi * k + j].score) for j in range(nout[qi])]
+            if got != [(h, sc) for h, sc, _ in exp]:
+                bad.append(qi)
+        parity = {"queries_checked": len(picks), "mismatches": len(bad), "checker": "oracle/yrwi_oracle.cpp",
+                  "queries": f"{len(picks)} of the {nq} queries of the timed batch, evenly spaced"}
+        if bad:
+            log(f"{label}: PARITY MISMATCH on queries {bad[:10]}")
+    lat = None
+    if nlat > 0:
+        one = (CHit * k)()
+        n1 = (ctypes.c_int32 * 1)()
+        ts = []
+        for i in range(min(nlat, nq)):
+            t1 = time.perf_counter()
+            R.ix.search_batch_raw(ctypes.byref(M["arr"][i]), 1, k, one, n1, CStats())
+            ts.append((time.perf_counter() - t1) * 1e3)
+        lat = {"p50": float(np.percentile(ts, 50)), "p99": float(np.percentile(ts, 99)), "n": len(ts),
+               "what": "one query per call (yrwi_query_batch, nq = 1): host call -> top-k in host memory"}
+    return parity, lat
 
 
-def roofline_kernels(iso, pmc):
-    """Per-kernel lines: the kernel's share of the §8(d) bytes (alg_bytes) and the
-    bytes its data layout makes it move (phys_bytes: 4-byte url ids in the joins,
-    32-byte ranking records in k_compact); frac = phys rate / peak."""
+def _frac(gbps):
+    """Fraction of the HBM peak, or None when the byte model's rate passes the peak
+    (then the model credits reads the kernel never makes: no fraction is claimed)."""
+    return round(gbps / HBM_PEAK_GBS, 4) if 0 < gbps <= HBM_PEAK_GBS else None
+
+
+def kernel_lines(iso, pmc):
+    """The join-phase kernels, each on its SURVEY.md §8(d) share of the bytes over
+    its mean launch time (library HIP events around each launch, isolated pass):
+      k_join    K of the merge-executed steps (K as the reference dispatches them, J3);
+      k_probe   sum of min(K, bytes the probe loads) over the probe-executed steps
+                (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id);
+      k_compact 23 B per include term and joined posting (23 t m_out).
+    traffic = rocprofv3 PMC HBM bytes per launch (profiles/pmc_<config>.json)."""
     n = max(1, iso["n_join_launches"])
+    pk = (pmc or {}).get("kernels", {})
     out = {}
-
-    def line(name, t_ns, alg, phys):
+    for name, t_ns, alg, extra in (
+            ("k_join", iso["t_join_ns"], iso["bytes_join"], {}),
+            ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"],
+             {"alg_bytes_model_K": int(iso["bytes_probe"] / n), "loaded_bytes": int(iso["bytes_probe_loaded"] / n)}),
+            ("k_compact", iso["t_compact_ns"], iso["bytes_features"], {})):
         t = t_ns / n * 1e-9
         if t <= 0:
-            return
-        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / n), "alg_GBps": round(alg / n / t / 1e9, 1),
-             "phys_bytes": int(phys / n), "phys_GBps": round(phys / n / t / 1e9, 1),
-             "frac": round(phys / n / t / 1e9 / HBM_PEAK_GBS, 4)}
-        kd = (pmc or {}).get("kernels", {}).get(name, {})
+            continue
+        gbps = alg / n / t / 1e9
+        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / n), "achieved": round(gbps, 1),
+             "frac": _frac(gbps)}
+        e.update(extra)
+        kd = pk.get(name, {})
         if kd.get("hbm_bytes_per_launch"):
             e["traffic"] = kd["hbm_bytes_per_launch"]
+            e["traffic_GBps"] = round(kd["hbm_bytes_per_launch"] / t / 1e9, 1)
+            if kd.get("avg_ns"):
+                e["rocprof_mean_launch_us"] = round(kd["avg_ns"] / 1e3, 2)
         out[name] = e
-
-    # k_join: K = 12 B per key of the merge jobs; it streams 4-byte url ids
-    line("k_join", iso["t_join_ns"], iso["bytes_join"], iso["bytes_join"] / 3)
-    # k_probe: the galloping bound of the skewed jobs (it reads at most that, in leaf lines)
-    line("k_probe", iso["t_probe_ns"], iso["bytes_probe"], iso["bytes_probe"] / 3)
-    # k_compact: 23 B of features per term and joined posting; it moves bytes_compact (96 B per joined row)
-    line("k_compact", iso["t_compact_ns"], 46 * iso["joined"], iso["bytes_compact"])
     return out
+
+
+def roofline_block(iso, timed, steps, ms_per_step, pmc):
+    """`roofline` of the bench line: the dominant kernel (longest mean launch among
+    k_join / k_probe / k_compact) with its §8(d) bytes (kernel_lines), plus the
+    path: B = sum K + 12 sum n_excl + 23 t m_out per batch with every
+    probe-executed step charged min(K, the bytes the probe loads), over (a) the
+    batch's kernel time in the isolated pass and (b) the timed region's time per
+    batch (batches in flight overlap)."""
+    kern = kernel_lines(iso, pmc)
+    nb = max(1, iso["batches"])
+    if not kern:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None}, kern
+    dom = max(kern, key=lambda k: kern[k]["mean_launch_us"])
+    d = kern[dom]
+    r = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": d["frac"], "traffic": d.get("traffic"),
+         "alg_bytes_per_launch": d["alg_bytes"], "mean_launch_us": d["mean_launch_us"],
+         "measured": "HIP events around each launch on the lane's stream (library statistics), isolated pass "
+                     "(one batch in flight, median of five batches)"}
+    if d.get("rocprof_mean_launch_us"):
+        r["rocprof_mean_launch_us"] = d["rocprof_mean_launch_us"]
+    if pmc:
+        r["traffic_source"] = (f"{pmc['_file']} (rocprofv3 --pmc: TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B "
+                               f"by request size; tag {pmc.get('tag')}, commit {pmc.get('head')})")
+    b_iso = (iso["bytes_alg"] - iso["bytes_probe"] + iso["bytes_probe_capped"]) / nb
+    t_iso = iso["t_kernels_ns"] / nb * 1e-9
+    path = {"bytes_per_batch": int(b_iso),
+            "bytes_per_batch_model": int(iso["bytes_alg"] / nb),
+            "rule": "SURVEY 8(d) B; probe-executed steps charged min(K, bytes loaded)"}
+    if t_iso > 0:
+        g = b_iso / t_iso / 1e9
+        path["isolated"] = {"achieved": round(g, 1), "frac": _frac(g), "kernel_us_per_batch": round(t_iso * 1e6, 1)}
+        if iso.get("isolated_runs_t_kernels_us"):
+            path["isolated"]["batches_kernel_us"] = iso["isolated_runs_t_kernels_us"]
+    if timed.get("bytes_alg") and ms_per_step > 0:
+        bt = (timed["bytes_alg"] - timed["bytes_probe"] + timed["bytes_probe_capped"]) / steps
+        g = bt / (ms_per_step * 1e-3) / 1e9
+        path["throughput_mode"] = {"achieved": round(g, 1), "frac": _frac(g), "per": "GPU",
+                                   "time": "ms_per_step (timed region, batches in flight)"}
+    if pmc and pmc.get("path_hbm_bytes_per_batch"):
+        path["traffic_per_batch"] = pmc["path_hbm_bytes_per_batch"]
+    r["path"] = path
+    return r, kern
 
 
 def run(args, rank, world, local):
@@ -446,7 +517,7 @@ def run(args, rank, world, local):
         cfg = full.shard(rank, world) if world > 1 else full
     idx, t_dict = R.open_index(cfg)
 
-    qs = synth.queries(full, args.nq, args.terms, max_terms, args.exclude)
+    qs = synth.queries(full, args.nq, args.terms, max_terms, args.exclude, qseed=args.qseed)
     prof = RankingProfile()
     if args.profile == "custom":  # exercises the authority path (coeff > 12)
         prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
@@ -457,46 +528,13 @@ def run(args, rank, world, local):
     ms_per_step = M["dt"] / args.steps * 1e3
     iso, timed = M["iso"], M["timed"]
     pmc = load_pmc(args.config) if world == 1 and args.shard_of == 1 else None
-    roof = roofline_path(iso, pmc, None)
-    # the same bytes over the timed region's time per batch (batches in flight overlap)
-    if timed.get("bytes_alg") and ms_per_step > 0:
-        ach = timed["bytes_alg"] / args.steps / (ms_per_step * 1e-3) / 1e9  # this rank's bytes: per GPU
-        roof["throughput_mode"] = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                                   "per": "GPU", "time": "ms_per_step (timed region, batches in flight)"}
-    kern = roofline_kernels(iso, pmc)
+    roof, kern = roofline_block(iso, timed, args.steps, ms_per_step, pmc)
 
-    # single-query latency (host call -> top-k in host memory)
-    lat = []
-    if rank == 0 and world == 1 and args.latency > 0:
-        import ctypes
-        from yacy_search_server_amd._lib import CHit, CStats
-        one = (CHit * args.k)()
-        n1 = (ctypes.c_int32 * 1)()
-        for i in range(min(args.latency, args.nq)):
-            t1 = time.perf_counter()
-            R.ix.search_batch_raw(ctypes.byref(M["arr"][i]), 1, args.k, one, n1, CStats())
-            lat.append((time.perf_counter() - t1) * 1e3)
-
-    # parity spot check of this very workload: the last batch's hits (pinned host
-    # buffers) of the first queries against the oracle (checker only)
-    parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as orc
-        oprof = orc.profile_from(prof)
-        hits, nout = M["bufs"][0][0], M["bufs"][0][1]  # the isolated pass ran last, on bufs[0]
-        nchk = min(args.nq, 64)
-        bad = 0
-        for qi in range(nchk):
-            inc, exc = qs[qi]
-            d = {idx.hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
-            exp = orc.search(d, [idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], profile=oprof,
-                             now_ms=NOW_MS, k=args.k)
-            got = [(bytes(hits[qi * args.k + j].urlhash), hits[qi * args.k + j].score) for j in range(nout[qi])]
-            bad += got != [(h, sc) for h, sc, _ in exp]
-        parity = {"queries_checked": nchk, "mismatches": bad, "checker": "oracle/yrwi_oracle.cpp"}
-        if bad:
-            log(f"PARITY MISMATCH on {bad} of {nchk} queries")
+    # parity of this very workload and single-query latency (outside the timed region)
+    parity = lat = None
+    if rank == 0 and world == 1:
+        parity, lat = check_and_latency(R, M, qs, idx.hashes, idx, prof, args.k, 0 if args.no_cpu else 64,
+                                        args.latency, args.config)
 
     cpu = cpu1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -550,8 +588,7 @@ def run(args, rank, world, local):
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
             "parity_sample": parity,
-            "latency_ms": ({"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
-                            "n": len(lat)} if lat else None),
+            "latency_ms": lat,
             "joined_per_step": timed["joined"] / args.steps,
             "bytes_alg_per_step": timed["bytes_alg"] / args.steps,
             # device-wide allocation events (scratch / pinned staging growth) inside the timed steps
@@ -592,30 +629,40 @@ LEG_DESC = {
 def run_leg(R, leg, args, rank, world):
     """An extra BASELINE config on the same ranks: C3 / C4 strong-scale the fixed
     1B corpus over the N ranks; C5 gives every rank one 625M-posting url-hash shard
-    of the 8-way partition of the 5B corpus."""
+    of the 8-way partition of the 5B corpus.  On one GPU every leg also checks
+    queries of its own timed batch against the oracle and times single queries."""
     from yacy_search_server_amd import RankingProfile, synth
     res = {}
+    check = rank == 0 and world == 1
+    nchk = 0 if args.no_cpu else args.leg_check
+    nlat = args.leg_latency
     if leg in ("C3", "C4"):
         full = synth.preset("C3")
         cfg = full.shard(rank, world) if world > 1 else full
         if getattr(R, "leg_cfg", None) != ("C3", rank, world):
             R.close()
-            R.open_index(cfg)
+            R.leg_idx = None
+            R.leg_idx, _ = R.open_index(cfg)
             R.leg_cfg = ("C3", rank, world)
         if leg == "C3":
             qs = synth.queries(full, 1000, 3, 3, 1)
         else:
             qs = synth.queries(full, 4096, 2, 4, 0, qseed=full.seed ^ 0xC4)
         hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
-        M = R.measure(qs, hashes, RankingProfile(), len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
+        prof = RankingProfile()
+        M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
                       isolated=True)
-        res[leg] = _leg_line(M, leg, len(qs), world, "strong")
+        res[leg] = _leg_line(M, leg, len(qs), world, "strong", load_pmc(leg) if world == 1 else None)
+        if check:
+            res[leg]["parity_sample"], res[leg]["latency_ms"] = check_and_latency(
+                R, M, qs, hashes, R.leg_idx, prof, 100, nchk, nlat, leg)
     elif leg == "C5":
         full = synth.preset("C5")
         parts = max(8, world)
         R.close()
         R.leg_cfg = None
-        R.open_index(full.shard(rank, parts))
+        R.leg_idx = None
+        idx, _ = R.open_index(full.shard(rank, parts))
         qs = synth.queries(full, 1000, 2, 4, 0)
         hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
         custom = RankingProfile()
@@ -624,27 +671,24 @@ def run_leg(R, leg, args, rank, world):
             M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
                           isolated=True)
             res[name] = _leg_line(M, "C5", len(qs), world, "weak")
+            if check:
+                res[name]["parity_sample"], res[name]["latency_ms"] = check_and_latency(
+                    R, M, qs, hashes, idx, prof, 100, nchk, nlat, name)
+        del idx
         R.close()
     else:
         raise ValueError(f"unknown leg {leg}")
     return res
 
 
-def _leg_line(M, leg, nq, world, scaling):
-    iso = M["iso"]
-    nb = max(1, iso["batches"])
-    t = iso["t_kernels_ns"] / nb * 1e-9
-    b = iso["bytes_alg"] / nb
-    roof = {"achieved": round(b / t / 1e9, 1) if t > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None,
-            "kernel_us_per_batch": round(t * 1e6, 1), "bytes_per_batch_alg": int(b)}
-    if roof["frac"] is not None and roof["frac"] > 1:  # see roofline_path: the model's rate, not a fraction of peak
-        roof["frac_alg"], roof["frac"] = roof["frac"], None
-        roof["note"] = "algorithmic bytes (SURVEY §8(d)) per kernel second exceed the HBM peak: the layout moves fewer bytes"
+def _leg_line(M, leg, nq, world, scaling, pmc=None):
+    ms = M["dt"] / M["steps"] * 1e3
+    roof, kern = roofline_block(M["iso"], M["timed"], M["steps"], ms, pmc)
     return {"workload": LEG_DESC[leg], "value": M["total_post"] / M["dt"], "unit": "postings/s", "n_gpus": world,
-            "scaling": scaling, "steps": M["steps"], "ms_per_step": M["dt"] / M["steps"] * 1e3,
+            "scaling": scaling, "steps": M["steps"], "ms_per_step": ms,
             "postings_per_step": M["total_post"] / M["steps"], "queries_per_step": nq,
-            "roofline": roof, "joined_per_step": M["timed"]["joined"] / M["steps"]}
+            "roofline": roof, "roofline_kernels": kern, "joined_per_step": M["timed"]["joined"] / M["steps"],
+            "realloc_events_timed": M["timed"]["n_realloc"]}
 
 
 def dry_run(args, rank, world):

@@ -109,12 +109,14 @@ typedef struct yrwi_stats {
   int64_t postings_in;   /* sum of include + exclude list lengths */
   int64_t joined;        /* rows of the joined container (before exclusion) */
   int64_t bytes_alg;     /* algorithmic bytes B = sum K + 12 sum n_excl + 23 t m_out */
-  int64_t bytes_join;    /* sum K over the merge-path join jobs (the k_join launches timed in t_join_ns) */
+  int64_t bytes_join;    /* sum K over the merge-path join jobs (the k_join launches timed in t_join_ns), K as the
+                            reference dispatches the step (J3) */
   int64_t t_join_ns;     /* device time of the k_join launches (HIP events on the context stream) */
   int64_t t_norm_ns, t_score_ns, t_total_ns;
   int32_t n_join_launches, n_enum_steps, n_test_steps;
   int32_t n_realloc;     /* device-wide allocation events (scratch or pinned staging growth) during the call */
-  int64_t bytes_probe;   /* sum K over the skewed (probe) join jobs, timed in t_probe_ns */
+  int64_t bytes_probe;   /* sum K over the probe-executed join jobs (timed in t_probe_ns), K as the reference
+                            dispatches the step (J3) */
   int64_t t_probe_ns;    /* device time of the k_probe launches */
   int64_t bytes_compact; /* bytes k_compact moves: per joined row 12 B pair + url id read, the 32-B ranking
                             record of the accumulated side and 16 B of the joined side's (by-test steps: one
@@ -122,6 +124,14 @@ typedef struct yrwi_stats {
   int64_t t_compact_ns;  /* device time of the k_compact launches */
   int64_t t_kernels_ns;  /* device time of all the batch's kernel launches (HIP events around every group of
                             back-to-back launches; host waits and collectives excluded) */
+  /* SURVEY.md §8(d) accounting of the probe-executed join steps: bytes_probe is their K under the
+     reference's own dispatch (J3); bytes_probe_loaded what the probe kernel loads (url-id bitmap: the
+     smaller side's 4-B ids + one 16-B bitmap word per id; range probe: the ids + the large list's
+     range or a 128-B leaf line per id, whichever is less); bytes_probe_capped = sum of
+     min(K, loaded) per step -- the path's bytes with no step credited for reads it never makes */
+  int64_t bytes_probe_loaded;
+  int64_t bytes_probe_capped;
+  int64_t bytes_features;  /* 23 t m_out: the ranking-feature bytes of the joined containers (k_compact's §8(d) share) */
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

@@ -64,7 +64,8 @@ class CStats(ctypes.Structure):
                 ("n_test_steps", ctypes.c_int32), ("n_realloc", ctypes.c_int32),
                 ("bytes_probe", ctypes.c_int64), ("t_probe_ns", ctypes.c_int64),
                 ("bytes_compact", ctypes.c_int64), ("t_compact_ns", ctypes.c_int64),
-                ("t_kernels_ns", ctypes.c_int64)]
+                ("t_kernels_ns", ctypes.c_int64), ("bytes_probe_loaded", ctypes.c_int64),
+                ("bytes_probe_capped", ctypes.c_int64), ("bytes_features", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):

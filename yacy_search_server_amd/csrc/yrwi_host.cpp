@@ -569,9 +569,11 @@ static int allsum_host(Lane* L, std::vector<int64_t>& v) {
   if (!d_v || !d_all) return L->fail(YRWI_E_NOMEM, "arena");
   if (upload(L, d_v, v)) return YRWI_E_HIP;
   if (int rc = coll_allgather(L, d_v, d_all, n * sizeof(int64_t))) return rc;
-  std::vector<int64_t> all(n * (size_t)L->world);
-  HIPCHK(L, hipMemcpyAsync(all.data(), d_all, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost, L->stream));
+  const uint8_t* hb = readback(L, &L->down_stage, d_all, (int64_t)n * L->world, 8, 8);
+  if (!hb) return YRWI_E_HIP;
   HIPCHK(L, lane_sync(L));
+  std::vector<int64_t> all(n * (size_t)L->world);
+  std::memcpy(all.data(), hb, all.size() * sizeof(int64_t));
   for (size_t i = 0; i < n; i++) {
     int64_t s = 0;
     for (int r = 0; r < L->world; r++) s += all[(size_t)r * n + i];
@@ -725,9 +727,19 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   const int nj = (int)jobs.size();
   const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
-    for (const JoinQ& J : jobs)  // a probe job reads at most the galloping bound, whatever the reference dispatch
-      (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) +=
-          step_bytes(J.algo == JA_MERGE ? J.mode : (int32_t)JM_TEST_LARGE_A, J.A.n, J.B.n);
+    for (const JoinQ& J : jobs) {  // §8(d) K of the step as the reference dispatches it
+      const int64_t K = step_bytes(J.mode, J.A.n, J.B.n);
+      if (J.algo == JA_MERGE) {
+        st->bytes_join += K;
+        continue;
+      }
+      const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
+      const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
+      const int64_t loaded = bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
+      st->bytes_probe += K;
+      st->bytes_probe_loaded += loaded;
+      st->bytes_probe_capped += std::min(K, loaded);
+    }
   // joined sizes land in pinned host memory: k_scan_tiles writes them through its
   // device address (no copy engine), the host reads them after the step's sync
   uint8_t* land = stage_reserve(ctx, &ctx->down_stage, (size_t)nj * sizeof(int64_t), true);
@@ -951,9 +963,11 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   if (upload(ctx, d_sb, slot_base)) return YRWI_E_HIP;
   if (launch_host_count(d_hkeys, nslots, W, d_ocnt, ctx->stream)) return ctx->fail(YRWI_E_HIP, "host count");
   if (int rc = coll_allgather(ctx, d_ocnt, d_M, (size_t)W * 4)) return rc;
-  std::vector<uint32_t> M((size_t)W * W);
-  HIPCHK(ctx, hipMemcpyAsync(M.data(), d_M, M.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+  const uint8_t* hm = readback(ctx, &ctx->down_stage, d_M, (int64_t)W * W, 4, 4);
+  if (!hm) return YRWI_E_HIP;
   HIPCHK(ctx, lane_sync(ctx));
+  std::vector<uint32_t> M((size_t)W * W);
+  std::memcpy(M.data(), hm, M.size() * 4);
   // row s of M = what rank s sends to each owner
   std::vector<int64_t> soff((size_t)W + 1, 0), roff((size_t)W + 1, 0);
   for (int p = 0; p < W; p++) {
@@ -1059,6 +1073,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     if (st) {
       st->joined += R.n;
       st->bytes_alg += 23 * (int64_t)P.seq.size() * R.n;  // ranking feature bytes per surviving posting and term
+      st->bytes_features += 23 * (int64_t)P.seq.size() * R.n;
     }
   }
   slot_base[(size_t)nq] = nslots;
@@ -1130,9 +1145,11 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     if (!d_flag) return 0;
     if (shx)
       if (int rc = coll_allreduce_i32(ctx, d_flag, (size_t)nf * 32, false)) return rc;
-    std::vector<int32_t> h((size_t)nf * 32);
-    HIPCHK(ctx, hipMemcpyAsync(h.data(), d_flag, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    const uint8_t* hf = readback(ctx, &ctx->down_stage, d_flag, (int64_t)nf * 32, 4, 4);
+    if (!hf) return YRWI_E_HIP;
     HIPCHK(ctx, lane_sync(ctx));
+    std::vector<int32_t> h((size_t)nf * 32);
+    std::memcpy(h.data(), hf, h.size() * 4);
     for (int qi = 0; qi < nq; qi++)
       if (fidx[(size_t)qi] >= 0 && plans[(size_t)qi].filter->flagcount)
         std::memcpy(plans[(size_t)qi].filter->flagcount, &h[(size_t)fidx[(size_t)qi] * 32], 32 * 4);
@@ -1313,6 +1330,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(5);
   if (upload(ctx, d_fptr, fptr, d_fcnt, fcnt)) return YRWI_E_HIP;
   std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
+  const uint8_t* hD_land = nullptr;
   if (!shx) {
     sp = span_open(ctx, tm);
     if (launch_emit(d_q, nq, d_fptr, d_fcnt, kmax, d_hits, d_nout, 0, ctx->stream))
@@ -1351,9 +1369,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
         launch_pull(d_q, nq, d_stack, d_scnt, kint, 0, kmax, d_hits, d_nout, ctx->stream))
       return ctx->fail(YRWI_E_HIP, "shard merge launch");
     span_close(ctx, tm, sp);
-    hD.resize((size_t)nq);
-    HIPCHK(ctx, hipMemcpy2DAsync(hD.data(), sizeof(int32_t), reinterpret_cast<const uint8_t*>(d_norm) + offsetof(NormState, D),
-                                 sizeof(NormState), sizeof(int32_t), (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
+    hD_land = readback(ctx, &ctx->down_stage, reinterpret_cast<const uint8_t*>(d_norm) + offsetof(NormState, D), nq,
+                       4, (int64_t)sizeof(NormState));
+    if (!hD_land) return YRWI_E_HIP;
   }
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
   mark(6);
@@ -1363,6 +1381,10 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     fprintf(stderr, "[yrwi rank] setup %.3f upload %.3f norm %.3f score %.3f topq %.3f emit %.3f sync %.3f ms\n",
             (hq[1] - hq[0]) / 1e6, (hq[2] - hq[1]) / 1e6, (hq[3] - hq[2]) / 1e6, (hq[4] - hq[3]) / 1e6,
             (hq[5] - hq[4]) / 1e6, (hq[6] - hq[5]) / 1e6, (hq[7] - hq[6]) / 1e6);
+  if (hD_land) {
+    hD.resize((size_t)nq);
+    std::memcpy(hD.data(), hD_land, (size_t)nq * 4);
+  }
   for (int32_t D : hD)
     if (D < 0) return ctx->fail(YRWI_E_UNSUPPORTED, "distance fold summary overflow");
   if (!direct) {
@@ -1571,6 +1593,9 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->bytes_alg += p.bytes_alg;
       st->bytes_join += p.bytes_join;
       st->bytes_probe += p.bytes_probe;
+      st->bytes_probe_loaded += p.bytes_probe_loaded;
+      st->bytes_probe_capped += p.bytes_probe_capped;
+      st->bytes_features += p.bytes_features;
       st->t_join_ns += p.t_join_ns;
       st->t_probe_ns += p.t_probe_ns;
       st->bytes_compact += p.bytes_compact;

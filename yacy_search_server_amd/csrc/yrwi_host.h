@@ -522,6 +522,22 @@ inline int upload(Lane* ctx, T* dst, const std::vector<T>& v, R&&... rest) {
   return upload_list(ctx, e, n);
 }
 
+// Device -> host readback by a kernel writing the lane's pinned staging S (no
+// copy engine on the query path): n elements of `elem` bytes, `stride` bytes
+// apart in device memory.  Returns the host address of the packed result, valid
+// after the next lane_sync; nullptr on failure.  One readback per stage at a time.
+inline uint8_t* readback(Lane* L, Stage* S, const void* d_src, int64_t n, int32_t elem, int64_t stride) {
+  uint8_t* h = stage_reserve(L, S, (size_t)std::max<int64_t>(n, 1) * elem, true);
+  if (!h) return nullptr;
+  uint8_t* d = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0) != hipSuccess ||
+      launch_gather_out(d, static_cast<const uint8_t*>(d_src), n, elem, stride, L->stream)) {
+    L->fail(YRWI_E_HIP, "readback launch");
+    return nullptr;
+  }
+  return h;
+}
+
 // start of a device pass: nothing is in flight any more, scratch can be reused
 inline int begin_pass(Lane* ctx) {
   HIPCHK(ctx, lane_sync(ctx));

@@ -258,6 +258,9 @@ struct CopyIn {
   int32_t n;
 };
 int launch_copy_in(const CopyIn& c, void* stream);
+// device -> pinned host readback (dst: device address of pinned host memory): n
+// elements of `elem` bytes, the source's `stride` bytes apart (4-B words when aligned)
+int launch_gather_out(uint8_t* dst, const uint8_t* src, int64_t n, int32_t elem, int64_t stride, void* stream);
 int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* stream);
 int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
                      int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* stream);

@@ -190,6 +190,26 @@ int launch_copy_in(const CopyIn& c, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+__global__ void k_gather_out(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n, int32_t elem,
+                             int64_t stride, int words) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (words) {
+    for (int b = 0; b < elem; b += 4)
+      *reinterpret_cast<uint32_t*>(dst + i * elem + b) = *reinterpret_cast<const uint32_t*>(src + i * stride + b);
+  } else {
+    for (int b = 0; b < elem; b++) dst[i * elem + b] = src[i * stride + b];
+  }
+}
+
+int launch_gather_out(uint8_t* dst, const uint8_t* src, int64_t n, int32_t elem, int64_t stride, void* stream) {
+  if (n <= 0) return 0;
+  const int words = (elem % 4 == 0 && stride % 4 == 0 && ((uintptr_t)dst % 4) == 0 && ((uintptr_t)src % 4) == 0);
+  hipLaunchKernelGGL(k_gather_out, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dst, src, n,
+                     elem, stride, words);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ====================================================== put_list validation
 // err bits: 1 = malformed hash, 2 = empty language cell, 4 = not strictly ascending
 __global__ void k_validate(const uint8_t* __restrict__ rows, int64_t n, uint64_t* __restrict__ khi,
