@@ -410,16 +410,17 @@ def _frac(gbps):
 def kernel_lines(iso, pmc):
     """The join-phase kernels, each on its SURVEY.md §8(d) share of the bytes over
     its mean launch time (library HIP events around each launch, isolated pass):
-      k_join    K of the merge-executed steps (K as the reference dispatches them, J3);
+      k_join    sum of min(K, 4-B ids of both sides) over the merge-executed steps;
       k_probe   sum of min(K, bytes the probe loads) over the probe-executed steps
                 (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id);
+                K as the reference dispatches the step (J3);
       k_compact 23 B per include term and joined posting (23 t m_out).
     traffic = rocprofv3 PMC HBM bytes per launch (profiles/pmc_<config>.json)."""
     n = max(1, iso["n_join_launches"])
     pk = (pmc or {}).get("kernels", {})
     out = {}
     for name, t_ns, alg, extra in (
-            ("k_join", iso["t_join_ns"], iso["bytes_join"], {}),
+            ("k_join", iso["t_join_ns"], iso["bytes_join_capped"], {"alg_bytes_model_K": int(iso["bytes_join"] / n)}),
             ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"],
              {"alg_bytes_model_K": int(iso["bytes_probe"] / n), "loaded_bytes": int(iso["bytes_probe_loaded"] / n)}),
             ("k_compact", iso["t_compact_ns"], iso["bytes_features"], {})):
@@ -443,8 +444,8 @@ def kernel_lines(iso, pmc):
 def roofline_block(iso, timed, steps, ms_per_step, pmc):
     """`roofline` of the bench line: the dominant kernel (longest mean launch among
     k_join / k_probe / k_compact) with its §8(d) bytes (kernel_lines), plus the
-    path: B = sum K + 12 sum n_excl + 23 t m_out per batch with every
-    probe-executed step charged min(K, the bytes the probe loads), over (a) the
+    path: B = sum K + 12 sum n_excl + 23 t m_out per batch with every join and
+    exclusion step charged min(K, the bytes its kernel loads), over (a) the
     batch's kernel time in the isolated pass and (b) the timed region's time per
     batch (batches in flight overlap)."""
     kern = kernel_lines(iso, pmc)
@@ -464,18 +465,18 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
     if pmc:
         r["traffic_source"] = (f"{pmc['_file']} (rocprofv3 --pmc: TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B "
                                f"by request size; tag {pmc.get('tag')}, commit {pmc.get('head')})")
-    b_iso = (iso["bytes_alg"] - iso["bytes_probe"] + iso["bytes_probe_capped"]) / nb
+    b_iso = iso["bytes_alg_capped"] / nb
     t_iso = iso["t_kernels_ns"] / nb * 1e-9
     path = {"bytes_per_batch": int(b_iso),
             "bytes_per_batch_model": int(iso["bytes_alg"] / nb),
-            "rule": "SURVEY 8(d) B; probe-executed steps charged min(K, bytes loaded)"}
+            "rule": "SURVEY 8(d) B with every join / exclusion step charged min(K, the bytes its kernel loads)"}
     if t_iso > 0:
         g = b_iso / t_iso / 1e9
         path["isolated"] = {"achieved": round(g, 1), "frac": _frac(g), "kernel_us_per_batch": round(t_iso * 1e6, 1)}
         if iso.get("isolated_runs_t_kernels_us"):
             path["isolated"]["batches_kernel_us"] = iso["isolated_runs_t_kernels_us"]
     if timed.get("bytes_alg") and ms_per_step > 0:
-        bt = (timed["bytes_alg"] - timed["bytes_probe"] + timed["bytes_probe_capped"]) / steps
+        bt = timed["bytes_alg_capped"] / steps
         g = bt / (ms_per_step * 1e-3) / 1e9
         path["throughput_mode"] = {"achieved": round(g, 1), "frac": _frac(g), "per": "GPU",
                                    "time": "ms_per_step (timed region, batches in flight)"}

@@ -124,14 +124,18 @@ typedef struct yrwi_stats {
   int64_t t_compact_ns;  /* device time of the k_compact launches */
   int64_t t_kernels_ns;  /* device time of all the batch's kernel launches (HIP events around every group of
                             back-to-back launches; host waits and collectives excluded) */
-  /* SURVEY.md §8(d) accounting of the probe-executed join steps: bytes_probe is their K under the
-     reference's own dispatch (J3); bytes_probe_loaded what the probe kernel loads (url-id bitmap: the
-     smaller side's 4-B ids + one 16-B bitmap word per id; range probe: the ids + the large list's
-     range or a 128-B leaf line per id, whichever is less); bytes_probe_capped = sum of
-     min(K, loaded) per step -- the path's bytes with no step credited for reads it never makes */
+  /* SURVEY.md §8(d) bytes with no step credited for reads its kernel never makes: every join step
+     (merge, probe, exclusion) is charged min(K, the bytes its kernel loads) -- merge tiles: 4-B url ids
+     of both sides; url-id bitmap probe: the smaller side's 4-B ids + one 16-B bitmap word per id;
+     range probe: the ids + the larger list's range or a 128-B leaf line per id, whichever is less.
+     bytes_probe_loaded / _capped: the probe-executed include steps (k_probe); bytes_join_capped: the
+     merge-executed include steps (k_join); bytes_alg_capped: the whole path (joins, exclusions and
+     23 t m_out) */
   int64_t bytes_probe_loaded;
   int64_t bytes_probe_capped;
-  int64_t bytes_features;  /* 23 t m_out: the ranking-feature bytes of the joined containers (k_compact's §8(d) share) */
+  int64_t bytes_features;    /* 23 t m_out: the ranking-feature bytes of the joined containers (k_compact's share) */
+  int64_t bytes_join_capped;
+  int64_t bytes_alg_capped;
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

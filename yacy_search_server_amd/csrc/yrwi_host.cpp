@@ -642,6 +642,17 @@ static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
   return 12 * (ns + std::min(nl, ns * (lg + 1)));
 }
 
+// bytes a join job's kernel loads (yrwi_stats.bytes_alg_capped): merge tiles
+// stream both sides' 4-B url ids; a bitmap probe reads the smaller side's ids and
+// one 16-B bitmap word per id; a range probe the ids and the larger list's range,
+// or a 128-B leaf line per id, whichever is less (layout_jobs has set J.algo)
+static int64_t loaded_bytes(const JoinQ& J) {
+  const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
+  if (J.algo == JA_MERGE) return 4 * (ns + nl);
+  const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
+  return bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
+}
+
 struct Timing {
   // per join step: before k_join, between k_join and k_probe, after k_probe
   std::vector<std::array<hipEvent_t, 3>> kjoin;
@@ -728,17 +739,11 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
     for (const JoinQ& J : jobs) {  // §8(d) K of the step as the reference dispatches it
-      const int64_t K = step_bytes(J.mode, J.A.n, J.B.n);
-      if (J.algo == JA_MERGE) {
-        st->bytes_join += K;
-        continue;
-      }
-      const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
-      const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
-      const int64_t loaded = bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
-      st->bytes_probe += K;
-      st->bytes_probe_loaded += loaded;
-      st->bytes_probe_capped += std::min(K, loaded);
+      const int64_t K = step_bytes(J.mode, J.A.n, J.B.n), loaded = loaded_bytes(J);
+      (J.algo == JA_MERGE ? st->bytes_join : st->bytes_probe) += K;
+      (J.algo == JA_MERGE ? st->bytes_join_capped : st->bytes_probe_capped) += std::min(K, loaded);
+      if (J.algo != JA_MERGE) st->bytes_probe_loaded += loaded;
+      st->bytes_alg_capped += std::min(K, loaded);
     }
   // joined sizes land in pinned host memory: k_scan_tiles writes them through its
   // device address (no copy engine), the host reads them after the step's sync
@@ -837,6 +842,8 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   int64_t merge_tiles, tiles;
   layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
   const int nj = (int)jobs.size();
+  if (st)
+    for (const JoinQ& J : jobs) st->bytes_alg_capped += std::min<int64_t>(12 * J.B.n, loaded_bytes(J));
   JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
   int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
   TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
@@ -1074,6 +1081,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       st->joined += R.n;
       st->bytes_alg += 23 * (int64_t)P.seq.size() * R.n;  // ranking feature bytes per surviving posting and term
       st->bytes_features += 23 * (int64_t)P.seq.size() * R.n;
+      st->bytes_alg_capped += 23 * (int64_t)P.seq.size() * R.n;
     }
   }
   slot_base[(size_t)nq] = nslots;
@@ -1596,6 +1604,8 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->bytes_probe_loaded += p.bytes_probe_loaded;
       st->bytes_probe_capped += p.bytes_probe_capped;
       st->bytes_features += p.bytes_features;
+      st->bytes_join_capped += p.bytes_join_capped;
+      st->bytes_alg_capped += p.bytes_alg_capped;
       st->t_join_ns += p.t_join_ns;
       st->t_probe_ns += p.t_probe_ns;
       st->bytes_compact += p.bytes_compact;
