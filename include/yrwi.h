@@ -176,6 +176,16 @@ int yrwi_build_url_ids(yrwi_ctx* ctx);
  * entries out of order (0 when consistent); *nurls = dictionary size (may be NULL). */
 int yrwi_check_url_ids(yrwi_ctx* ctx, int64_t* bad, int64_t* nurls);
 int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes);
+/* Index maintenance counters (diagnostics and tests). */
+typedef struct yrwi_index_info {
+  int64_t full_rebuilds;        /* url dictionary built from every key */
+  int64_t incremental_updates;  /* changed lists merged into an existing dictionary */
+  int64_t repacks;              /* index memory compactions (dead bytes of replaced lists reclaimed) */
+  int64_t index_bytes;          /* device bytes of the index arena (rows, keys, records, incremental ids) */
+  int64_t index_bytes_used;     /* of which allocated so far (live + not yet reclaimed) */
+  int64_t bitmap_lists;         /* lists with a url-id bitmap */
+} yrwi_index_info;
+int yrwi_index_info_get(yrwi_ctx* ctx, yrwi_index_info* info);
 /* Device-wide allocation events of the process so far (scratch arena growth,
  * pinned staging growth: each one stalls every lane of the device while it
  * runs).  A caller counts them around a timed region without per-batch

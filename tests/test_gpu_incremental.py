@@ -97,6 +97,8 @@ def test_incremental_dictionary(monkeypatch):
         # 4: the remaining lists
         steps.append([("add", t, idx.list_rows(t)) for t in rest[len(rest) // 3:-1]])
         nprev = n0
+        base = ix.index_info()
+        assert base["full_rebuilds"] == 1 and base["incremental_updates"] == 0, base
         for si, step in enumerate(steps):
             for op, t, rows in step:
                 h = hashes[t]
@@ -109,8 +111,13 @@ def test_incremental_dictionary(monkeypatch):
                 else:
                     ix.add(h, rows)
                     lists[h] = rows
+            before = ix.index_info()
             bad, nurls = ix.check_url_ids()
             assert bad == 0, si
+            after = ix.index_info()
+            if si in (1, 2):  # small changes: merged into the dictionary, not rebuilt
+                assert after["incremental_updates"] == before["incremental_updates"] + 1, (si, after)
+                assert after["full_rebuilds"] == before["full_rebuilds"], (si, after)
             assert nurls >= nprev, si  # keys of removed postings stay until a full rebuild
             if si == 1:
                 assert nurls == nprev  # no new key: nothing moved
@@ -118,5 +125,80 @@ def test_incremental_dictionary(monkeypatch):
             exp, nfull = _fresh(lists, qs, hashes, monkeypatch)
             assert nfull <= nurls
             _results(ix, lists, qs, hashes, fresh=exp)
+    finally:
+        ix.close()
+
+
+def test_incremental_with_bitmap_lists(monkeypatch):
+    """A bitmap-sized list (>= 1/64 of the url ids) replaced incrementally: the
+    remapped ids, line heads and bitmaps must give the oracle's results."""
+    cfg = synth.preset("small")
+    idx = synth.build_index(cfg)
+    hashes = idx.hashes
+    rng = np.random.default_rng(11)
+    lists = {hashes[t]: idx.list_rows(t) for t in range(len(hashes)) if idx.sizes[t]}
+    big = [int(t) for t in np.argsort(-idx.sizes)[:4]]
+    qs = [([big[0], big[1]], []), ([big[1], big[2]], [big[3]]), ([big[0], big[3], big[2]], [])]
+    qs += synth.queries(cfg, 30, 2, 3, 1)
+    ix = RWIIndex(0)
+    try:
+        for h, r in lists.items():
+            ix.add(h, r)
+        _results(ix, lists, qs, hashes)
+        info = ix.index_info()
+        assert info["bitmap_lists"] > 0, info
+        # the largest list loses a third of its rows and gains rows of another list (new urls for it)
+        h = hashes[big[0]]
+        new = _mixed(lists[h], idx.list_rows(big[5] if len(big) > 5 else int(np.argsort(-idx.sizes)[5])), rng)
+        ix.add(h, new, sorted=False)
+        lists[h] = _sorted_unique(new)
+        bad, _ = ix.check_url_ids()
+        assert bad == 0
+        info2 = ix.index_info()
+        assert info2["incremental_updates"] == info["incremental_updates"] + 1, info2
+        assert info2["bitmap_lists"] > 0, info2
+        exp, _ = _fresh(lists, qs, hashes, monkeypatch)
+        _results(ix, lists, qs, hashes, fresh=exp)
+    finally:
+        ix.close()
+
+
+def test_index_memory_repacked(monkeypatch):
+    """A list re-put again and again (IndexCell.add): the replaced lists' device
+    memory is reclaimed (index arena repacked once dead bytes pass the live ones),
+    so the arena stays bounded, and the results stay exact across the moves."""
+    monkeypatch.setenv("YRWI_REPACK_MIN_MB", "1")
+    cfg = synth.preset("small")
+    idx = synth.build_index(cfg)
+    hashes = idx.hashes
+    rng = np.random.default_rng(3)
+    top = [int(t) for t in np.argsort(-idx.sizes)[:40]]  # a small live index: the re-puts dominate the arena
+    lists = {hashes[t]: idx.list_rows(t) for t in top}
+    big = top[:6]
+    qs = [([big[0], big[1]], []), ([big[0], big[2]], [big[3]])]
+    qs += [([int(a), int(b)], []) for a, b in rng.choice(top, size=(18, 2), replace=True) if a != b]
+    ix = RWIIndex(0)
+    try:
+        for h, r in lists.items():
+            ix.add(h, r)
+        _results(ix, lists, qs, hashes)
+        first = ix.index_info()
+        h = hashes[big[0]]
+        for it in range(24):
+            donor = idx.list_rows(big[1 + it % 5])
+            new = _mixed(lists[h], donor, rng)
+            ix.add(h, new, sorted=False)
+            lists[h] = _sorted_unique(new)
+            if it % 6 == 5:
+                _results(ix, lists, qs, hashes)
+        bad, _ = ix.check_url_ids()
+        assert bad == 0
+        last = ix.index_info()
+        assert last["repacks"] > 0, last
+        # reclaimed: at most the live lists plus the dead bytes that trigger the next repack
+        # (the live bytes again); without repacks the 24 re-puts alone add ~2x the live index
+        live = sum(len(r) for r in lists.values()) * 85
+        assert last["index_bytes_used"] < 2.2 * live + (16 << 20), (last, live)
+        _results(ix, lists, qs, hashes)
     finally:
         ix.close()

@@ -97,6 +97,11 @@ class CPeerRequest(ctypes.Structure):
                 ("url_n", ctypes.c_int64)]
 
 
+class CIndexInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("full_rebuilds", "incremental_updates", "repacks", "index_bytes",
+                                              "index_bytes_used", "bitmap_lists")]
+
+
 class CLoadStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
                                               "dropped_terms")]
@@ -120,6 +125,7 @@ SIGNATURES = {
     "yrwi_index_stats": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
     "yrwi_realloc_events": (ctypes.c_int64, []),
+    "yrwi_index_info_get": (ctypes.c_int, [_VP, ctypes.POINTER(CIndexInfo)]),
     "yrwi_query": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.POINTER(CHit),
                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(CStats)]),
     "yrwi_query_batch": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), ctypes.c_int32, ctypes.c_int32,

@@ -631,6 +631,69 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   return 0;
 }
 
+// Index memory is a bump arena: a replaced or removed list's rows, keys, records
+// and (incrementally assigned) url ids stay allocated.  Once the dead bytes pass
+// the live ones (and 256 MB), every live list is copied into one fresh chunk and
+// the old chunks are freed, so a list re-put again and again (IndexCell.add)
+// costs device memory in proportion to its current size, not to its history.
+// Url ids inside uid_all (full rebuild) stay where they are.  No batch is in
+// flight (callers drain).
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+int repack_index(CtxBase* ctx, bool force) {
+  auto in_uid_all = [&](const ListRec& L) {
+    return ctx->uid_all && L.uid >= ctx->uid_all && L.uid < ctx->uid_all + ctx->uid_cap;
+  };
+  size_t live = 0;
+  for (auto& kv : ctx->lists) {
+    const ListRec& L = kv.second;
+    if (L.n == 0) continue;
+    live += al256((size_t)L.n * 40) + al256((size_t)L.n * 8) + al256((size_t)L.n);
+    if (L.feat) live += al256((size_t)L.n * FEAT_BYTES);
+    if (L.uid && !in_uid_all(L)) live += al256((size_t)L.n * 4);
+  }
+  const size_t used = ctx->index_mem.total_used;
+  const size_t dead = used > live ? used - live : 0;
+  static const size_t min_dead = (size_t)(getenv("YRWI_REPACK_MIN_MB") ? atof(getenv("YRWI_REPACK_MIN_MB")) : 256.0) << 20;
+  if (!force && (dead <= live || dead < min_dead)) return 0;
+  hipStream_t st = ctx->stream;
+  Arena fresh(ctx->index_mem.min_chunk);
+  if (live > 0) fresh.reserve(live);
+  auto move = [&](auto*& ptr, size_t bytes) -> bool {
+    using T = std::remove_reference_t<decltype(*ptr)>;
+    if (!ptr || bytes == 0) return true;
+    uint8_t* q = fresh.alloc(bytes);
+    if (!q) return false;
+    if (hipMemcpyAsync(q, ptr, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) return false;
+    ptr = reinterpret_cast<T*>(q);
+    return true;
+  };
+  for (auto& kv : ctx->lists) {
+    ListRec& L = kv.second;
+    if (L.n == 0) continue;
+    const size_t n = (size_t)L.n;
+    bool ok = move(L.rows, n * 40) && move(L.khi, n * 8) && move(L.klo, n) &&
+              (L.feat ? move(L.feat, n * FEAT_BYTES) : true) && (L.uid && !in_uid_all(L) ? move(L.uid, n * 4) : true);
+    if (!ok) {  // the lists moved so far live in `fresh`, the others in the old chunks: keep both
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      for (auto& c : fresh.chunks) ctx->index_mem.chunks.push_back(c);
+      fresh.chunks.clear();
+      ctx->index_mem.cur = ctx->index_mem.chunks.size();  // the next allocation opens a new chunk
+      return ctx->fail(YRWI_E_NOMEM, "index repack");
+    }
+  }
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  ctx->index_mem.release();
+  ctx->index_mem.chunks.swap(fresh.chunks);
+  ctx->index_mem.used = fresh.used;
+  ctx->index_mem.cur = fresh.cur;
+  ctx->index_mem.total_used = fresh.total_used;
+  ctx->index_repacks++;
+  // the line heads and bitmaps point at url ids that may have moved: rebuilt next
+  ctx->uid_dirty = true;
+  return 0;
+}
+
 }  // namespace
 
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
@@ -642,6 +705,8 @@ void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
 
 int ensure_url_ids(CtxBase* ctx) {
   if (!ctx->uid_dirty) return 0;
+  static const bool force_repack = getenv("YRWI_REPACK_ALWAYS") && atoi(getenv("YRWI_REPACK_ALWAYS"));
+  if (int rc = repack_index(ctx, force_repack)) return rc;
   hipStream_t st = ctx->stream;
   std::vector<ListRec*> lists, changed, others;
   int64_t n = 0, nchanged = 0;
@@ -674,6 +739,8 @@ int ensure_url_ids(CtxBase* ctx) {
     const bool full = !ctx->dict_valid || ctx->nurls == 0 || (e && atoi(e)) || 4 * nchanged > n ||
                       2 * ctx->dict_churn > n;
     rc = full ? full_rebuild(ctx, lists, n) : (changed.empty() ? 0 : incremental(ctx, changed, others));
+    if (!rc && full) ctx->dict_full_builds++;
+    if (!rc && !full && !changed.empty()) ctx->dict_incremental++;
   }
   if (rc) {
     ctx->dict_valid = false;  // the next call rebuilds in full

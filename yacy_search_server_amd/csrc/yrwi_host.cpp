@@ -408,6 +408,18 @@ extern "C" int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n)
 
 extern "C" int64_t yrwi_realloc_events(void) { return g_realloc.load(); }
 
+extern "C" int yrwi_index_info_get(yrwi_ctx* ctx, yrwi_index_info* info) {
+  if (!ctx || !info) return YRWI_E_ARG;
+  std::memset(info, 0, sizeof(*info));
+  info->full_rebuilds = ctx->dict_full_builds;
+  info->incremental_updates = ctx->dict_incremental;
+  info->repacks = ctx->index_repacks;
+  info->index_bytes = (int64_t)ctx->index_mem.capacity();
+  info->index_bytes_used = (int64_t)ctx->index_mem.total_used;
+  for (auto& kv : ctx->lists) info->bitmap_lists += kv.second.bm != nullptr;
+  return 0;
+}
+
 extern "C" int yrwi_index_stats(yrwi_ctx* ctx, int64_t* nterms, int64_t* npostings, int64_t* device_bytes) {
   if (!ctx) return YRWI_E_ARG;
   if (nterms) *nterms = (int64_t)ctx->lists.size();

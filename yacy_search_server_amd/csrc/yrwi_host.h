@@ -389,6 +389,8 @@ struct CtxBase {
   std::unordered_set<KeyT, KeyHash> dict_pending;
   bool dict_valid = false;   // every list outside dict_pending has url ids in the dictionary
   int64_t dict_churn = 0;    // postings removed or replaced since the last full rebuild
+  int64_t index_repacks = 0; // index memory compactions (yrwi_dict.hip repack_index)
+  int64_t dict_full_builds = 0, dict_incremental = 0;
   std::string err;
   int64_t npostings = 0;
 

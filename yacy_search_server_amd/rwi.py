@@ -273,6 +273,13 @@ class RWIIndex:
         _check(self._h, _lib.lib().yrwi_check_url_ids(self._h, ctypes.byref(bad), ctypes.byref(nurls)))
         return bad.value, nurls.value
 
+    def index_info(self) -> dict:
+        """Index maintenance counters (yrwi_index_info_get): dictionary full rebuilds /
+        incremental updates, memory repacks, index arena bytes, bitmap lists."""
+        info = _lib.CIndexInfo()
+        _check(self._h, _lib.lib().yrwi_index_info_get(self._h, ctypes.byref(info)))
+        return {f: getattr(info, f) for f, _ in _lib.CIndexInfo._fields_}
+
     def get_size(self, term: bytes) -> int:
         n = ctypes.c_int64()
         _check(self._h, _lib.lib().yrwi_list_size(self._h, bytes(term), ctypes.byref(n)))
