@@ -654,7 +654,8 @@ int repack_index(CtxBase* ctx, bool force) {
   }
   const size_t used = ctx->index_mem.total_used;
   const size_t dead = used > live ? used - live : 0;
-  static const size_t min_dead = (size_t)(getenv("YRWI_REPACK_MIN_MB") ? atof(getenv("YRWI_REPACK_MIN_MB")) : 256.0) << 20;
+  const char* e = getenv("YRWI_REPACK_MIN_MB");  // read per call: tests lower it
+  const size_t min_dead = (size_t)((e ? atof(e) : 256.0) * (double)(1 << 20));
   if (!force && (dead <= live || dead < min_dead)) return 0;
   hipStream_t st = ctx->stream;
   Arena fresh(ctx->index_mem.min_chunk);
@@ -705,7 +706,7 @@ void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
 
 int ensure_url_ids(CtxBase* ctx) {
   if (!ctx->uid_dirty) return 0;
-  static const bool force_repack = getenv("YRWI_REPACK_ALWAYS") && atoi(getenv("YRWI_REPACK_ALWAYS"));
+  const bool force_repack = getenv("YRWI_REPACK_ALWAYS") && atoi(getenv("YRWI_REPACK_ALWAYS"));
   if (int rc = repack_index(ctx, force_repack)) return rc;
   hipStream_t st = ctx->stream;
   std::vector<ListRec*> lists, changed, others;
