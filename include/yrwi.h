@@ -161,6 +161,12 @@ const char* yrwi_last_error(yrwi_ctx* ctx);
  * sorts (duplicate url hashes: the first occurrence wins, RowSet.mergeEnum). */
 int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted);
 int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n);
+/* Index.get(termHash) for callers off the query path (AbstractIndex.java:116,
+ * IndexCell.java:353-386; e.g. TermSearch.inclusion() for the index abstracts,
+ * SearchEvent.java:513-531): the 40-byte rows of `term`'s list on this context
+ * (its url-hash shard when sharded), ascending by url hash.  *n = the list size
+ * (0: no list); YRWI_E_ARG when cap < *n (nothing copied). */
+int yrwi_get_list(yrwi_ctx* ctx, const uint8_t term[12], uint8_t* rows40, int64_t cap, int64_t* n);
 /* Brings the url dictionary (url hash -> order-preserving 32-bit url id, the
  * join key in HBM) up to date now instead of at the next query.  The first
  * build sorts every key; later put_list / removal / load_heaps changes are

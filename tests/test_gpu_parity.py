@@ -217,6 +217,9 @@ def test_put_list_validation():
         ix.add(b"TERMuns_____", unsorted, sorted=True)
     ix.add(b"TERMuns_____", unsorted, sorted=False)
     assert ix.get_size(b"TERMuns_____") == len(good)
+    # Index.get: the stored list comes back sorted, byte for byte (yrwi_get_list)
+    assert np.array_equal(ix.get_list(b"TERMuns_____"), good)
+    assert ix.get_list(b"TERMnone____").shape == (0, 40)
     nolang = good.copy()
     nolang[0, 22:24] = 0
     with pytest.raises(Exception):

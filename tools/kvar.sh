@@ -1,0 +1,27 @@
+#!/bin/bash
+# Kernel stats of library variants: for each NAME=LIB[:ENV=VAL] one isolated
+# rocprofv3 kernel-stats run (tools/kstats.sh) and the headline bench line.
+#   bash tools/kvar.sh cur=cur base=cur:YRWI_BAND_ORDER=0 ct2=gpurun_var/libyrwi_ct2.so
+set -o pipefail
+R=$(pwd)
+mkdir -p gpurun_out/kvar
+for nv in "$@"; do
+  n=${nv%%=*}; rest=${nv#*=}; p=${rest%%:*}; e=""
+  [ "$rest" != "$p" ] && e=${rest#*:}
+  ( if [ "$p" = cur ]; then unset YRWI_LIB; else export YRWI_LIB=$R/$p; fi
+    [ -n "$e" ] && export "$e"
+    bash tools/kstats.sh kv_$n || exit 1
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu --latency 0 --legs none > gpurun_out/kvar/$n.json 2> gpurun_out/kvar/$n.err || exit 1
+  ) || exit 1
+  mv gpurun_out/kv_${n}_kstats.txt gpurun_out/kvar/
+  python3 - $n <<'PY'
+import json, sys
+n = sys.argv[1]
+k = {}
+for l in open(f"gpurun_out/kvar/kv_{n}_kstats.txt"):
+    f = l.split()
+    if len(f) >= 4: k[f[0].split("::")[-1]] = float(f[-2])
+d = json.load(open(f"gpurun_out/kvar/{n}.json"))
+print(n, "ms/step %.4f" % d["ms_per_step"], " ".join("%s %.1f" % (x, k.get(x, 0)) for x in ("k_compact", "k_probe", "k_tile_order", "k_join", "k_score", "k_reduce")))
+PY
+done

@@ -122,6 +122,7 @@ SIGNATURES = {
     "yrwi_put_list": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, ctypes.c_int64, ctypes.c_int]),
     "yrwi_build_url_ids": (ctypes.c_int, [_VP]),
     "yrwi_list_size": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_get_list": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "yrwi_index_stats": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
     "yrwi_realloc_events": (ctypes.c_int64, []),

@@ -375,6 +375,7 @@ void publish_dict(CtxBase* ctx) {
   for (Lane* L : ctx->lanes) {  // no batch is in flight while the dictionary changes
     L->dkhi = ctx->dkhi;
     L->dklo = ctx->dklo;
+    L->nurls = ctx->nurls;
   }
 }
 

@@ -406,6 +406,20 @@ extern "C" int yrwi_list_size(yrwi_ctx* ctx, const uint8_t term[12], int64_t* n)
   return 0;
 }
 
+extern "C" int yrwi_get_list(yrwi_ctx* ctx, const uint8_t term[12], uint8_t* rows40, int64_t cap, int64_t* n) {
+  KeyT tk;
+  if (!ctx || !n || cap < 0 || (cap > 0 && !rows40)) return YRWI_E_ARG;
+  if (!key_of(term, &tk)) return ctx->fail(YRWI_E_HASH, "term hash is not well-formed Base64");
+  auto it = ctx->lists.find(tk);
+  *n = it == ctx->lists.end() ? 0 : it->second.n;
+  if (*n == 0) return 0;
+  if (cap < *n) return ctx->fail(YRWI_E_ARG, "row buffer smaller than the list");
+  hipSetDevice(ctx->device);
+  HIPCHK(ctx, hipMemcpyAsync(rows40, it->second.rows, (size_t)*n * 40, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
 extern "C" int64_t yrwi_realloc_events(void) { return g_realloc.load(); }
 
 extern "C" int yrwi_index_info_get(yrwi_ctx* ctx, yrwi_index_info* info) {
@@ -738,6 +752,23 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
 
 static int64_t now_ns();
 
+// band-major compaction schedule of a step's tiles (BandOrder, k_order_hist /
+// k_order_scatter):
+// scratch for the tile keys and the order; job order when disabled
+static BandOrder band_order(Lane* ctx, int64_t tiles) {
+  BandOrder bo;
+  if (!ctx->band_order || tiles <= 1 || tiles > INT32_MAX) return bo;
+  bo.nslices = (int32_t)std::min<int64_t>(64, (tiles + ORDER_SLICE_MIN - 1) / ORDER_SLICE_MIN);
+  bo.key = arena_alloc<uint32_t>(ctx, tiles);
+  bo.perm = arena_alloc<int32_t>(ctx, tiles);
+  bo.hist = arena_alloc<int32_t>(ctx, (int64_t)bo.nslices * 4096);
+  if (!bo.key || !bo.perm || !bo.hist) return BandOrder{};
+  int bits = 0;  // url ids < 2^bits; 2^12 bands (ORDER_BUCKETS = 4096)
+  while (bits < 32 && ((int64_t)1 << bits) < ctx->nurls) bits++;
+  bo.shift = std::max(0, bits - 12);
+  return bo;
+}
+
 // One fold step's join jobs: layout, launch, joined sizes back to the plans.
 static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>& jobs, std::vector<int>& owner,
                          yrwi_stats* st, Timing* tm) {
@@ -789,8 +820,9 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
+  const BandOrder bo = band_order(ctx, tiles);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
-                       false,
+                       false, bo,
                        ctx->stream, e0, em, e1, c0, c1))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
@@ -864,7 +896,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, true,
+                       nullptr, true, BandOrder{},
                        ctx->stream, nullptr, nullptr, nullptr))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
   span_close(ctx, tm, sp);

@@ -248,6 +248,8 @@ struct Lane {
   Stage out_stage;           // pinned landing buffer for results
   Stage down_stage;          // pinned landing buffer for small per-step readbacks (joined sizes)
   int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
+  bool band_order = true;    // band-major compaction schedule (BandOrder); YRWI_BAND_ORDER
+  int64_t nurls = 0;         // url ids of the context's dictionary (set with dkhi)
   const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
   const uint8_t* dklo = nullptr;
   Arena arena{(size_t)256 << 20};
@@ -552,6 +554,8 @@ inline int begin_pass(Lane* ctx) {
   ctx->evnext = 0;
   const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
   ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)8;
+  const char* b = getenv("YRWI_BAND_ORDER");  // 0: job-order tile schedule (A/B measurements; same results)
+  ctx->band_order = !(b && b[0] == '0');
   return 0;
 }
 

@@ -277,11 +277,24 @@ int launch_features(const uint8_t* rows, int64_t n, uint64_t* feat, void* stream
 // key of url id uid[i] from the dictionary, the record's columns, freshUntil from "now"
 int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* dkhi, const uint8_t* dklo, int64_t n,
                      int64_t now_ms, uint8_t* rows, void* stream);
+// Band-major compaction schedule of a join step (k_order_hist and
+// k_order_scatter in yrwi_kernels.hip): the url id each tile starts at (key,
+// one per tile) and the tiles in band order (perm); band = key >> shift.
+// key == nullptr: job order.
+struct BandOrder {
+  uint32_t* key = nullptr;
+  int32_t* perm = nullptr;
+  int32_t* hist = nullptr;  // nslices x ORDER_BUCKETS band counts (scratch)
+  int32_t shift = 0;
+  int32_t nslices = 1;      // counting-sort workgroups
+};
+constexpr int ORDER_SLICE_MIN = 2048;  // tiles per counting-sort workgroup (at most 64 of them)
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src,
-                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, void* stream, void* ev_begin,
+                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, const BandOrder& bo, void* stream,
+                     void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);

@@ -363,7 +363,8 @@ __device__ __forceinline__ uint64_t key_host36(uint64_t hi, uint32_t lo) {
 // One thread per merge tile: the merge-path split of the tile's first and last
 // diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
 __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                            int64_t total_tiles, TileDesc* __restrict__ desc, int64_t* __restrict__ tile_src) {
+                            int64_t total_tiles, TileDesc* __restrict__ desc, int64_t* __restrict__ tile_src,
+                            uint32_t* __restrict__ tile_key) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total_tiles) return;
   const int j = find_job(tile_base, njobs, b);
@@ -398,6 +399,10 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   D.pad = 0;
   desc[b] = D;
   if (tile_src) tile_src[b] = min(D.na, D.nbl);  // matches of the tile <= min(#A, #B + lookahead); k_scan_bounds: its run
+  if (tile_key) {  // url id the tile starts at (k_order_hist / k_order_scatter)
+    const uint32_t ka = D.na > 0 ? A[lo0] : 0xFFFFFFFFu, kb = D.nb > 0 ? B[D.b0] : 0xFFFFFFFFu;
+    tile_key[b] = min(ka, kb);
+  }
 }
 
 // joined worddistance (WordReferenceVars.distance :287-294 after join :465-499)
@@ -576,15 +581,82 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 #ifndef YRWI_XCD_SWZ
 #define YRWI_XCD_SWZ 0  // measured: k_compact 274 -> 465 us, k_probe 201 -> 214 us with the remap (profiles/r02h_xcd_swizzle.txt)
 #endif
-__device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t n) {
-#if YRWI_XCD_SWZ
+__device__ __forceinline__ int64_t xcd_slice(int64_t bid, int64_t n) {
   const int64_t q = n >> 3, r = n & 7;  // XCD group x holds q + (x < r) blocks
   const int64_t x = bid & 7, k = bid >> 3;
   return x * q + (x < r ? x : r) + k;
+}
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t n) {
+#if YRWI_XCD_SWZ
+  return xcd_slice(bid, n);
 #else
   (void)n;
   return bid;
 #endif
+}
+
+// ======================================================= join: band order
+// Band-major compaction schedule.  A batch's queries draw their terms by df, so
+// the big lists recur across it, and the queries' joins gather ranking records
+// of the same lists in the same url-id ranges.  In job order those re-reads are
+// spread over the whole launch and all eight L2s; k_order_hist and
+// k_order_scatter counting-sort the step's tiles by the url id they start at (ORDER_BUCKETS bands) and
+// k_compact gives every XCD group of blocks one contiguous slice of that order
+// (xcd_slice), so the blocks resident on an XCD gather from one url-id band of
+// every list and its L2 serves the re-reads (C2: k_compact 264 -> 225 us).
+// Only the schedule changes: every tile writes its own output slots.  (k_probe
+// keeps job order: the jobs of one large list run back to back and its bitmap
+// stays in L2; in band order k_probe took 165 -> 171 us.)
+// Counting sort over G workgroups (LDS atomics run at about one lane per clock
+// on a CU, so one workgroup took 30-35 us for C2's ~45k tiles): k_order_hist
+// counts each workgroup's slice of tiles per band, k_order_scatter derives its
+// slice's first slot per band from all the counts and places its tiles.
+constexpr int ORDER_BUCKETS = 4096;
+constexpr int ORDER_THREADS = 1024;
+__device__ __forceinline__ int order_bucket(uint32_t k, int shift) {
+  return (int)min(k >> shift, (uint32_t)(ORDER_BUCKETS - 1));
+}
+__global__ __launch_bounds__(ORDER_THREADS) void k_order_hist(const uint32_t* __restrict__ key, int64_t n,
+                                                              int64_t slice, int shift, int32_t* __restrict__ hist) {
+  __shared__ int32_t cnt[ORDER_BUCKETS];
+  for (int i = threadIdx.x; i < ORDER_BUCKETS; i += ORDER_THREADS) cnt[i] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * slice, t1 = min(n, t0 + slice);
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += ORDER_THREADS) atomicAdd(&cnt[order_bucket(key[t], shift)], 1);
+  __syncthreads();
+  int4* h = reinterpret_cast<int4*>(hist + (int64_t)blockIdx.x * ORDER_BUCKETS);
+  h[threadIdx.x] = reinterpret_cast<const int4*>(cnt)[threadIdx.x];
+}
+__global__ __launch_bounds__(ORDER_THREADS) void k_order_scatter(const uint32_t* __restrict__ key, int64_t n,
+                                                                 int64_t slice, int shift,
+                                                                 const int32_t* __restrict__ hist,
+                                                                 int32_t* __restrict__ perm) {
+  __shared__ int32_t cnt[ORDER_BUCKETS];
+  __shared__ int32_t wsum[ORDER_THREADS / 64];
+  static_assert(ORDER_BUCKETS == 4 * ORDER_THREADS, "four buckets per thread");
+  // buckets 4i..4i+3: totals over every slice, and the counts of the slices before this one
+  int4 tot = make_int4(0, 0, 0, 0), pre = make_int4(0, 0, 0, 0);
+  for (int w = 0; w < (int)gridDim.x; w++) {
+    const int4 h = reinterpret_cast<const int4*>(hist + (int64_t)w * ORDER_BUCKETS)[threadIdx.x];
+    tot.x += h.x; tot.y += h.y; tot.z += h.z; tot.w += h.w;
+    if (w < (int)blockIdx.x) { pre.x += h.x; pre.y += h.y; pre.z += h.z; pre.w += h.w; }
+  }
+  const int32_t s = tot.x + tot.y + tot.z + tot.w;
+  const int32_t inc = wave_incl_sum(s);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wsum[wv] = inc;
+  __syncthreads();
+  int32_t off = inc - s;
+  for (int w = 0; w < wv; w++) off += wsum[w];
+  const int i4 = 4 * threadIdx.x;
+  cnt[i4] = off + pre.x;
+  cnt[i4 + 1] = off + tot.x + pre.y;
+  cnt[i4 + 2] = off + tot.x + tot.y + pre.z;
+  cnt[i4 + 3] = off + tot.x + tot.y + tot.z + pre.w;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * slice, t1 = min(n, t0 + slice);
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += ORDER_THREADS)
+    perm[atomicAdd(&cnt[order_bucket(key[t], shift)], 1)] = (int32_t)t;
 }
 
 #ifndef YRWI_PROBE_LDS
@@ -666,7 +738,8 @@ __device__ __forceinline__ bool probe_heads(const DList& Lg, int64_t lo, int64_t
 #endif
 
 __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                             int64_t tile0, int64_t ntiles, ProbeDesc* __restrict__ pdesc) {
+                             int64_t tile0, int64_t ntiles, ProbeDesc* __restrict__ pdesc,
+                             uint32_t* __restrict__ tile_key) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
@@ -675,6 +748,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const int64_t s0 = (tile0 + t - tile_base[j]) * J.ptile;
   const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
+  if (tile_key) tile_key[tile0 + t] = Sm.uid[s0];  // url id the tile starts at (k_order_hist / k_order_scatter)
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
@@ -977,14 +1051,17 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const uint32_t* __restrict__ pair_uid,
                                                  const int64_t* __restrict__ tile_src,
                                                  const int32_t* __restrict__ tile_cnt,
-                                                 const int64_t* __restrict__ tile_off) {
+                                                 const int64_t* __restrict__ tile_off,
+                                                 const int32_t* __restrict__ perm) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
-  const int64_t t0 = xcd_swizzle(blockIdx.x, gridDim.x) * COMPACT_TILES;
+  // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
+  const int64_t p0 = (perm ? xcd_slice(blockIdx.x, gridDim.x) : xcd_swizzle(blockIdx.x, gridDim.x)) * COMPACT_TILES;
   if (threadIdx.x < 64) {
-    const int64_t t = t0 + threadIdx.x;
+    const int64_t p = p0 + threadIdx.x;
     int32_t c = 0;
-    if (threadIdx.x < COMPACT_TILES && t < ntiles) {
+    if (threadIdx.x < COMPACT_TILES && p < ntiles) {
+      const int64_t t = perm ? (int64_t)perm[p] : p;
       c = tile_cnt[t];
       if (c) {
         const JoinQ& J = jobs[find_job(tile_base, njobs, t)];
@@ -3055,10 +3132,14 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
-                     int64_t* d_tile_off, bool mark,
+                     int64_t* d_tile_off, bool mark, const BandOrder& bo,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1) {
   if (total_tiles <= 0) return 0;
+  const int64_t probe_tiles = total_tiles - merge_tiles;
+  // band order of the tiles for k_compact (k_order_hist / k_order_scatter)
+  int32_t* perm = bo.key && !mark ? bo.perm : nullptr;
+  uint32_t* tkey = perm ? bo.key : nullptr;
   static int join_grid = 0;  // resident k_join workgroups on the whole device
   if (!join_grid) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -3069,15 +3150,21 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
       return YRWI_E_HIP;
     join_grid = std::max(1, cus * std::max(1, per_cu));
   }
-  const int64_t probe_tiles = total_tiles - merge_tiles;
   if (merge_tiles > 0) {
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src);
+                       d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src, tkey);
     if (!mark) hipLaunchKernelGGL(k_scan_bounds, dim3((unsigned)nmerge), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_src);
   }
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc);
+                       d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc, tkey);
+  if (perm) {
+    const int64_t slice = (total_tiles + bo.nslices - 1) / bo.nslices;
+    hipLaunchKernelGGL(k_order_hist, dim3((unsigned)bo.nslices), dim3(ORDER_THREADS), 0, S(st), tkey, total_tiles,
+                       slice, bo.shift, bo.hist);
+    hipLaunchKernelGGL(k_order_scatter, dim3((unsigned)bo.nslices), dim3(ORDER_THREADS), 0, S(st), tkey,
+                       total_tiles, slice, bo.shift, (const int32_t*)bo.hist, perm);
+  }
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
@@ -3093,7 +3180,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
                        S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
-                       d_tile_off);
+                       d_tile_off, (const int32_t*)perm);
     if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
   }
   return rc(hipGetLastError());

@@ -285,6 +285,15 @@ class RWIIndex:
         _check(self._h, _lib.lib().yrwi_list_size(self._h, bytes(term), ctypes.byref(n)))
         return n.value
 
+    def get_list(self, term: bytes) -> np.ndarray:
+        """Index.get(termHash) (AbstractIndex.java:116): the list's (n, 40) uint8 rows
+        in url-hash order, (0, 40) when the term has no list (yrwi_get_list)."""
+        n = self.get_size(term)
+        out = np.zeros((max(n, 1), 40), dtype=np.uint8)
+        m = ctypes.c_int64()
+        _check(self._h, _lib.lib().yrwi_get_list(self._h, bytes(term), out.ctypes.data, n, ctypes.byref(m)))
+        return out[:m.value]
+
     def stats(self) -> Tuple[int, int, int]:
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         _check(self._h, _lib.lib().yrwi_index_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
