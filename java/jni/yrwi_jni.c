@@ -285,24 +285,67 @@ JNIEXPORT void JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventClose(JNIEnv* env,
   yrwi_event_close((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev);
 }
 
-/* ---- index abstracts: compressIndex per term (searchConjunction), joined by '\n' ---- */
-JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_indexAbstracts(JNIEnv* env, jclass c, jlong ctx,
-                                                                             jbyteArray terms, jint nterms,
-                                                                             jlong cap) {
+/* ---- index abstracts: compressIndex per term (searchConjunction), one String each ---- */
+JNIEXPORT jobjectArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_indexAbstracts(JNIEnv* env, jclass c, jlong ctx,
+                                                                               jbyteArray terms, jint nterms,
+                                                                               jlong cap) {
   jbyte* tb = (*env)->GetByteArrayElements(env, terms, NULL);
-  char* out = (char*)malloc((size_t)(cap > 0 ? cap : 1));
+  char* out = (char*)malloc((size_t)(cap > 0 ? cap : 1) + 1);
   int64_t* off = (int64_t*)calloc((size_t)nterms + 1, sizeof(int64_t));
   int32_t nout = 0;
   int rc = yrwi_index_abstracts((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)tb, nterms, NULL, out, cap, off, &nout);
   (*env)->ReleaseByteArrayElements(env, terms, tb, JNI_ABORT);
-  jbyteArray res = NULL;
-  if (rc == 0) {  /* abstract i = bytes [off[i], off[i+1]) */
-    res = (*env)->NewByteArray(env, (jsize)off[nout]);
-    (*env)->SetByteArrayRegion(env, res, 0, (jsize)off[nout], (const jbyte*)out);
+  jobjectArray res = NULL;
+  if (rc == 0) {  /* abstract i = bytes [off[i], off[i+1]) (ASCII); none when a term has no list */
+    res = (*env)->NewObjectArray(env, nout, (*env)->FindClass(env, "java/lang/String"), NULL);
+    for (int32_t i = 0; i < nout; i++) {
+      const char save = out[off[i + 1]];
+      out[off[i + 1]] = 0;
+      jstring s = (*env)->NewStringUTF(env, out + off[i]);
+      out[off[i + 1]] = save;
+      (*env)->SetObjectArrayElement(env, res, i, s);
+      (*env)->DeleteLocalRef(env, s);
+    }
   }
   free(out);
   free(off);
   return res;
+}
+
+/* ---- Index.size / Index.get of the GPU index (J1 sizes, TermSearch.inclusion) ---- */
+JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_listSizes(JNIEnv* env, jclass c, jlong ctx,
+                                                                        jbyteArray terms, jint nterms) {
+  jbyte* tb = (*env)->GetByteArrayElements(env, terms, NULL);
+  jlong* v = (jlong*)calloc((size_t)(nterms > 0 ? nterms : 1), sizeof(jlong));
+  int rc = 0;
+  for (jint i = 0; i < nterms && rc == 0; i++) {
+    int64_t n = 0;
+    rc = yrwi_list_size((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)tb + 12 * i, &n);
+    v[i] = n;
+  }
+  (*env)->ReleaseByteArrayElements(env, terms, tb, JNI_ABORT);
+  jlongArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewLongArray(env, nterms);
+    (*env)->SetLongArrayRegion(env, res, 0, nterms, v);
+  }
+  free(v);
+  return res;
+}
+
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_getList(JNIEnv* env, jclass c, jlong ctx,
+                                                                      jbyteArray term) {
+  yrwi_ctx* x = (yrwi_ctx*)(intptr_t)ctx;
+  jbyte t[12];
+  (*env)->GetByteArrayRegion(env, term, 0, 12, t);
+  int64_t n = 0, m = 0;
+  if (yrwi_list_size(x, (const uint8_t*)t, &n) != 0) return NULL;
+  jbyteArray res = (*env)->NewByteArray(env, (jsize)(n * 40));
+  if (n == 0) return res;
+  void* p = (*env)->GetPrimitiveArrayCritical(env, res, NULL);  /* the device copy lands in the Java array */
+  int rc = yrwi_get_list(x, (const uint8_t*)t, (uint8_t*)p, n, &m);
+  (*env)->ReleasePrimitiveArrayCritical(env, res, p, 0);
+  return rc == 0 && m == n ? res : NULL;
 }
 
 /* ---- Solr node stack: cardinal(URIMetadataNode); nodes = packed yrwi_node records ---- */

@@ -5,7 +5,8 @@
 // they have not been compiled here.  See INTEGRATION.md.
 //
 // Drop-in points (paths relative to source/net/yacy):
-//   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.joinExclude(...)
+//   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.listSizes(...) + joinExclude(...) (GpuTermSearch)
+//   kelondro/rwi/AbstractIndex.java:116        -> GpuRWI.getList(...) (TermSearch.inclusion, on demand)
 //   kelondro/rwi/ReferenceContainer.java:310   -> GpuRWI.joinExclude(...)
 //   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.normalizeScore(...)
 //   search/query/SearchEvent.java:612-631      -> GpuRWI.query(...) (whole local RWI path)
@@ -27,6 +28,18 @@ public final class GpuRWI implements AutoCloseable {
     /** IndexCell.add for a whole container: the RowSet chunkcache bytes (n * 40, sorted). */
     public void putList(final byte[] termHash, final byte[] chunkcache, final int n) {
         check(putList(this.ctx, termHash, chunkcache, n, 1));
+    }
+
+    /** Index.size(termHash) of each term on the GPU index (yrwi_list_size; 0: no list). */
+    public long[] listSizes(final byte[][] terms) {
+        return listSizes(this.ctx, flatten(terms), terms.length);
+    }
+
+    /** Index.get(termHash) off the query path (yrwi_get_list): the list's sorted rows (n * 40 bytes). */
+    public byte[] getList(final byte[] term) {
+        final byte[] rows = getList(this.ctx, term);
+        if (rows == null) throw new IllegalStateException("yrwi_get_list failed");
+        return rows;
     }
 
     /** TermSearch + joinExcludeContainers: returns the joined container's rows (m * 40 bytes). */
@@ -119,8 +132,8 @@ public final class GpuRWI implements AutoCloseable {
     }
 
     /** WordReferenceFactory.compressIndex of each include word's list (search.java:264-281):
-     *  the abstracts back to back, each "{...}". */
-    public byte[] indexAbstracts(final byte[][] words, final long capacity) {
+     *  one "{...}" per word; empty when a word has no list (searchConjunction is empty). */
+    public String[] indexAbstracts(final byte[][] words, final long capacity) {
         return indexAbstracts(this.ctx, flatten(words), words.length, capacity);
     }
 
@@ -188,7 +201,9 @@ public final class GpuRWI implements AutoCloseable {
     private static native byte[] eventResult(long ctx, long event, int maxn);
     private static native byte[] eventPull(long ctx, long event, boolean skipDoubleDom, int maxn);
     private static native void eventClose(long ctx, long event);
-    private static native byte[] indexAbstracts(long ctx, byte[] words, int nwords, long capacity);
+    private static native String[] indexAbstracts(long ctx, byte[] words, int nwords, long capacity);
+    private static native long[] listSizes(long ctx, byte[] terms, int nterms);
+    private static native byte[] getList(long ctx, byte[] term);
     private static native long[] scoreNodes(long ctx, byte[] nodes, int n, int[] profile32, String language,
                                             int maxdomcount);
 }

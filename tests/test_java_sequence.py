@@ -4,13 +4,20 @@ java/net/yacy/kelondro/rwi/GpuTermSearch.java and
 java/net/yacy/search/ranking/GpuReferenceOrder.java cannot be compiled here (no
 JDK); this test makes exactly the libyrwi calls they make for one SearchEvent:
 
-  TermSearch  -> GpuTermSearch.joinExclude  -> yrwi_join_exclude (joined rows)
-  addRWIs     -> GpuReferenceOrder.normalizeWith -> yrwi_normalize_score (one
-                 settled score per row), then cardinal(e) = that score, fed in
-                 container order into rwiStack (WeakPriorityBlockingQueue order)
+  TermSearch  -> GpuTermSearch(...): yrwi_list_size per include word (J1; no
+                 CPU container is fetched), yrwi_join_exclude (joined rows)
+  addRWIs     -> GpuReferenceOrder.normalizeWith -> yrwi_normalize_score on the
+                 container's own rows: one settled score per row in a long[];
+                 every queued entry carries its position, cardinal(e) =
+                 scores[pos], fed in container order into rwiStack
+                 (WeakPriorityBlockingQueue order)
+  abstracts   -> GpuTermSearch.inclusion(): yrwi_get_list per include word (only
+                 when asked); inclusionSizes() / abstracts(): yrwi_list_size,
+                 yrwi_index_abstracts
 
 and checks that the stack equals both the whole-query path (yrwi_query) and the
-oracle (SearchEvent.java:697-816, ReferenceOrder.java:70,223)."""
+oracle (SearchEvent.java:697-816, ReferenceOrder.java:70,223), and that
+inclusion() holds the index's lists (TermSearch.java:50-56)."""
 
 import numpy as np
 import pytest
@@ -45,14 +52,19 @@ def test_termsearch_then_reference_order(corpus, profile):
     for inc, exc in synth.queries(cfg, 24, 1, 3, 1, qseed=123):
         ih = [idx.hashes[t] for t in inc]
         eh = [idx.hashes[t] for t in exc]
-        rows = ix.term_search(ih, eh, now_ms=NOW)                     # GpuTermSearch.joinExclude
+        sizes = [ix.get_size(h) for h in ih]                          # GpuTermSearch: listSizes (J1)
+        complete = all(sizes)
+        rows = ix.term_search(ih, eh, now_ms=NOW)                     # GpuTermSearch: joinExclude
         assert np.array_equal(rows, orc.term_search(whole, ih, eh, 2147483647, NOW))
+        if complete:                                                  # inclusion(), on demand: the lists
+            for h in ih:
+                assert np.array_equal(ix.get_list(h), whole[h])
         if len(rows) == 0:
             continue
         n += 1
         scores = ix.normalize_score(rows, prof, "en", NOW)            # GpuReferenceOrder.normalizeWith
-        card = {bytes(r[:12]): int(s) for r, s in zip(rows, scores)}  # GpuReferenceOrder.cardinal
-        ordered = np.array([card[bytes(r[:12])] for r in rows], dtype=np.int64)  # addRWIs pollloop order
+        queue = list(range(len(rows)))                                # Entry(pos) per posting, container order
+        ordered = np.array([scores[pos] for pos in queue], dtype=np.int64)  # cardinal(e) = scores[pos]
         stack = orc.topk(rows, ordered, 100)                          # rwiStack (WeakPriorityBlockingQueue)
         exp_scores, _ = orc.normalize_score(rows, orc.profile_from(prof), "en", NOW)
         assert np.array_equal(scores, exp_scores)
@@ -93,3 +105,24 @@ def test_join_into_direct_buffer_and_query_stats(corpus):
         assert st.joined >= m and st.t_total_ns > 0
         done += 1
     assert done > 0
+
+
+def test_inclusion_sizes_and_abstracts(corpus):
+    """GpuTermSearch.inclusionSizes() / abstracts(): the IACount / IAResults that
+    SearchEvent builds from inclusion() (SearchEvent.java:515-531), taken from the
+    GPU index -- sizes equal the lists', each abstract equals the abstract of that
+    word alone, and a query with an unknown word has neither (J1)."""
+    cfg, idx, ix = corpus
+    whole = idx.as_dict()
+    done = 0
+    for inc, _ in synth.queries(cfg, 8, 2, 3, 0, qseed=77):
+        ih = [idx.hashes[t] for t in inc]
+        sizes = [ix.get_size(h) for h in ih]
+        assert sizes == [len(whole[h]) for h in ih]
+        ab = ix.index_abstracts(ih)
+        assert len(ab) == len(ih)
+        for h, a in zip(ih, ab):
+            assert ix.index_abstracts([h]) == [a] and a.startswith(b"{") and a.endswith(b"}")
+        done += 1
+    assert done > 0
+    assert ix.index_abstracts([idx.hashes[inc[0]], b"AAAAAAAAAAAA"]) == []
