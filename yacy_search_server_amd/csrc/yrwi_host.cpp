@@ -737,8 +737,13 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
   *nmerge = 0;
   *merge_tiles = 0;
   *tiles = 0;
+  uintptr_t prev_big = 0;
+  int32_t group = -1;
   for (size_t i : order) {
     JoinQ J = jobs[i];
+    if (big(J) != prev_big) group++;  // probe jobs of one large list are consecutive
+    prev_big = big(J);
+    J.lgroup = group;
     J.tile_base = *tiles;
     tile_base.push_back(*tiles);
     *tiles += J.ntiles;
@@ -755,17 +760,28 @@ static int64_t now_ns();
 // band-major compaction schedule of a step's tiles (BandOrder, k_order_hist /
 // k_order_scatter):
 // scratch for the tile keys and the order; job order when disabled
-static BandOrder band_order(Lane* ctx, int64_t tiles) {
+static BandOrder band_order(Lane* ctx, int64_t tiles, int64_t merge_tiles, bool compact) {
   BandOrder bo;
-  if (!ctx->band_order || tiles <= 1 || tiles > INT32_MAX) return bo;
-  bo.nslices = (int32_t)std::min<int64_t>(64, (tiles + ORDER_SLICE_MIN - 1) / ORDER_SLICE_MIN);
-  bo.key = arena_alloc<uint32_t>(ctx, tiles);
-  bo.perm = arena_alloc<int32_t>(ctx, tiles);
-  bo.hist = arena_alloc<int32_t>(ctx, (int64_t)bo.nslices * 4096);
-  if (!bo.key || !bo.perm || !bo.hist) return BandOrder{};
-  int bits = 0;  // url ids < 2^bits; 2^12 bands (ORDER_BUCKETS = 4096)
+  if (tiles <= 0 || tiles > INT32_MAX) return bo;
+  bo.tile_job = arena_alloc<int32_t>(ctx, tiles);
+  if (!ctx->band_order || tiles <= 1 || !bo.tile_job) return bo;
+  bo.hist = arena_alloc<int32_t>(ctx, (int64_t)ORDER_HIST_SLICES * 4096);
+  if (compact) {
+    bo.key = arena_alloc<uint32_t>(ctx, tiles);
+    bo.perm = arena_alloc<int2>(ctx, tiles);
+  }
+  if (tiles - merge_tiles > 1) {
+    bo.pkey = arena_alloc<uint32_t>(ctx, tiles - merge_tiles);
+    bo.pperm = arena_alloc<int2>(ctx, tiles - merge_tiles);
+  }
+  if (!bo.hist || (compact && (!bo.key || !bo.perm)) || (bo.pkey && !bo.pperm)) {
+    bo.key = bo.pkey = nullptr;
+    return bo;
+  }
+  int bits = 0;  // url ids < 2^bits; 2^12 bands for compaction, 2^4 per large list for the probe
   while (bits < 32 && ((int64_t)1 << bits) < ctx->nurls) bits++;
   bo.shift = std::max(0, bits - 12);
+  bo.pshift = std::max(0, bits - 4);
   return bo;
 }
 
@@ -820,7 +836,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
-  const BandOrder bo = band_order(ctx, tiles);
+  const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
                        false, bo,
                        ctx->stream, e0, em, e1, c0, c1))
@@ -894,9 +910,10 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
   if (!d_jobs || !d_tb || !d_split || !d_pdesc) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
+  const BandOrder bo = band_order(ctx, tiles, merge_tiles, false);
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, true, BandOrder{},
+                       nullptr, true, bo,
                        ctx->stream, nullptr, nullptr, nullptr))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
   span_close(ctx, tm, sp);

@@ -109,7 +109,7 @@ struct JoinQ {
   int32_t algo;        // JoinAlgo
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   int32_t ptile;       // JA_PROBE: small-list elements per tile (PROBE_TILE, BM_TILE with a bitmap)
-  int32_t pad_;
+  int32_t lgroup;      // JA_PROBE: rank of its large list among the step's (k_probe's band order)
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
@@ -277,18 +277,36 @@ int launch_features(const uint8_t* rows, int64_t n, uint64_t* feat, void* stream
 // key of url id uid[i] from the dictionary, the record's columns, freshUntil from "now"
 int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* dkhi, const uint8_t* dklo, int64_t n,
                      int64_t now_ms, uint8_t* rows, void* stream);
-// Band-major compaction schedule of a join step (k_order_hist and
-// k_order_scatter in yrwi_kernels.hip): the url id each tile starts at (key,
-// one per tile) and the tiles in band order (perm); band = key >> shift.
-// key == nullptr: job order.
+// Band-major schedules of a join step (k_order_hist and k_order_scatter in
+// yrwi_kernels.hip).  Compaction: the url id each tile starts at (key, one per
+// tile), band = key >> shift, the tiles in that order (perm: tile, job).
+// Probe: (large-list group, 16 bands) per probe tile (pkey, bands of
+// pshift-shifted ids), the probe tiles in that order (pperm; tile index relative
+// to the first probe tile).  key / pkey == nullptr: job order.  tile_job (any
+// order) spares k_compact a search of the job table per tile.
 struct BandOrder {
+  int32_t* tile_job = nullptr;  // job of every tile (k_partition / k_probe_part; k_compact reads it)
   uint32_t* key = nullptr;
-  int32_t* perm = nullptr;
-  int32_t* hist = nullptr;  // nslices x ORDER_BUCKETS band counts (scratch)
-  int32_t shift = 0;
-  int32_t nslices = 1;      // counting-sort workgroups
+  int2* perm = nullptr;
+  uint32_t* pkey = nullptr;
+  int2* pperm = nullptr;
+  int32_t* hist = nullptr;      // bucket counts of both sorts' workgroups (scratch, ORDER_HIST_SLICES x 4096)
+  int32_t shift = 0, pshift = 0;
 };
-constexpr int ORDER_SLICE_MIN = 2048;  // tiles per counting-sort workgroup (at most 64 of them)
+constexpr int ORDER_SLICE_MIN = 2048;  // tiles per counting-sort workgroup (at most 64 per order)
+constexpr int ORDER_HIST_SLICES = 128;
+struct OrderProb {
+  const uint32_t* key;
+  int64_t n, slice;
+  int32_t shift, nslices;
+  const int32_t* tile_job;
+  int2* perm;
+  int32_t* hist;
+};
+struct OrderArgs {
+  OrderProb p[2];
+};
+
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,

@@ -364,7 +364,7 @@ __device__ __forceinline__ uint64_t key_host36(uint64_t hi, uint32_t lo) {
 // diagonal (two interleaved binary searches on the url-hash keys) -> TileDesc.
 __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
                             int64_t total_tiles, TileDesc* __restrict__ desc, int64_t* __restrict__ tile_src,
-                            uint32_t* __restrict__ tile_key) {
+                            uint32_t* __restrict__ tile_key, int32_t* __restrict__ tile_job) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total_tiles) return;
   const int j = find_job(tile_base, njobs, b);
@@ -399,6 +399,7 @@ __global__ void k_partition(const JoinQ* __restrict__ jobs, const int64_t* __res
   D.pad = 0;
   desc[b] = D;
   if (tile_src) tile_src[b] = min(D.na, D.nbl);  // matches of the tile <= min(#A, #B + lookahead); k_scan_bounds: its run
+  if (tile_job) tile_job[b] = j;
   if (tile_key) {  // url id the tile starts at (k_order_hist / k_order_scatter)
     const uint32_t ka = D.na > 0 ? A[lo0] : 0xFFFFFFFFu, kb = D.nb > 0 ? B[D.b0] : 0xFFFFFFFFu;
     tile_key[b] = min(ka, kb);
@@ -596,50 +597,60 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t n) {
 }
 
 // ======================================================= join: band order
-// Band-major compaction schedule.  A batch's queries draw their terms by df, so
-// the big lists recur across it, and the queries' joins gather ranking records
-// of the same lists in the same url-id ranges.  In job order those re-reads are
-// spread over the whole launch and all eight L2s; k_order_hist and
-// k_order_scatter counting-sort the step's tiles by the url id they start at (ORDER_BUCKETS bands) and
-// k_compact gives every XCD group of blocks one contiguous slice of that order
-// (xcd_slice), so the blocks resident on an XCD gather from one url-id band of
-// every list and its L2 serves the re-reads (C2: k_compact 264 -> 225 us).
-// Only the schedule changes: every tile writes its own output slots.  (k_probe
-// keeps job order: the jobs of one large list run back to back and its bitmap
-// stays in L2; in band order k_probe took 165 -> 171 us.)
-// Counting sort over G workgroups (LDS atomics run at about one lane per clock
-// on a CU, so one workgroup took 30-35 us for C2's ~45k tiles): k_order_hist
-// counts each workgroup's slice of tiles per band, k_order_scatter derives its
-// slice's first slot per band from all the counts and places its tiles.
+// Band-major schedules.  A batch's queries draw their terms by df, so the big
+// lists recur across it, and the queries' joins touch the same lists in the same
+// url-id ranges: the bitmap words k_probe reads and the ranking records
+// k_compact gathers.  In job order those re-reads are spread over the whole
+// launch and all eight L2s.  k_order_hist and k_order_scatter counting-sort the
+// step's tiles (ORDER_BUCKETS buckets), and k_probe / k_compact give every XCD
+// group of blocks one contiguous slice of that order (xcd_slice), so the blocks
+// resident on an XCD work on one url-id band and its L2 serves the re-reads:
+//  * compaction: all tiles by the url id they start at (4096 bands): every list's
+//    records of one band (C2: k_compact 268 -> 230 us, 11.7 -> 7.7 M lines read);
+//  * probe: the probe tiles by (large list, 16 bands of url ids): the jobs of one
+//    large list in band order, so an XCD holds the band of one or two bitmaps.
+// Only the schedule changes: every tile writes its own slots.  Counting sort
+// over G workgroups per order (LDS atomics run at about one lane per clock on a
+// CU, so one workgroup took 30-35 us for C2's ~45k tiles): k_order_hist counts
+// each workgroup's slice of tiles per bucket, k_order_scatter derives its
+// slice's first slot per bucket from all the counts and places its tiles.
+// Both orders run in the same two launches (OrderArgs: blocks of problem 0,
+// then of problem 1).
 constexpr int ORDER_BUCKETS = 4096;
 constexpr int ORDER_THREADS = 1024;
 __device__ __forceinline__ int order_bucket(uint32_t k, int shift) {
   return (int)min(k >> shift, (uint32_t)(ORDER_BUCKETS - 1));
 }
-__global__ __launch_bounds__(ORDER_THREADS) void k_order_hist(const uint32_t* __restrict__ key, int64_t n,
-                                                              int64_t slice, int shift, int32_t* __restrict__ hist) {
+__device__ __forceinline__ const OrderProb& order_prob(const OrderArgs& A, int& blk) {
+  blk = (int)blockIdx.x;
+  if (blk < A.p[0].nslices) return A.p[0];
+  blk -= A.p[0].nslices;
+  return A.p[1];
+}
+__global__ __launch_bounds__(ORDER_THREADS) void k_order_hist(OrderArgs A) {
   __shared__ int32_t cnt[ORDER_BUCKETS];
+  int blk;
+  const OrderProb& P = order_prob(A, blk);
   for (int i = threadIdx.x; i < ORDER_BUCKETS; i += ORDER_THREADS) cnt[i] = 0;
   __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * slice, t1 = min(n, t0 + slice);
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += ORDER_THREADS) atomicAdd(&cnt[order_bucket(key[t], shift)], 1);
+  const int64_t t0 = (int64_t)blk * P.slice, t1 = min(P.n, t0 + P.slice);
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += ORDER_THREADS) atomicAdd(&cnt[order_bucket(P.key[t], P.shift)], 1);
   __syncthreads();
-  int4* h = reinterpret_cast<int4*>(hist + (int64_t)blockIdx.x * ORDER_BUCKETS);
+  int4* h = reinterpret_cast<int4*>(P.hist + (int64_t)blk * ORDER_BUCKETS);
   h[threadIdx.x] = reinterpret_cast<const int4*>(cnt)[threadIdx.x];
 }
-__global__ __launch_bounds__(ORDER_THREADS) void k_order_scatter(const uint32_t* __restrict__ key, int64_t n,
-                                                                 int64_t slice, int shift,
-                                                                 const int32_t* __restrict__ hist,
-                                                                 int32_t* __restrict__ perm) {
+__global__ __launch_bounds__(ORDER_THREADS) void k_order_scatter(OrderArgs A) {
   __shared__ int32_t cnt[ORDER_BUCKETS];
   __shared__ int32_t wsum[ORDER_THREADS / 64];
   static_assert(ORDER_BUCKETS == 4 * ORDER_THREADS, "four buckets per thread");
+  int blk;
+  const OrderProb& P = order_prob(A, blk);
   // buckets 4i..4i+3: totals over every slice, and the counts of the slices before this one
   int4 tot = make_int4(0, 0, 0, 0), pre = make_int4(0, 0, 0, 0);
-  for (int w = 0; w < (int)gridDim.x; w++) {
-    const int4 h = reinterpret_cast<const int4*>(hist + (int64_t)w * ORDER_BUCKETS)[threadIdx.x];
+  for (int w = 0; w < P.nslices; w++) {
+    const int4 h = reinterpret_cast<const int4*>(P.hist + (int64_t)w * ORDER_BUCKETS)[threadIdx.x];
     tot.x += h.x; tot.y += h.y; tot.z += h.z; tot.w += h.w;
-    if (w < (int)blockIdx.x) { pre.x += h.x; pre.y += h.y; pre.z += h.z; pre.w += h.w; }
+    if (w < blk) { pre.x += h.x; pre.y += h.y; pre.z += h.z; pre.w += h.w; }
   }
   const int32_t s = tot.x + tot.y + tot.z + tot.w;
   const int32_t inc = wave_incl_sum(s);
@@ -654,9 +665,9 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_scatter(const uint32_t*
   cnt[i4 + 2] = off + tot.x + tot.y + pre.z;
   cnt[i4 + 3] = off + tot.x + tot.y + tot.z + pre.w;
   __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * slice, t1 = min(n, t0 + slice);
+  const int64_t t0 = (int64_t)blk * P.slice, t1 = min(P.n, t0 + P.slice);
   for (int64_t t = t0 + threadIdx.x; t < t1; t += ORDER_THREADS)
-    perm[atomicAdd(&cnt[order_bucket(key[t], shift)], 1)] = (int32_t)t;
+    P.perm[atomicAdd(&cnt[order_bucket(P.key[t], P.shift)], 1)] = make_int2((int32_t)t, P.tile_job[t]);
 }
 
 #ifndef YRWI_PROBE_LDS
@@ -739,7 +750,8 @@ __device__ __forceinline__ bool probe_heads(const DList& Lg, int64_t lo, int64_t
 
 __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
                              int64_t tile0, int64_t ntiles, ProbeDesc* __restrict__ pdesc,
-                             uint32_t* __restrict__ tile_key) {
+                             uint32_t* __restrict__ tile_key, int32_t* __restrict__ tile_job,
+                             uint32_t* __restrict__ probe_key, int probe_shift) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
@@ -749,6 +761,9 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const int64_t s0 = (tile0 + t - tile_base[j]) * J.ptile;
   const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
   if (tile_key) tile_key[tile0 + t] = Sm.uid[s0];  // url id the tile starts at (k_order_hist / k_order_scatter)
+  if (tile_job) tile_job[tile0 + t] = j;
+  if (probe_key)  // (large list, 16 bands): k_probe's order
+    probe_key[t] = (uint32_t)min(J.lgroup, 255) << 4 | min(Sm.uid[s0] >> probe_shift, 15u);
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
@@ -786,12 +801,12 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
-                                                     int mark) {
+                                                     int mark, const int2* __restrict__ perm) {
   __shared__ int32_t sScan[4];
 #if PROBE_LDS > 0
   __shared__ uint32_t sL[PROBE_LDS];
 #endif
-  const int64_t t = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t t = perm ? (int64_t)perm[xcd_slice(blockIdx.x, gridDim.x)].x : xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t b = tile0 + t;
   const ProbeDesc D = pdesc[t];
   const JoinQ& J = jobs[D.job];
@@ -1052,7 +1067,8 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const int64_t* __restrict__ tile_src,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off,
-                                                 const int32_t* __restrict__ perm) {
+                                                 const int2* __restrict__ perm,
+                                                 const int32_t* __restrict__ tile_job) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
   // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
@@ -1061,10 +1077,19 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     const int64_t p = p0 + threadIdx.x;
     int32_t c = 0;
     if (threadIdx.x < COMPACT_TILES && p < ntiles) {
-      const int64_t t = perm ? (int64_t)perm[p] : p;
+      // tile and job: one load in band order (k_order_scatter packs them)
+      int64_t t = p;
+      int j;
+      if (perm) {
+        const int2 tj = perm[p];
+        t = tj.x;
+        j = tj.y;
+      } else {
+        j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+      }
       c = tile_cnt[t];
       if (c) {
-        const JoinQ& J = jobs[find_job(tile_base, njobs, t)];
+        const JoinQ& J = jobs[j];
         CompactJob& X = sJ[threadIdx.x];
         X.af = J.A.feat;
         X.bf = J.B.feat;
@@ -3137,9 +3162,12 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* evm, void* ev1, void* evc0, void* evc1) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
-  // band order of the tiles for k_compact (k_order_hist / k_order_scatter)
-  int32_t* perm = bo.key && !mark ? bo.perm : nullptr;
+  // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
+  int2* perm = bo.key && bo.tile_job && !mark ? bo.perm : nullptr;
+  int2* pperm = bo.pkey && bo.tile_job && probe_tiles > 1 ? bo.pperm : nullptr;
   uint32_t* tkey = perm ? bo.key : nullptr;
+  uint32_t* pkey = pperm ? bo.pkey : nullptr;
+  int32_t* tjob = bo.tile_job;
   static int join_grid = 0;  // resident k_join workgroups on the whole device
   if (!join_grid) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -3152,18 +3180,31 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   }
   if (merge_tiles > 0) {
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src, tkey);
+                       d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src, tkey, tjob);
     if (!mark) hipLaunchKernelGGL(k_scan_bounds, dim3((unsigned)nmerge), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_src);
   }
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                       d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc, tkey);
-  if (perm) {
-    const int64_t slice = (total_tiles + bo.nslices - 1) / bo.nslices;
-    hipLaunchKernelGGL(k_order_hist, dim3((unsigned)bo.nslices), dim3(ORDER_THREADS), 0, S(st), tkey, total_tiles,
-                       slice, bo.shift, bo.hist);
-    hipLaunchKernelGGL(k_order_scatter, dim3((unsigned)bo.nslices), dim3(ORDER_THREADS), 0, S(st), tkey,
-                       total_tiles, slice, bo.shift, (const int32_t*)bo.hist, perm);
+                       d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc, tkey, tjob, pkey, bo.pshift);
+  if (perm || pperm) {
+    OrderArgs oa{};
+    int nb = 0;
+    auto prob = [&](int i, const uint32_t* key, int64_t n, int shift, const int32_t* job, int2* out) {
+      OrderProb& P = oa.p[i];
+      P.key = key;
+      P.n = n;
+      P.nslices = (int32_t)std::min<int64_t>(64, (n + ORDER_SLICE_MIN - 1) / ORDER_SLICE_MIN);
+      P.slice = (n + P.nslices - 1) / P.nslices;
+      P.shift = shift;
+      P.tile_job = job;
+      P.perm = out;
+      P.hist = bo.hist + (int64_t)nb * ORDER_BUCKETS;
+      nb += P.nslices;
+    };
+    if (perm) prob(0, tkey, total_tiles, bo.shift, tjob, perm);
+    if (pperm) prob(perm ? 1 : 0, pkey, probe_tiles, 0, tjob + merge_tiles, pperm);
+    hipLaunchKernelGGL(k_order_hist, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
+    hipLaunchKernelGGL(k_order_scatter, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
   }
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
@@ -3172,7 +3213,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0, (const int2*)pperm);
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
@@ -3180,7 +3221,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
                        S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
-                       d_tile_off, (const int32_t*)perm);
+                       d_tile_off, (const int2*)perm, (const int32_t*)tjob);
     if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
   }
   return rc(hipGetLastError());
