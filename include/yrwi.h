@@ -201,7 +201,9 @@ int64_t yrwi_realloc_events(void);
  * `rank` of `world` processes / threads sharing group id `id` runs `nparts`
  * batch parts of `ncalls` exchanges each, vectors of n values (rank + part +
  * call + i), and checks every sum.  0 when all sums are right; YRWI_E_RCCL on a
- * wrong sum or a peer that never arrives; 1 when the mailbox is unavailable. */
+ * wrong sum or a peer that never arrives; 1 when the mailbox is unavailable.
+ * n < 0 (vectors of -n values): the last rank's first part fails and aborts the
+ * mailbox, as a failing batch part does; the others return YRWI_E_RCCL at once. */
 int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, int64_t nparts, int32_t ncalls, int64_t n);
 
 /* ---- YaCy on-disk index ---- */

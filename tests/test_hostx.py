@@ -34,6 +34,24 @@ def test_hostx_processes(world, nparts, ncalls, n):
     assert after <= before  # rank 0 unlinked the mailbox
 
 
+def test_hostx_failed_part_fails_peers_fast():
+    """A rank whose batch part fails aborts the mailbox (run_batch_part): its peers'
+    exchanges fail at once instead of spinning for the whole timeout (60 s)."""
+    import time
+    uid = b"YRWI-HOSTX-TEST" + os.urandom(113)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    t0 = time.time()
+    ps = [ctx.Process(target=_rank, args=(uid, 3, r, 4, 2, -100, 0.3 if r == 2 else 0.0, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: -6, 1: -6, 2: -6}, res  # YRWI_E_RCCL everywhere
+    assert time.time() - t0 < 30
+
+
 def test_hostx_oversized_vector_not_handled():
     """Vectors longer than the mailbox's slots fall back to the device all-gather."""
     from yacy_search_server_amd import _lib

@@ -164,10 +164,13 @@ struct HxSlot {
 };
 }  // namespace
 
-// segment header: ranks that mapped it (the last of `world` unlinks the name)
+// segment header: ranks that mapped it (the last of `world` unlinks the name);
+// aborted: a rank's batch part failed, every wait of every rank gives up at once
+// (its peers would otherwise each hold a core for the whole timeout per exchange)
 struct HxHead {
   std::atomic<int32_t> attached;
-  char pad[60];
+  std::atomic<int32_t> aborted;
+  char pad[56];
 };
 
 struct HostX {
@@ -217,6 +220,10 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank) {
 
 int hostx_attached(const HostX* x) { return x ? x->head()->attached.load(std::memory_order_acquire) : 0; }
 
+void hostx_abort(HostX* x) {
+  if (x) x->head()->aborted.store(1, std::memory_order_release);
+}
+
 void hostx_close(HostX* x, bool unlink_name) {
   if (!x) return;
   munmap(x->base, x->bytes);
@@ -227,11 +234,12 @@ void hostx_close(HostX* x, bool unlink_name) {
 // spin, then yield; false after YRWI_HOSTX_TIMEOUT_S (default 60 s: a peer that
 // never arrives fails the batch instead of hanging it)
 template <class F>
-static bool hx_wait(F ready) {
+static bool hx_wait(const HostX* x, F ready) {
   static const double limit_s = getenv("YRWI_HOSTX_TIMEOUT_S") ? atof(getenv("YRWI_HOSTX_TIMEOUT_S")) : 60.0;
   const auto t0 = std::chrono::steady_clock::now();
   for (int64_t i = 0;; i++) {
     if (ready()) return true;
+    if (x->head()->aborted.load(std::memory_order_acquire)) return false;
     if (i < 2000) {
       __builtin_ia32_pause();
       continue;
@@ -251,19 +259,21 @@ int hostx_allsum(Lane* L, std::vector<int64_t>& v) {
   const int si = (int)(key % HX_SLOTS);
   HxSlot* S = x->slot(si);
   // claim (or join) the slot for this key
-  if (!hx_wait([&] {
+  if (!hx_wait(x, [&] {
         int64_t cur = S->owner.load(std::memory_order_acquire);
         if (cur == key + 1) return true;
         if (cur != 0) return false;
         return S->owner.compare_exchange_strong(cur, key + 1, std::memory_order_acq_rel) || cur == key + 1;
       }))
-    return L->fail(YRWI_E_RCCL, "host exchange: slot never freed");
+    return L->fail(YRWI_E_RCCL, x->head()->aborted.load() ? "host exchange: a peer's batch failed"
+                                                          : "host exchange: slot never freed");
   HxEntry* me = x->entry(si, x->rank);
   me->n = (int64_t)v.size();
   std::memcpy(me->v, v.data(), v.size() * sizeof(int64_t));
   S->nwritten.fetch_add(1, std::memory_order_acq_rel);
-  if (!hx_wait([&] { return S->nwritten.load(std::memory_order_acquire) == x->world; }))
-    return L->fail(YRWI_E_RCCL, "host exchange: a rank never arrived");
+  if (!hx_wait(x, [&] { return S->nwritten.load(std::memory_order_acquire) == x->world; }))
+    return L->fail(YRWI_E_RCCL, x->head()->aborted.load() ? "host exchange: a peer's batch failed"
+                                                          : "host exchange: a rank never arrived");
   std::vector<int64_t> sum(v.size(), 0);
   for (int r = 0; r < x->world; r++) {
     const HxEntry* e = x->entry(si, r);
@@ -286,6 +296,10 @@ extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, i
   using namespace yrwi;
   HostX* x = hostx_open(id, world, rank);
   if (!x) return 1;
+  // n < 0: the last rank's first batch part fails before its exchanges (it aborts
+  // the mailbox, as run_batch_part does); every other rank must fail fast
+  const bool fail_last = n < 0;
+  if (fail_last) n = -n;
   Lane L;  // host-side state only: no stream, no worker thread
   L.world = world;
   L.rank = rank;
@@ -294,6 +308,11 @@ extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, i
   for (int64_t p = 0; p < nparts && rc == 0; p++) {
     L.seq = p;
     L.xcall = 0;
+    if (fail_last && rank == world - 1) {
+      hostx_abort(x);
+      rc = YRWI_E_RCCL;
+      break;
+    }
     for (int32_t c = 0; c < ncalls && rc == 0; c++) {
       std::vector<int64_t> v((size_t)n);
       for (int64_t i = 0; i < n; i++) v[(size_t)i] = rank + p + c + i;

@@ -1506,6 +1506,7 @@ static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q,
                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   L->enter();
   const int rc = run_batch_part_(ix, L, q, nq, kmax, out, nout, st);
+  if (rc && L->hostx) hostx_abort(L->hostx);  // peers waiting on this part's exchanges fail fast
   turn_release(L);  // error paths, parts without collectives: the turn still passes in order
   L->release_after_final = false;
   L->leave();

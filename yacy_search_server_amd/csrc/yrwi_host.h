@@ -575,6 +575,7 @@ int check_url_ids(CtxBase* ctx, int64_t* bad);
 
 HostX* hostx_open(const uint8_t id[128], int world, int rank);  // nullptr: not available (device fallback)
 void hostx_close(HostX* x, bool unlink_name);
+void hostx_abort(HostX* x);  // a batch part failed: every rank's pending and later exchanges fail at once
 int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)
