@@ -43,12 +43,15 @@ def counters(path):
 
 
 def main(tag, config):
-    base = os.path.join(ROOT, "gpurun_out", "prof", tag)
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    # PROF_BASE: where tools/profile_gpu.sh left the raw output; PROF_OUT: where the
+    # summaries go (on the GPU box: a directory under gpurun_out/, copied into profiles/)
+    base = os.path.join(os.environ.get("PROF_BASE", os.path.join(ROOT, "gpurun_out", "prof")), tag)
+    pout = os.environ.get("PROF_OUT", os.path.join(ROOT, "profiles"))
+    os.makedirs(pout, exist_ok=True)
     stats = find(os.path.join(base, "kt", "**", "*kernel_stats.csv"))
     out = {"tag": tag, "config": config, "kernels": {}}
     if stats:
-        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+        shutil.copy(stats[0], os.path.join(pout, f"{tag}_kernel_stats.csv"))
         for row in csv.DictReader(open(stats[0])):
             k = short(row["Name"])
             out["kernels"].setdefault(k, {})
@@ -85,10 +88,12 @@ def main(tag, config):
         out["path_hbm_bytes_per_batch"] = tot / nb
         out["batches_profiled"] = nb
     import subprocess
-    try:
-        out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
-    except Exception:
-        pass
+    out["head"] = os.environ.get("PROF_HEAD")  # the commit measured (the GPU box has no .git)
+    if not out["head"]:
+        try:
+            out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
+        except Exception:
+            pass
     for name in ("k_compact", "k_join", "k_probe"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
@@ -99,7 +104,7 @@ def main(tag, config):
             for line in open(p):
                 if line.startswith("{") and '"metric"' in line:
                     out.setdefault("bench_lines", {})[log] = json.loads(line)
-    with open(os.path.join(ROOT, "profiles", f"pmc_{config}.json"), "w") as f:
+    with open(os.path.join(pout, f"pmc_{config}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench_lines"}, indent=1))
 

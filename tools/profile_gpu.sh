@@ -5,14 +5,16 @@
 #   pass 3: --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum         -> write requests (64 B, the rest 32 B)
 # Each counter pass is its own run (MI355X_MICROARCH.md, HBM / rocprofv3).  Request
 # sizes are counted exactly, so no FETCH_SIZE correction is needed: on this path the
-# reads are 128-B requests (gathers and streams alike).  Outputs under
-# gpurun_out/prof/<tag>/ ; tools/pmc_summary.py turns them into profiles/*.
+# reads are 128-B requests (gathers and streams alike).  Raw rocprofv3 output goes
+# to /tmp/prof/<tag>/ on the box (it is far larger than what gpurun copies back);
+# tools/pmc_summary.py, run right after on the box with PROF_BASE=/tmp/prof and
+# PROF_OUT=gpurun_out/profiles, writes the summaries that are kept.
 set -e
 TAG=${1:-r02}
 shift || true
 ARGS=${@:---steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 --legs none}
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/prof/$TAG
+OUT=/tmp/prof/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $ROOT/bench.py $ARGS > $OUT/kt.log 2>&1
