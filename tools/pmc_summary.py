@@ -23,7 +23,8 @@ def find(pattern):
 
 
 def short(name):
-    for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine",
+    for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
+              "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
               "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
             return k
@@ -76,8 +77,9 @@ def main(tag, config):
             d["hbm_bytes_per_launch"] = d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
     # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
     # (k_combine runs once per batch pass); index build, uploads and fills excluded
-    path = ("k_partition", "k_probe_part", "k_join", "k_probe", "k_scan_tiles", "k_compact", "k_reduce",
-            "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq", "k_emit")
+    path = ("k_partition", "k_probe_part", "k_scan_bounds", "k_order_hist", "k_order_scatter", "k_join", "k_probe",
+            "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
+            "k_emit")
     nb = out["kernels"].get("k_combine", {}).get("calls")
     if nb:
         tot = 0.0
