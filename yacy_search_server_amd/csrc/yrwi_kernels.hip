@@ -103,6 +103,56 @@ __device__ __forceinline__ int find_job(const int64_t* base, int n, T b) {
   return lo;
 }
 
+// Global (address space 1) accesses through device pointers that reach a kernel
+// inside structs (JoinQ, RankQ, LDS copies of them).  Through a generic pointer
+// the compiler emits FLAT instructions, which count in lgkmcnt as well as vmcnt:
+// every LDS wait after such a load also waited for the memory, so a thread's
+// gathers ran one after another (k_score had 483 flat loads, k_compact 60, and a
+// vmcnt(0) wait after nearly each).  Every pointer here is device memory.
+template <class T>
+__device__ __forceinline__ T ldg(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ void stg(T* p, const T& v) {
+  *(__attribute__((address_space(1))) T*)p = v;
+}
+// HIP's vector types are classes: copying one out of an address-space-1 lvalue
+// binds its copy constructor's generic reference (a FLAT load again), so the
+// 16-byte forms go through clang's native vector types
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x3_t __attribute__((ext_vector_type(3)));
+// the J5 inputs of a joined side: word 0 and the low half of word 1 (12 B: a
+// 16-B load whose unused top dword the compiler reused made the next gather wait)
+__device__ __forceinline__ ulonglong2 ldg_j5(const uint64_t* p) {
+  const u32x3_t v = *(const __attribute__((address_space(1))) u32x3_t*)p;
+  return make_ulonglong2((uint64_t)v.y << 32 | v.x, (uint64_t)v.z);
+}
+template <>
+__device__ __forceinline__ ulonglong2 ldg(const ulonglong2* p) {
+  const u64x2_t v = *(const __attribute__((address_space(1))) u64x2_t*)p;
+  return make_ulonglong2(v.x, v.y);
+}
+template <>
+__device__ __forceinline__ uint4 ldg(const uint4* p) {
+  const u32x4_t v = *(const __attribute__((address_space(1))) u32x4_t*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <>
+__device__ __forceinline__ uint2 ldg(const uint2* p) {
+  const u32x2_t v = *(const __attribute__((address_space(1))) u32x2_t*)p;
+  return make_uint2(v.x, v.y);
+}
+template <>
+__device__ __forceinline__ void stg(ulonglong2* p, const ulonglong2& v) {
+  u64x2_t w;
+  w.x = v.x;
+  w.y = v.y;
+  *(__attribute__((address_space(1))) u64x2_t*)p = w;
+}
+
 // wave (64-lane) inclusive scan / reductions
 __device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
   const int lane = threadIdx.x & 63;
@@ -304,7 +354,7 @@ __device__ __forceinline__ Rec rec_of_row(const Row& r) {
 // record loads: every feat array starts 256-B aligned, records are 32 B
 __device__ __forceinline__ Rec load_rec(const uint64_t* f, int64_t e) {
   const ulonglong2* p = reinterpret_cast<const ulonglong2*>(f + e * FEAT_WORDS);
-  const ulonglong2 x = p[0], y = p[1];
+  const ulonglong2 x = ldg(p), y = ldg(p + 1);
   Rec q;
   q.w[0] = x.x;
   q.w[1] = x.y;
@@ -314,8 +364,8 @@ __device__ __forceinline__ Rec load_rec(const uint64_t* f, int64_t e) {
 }
 __device__ __forceinline__ void store_rec(uint64_t* f, int64_t e, const Rec& q) {
   ulonglong2* p = reinterpret_cast<ulonglong2*>(f + e * FEAT_WORDS);
-  p[0] = make_ulonglong2(q.w[0], q.w[1]);
-  p[1] = make_ulonglong2(q.w[2], q.w[3]);
+  stg(p, make_ulonglong2(q.w[0], q.w[1]));
+  stg(p + 1, make_ulonglong2(q.w[2], q.w[3]));
 }
 
 __device__ __forceinline__ Feat decode_rec(const Rec& q) {
@@ -346,12 +396,12 @@ __device__ __forceinline__ Feat decode_rec(const Rec& q) {
 // 72-bit url-hash key of container element e: its own key, or its url id's in the dictionary
 __device__ __forceinline__ void key_at(const RankQ& Q, int64_t e, uint64_t& hi, uint32_t& lo) {
   if (Q.uid) {
-    const uint32_t u = Q.uid[e];
-    hi = Q.dkhi[u];
-    lo = Q.dklo[u];
+    const uint32_t u = ldg(Q.uid + e);
+    hi = ldg(Q.dkhi + u);
+    lo = ldg(Q.dklo + u);
   } else {
-    hi = Q.ekhi[e];
-    lo = Q.eklo[e];
+    hi = ldg(Q.ekhi + e);
+    lo = ldg(Q.eklo + e);
   }
 }
 // url-hash chars 6..11 (the host hash, DigestURL :229-296) = the key's low 36 bits
@@ -541,7 +591,7 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
       for (uint32_t m = mbits; m; m &= m - 1) {
         const int st = __ffs(m) - 1;
         if (mark) {
-          J.removed[a0 + a_at(st)] = 1;
+          stg(J.removed + a0 + a_at(st), (uint8_t)1);
         } else {
           const uint64_t* fa = J.A.feat + (a0 + a_at(st)) * FEAT_WORDS;
           const uint64_t* fb = J.B.feat + (b0 + b_at(st)) * FEAT_WORDS;
@@ -678,7 +728,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_order_scatter(OrderArgs A) {
 __device__ __forceinline__ int64_t lower_bound_uid(const uint32_t* __restrict__ u, int64_t lo, int64_t hi, uint32_t x) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (u[mid] < x) lo = mid + 1; else hi = mid;
+    if (ldg(u + mid) < x) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
@@ -743,7 +793,7 @@ __device__ __forceinline__ bool probe_heads(const DList& Lg, int64_t lo, int64_t
   }
   const int64_t p = lower_bound_uid(Lg.uid, wl, wr, key);
   *jl = p;
-  *hit = p < hi && Lg.uid[p] == key;
+  *hit = p < hi && ldg(Lg.uid + p) == key;
   return true;
 }
 #endif
@@ -760,10 +810,10 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const int64_t s0 = (tile0 + t - tile_base[j]) * J.ptile;
   const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
-  if (tile_key) tile_key[tile0 + t] = Sm.uid[s0];  // url id the tile starts at (k_order_hist / k_order_scatter)
+  if (tile_key) tile_key[tile0 + t] = ldg(Sm.uid + s0);  // url id the tile starts at (k_order_hist / k_order_scatter)
   if (tile_job) tile_job[tile0 + t] = j;
   if (probe_key)  // (large list, 16 bands): k_probe's order
-    probe_key[t] = (uint32_t)min(J.lgroup, 255) << 4 | min(Sm.uid[s0] >> probe_shift, 15u);
+    probe_key[t] = (uint32_t)min(J.lgroup, 255) << 4 | min(ldg(Sm.uid + s0) >> probe_shift, 15u);
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
@@ -772,7 +822,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
     pdesc[t] = D;
     return;
   }
-  const uint32_t k0 = Sm.uid[s0], k1 = Sm.uid[s1 - 1];
+  const uint32_t k0 = ldg(Sm.uid + s0), k1 = ldg(Sm.uid + s1 - 1);
   if (Lg.head) {  // index list: through its line heads (level 2, one level-1 line, one leaf line)
     D.lo = lower_bound_list(Lg, k0);
     D.hi = lower_bound_list(Lg, k1 + 1u);  // ids < 2^32 - 1: k1 + 1 does not wrap
@@ -784,11 +834,11 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   while (lo0 < hi0 || lo1 < hi1) {
     if (lo0 < hi0) {
       const int64_t mid = (lo0 + hi0) >> 1;
-      if (Lg.uid[mid] < k0) lo0 = mid + 1; else hi0 = mid;
+      if (ldg(Lg.uid + mid) < k0) lo0 = mid + 1; else hi0 = mid;
     }
     if (lo1 < hi1) {
       const int64_t mid = (lo1 + hi1) >> 1;
-      if (Lg.uid[mid] <= k1) lo1 = mid + 1; else hi1 = mid;
+      if (ldg(Lg.uid + mid) <= k1) lo1 = mid + 1; else hi1 = mid;
     }
   }
   D.lo = lo0;
@@ -826,20 +876,31 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
         const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
 #pragma unroll
         for (int v = 0; v < KPT / 4; v++) {
-          const uint4 u = q[v];
+          const uint4 u = ldg(q + v);
           keys[4 * v] = u.x; keys[4 * v + 1] = u.y; keys[4 * v + 2] = u.z; keys[4 * v + 3] = u.w;
         }
       } else {
         const uint2* q = reinterpret_cast<const uint2*>(Sm.uid + i0);
 #pragma unroll
         for (int v = 0; v < KPT / 2; v++) {
-          const uint2 u = q[v];
+          const uint2 u = ldg(q + v);
           keys[2 * v] = u.x; keys[2 * v + 1] = u.y;
         }
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < KPT; k++) keys[k] = i0 + k < Sm.n ? Sm.uid[i0 + k] : 0u;
+      for (int k = 0; k < KPT; k++) keys[k] = i0 + k < Sm.n ? ldg(Sm.uid + i0 + k) : 0u;
+    }
+    // every bitmap word of the thread in flight at once: whole 16-B buffer loads
+    // (a plain load was split, its second half loaded only on a hit, and each
+    // key waited for the previous one)
+    const __amdgpu_buffer_rsrc_t rbm =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(Lg.bm), 0, 0x7FFFFFFF, 0x00020000);
+    uint4 E[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const int o = i0 + k < Sm.n ? (int)(keys[k] >> 6) : 0;
+      E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, o * 16, 0, 0));
     }
     uint32_t hm = 0;
     int64_t jls[KPT];
@@ -847,11 +908,11 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     for (int k = 0; k < KPT; k++) {
       jls[k] = 0;
       if (i0 + k >= Sm.n) continue;
-      const ulonglong2 E = reinterpret_cast<const ulonglong2*>(Lg.bm)[keys[k] >> 6];
+      const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
       const uint64_t bit = 1ull << (keys[k] & 63u);
-      if (E.x & bit) {
+      if (ex & bit) {
         hm |= 1u << k;
-        jls[k] = (int64_t)E.y + __popcll(E.x & (bit - 1ull));
+        jls[k] = (int64_t)ey + __popcll(ex & (bit - 1ull));
       }
     }
 #pragma unroll
@@ -859,7 +920,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
       if (!((hm >> k) & 1u)) continue;
       const int64_t ia = J.small_is_A ? i0 + k : jls[k], ib = J.small_is_A ? jls[k] : i0 + k;
       if (mark) {
-        J.removed[ia] = 1;
+        stg(J.removed + ia, (uint8_t)1);
       } else if (J.maxd < 65535 &&
                  joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) {
         hm &= ~(1u << k);
@@ -895,7 +956,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     // id instead of the two or three sector gathers per key of the lower levels
     const uint32_t* __restrict__ g = Lg.uid + D.lo;
     for (int x = threadIdx.x; x < (int)R; x += PROBE_TILE) sL[x] = g[x];
-    if (i < Sm.n) key = Sm.uid[i];
+    if (i < Sm.n) key = ldg(Sm.uid + i);
     __syncthreads();
     if (i < Sm.n) {
       int lo = 0, hi = (int)R;
@@ -912,16 +973,16 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
 #endif
   if (i < Sm.n) {
     // the upper levels of the 256 searches share lines of the range (L2 hits)
-    key = Sm.uid[i];
+    key = ldg(Sm.uid + i);
     jl = lower_bound_uid(Lg.uid, D.lo, D.hi, key);
-    hit = jl < D.hi && Lg.uid[jl] == key;
+    hit = jl < D.hi && ldg(Lg.uid + jl) == key;
   }
   const int64_t ia = J.small_is_A ? i : jl, ib = J.small_is_A ? jl : i;
   if (hit && !mark && J.maxd < 65535) {
     if (joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) hit = false;
   }
   if (mark) {
-    if (hit) J.removed[ia] = 1;
+    if (hit) stg(J.removed + ia, (uint8_t)1);
     return;
   }
   int32_t tot;
@@ -1055,7 +1116,7 @@ __device__ __forceinline__ Rec fold_deferred(const FoldSrc& F, const int32_t* __
     const int64_t e = r[s + 1];
     ulonglong2 b = make_ulonglong2(0, 0);
     if (m == JM_TEST_LARGE_B) acc = load_rec(F.feat[s + 1], e);  // self-join of the larger side
-    else if (m == JM_ENUM) b = *reinterpret_cast<const ulonglong2*>(F.feat[s + 1] + e * FEAT_WORDS);
+    else if (m == JM_ENUM) b = ldg(reinterpret_cast<const ulonglong2*>(F.feat[s + 1] + e * FEAT_WORDS));
     acc = joined_rec(acc, b.x, b.y, m, now_ms);
   }
   return acc;
@@ -1071,6 +1132,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const int32_t* __restrict__ tile_job) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
+  __shared__ int32_t sDefA;
   // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
   const int64_t p0 = (perm ? xcd_slice(blockIdx.x, gridDim.x) : xcd_swizzle(blockIdx.x, gridDim.x)) * COMPACT_TILES;
   if (threadIdx.x < 64) {
@@ -1109,9 +1171,14 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     const int32_t inc = wave_incl_sum(c);
     if (threadIdx.x < COMPACT_TILES) sPre[threadIdx.x + 1] = inc;
     if (threadIdx.x == 0) sPre[0] = 0;
+    // a tile whose accumulated side is deferred (multi-term fold): the general gather path
+    const bool d = threadIdx.x < COMPACT_TILES && c && sJ[threadIdx.x].atw;
+    if (threadIdx.x == 0) sDefA = 0;
+    if (__any(d) && threadIdx.x == 0) sDefA = 1;
   }
   __syncthreads();
   const int32_t total = sPre[COMPACT_TILES];
+  const bool defA = sDefA != 0;
   for (int m0 = threadIdx.x; m0 < total; m0 += COMPACT_UNROLL * 256) {
     int tl[COMPACT_UNROLL];
     int64_t pi[COMPACT_UNROLL];
@@ -1144,25 +1211,48 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       int32_t* dst = X.otup + o * X.otw;
       if (X.atw) {
         const int32_t* srcr = X.atup + (int64_t)pr[u].x * X.atw;
-        for (int j = 0; j < X.atw; j++) dst[j] = srcr[j];
+        for (int j = 0; j < X.atw; j++) stg(dst + j, ldg(srcr + j));
       } else {
-        dst[0] = (int32_t)pr[u].x;
+        stg(dst, (int32_t)pr[u].x);
       }
-      dst[X.otw - 1] = (int32_t)pr[u].y;
-      X.ouid[o] = uid[u];
+      stg(dst + X.otw - 1, (int32_t)pr[u].y);
+      stg(X.ouid + o, uid[u]);
       tl[u] = -1;
     }
     Rec A[COMPACT_UNROLL];
     ulonglong2 B[COMPACT_UNROLL];
+    if (!defA) {
+      // every thread's gathers in flight together, branch-free: one record (the
+      // accumulated side's, or the larger side's in a by-test step) and 16 B of
+      // the joined side (by-test rows: the first half of that same record, an L1
+      // hit); slots without a match read the pair array's first row (conditional
+      // loads made the compiler reuse a pending load's registers, and every slot
+      // then waited for all earlier gathers)
+      const uint64_t* dummy = reinterpret_cast<const uint64_t*>(pairs);
 #pragma unroll
-    for (int u = 0; u < COMPACT_UNROLL; u++) {
-      B[u] = make_ulonglong2(0, 0);
-      if (tl[u] < 0) continue;
-      const CompactJob& X = sJ[tl[u]];
-      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
-      else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
-      else A[u] = load_rec(X.af, pr[u].x);
-      if (X.mode == JM_ENUM) B[u] = *reinterpret_cast<const ulonglong2*>(X.bf + (int64_t)pr[u].y * FEAT_WORDS);
+      for (int u = 0; u < COMPACT_UNROLL; u++) {
+        const bool live = tl[u] >= 0;
+        const CompactJob& X = sJ[live ? tl[u] : 0];
+        const int mode = live ? X.mode : JM_MARK;
+        const bool lg = mode == JM_TEST_LARGE_B, en = mode == JM_ENUM;
+        const uint64_t* af = live ? (lg ? X.bf : X.af) : dummy;
+        const int64_t ar = live ? (int64_t)(lg ? pr[u].y : pr[u].x) : 0;
+        const uint64_t* bf = en ? X.bf : af;
+        const int64_t br = en ? (int64_t)pr[u].y : ar;
+        A[u] = load_rec(af, ar);
+        B[u] = ldg_j5(bf + br * FEAT_WORDS);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < COMPACT_UNROLL; u++) {
+        B[u] = make_ulonglong2(0, 0);
+        if (tl[u] < 0) continue;
+        const CompactJob& X = sJ[tl[u]];
+        if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+        else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
+        else A[u] = load_rec(X.af, pr[u].x);
+        if (X.mode == JM_ENUM) B[u] = ldg(reinterpret_cast<const ulonglong2*>(X.bf + (int64_t)pr[u].y * FEAT_WORDS));
+      }
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
@@ -1170,7 +1260,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       const CompactJob& X = sJ[tl[u]];
       const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
       store_rec(X.ofeat, o, joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
-      X.ouid[o] = uid[u];
+      stg(X.ouid + o, uid[u]);
     }
   }
 }
@@ -1333,7 +1423,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int eo = s * CHUNK_THREADS + (int)threadIdx.x;
     const int64_t e = c * CHUNK + eo;
-    const bool v = e < Q.n && !(Q.removed && Q.removed[e]);
+    const bool v = e < Q.n && !(Q.removed && ldg(Q.removed + e));
     av[s] = -1;
     uint32_t po = 0;
     if (v) {
@@ -1643,11 +1733,11 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
   const int64_t e0 = c * CHUNK, e1 = min((int64_t)(c + 1) * CHUNK, Q.n);
   for (int64_t b = e0; b < e1; b += 64) {
     const int64_t e = b + lane;
-    bool ok = e < e1 && e > first && !(Q.removed && Q.removed[e]);
+    bool ok = e < e1 && e > first && !(Q.removed && ldg(Q.removed + e));
     int32_t p = -1, od = 0;
     if (ok) {
-      p = (int32_t)(Q.feat[e * FEAT_WORDS] & 0xFFFF);
-      od = (int32_t)((Q.feat[e * FEAT_WORDS + 1] >> 16) & 0xFF);
+      p = (int32_t)(ldg(Q.feat + e * FEAT_WORDS) & 0xFFFF);
+      od = (int32_t)((ldg(Q.feat + e * FEAT_WORDS + 1) >> 16) & 0xFF);
     }
     if (__all(!ok || p <= L.prun)) {
       const int32_t m = wave_max_i(ok ? od : 0);
@@ -1874,9 +1964,9 @@ __global__ void k_combine(const RankQ* __restrict__ qs, int nq, const ShardSum* 
       // exact sequential fold over the whole container
       bool first = true;
       for (int64_t e = 0; e < Q.n; e++) {
-        if (Q.removed && Q.removed[e]) continue;
-        int32_t p = (int32_t)(Q.feat[e * FEAT_WORDS] & 0xFFFF);
-        int32_t od = (int32_t)((Q.feat[e * FEAT_WORDS + 1] >> 16) & 0xFF);
+        if (Q.removed && ldg(Q.removed + e)) continue;
+        int32_t p = (int32_t)(ldg(Q.feat + e * FEAT_WORDS) & 0xFFFF);
+        int32_t od = (int32_t)((ldg(Q.feat + e * FEAT_WORDS + 1) >> 16) & 0xFF);
         if (first) { fd.P = p; first = false; }
         else fd.piece(p, od, od);
       }
@@ -2368,7 +2458,7 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
       e = c * CHUNK + idx[i];
     } else {
       e = c * CHUNK + i;
-      if (e >= Q.n || (Q.removed && Q.removed[e])) continue;
+      if (e >= Q.n || (Q.removed && ldg(Q.removed + e))) continue;
     }
     const Rec q = load_rec(Q.feat, e);
     uint64_t khi = 0;
@@ -2409,8 +2499,8 @@ __device__ __forceinline__ int32_t prune_chunk(const RankQ& Q, const NormState& 
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int i = s * CHUNK_THREADS + (int)threadIdx.x;  // coalesced; the order of idx does not matter
     const int64_t e = c * CHUNK + i;
-    if (e >= Q.n || (Q.removed && Q.removed[e])) continue;
-    const ulonglong2 w23 = reinterpret_cast<const ulonglong2*>(Q.feat + e * FEAT_WORDS)[1];
+    if (e >= Q.n || (Q.removed && ldg(Q.removed + e))) continue;
+    const ulonglong2 w23 = ldg(reinterpret_cast<const ulonglong2*>(Q.feat + e * FEAT_WORDS) + 1);
     Rec q;
     q.w[0] = q.w[1] = 0;
     q.w[2] = w23.x;
@@ -2559,7 +2649,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
       if ((vm >> s) & 1u) {
         const int i = s * CHUNK_THREADS + tid;
         const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-        const uint32_t h = (uint32_t)Q.feat[e * FEAT_WORDS + 3];  // ByteArray.hashCode (ByteArray.java:80-84)
+        const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
         out[voff].k1 = a[s];
         out[voff].k2 = ((uint64_t)(h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
         voff++;
@@ -2583,7 +2673,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (((vm >> s) & 1u) && a[s] >= T) {
       const int i = s * CHUNK_THREADS + tid;
       const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-      const uint32_t h = (uint32_t)Q.feat[e * FEAT_WORDS + 3];  // ByteArray.hashCode (ByteArray.java:80-84)
+      const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       off++;
