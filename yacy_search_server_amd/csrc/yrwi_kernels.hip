@@ -1419,15 +1419,34 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   int32_t hmax = 0;  // largest host count this thread saw (one atomicMax per wave below)
   int32_t tcn = -1, tdn = 1, tcx = -1, tdx = 1;  // tf min / max as fractions (-1: none yet)
   int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
+  // RED_GROUP elements at a time: their exclusion marks, then their records, all
+  // in flight together (in bounds whatever the element: the last row stands in
+  // past the end), so a thread waits for memory twice per group, not per element
+  constexpr int RED_GROUP = 4;
+  bool vg[RED_GROUP];
+  Rec rg[RED_GROUP];
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int eo = s * CHUNK_THREADS + (int)threadIdx.x;
     const int64_t e = c * CHUNK + eo;
-    const bool v = e < Q.n && !(Q.removed && ldg(Q.removed + e));
+    if (s % RED_GROUP == 0) {
+#pragma unroll
+      for (int u = 0; u < RED_GROUP; u++) vg[u] = e + (int64_t)u * CHUNK_THREADS < Q.n;
+      uint8_t mk[RED_GROUP];
+#pragma unroll
+      for (int u = 0; u < RED_GROUP; u++) {
+        const int64_t eu = min(e + (int64_t)u * CHUNK_THREADS, Q.n - 1);
+        mk[u] = Q.removed ? ldg(Q.removed + eu) : (uint8_t)0;
+        rg[u] = load_rec(Q.feat, eu);
+      }
+#pragma unroll
+      for (int u = 0; u < RED_GROUP; u++) vg[u] = vg[u] & (mk[u] == 0);
+    }
+    const bool v = vg[s % RED_GROUP];
     av[s] = -1;
     uint32_t po = 0;
     if (v) {
-      const Feat F = decode_rec(load_rec(Q.feat, e));
+      const Feat F = decode_rec(rg[s % RED_GROUP]);
 #pragma unroll
       for (int j = 0; j < NP2; j++) {
         const uint32_t w = (uint32_t)F.f[2 * j] | (2 * j + 1 < NF ? (uint32_t)F.f[2 * j + 1] << 16 : 0u);
