@@ -189,6 +189,27 @@ __device__ __forceinline__ int32_t block_excl_sum256(int32_t v, int32_t* sh /*4*
   *tot = all;
   return off + inc - v;
 }
+// the same for 64-bit sums (packed counters)
+__device__ __forceinline__ uint64_t block_excl_sum256_u64(uint64_t v, uint64_t* sh /*4*/, uint64_t* tot) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  uint64_t off = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i < wv) off += sh[i];
+    all += sh[i];
+  }
+  __syncthreads();
+  *tot = all;
+  return off + inc - v;
+}
 __device__ __forceinline__ int32_t block_excl_max256(int32_t v, int32_t* sh /*4*/) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int32_t inc = wave_incl_max(v);
@@ -853,6 +874,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
                                                      int mark, const int2* __restrict__ perm) {
   __shared__ int32_t sScan[4];
+  __shared__ uint64_t sScan64[4];
 #if PROBE_LDS > 0
   __shared__ uint32_t sL[PROBE_LDS];
 #endif
@@ -865,49 +887,31 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   if (Lg.bm) {
     // url-id bitmap of the large list: one 16-B load per key gives membership and,
     // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
-    // small-list ids per tile, 8 consecutive ones per thread (hits stay in order).
+    // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
+    // one load instruction's 64 lanes read 64 consecutive small-list ids and their
+    // bitmap words fall into a few 128-B lines (thread-consecutive keys spread an
+    // instruction over up to 64 lines: C2 k_probe 123 -> 114 us)
     constexpr int KPT = BM_TILE / PROBE_TILE;
-    static_assert(KPT % 2 == 0 && KPT <= 32, "bitmap tile: whole uint2 / uint4 loads, one hit bit per key");
+    static_assert(KPT <= 4, "bitmap tile: one 16-bit prefix field per key slot");
     const int64_t s0 = (b - tile_base[D.job]) * BM_TILE;
-    const int64_t i0 = s0 + (int64_t)threadIdx.x * KPT;
-    uint32_t keys[KPT];
-    if (i0 + KPT <= Sm.n) {
-      if constexpr (KPT % 4 == 0) {
-        const uint4* q = reinterpret_cast<const uint4*>(Sm.uid + i0);
-#pragma unroll
-        for (int v = 0; v < KPT / 4; v++) {
-          const uint4 u = ldg(q + v);
-          keys[4 * v] = u.x; keys[4 * v + 1] = u.y; keys[4 * v + 2] = u.z; keys[4 * v + 3] = u.w;
-        }
-      } else {
-        const uint2* q = reinterpret_cast<const uint2*>(Sm.uid + i0);
-#pragma unroll
-        for (int v = 0; v < KPT / 2; v++) {
-          const uint2 u = ldg(q + v);
-          keys[2 * v] = u.x; keys[2 * v + 1] = u.y;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < KPT; k++) keys[k] = i0 + k < Sm.n ? ldg(Sm.uid + i0 + k) : 0u;
-    }
-    // every bitmap word of the thread in flight at once: whole 16-B buffer loads
-    // (a plain load was split, its second half loaded only on a hit, and each
-    // key waited for the previous one)
     const __amdgpu_buffer_rsrc_t rbm =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(Lg.bm), 0, 0x7FFFFFFF, 0x00020000);
+    uint32_t keys[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) keys[k] = ldg(Sm.uid + min(s0 + k * PROBE_TILE + (int64_t)threadIdx.x, Sm.n - 1));
+    // every bitmap word of the thread in flight at once: whole 16-B buffer loads
+    // (a plain load was split, its second half loaded only on a hit, and each key
+    // waited for the previous one)
     uint4 E[KPT];
 #pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      const int o = i0 + k < Sm.n ? (int)(keys[k] >> 6) : 0;
-      E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, o * 16, 0, 0));
-    }
+    for (int k = 0; k < KPT; k++)
+      E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(keys[k] >> 6) * 16, 0, 0));
     uint32_t hm = 0;
     int64_t jls[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
       jls[k] = 0;
-      if (i0 + k >= Sm.n) continue;
+      if (s0 + k * PROBE_TILE + (int64_t)threadIdx.x >= Sm.n) continue;
       const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
       const uint64_t bit = 1ull << (keys[k] & 63u);
       if (ex & bit) {
@@ -918,7 +922,8 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
       if (!((hm >> k) & 1u)) continue;
-      const int64_t ia = J.small_is_A ? i0 + k : jls[k], ib = J.small_is_A ? jls[k] : i0 + k;
+      const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
+      const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
       if (mark) {
         stg(J.removed + ia, (uint8_t)1);
       } else if (J.maxd < 65535 &&
@@ -927,20 +932,33 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
       }
     }
     if (mark) return;
-    int32_t tot;
-    int32_t off = block_excl_sum256(__popc(hm), sScan, &tot);
+    // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
+    // of four 16-bit per-slot counts gives every hit's place in its slot
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; k++) cnt |= (uint64_t)((hm >> k) & 1u) << (16 * k);
+    uint64_t tot64;
+    const uint64_t ex = block_excl_sum256_u64(cnt, sScan64, &tot64);
     const int64_t src = J.pair_base + s0;  // BM_TILE pair slots per tile
+    int32_t base[KPT];
+    int32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      base[k] = run;
+      run += (int32_t)((tot64 >> (16 * k)) & 0xFFFFu);
+    }
     if (threadIdx.x == 0) {
       tile_src[b] = src;
-      tile_cnt[b] = tot;
+      tile_cnt[b] = run;
     }
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
       if (!((hm >> k) & 1u)) continue;
-      const int64_t ia = J.small_is_A ? i0 + k : jls[k], ib = J.small_is_A ? jls[k] : i0 + k;
-      pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
-      pair_uid[src + off] = keys[k];
-      off++;
+      const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
+      const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
+      const int64_t o = src + base[k] + (int64_t)((ex >> (16 * k)) & 0xFFFFu);
+      pairs[o] = make_uint2((uint32_t)ia, (uint32_t)ib);
+      pair_uid[o] = keys[k];
     }
     return;
   }
