@@ -5,7 +5,8 @@ set -e
 TAG=${1:-k}
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kst -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 --legs none > /tmp/kst.log 2>&1
+rm -rf /tmp/kst
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kst -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --latency 0 --inflight 1 --legs none $KARGS > /tmp/kst.log 2>&1
 python3 - "$R/gpurun_out/${TAG}_kstats.txt" <<'PY'
 import csv, glob, sys
 f = glob.glob("/tmp/kst/**/*kernel_stats.csv", recursive=True)[0]

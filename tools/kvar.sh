@@ -2,6 +2,7 @@
 # Kernel stats of library variants: for each NAME=LIB[:ENV=VAL] one isolated
 # rocprofv3 kernel-stats run (tools/kstats.sh) and the headline bench line.
 #   bash tools/kvar.sh cur=cur base=cur:YRWI_BAND_ORDER=0 ct2=gpurun_var/libyrwi_ct2.so
+# KARGS: extra bench.py arguments for both runs (e.g. the C3 workload)
 set -o pipefail
 R=$(pwd)
 mkdir -p gpurun_out/kvar
@@ -11,7 +12,7 @@ for nv in "$@"; do
   ( if [ "$p" = cur ]; then unset YRWI_LIB; else export YRWI_LIB=$R/$p; fi
     [ -n "$e" ] && export "$e"
     bash tools/kstats.sh kv_$n || exit 1
-    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu --latency 0 --legs none > gpurun_out/kvar/$n.json 2> gpurun_out/kvar/$n.err || exit 1
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 16 --no-cpu --latency 0 --legs none $KARGS > gpurun_out/kvar/$n.json 2> gpurun_out/kvar/$n.err || exit 1
   ) || exit 1
   mv gpurun_out/kv_${n}_kstats.txt gpurun_out/kvar/
   python3 - $n <<'PY'

@@ -1150,7 +1150,6 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const int32_t* __restrict__ tile_job) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
-  __shared__ int32_t sDefA;
   // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
   const int64_t p0 = (perm ? xcd_slice(blockIdx.x, gridDim.x) : xcd_swizzle(blockIdx.x, gridDim.x)) * COMPACT_TILES;
   if (threadIdx.x < 64) {
@@ -1189,14 +1188,9 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     const int32_t inc = wave_incl_sum(c);
     if (threadIdx.x < COMPACT_TILES) sPre[threadIdx.x + 1] = inc;
     if (threadIdx.x == 0) sPre[0] = 0;
-    // a tile whose accumulated side is deferred (multi-term fold): the general gather path
-    const bool d = threadIdx.x < COMPACT_TILES && c && sJ[threadIdx.x].atw;
-    if (threadIdx.x == 0) sDefA = 0;
-    if (__any(d) && threadIdx.x == 0) sDefA = 1;
   }
   __syncthreads();
   const int32_t total = sPre[COMPACT_TILES];
-  const bool defA = sDefA != 0;
   for (int m0 = threadIdx.x; m0 < total; m0 += COMPACT_UNROLL * 256) {
     int tl[COMPACT_UNROLL];
     int64_t pi[COMPACT_UNROLL];
@@ -1239,38 +1233,21 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
     }
     Rec A[COMPACT_UNROLL];
     ulonglong2 B[COMPACT_UNROLL];
-    if (!defA) {
-      // every thread's gathers in flight together, branch-free: one record (the
-      // accumulated side's, or the larger side's in a by-test step) and 16 B of
-      // the joined side (by-test rows: the first half of that same record, an L1
-      // hit); slots without a match read the pair array's first row (conditional
-      // loads made the compiler reuse a pending load's registers, and every slot
-      // then waited for all earlier gathers)
-      const uint64_t* dummy = reinterpret_cast<const uint64_t*>(pairs);
+    // one record (the accumulated side's; a by-test step's larger side's; a
+    // deferred side's fold) and the joined side's 12 J5 bytes per match, the
+    // gathers of all COMPACT_UNROLL matches in flight together (a 16-B load of the
+    // joined side left its top dword dead, the compiler reused that register and
+    // the next gather waited; a second, branch-free loop for steps without
+    // deferred sides cost 4-10 %: more registers for both)
 #pragma unroll
-      for (int u = 0; u < COMPACT_UNROLL; u++) {
-        const bool live = tl[u] >= 0;
-        const CompactJob& X = sJ[live ? tl[u] : 0];
-        const int mode = live ? X.mode : JM_MARK;
-        const bool lg = mode == JM_TEST_LARGE_B, en = mode == JM_ENUM;
-        const uint64_t* af = live ? (lg ? X.bf : X.af) : dummy;
-        const int64_t ar = live ? (int64_t)(lg ? pr[u].y : pr[u].x) : 0;
-        const uint64_t* bf = en ? X.bf : af;
-        const int64_t br = en ? (int64_t)pr[u].y : ar;
-        A[u] = load_rec(af, ar);
-        B[u] = ldg_j5(bf + br * FEAT_WORDS);
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < COMPACT_UNROLL; u++) {
-        B[u] = make_ulonglong2(0, 0);
-        if (tl[u] < 0) continue;
-        const CompactJob& X = sJ[tl[u]];
-        if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
-        else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
-        else A[u] = load_rec(X.af, pr[u].x);
-        if (X.mode == JM_ENUM) B[u] = ldg(reinterpret_cast<const ulonglong2*>(X.bf + (int64_t)pr[u].y * FEAT_WORDS));
-      }
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      B[u] = make_ulonglong2(0, 0);
+      if (tl[u] < 0) continue;
+      const CompactJob& X = sJ[tl[u]];
+      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+      else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
+      else A[u] = load_rec(X.af, pr[u].x);
+      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * FEAT_WORDS);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
