@@ -705,7 +705,8 @@ static void span_close(Lane* L, Timing* tm, hipEvent_t b) {
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
 static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vector<int>& owner, std::vector<int64_t>& tile_base,
-                        int* nmerge, int64_t* merge_tiles, int64_t* tiles) {
+                        int* nmerge, int64_t* merge_tiles, int64_t* tiles, bool* long_tiles) {
+  *long_tiles = false;
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
     JoinQ& J = jobs[i];
@@ -715,7 +716,12 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
     // probed at any ratio (the small side's ids stream, the bitmap stays in L2)
     const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
     J.algo = (bm || nl > probe_ratio * ns) ? JA_PROBE : JA_MERGE;
-    J.ptile = bm ? BM_TILE : PROBE_TILE;
+    // long bitmap tiles only where no record is gathered per match (a deferred
+    // step writes sources, an exclusion marks): a final step's compaction keeps
+    // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
+    const bool light = J.out_tup != nullptr || J.mode == JM_MARK;
+    J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
+    if (J.ptile == KPT_LARGE * PROBE_TILE) *long_tiles = true;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
     order[i] = i;
   }
@@ -793,7 +799,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   int64_t merge_tiles, tiles;
   static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
   const int64_t h0 = hprof ? now_ns() : 0;
-  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+  bool long_tiles;
+  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
@@ -838,7 +845,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   hipEvent_t sp = span_open(ctx, tm);
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
-                       false, bo,
+                       false, long_tiles, bo,
                        ctx->stream, e0, em, e1, c0, c1))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
@@ -900,7 +907,8 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   if (jobs.empty()) return 0;
   int nmerge;
   int64_t merge_tiles, tiles;
-  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles);
+  bool long_tiles;
+  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   if (st)
     for (const JoinQ& J : jobs) st->bytes_alg_capped += std::min<int64_t>(12 * J.B.n, loaded_bytes(J));
@@ -913,7 +921,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, false);
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, true, bo,
+                       nullptr, true, long_tiles, bo,
                        ctx->stream, nullptr, nullptr, nullptr))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
   span_close(ctx, tm, sp);

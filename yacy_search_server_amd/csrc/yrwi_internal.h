@@ -90,7 +90,9 @@ constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
 #ifndef YRWI_BM_TILE
 #define YRWI_BM_TILE 1024
 #endif
-constexpr int BM_TILE = YRWI_BM_TILE;  // small-list elements per bitmap-probe workgroup (4 per thread; 2048: probe 168 -> 198 us on C2, 4096: 243)
+constexpr int BM_TILE = YRWI_BM_TILE;  // small-list elements per bitmap-probe workgroup (4 per thread; 512: C2 probe 111 -> 150 us)
+constexpr int KPT_LARGE = 8;           // ids per thread of a bitmap probe whose small side is long
+constexpr int64_t BM_LARGE_MIN = 1 << 18;  // small-side ids from which a bitmap job takes KPT_LARGE
 
 // The lists of a multi-term fold and the join mode of each step, for the last
 // step's k_compact: it folds the deferred rows' records (J5/J6 step by step,
@@ -311,7 +313,8 @@ struct OrderArgs {
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src,
-                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, const BandOrder& bo, void* stream,
+                     int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
+                     void* stream,
                      void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,

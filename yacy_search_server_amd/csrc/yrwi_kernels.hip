@@ -867,6 +867,98 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   pdesc[t] = D;
 }
 
+// Bitmap probe of one tile (k_probe): KPT small-list ids per thread, KPT * 256 per
+// workgroup.  Deferred and exclusion steps with a small side of at least
+// BM_LARGE_MIN ids take KPT = 8 (fewer, longer workgroups; their compaction
+// gathers nothing: C3 k_probe 265 -> 243 us, k_compact 202 -> 180 with every
+// long job at 8), the others KPT = 4 (a final step's compaction keeps its band
+// order per tile: C2 at 8 took k_probe 111 -> 116 and k_compact 220 -> 237 us).
+template <int KPT>
+__device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, const DList& Lg, int64_t b,
+                                             int64_t tile_base0, uint2* __restrict__ pairs,
+                                             uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
+                                             int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64) {
+  // url-id bitmap of the large list: one 16-B load per key gives membership and,
+  // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
+  // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
+  // one load instruction's 64 lanes read 64 consecutive small-list ids and their
+  // bitmap words fall into a few 128-B lines (thread-consecutive keys spread an
+  // instruction over up to 64 lines: C2 k_probe 123 -> 114 us)
+  static_assert(KPT <= 8, "bitmap tile: one 16-bit prefix field per key slot, four per 64-bit scan");
+  const int64_t s0 = (b - tile_base0) * (KPT * PROBE_TILE);
+  const __amdgpu_buffer_rsrc_t rbm =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(Lg.bm), 0, 0x7FFFFFFF, 0x00020000);
+  uint32_t keys[KPT];
+#pragma unroll
+  for (int k = 0; k < KPT; k++) keys[k] = ldg(Sm.uid + min(s0 + k * PROBE_TILE + (int64_t)threadIdx.x, Sm.n - 1));
+  // every bitmap word of the thread in flight at once: whole 16-B buffer loads
+  // (a plain load was split, its second half loaded only on a hit, and each key
+  // waited for the previous one)
+  uint4 E[KPT];
+#pragma unroll
+  for (int k = 0; k < KPT; k++)
+    E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(keys[k] >> 6) * 16, 0, 0));
+  uint32_t hm = 0;
+  int64_t jls[KPT];
+#pragma unroll
+  for (int k = 0; k < KPT; k++) {
+    jls[k] = 0;
+    if (s0 + k * PROBE_TILE + (int64_t)threadIdx.x >= Sm.n) continue;
+    const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
+    const uint64_t bit = 1ull << (keys[k] & 63u);
+    if (ex & bit) {
+      hm |= 1u << k;
+      jls[k] = (int64_t)ey + __popcll(ex & (bit - 1ull));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; k++) {
+    if (!((hm >> k) & 1u)) continue;
+    const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
+    const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
+    if (mark) {
+      stg(J.removed + ia, (uint8_t)1);
+    } else if (J.maxd < 65535 &&
+               joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) {
+      hm &= ~(1u << k);
+    }
+  }
+  if (mark) return;
+  // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
+  // of four 16-bit per-slot counts gives every hit's place in its slot
+  constexpr int NSC = (KPT + 3) / 4;  // 64-bit scans of four slot counts each
+  uint64_t ex[NSC], tot64[NSC];
+#pragma unroll
+  for (int q = 0; q < NSC; q++) {
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int k = 4 * q; k < KPT && k < 4 * q + 4; k++) cnt |= (uint64_t)((hm >> k) & 1u) << (16 * (k - 4 * q));
+    ex[q] = block_excl_sum256_u64(cnt, sScan64, &tot64[q]);
+  }
+  const int64_t src = J.pair_base + s0;  // KPT * PROBE_TILE pair slots per tile
+  int32_t base[KPT];
+  int32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < KPT; k++) {
+    base[k] = run;
+    run += (int32_t)((tot64[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+  }
+  if (threadIdx.x == 0) {
+    tile_src[b] = src;
+    tile_cnt[b] = run;
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; k++) {
+    if (!((hm >> k) & 1u)) continue;
+    const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
+    const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
+    const int64_t o = src + base[k] + (int64_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+    pairs[o] = make_uint2((uint32_t)ia, (uint32_t)ib);
+    pair_uid[o] = keys[k];
+  }
+}
+
+template <bool LONG>
 __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
@@ -885,81 +977,13 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
   if (Lg.bm) {
-    // url-id bitmap of the large list: one 16-B load per key gives membership and,
-    // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
-    // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
-    // one load instruction's 64 lanes read 64 consecutive small-list ids and their
-    // bitmap words fall into a few 128-B lines (thread-consecutive keys spread an
-    // instruction over up to 64 lines: C2 k_probe 123 -> 114 us)
-    constexpr int KPT = BM_TILE / PROBE_TILE;
-    static_assert(KPT <= 4, "bitmap tile: one 16-bit prefix field per key slot");
-    const int64_t s0 = (b - tile_base[D.job]) * BM_TILE;
-    const __amdgpu_buffer_rsrc_t rbm =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(Lg.bm), 0, 0x7FFFFFFF, 0x00020000);
-    uint32_t keys[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; k++) keys[k] = ldg(Sm.uid + min(s0 + k * PROBE_TILE + (int64_t)threadIdx.x, Sm.n - 1));
-    // every bitmap word of the thread in flight at once: whole 16-B buffer loads
-    // (a plain load was split, its second half loaded only on a hit, and each key
-    // waited for the previous one)
-    uint4 E[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; k++)
-      E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(keys[k] >> 6) * 16, 0, 0));
-    uint32_t hm = 0;
-    int64_t jls[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      jls[k] = 0;
-      if (s0 + k * PROBE_TILE + (int64_t)threadIdx.x >= Sm.n) continue;
-      const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
-      const uint64_t bit = 1ull << (keys[k] & 63u);
-      if (ex & bit) {
-        hm |= 1u << k;
-        jls[k] = (int64_t)ey + __popcll(ex & (bit - 1ull));
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      if (!((hm >> k) & 1u)) continue;
-      const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
-      const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
-      if (mark) {
-        stg(J.removed + ia, (uint8_t)1);
-      } else if (J.maxd < 65535 &&
-                 joined_distance(J.A.feat + ia * FEAT_WORDS, J.B.feat + ib * FEAT_WORDS, J.mode) > J.maxd) {
-        hm &= ~(1u << k);
-      }
-    }
-    if (mark) return;
-    // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
-    // of four 16-bit per-slot counts gives every hit's place in its slot
-    uint64_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < KPT; k++) cnt |= (uint64_t)((hm >> k) & 1u) << (16 * k);
-    uint64_t tot64;
-    const uint64_t ex = block_excl_sum256_u64(cnt, sScan64, &tot64);
-    const int64_t src = J.pair_base + s0;  // BM_TILE pair slots per tile
-    int32_t base[KPT];
-    int32_t run = 0;
-#pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      base[k] = run;
-      run += (int32_t)((tot64 >> (16 * k)) & 0xFFFFu);
-    }
-    if (threadIdx.x == 0) {
-      tile_src[b] = src;
-      tile_cnt[b] = run;
-    }
-#pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      if (!((hm >> k) & 1u)) continue;
-      const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
-      const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
-      const int64_t o = src + base[k] + (int64_t)((ex >> (16 * k)) & 0xFFFFu);
-      pairs[o] = make_uint2((uint32_t)ia, (uint32_t)ib);
-      pair_uid[o] = keys[k];
-    }
+    // a launch without long tiles does not carry the KPT_LARGE code (its registers
+    // cost C2 a wave per SIMD: k_probe 111 -> 119 us)
+    if (LONG && J.ptile == KPT_LARGE * PROBE_TILE)
+      probe_bitmap<KPT_LARGE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark, sScan64);
+    else
+      probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark,
+                                         sScan64);
     return;
   }
   const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
@@ -3261,7 +3285,7 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
-                     int64_t* d_tile_off, bool mark, const BandOrder& bo,
+                     int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1) {
   if (total_tiles <= 0) return 0;
@@ -3315,9 +3339,16 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
-  if (probe_tiles > 0)
-    hipLaunchKernelGGL(k_probe, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0, (const int2*)pperm);
+  if (probe_tiles > 0) {
+    if (long_tiles)
+      hipLaunchKernelGGL(k_probe<true>, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base,
+                         d_pdesc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0,
+                         (const int2*)pperm);
+    else
+      hipLaunchKernelGGL(k_probe<false>, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base,
+                         d_pdesc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0,
+                         (const int2*)pperm);
+  }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
