@@ -743,13 +743,8 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
   *nmerge = 0;
   *merge_tiles = 0;
   *tiles = 0;
-  uintptr_t prev_big = 0;
-  int32_t group = -1;
   for (size_t i : order) {
     JoinQ J = jobs[i];
-    if (big(J) != prev_big) group++;  // probe jobs of one large list are consecutive
-    prev_big = big(J);
-    J.lgroup = group;
     J.tile_base = *tiles;
     tile_base.push_back(*tiles);
     *tiles += J.ntiles;
@@ -784,7 +779,7 @@ static BandOrder band_order(Lane* ctx, int64_t tiles, int64_t merge_tiles, bool 
     bo.key = bo.pkey = nullptr;
     return bo;
   }
-  int bits = 0;  // url ids < 2^bits; 2^12 bands for compaction, 2^4 per large list for the probe
+  int bits = 0;  // url ids < 2^bits; 2^12 bands for compaction, 2^4 for the probe
   while (bits < 32 && ((int64_t)1 << bits) < ctx->nurls) bits++;
   bo.shift = std::max(0, bits - 12);
   bo.pshift = std::max(0, bits - 4);

@@ -111,7 +111,7 @@ struct JoinQ {
   int32_t algo;        // JoinAlgo
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   int32_t ptile;       // JA_PROBE: small-list elements per tile (PROBE_TILE, BM_TILE with a bitmap)
-  int32_t lgroup;      // JA_PROBE: rank of its large list among the step's (k_probe's band order)
+  int32_t pad_;
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
@@ -282,9 +282,8 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
 // Band-major schedules of a join step (k_order_hist and k_order_scatter in
 // yrwi_kernels.hip).  Compaction: the url id each tile starts at (key, one per
 // tile), band = key >> shift, the tiles in that order (perm: tile, job).
-// Probe: (large-list group, 16 bands) per probe tile (pkey, bands of
-// pshift-shifted ids), the probe tiles in that order (pperm; tile index relative
-// to the first probe tile).  key / pkey == nullptr: job order.  tile_job (any
+// Probe: 16 url-id bands per probe tile (pkey = first id >> pshift), the probe
+// tiles in that order (pperm; tile index relative to the first probe tile).  key / pkey == nullptr: job order.  tile_job (any
 // order) spares k_compact a search of the job table per tile.
 struct BandOrder {
   int32_t* tile_job = nullptr;  // job of every tile (k_partition / k_probe_part; k_compact reads it)

@@ -678,8 +678,10 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t n) {
 // resident on an XCD work on one url-id band and its L2 serves the re-reads:
 //  * compaction: all tiles by the url id they start at (4096 bands): every list's
 //    records of one band (C2: k_compact 268 -> 230 us, 11.7 -> 7.7 M lines read);
-//  * probe: the probe tiles by (large list, 16 bands of url ids): the jobs of one
-//    large list in band order, so an XCD holds the band of one or two bitmaps.
+//  * probe: the probe tiles by 16 coarse url-id bands (every XCD sweeps its band
+//    of every bitmap; 4 or 64 bands, or grouping by large list first, measured
+//    slower: C3 k_probe 508 / 508 / 533 us per deferred step against 508, C2
+//    123 / 123 / 114 against 115).
 // Only the schedule changes: every tile writes its own slots.  Counting sort
 // over G workgroups per order (LDS atomics run at about one lane per clock on a
 // CU, so one workgroup took 30-35 us for C2's ~45k tiles): k_order_hist counts
@@ -834,7 +836,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   if (tile_key) tile_key[tile0 + t] = ldg(Sm.uid + s0);  // url id the tile starts at (k_order_hist / k_order_scatter)
   if (tile_job) tile_job[tile0 + t] = j;
   if (probe_key)  // (large list, 16 bands): k_probe's order
-    probe_key[t] = (uint32_t)min(J.lgroup, 255) << 4 | min(ldg(Sm.uid + s0) >> probe_shift, 15u);
+    probe_key[t] = ldg(Sm.uid + s0) >> probe_shift;  // 16 url-id bands: k_probe's order
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
