@@ -54,11 +54,12 @@ def main(tag, config):
     if stats:
         shutil.copy(stats[0], os.path.join(pout, f"{tag}_kernel_stats.csv"))
         for row in csv.DictReader(open(stats[0])):
-            k = short(row["Name"])
-            out["kernels"].setdefault(k, {})
-            out["kernels"][k]["calls"] = int(row["Calls"])
-            out["kernels"][k]["avg_ns"] = float(row["AverageNs"])
-            out["kernels"][k]["pct"] = float(row.get("Percentage", 0))
+            k = short(row["Name"])  # template instances (k_probe<true> / <false>) pool into one entry
+            d = out["kernels"].setdefault(k, {"calls": 0, "total_ns": 0.0, "pct": 0.0})
+            d["calls"] += int(row["Calls"])
+            d["total_ns"] += float(row["AverageNs"]) * int(row["Calls"])
+            d["avg_ns"] = d["total_ns"] / d["calls"]
+            d["pct"] += float(row.get("Percentage", 0))
     rd, nr = counters(os.path.join(base, "rd"))
     wr, nw = counters(os.path.join(base, "wr"))
     for k in set(rd) | set(wr):
