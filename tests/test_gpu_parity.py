@@ -247,6 +247,45 @@ def test_c1_sample_bit_exact():
     ix.close()
 
 
+@pytest.fixture(scope="module")
+def long_lists():
+    """C2's eight longest lists (0.7-3.7 M postings each, every one with a url-id
+    bitmap), resident on one context."""
+    cfg = synth.preset("C2")
+    df = synth.counts(cfg)
+    big = [int(t) for t in np.argsort(-df, kind="stable")[:8]]
+    idx = synth.build_index(cfg, terms=np.array(sorted(big)))
+    ix = RWIIndex(0)
+    for t in big:
+        ix.add(idx.hashes[t], idx.list_rows(t))
+    yield cfg, df, big, idx, ix
+    ix.close()
+
+
+@pytest.mark.parametrize("band_order", ["1", "0"])
+def test_long_bitmap_tiles_and_schedules(long_lists, band_order, monkeypatch):
+    """3-4 term queries with an excluded term over lists of >= 2^18 postings: the
+    deferred fold steps and the exclusion probe take 2048-id bitmap tiles
+    (k_probe<true>, BM_LARGE_MIN), the final step 1024-id tiles; in band-major
+    order (default) and in job order (YRWI_BAND_ORDER=0) the results are the
+    oracle's, byte for byte (the schedules only reorder tiles)."""
+    monkeypatch.setenv("YRWI_BAND_ORDER", band_order)
+    cfg, df, big, idx, ix = long_lists
+    assert df[big[-1]] >= (1 << 18)
+    rng = np.random.default_rng(5)
+    qs = []
+    for _ in range(12):
+        pick = [int(x) for x in rng.permutation(big)[:5]]
+        n = int(rng.integers(3, 5))
+        qs.append((pick[:n], pick[n:n + 1]))
+    d = idx.as_dict()
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW) for inc, exc in qs]
+    got = ix.search_batch(batch)
+    for q, g in zip(batch, got):
+        exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=100)
+        assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp
+
+
 @pytest.mark.parametrize("ratio", ["1", "1000000000"])
 def test_forced_join_algorithm(corpus, ratio, monkeypatch):
     """Every join/exclusion step through the probe kernel (ratio 1) or through
