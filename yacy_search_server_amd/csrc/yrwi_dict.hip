@@ -247,6 +247,8 @@ struct BmSeg {
   const uint32_t* uid;
   uint64_t* bm;
   int64_t n;
+  const uint64_t* feat;  // the list's records, and
+  uint64_t* j5;          // their words 0-1 (DList::j5), nullptr: none
 };
 __global__ void k_bitmap_set(const BmSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -262,6 +264,7 @@ __global__ void k_bitmap_set(const BmSeg* __restrict__ segs, const int64_t* __re
   const uint64_t w = u >> 6;
   atomicOr(reinterpret_cast<unsigned long long*>(S.bm + 2 * w), 1ull << (u & 63u));
   if (j == 0 || (S.uid[j - 1] >> 6) != w) S.bm[2 * w + 1] = (uint64_t)j;
+  if (S.j5) reinterpret_cast<ulonglong2*>(S.j5)[j] = reinterpret_cast<const ulonglong2*>(S.feat + j * FEAT_WORDS)[0];
 }
 
 // bitmap lists: every posting's bit is set and its word's rank + the bits below give its position
@@ -279,6 +282,8 @@ __global__ void k_bitmap_check(const BmSeg* __restrict__ segs, const int64_t* __
   const uint32_t u = S.uid[j];
   const uint64_t bits = S.bm[2 * (u >> 6)], bit = 1ull << (u & 63u);
   if (!(bits & bit) || (int64_t)S.bm[2 * (u >> 6) + 1] + __popcll(bits & (bit - 1ull)) != j) atomicAdd(bad, 1ull);
+  if (S.j5 && (S.j5[2 * j] != S.feat[j * FEAT_WORDS] || S.j5[2 * j + 1] != S.feat[j * FEAT_WORDS + 1]))
+    atomicAdd(bad, 1ull);
 }
 
 __global__ void k_heads_check(const HeadSeg* __restrict__ segs, const int64_t* __restrict__ hoff, int nseg,
@@ -584,9 +589,13 @@ int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
 // Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 64) of the url
 // ids (and 4096 postings): nurls/4 bytes each, so at most 16x the list's own ids
 // (at 1/64 density); total capped by YRWI_BM_GB (default 8).  YRWI_BM_DIV=0: none.
+// The same lists get DList::j5 (16 B per posting) unless YRWI_J5=0: they are the
+// dense ones, where an enumeration's matches sit a few postings apart.
 int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   hipStream_t st = ctx->stream;
-  for (ListRec* L : lists) L->bm = nullptr;
+  for (ListRec* L : lists) L->bm = L->j5 = nullptr;
+  const char* ej = getenv("YRWI_J5");
+  const bool j5 = !ej || atoi(ej) != 0;
   const char* e = getenv("YRWI_BM_DIV");
   const int64_t div = e ? atoll(e) : 64;
   const char* g = getenv("YRWI_BM_GB");
@@ -599,9 +608,15 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   for (ListRec* L : lists)
     if (L->n >= thr) big.push_back(L);
   std::sort(big.begin(), big.end(), [](const ListRec* a, const ListRec* b) { return a->n > b->n; });
-  while (!big.empty() && (int64_t)big.size() * per * 8 > cap_bytes) big.pop_back();  // the largest lists first
+  int64_t nbig = 0;  // their postings
+  for (const ListRec* L : big) nbig += L->n;
+  auto bytes = [&]() { return ((int64_t)big.size() * per + (j5 ? 2 * nbig : 0)) * 8; };
+  while (!big.empty() && bytes() > cap_bytes) {  // the largest lists first
+    nbig -= big.back()->n;
+    big.pop_back();
+  }
   if (big.empty()) return 0;
-  const size_t need = (size_t)big.size() * (size_t)per;
+  const size_t need = (size_t)(bytes() / 8);
   if (need > ctx->bm_cap) {
     if (ctx->bm_all) hipFree(ctx->bm_all);
     ctx->bm_all = nullptr;
@@ -616,7 +631,8 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   int64_t n = 0;
   for (size_t k = 0; k < big.size(); k++) {
     big[k]->bm = ctx->bm_all + (size_t)k * (size_t)per;
-    segs.push_back({big[k]->uid, big[k]->bm, big[k]->n});
+    if (j5) big[k]->j5 = ctx->bm_all + big.size() * (size_t)per + 2 * (size_t)n;
+    segs.push_back({big[k]->uid, big[k]->bm, big[k]->n, big[k]->feat, big[k]->j5});
     off.push_back(n);
     n += big[k]->n;
   }
@@ -804,7 +820,7 @@ int check_url_ids(CtxBase* ctx, int64_t* bad) {
   int64_t nbm = 0;
   for (ListRec* L : lists)
     if (L->bm) {
-      vbs.push_back({L->uid, L->bm, L->n});
+      vbs.push_back({L->uid, L->bm, L->n, L->feat, L->j5});
       vbo.push_back(nbm);
       nbm += L->n;
     }

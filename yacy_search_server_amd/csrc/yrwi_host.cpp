@@ -982,7 +982,10 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         if (!J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
         if (J.A.tup) {
           FoldSrc F{};
-          for (int l = 0; l < J.A.tw; l++) F.feat[l] = P.seq[(size_t)l]->feat;
+          for (int l = 0; l < J.A.tw; l++) {
+            F.feat[l] = P.seq[(size_t)l]->feat;
+            F.j5[l] = P.seq[(size_t)l]->j5;
+          }
           for (size_t t = 0; t < s; t++) F.mode[t] = P.step_mode[t];
           fold.push_back(F);
           fold_job.push_back((int)jobs.size());

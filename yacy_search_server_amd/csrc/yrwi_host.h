@@ -80,7 +80,8 @@ struct ListRec {
   uint64_t* feat = nullptr; // ranking records (built with the url dictionary)
   uint32_t* head = nullptr; // line heads of uid (DList::head; rebuilt with the url ids)
   uint64_t* bm = nullptr;   // url-id bitmap (DList::bm; large lists only, rebuilt with the url ids)
-  DList dl() const { return DList{khi, klo, rows, n, uid, feat, head, nullptr, 0, bm}; }
+  uint64_t* j5 = nullptr;   // record words 0-1 of the bitmap lists (DList::j5)
+  DList dl() const { return DList{khi, klo, rows, n, uid, feat, head, nullptr, 0, bm, j5}; }
 };
 
 // device-wide allocation events (hipMalloc / hipFree / hipHostMalloc / hipHostFree

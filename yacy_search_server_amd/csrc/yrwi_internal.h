@@ -54,6 +54,10 @@ struct DList {
   // of word 2w (rank): membership and position of an id in one 16-B load.
   // k_probe looks the smaller side's ids up in it instead of searching the list.
   const uint64_t* bm;
+  // words 0-1 of every posting's record (2 per posting; bitmap lists only, else
+  // nullptr): the J5 fields k_compact gathers from an enumeration's joined side,
+  // 8 postings per 128-B line instead of 4
+  const uint64_t* j5;
 };
 // the two head levels of a list of n postings (each level padded to 32 entries)
 __host__ __device__ constexpr int64_t head1_n(int64_t n) { return (n + 31) >> 5; }
@@ -99,6 +103,7 @@ constexpr int64_t BM_LARGE_MIN = 1 << 18;  // small-side ids from which a bitmap
 // exactly as materialising every step would) before joining the last list.
 struct FoldSrc {
   const uint64_t* feat[YRWI_MAX_TERMS];  // ranking records of the fold's lists, in fold order
+  const uint64_t* j5[YRWI_MAX_TERMS];    // their DList::j5 (nullptr: none)
   int32_t mode[YRWI_MAX_TERMS];          // JoinMode of step s (lists 0..s with list s+1)
 };
 

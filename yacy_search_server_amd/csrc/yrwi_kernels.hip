@@ -1148,7 +1148,8 @@ struct CompactJob {
   const int32_t* atup;
   int32_t* otup;         // deferred output (otw > 0)
   const FoldSrc* fold;   // A deferred, this the last step: the fold's lists and modes
-  int32_t otw, pad;
+  int32_t otw;
+  int32_t bw;            // words per posting of bf (FEAT_WORDS, or 2 for an enumeration's DList::j5)
 };
 
 // the record of a deferred row (sources r[0..tw-1] in the fold's lists): J5/J6
@@ -1160,7 +1161,9 @@ __device__ __forceinline__ Rec fold_deferred(const FoldSrc& F, const int32_t* __
     const int64_t e = r[s + 1];
     ulonglong2 b = make_ulonglong2(0, 0);
     if (m == JM_TEST_LARGE_B) acc = load_rec(F.feat[s + 1], e);  // self-join of the larger side
-    else if (m == JM_ENUM) b = ldg(reinterpret_cast<const ulonglong2*>(F.feat[s + 1] + e * FEAT_WORDS));
+    else if (m == JM_ENUM)
+      b = F.j5[s + 1] ? ldg(reinterpret_cast<const ulonglong2*>(F.j5[s + 1]) + e)
+                      : ldg(reinterpret_cast<const ulonglong2*>(F.feat[s + 1] + e * FEAT_WORDS));
     acc = joined_rec(acc, b.x, b.y, m, now_ms);
   }
   return acc;
@@ -1197,7 +1200,8 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         const JoinQ& J = jobs[j];
         CompactJob& X = sJ[threadIdx.x];
         X.af = J.A.feat;
-        X.bf = J.B.feat;
+        X.bf = J.mode == JM_ENUM && J.B.j5 ? J.B.j5 : J.B.feat;
+        X.bw = J.mode == JM_ENUM && J.B.j5 ? 2 : FEAT_WORDS;
         X.ofeat = J.out_feat;
         X.ouid = J.out_uid;
         X.now_ms = J.now_ms;
@@ -1273,7 +1277,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
       else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
       else A[u] = load_rec(X.af, pr[u].x);
-      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * FEAT_WORDS);
+      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
