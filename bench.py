@@ -431,6 +431,10 @@ def kernel_lines(iso, pmc):
         e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / n), "achieved": round(gbps, 1),
              "frac": _frac(gbps)}
         e.update(extra)
+        if name == "k_probe" and iso.get("n_probe_dispatches"):
+            # rocprofv3 averages every k_probe dispatch, exclusion steps' too: the
+            # library's mean over the same dispatches is the figure to hold it against
+            e["mean_dispatch_us_all_steps"] = round(iso["t_probe_all_ns"] / iso["n_probe_dispatches"] / 1e3, 2)
         kd = pk.get(name, {})
         if kd.get("hbm_bytes_per_launch"):
             e["traffic"] = kd["hbm_bytes_per_launch"]
@@ -462,6 +466,8 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
                      "(one batch in flight, median of five batches)"}
     if d.get("rocprof_mean_launch_us"):
         r["rocprof_mean_launch_us"] = d["rocprof_mean_launch_us"]
+    if d.get("mean_dispatch_us_all_steps"):
+        r["mean_dispatch_us_all_steps"] = d["mean_dispatch_us_all_steps"]
     if pmc:
         r["traffic_source"] = (f"{pmc['_file']} (rocprofv3 --pmc: TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B "
                                f"by request size; tag {pmc.get('tag')}, commit {pmc.get('head')})")

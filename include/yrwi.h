@@ -136,6 +136,10 @@ typedef struct yrwi_stats {
   int64_t bytes_features;    /* 23 t m_out: the ranking-feature bytes of the joined containers (k_compact's share) */
   int64_t bytes_join_capped;
   int64_t bytes_alg_capped;
+  /* every k_probe dispatch of the call, include and exclusion steps alike (rocprofv3 counts them all):
+     their number and device time (HIP events around each) */
+  int64_t n_probe_dispatches;
+  int64_t t_probe_all_ns;
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

@@ -66,7 +66,8 @@ class CStats(ctypes.Structure):
                 ("bytes_compact", ctypes.c_int64), ("t_compact_ns", ctypes.c_int64),
                 ("t_kernels_ns", ctypes.c_int64), ("bytes_probe_loaded", ctypes.c_int64),
                 ("bytes_probe_capped", ctypes.c_int64), ("bytes_features", ctypes.c_int64),
-                ("bytes_join_capped", ctypes.c_int64), ("bytes_alg_capped", ctypes.c_int64)]
+                ("bytes_join_capped", ctypes.c_int64), ("bytes_alg_capped", ctypes.c_int64),
+                ("n_probe_dispatches", ctypes.c_int64), ("t_probe_all_ns", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):

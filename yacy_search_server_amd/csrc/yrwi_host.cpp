@@ -682,6 +682,7 @@ static int64_t loaded_bytes(const JoinQ& J) {
 struct Timing {
   // per join step: before k_join, between k_join and k_probe, after k_probe
   std::vector<std::array<hipEvent_t, 3>> kjoin;
+  std::vector<std::array<hipEvent_t, 2>> kexcl;  // around each exclusion step's k_probe
   std::vector<std::array<hipEvent_t, 2>> kcompact;  // around each k_compact launch
   // around every group of back-to-back kernel launches of the batch (no host
   // synchronisation inside a span): their sum is the batch's kernel time
@@ -848,7 +849,10 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     tm->kcompact.push_back({c0, c1});
     tm->spans.push_back({sp, c1});
   }
-  if (st) st->n_join_launches++;
+  if (st) {
+    st->n_join_launches++;
+    st->n_probe_dispatches += tiles > merge_tiles;
+  }
   const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
   const int64_t h5 = hprof ? now_ns() : 0;
@@ -915,11 +919,14 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, false);
   hipEvent_t sp = span_open(ctx, tm);
+  hipEvent_t pm = tm ? ctx->event() : nullptr, p1 = tm ? ctx->event() : nullptr;
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, nullptr, nullptr, nullptr, nullptr,
                        nullptr, true, long_tiles, bo,
-                       ctx->stream, nullptr, nullptr, nullptr))
+                       ctx->stream, nullptr, pm, p1))
     return ctx->fail(YRWI_E_HIP, "exclude launch");
   span_close(ctx, tm, sp);
+  if (tm) tm->kexcl.push_back({pm, p1});
+  if (st) st->n_probe_dispatches += tiles > merge_tiles;
   return 0;
 }
 
@@ -1574,8 +1581,13 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
       float ms = 0;
       for (auto& ev : tm.kjoin) {
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_join_ns += (int64_t)(ms * 1e6);
-        if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) st->t_probe_ns += (int64_t)(ms * 1e6);
+        if (hipEventElapsedTime(&ms, ev[1], ev[2]) == hipSuccess) {
+          st->t_probe_ns += (int64_t)(ms * 1e6);
+          st->t_probe_all_ns += (int64_t)(ms * 1e6);
+        }
       }
+      for (auto& ev : tm.kexcl)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_probe_all_ns += (int64_t)(ms * 1e6);
       for (auto& ev : tm.kcompact)
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_compact_ns += (int64_t)(ms * 1e6);
       for (auto& ev : tm.spans)
@@ -1685,6 +1697,8 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->n_enum_steps += p.n_enum_steps;
       st->n_test_steps += p.n_test_steps;
       st->n_realloc += p.n_realloc;
+      st->n_probe_dispatches += p.n_probe_dispatches;
+      st->t_probe_all_ns += p.t_probe_all_ns;
     }
     st->t_total_ns = now_ns() - t0;
   }
