@@ -63,3 +63,33 @@ def test_no_gpu_open_fails_loudly():
     from yacy_search_server_amd import RWIIndex
     with pytest.raises(Exception):
         RWIIndex(0)
+
+
+# every ctypes mirror in _lib.py against the C compiler's layout of include/yrwi.h
+ABI_STRUCTS = {"CProfile": "yrwi_profile", "CHit": "yrwi_hit", "CFilter": "yrwi_filter", "CQuery": "yrwi_query_desc",
+               "CStats": "yrwi_stats", "CNode": "yrwi_node", "CArrival": "yrwi_arrival", "CEventInfo": "yrwi_event_info",
+               "CAbstract": "yrwi_abstract", "CPeerRequest": "yrwi_peer_request", "CIndexInfo": "yrwi_index_info",
+               "CLoadStats": "yrwi_load_stats"}
+
+
+def test_ctypes_mirrors_match_header(tmp_path):
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    lines = ["#include <stddef.h>", "#include <stdio.h>", '#include "yrwi.h"', "int main(void) {"]
+    want = []
+    for py, c in ABI_STRUCTS.items():
+        cls = getattr(_lib, py)
+        lines.append(f'  printf("{c} %zu\\n", sizeof({c}));')
+        want.append(f"{c} {ctypes.sizeof(cls)}")
+        for name, _ in cls._fields_:
+            lines.append(f'  printf("{c}.{name} %zu\\n", offsetof({c}, {name}));')
+            want.append(f"{c}.{name} {getattr(cls, name).offset}")
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "abi.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "abi"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    assert [g for g in got if g] == want
