@@ -286,6 +286,35 @@ def test_long_bitmap_tiles_and_schedules(long_lists, band_order, monkeypatch):
         assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp
 
 
+@pytest.mark.parametrize("j5", [("1", None), ("0", None), ("1", "0.06")], ids=["j5", "no_j5", "j5_largest_only"])
+def test_j5_side_arrays(long_lists, j5, monkeypatch):
+    """The joined side's J5 words come from the 16-B side arrays of the bitmap
+    lists (DList::j5), from the 32-B records (YRWI_J5=0), or from either when
+    YRWI_J5_GB leaves only the largest list one: enumeration steps, the deferred
+    folds of 3-4 term queries and the final top-k equal the oracle's."""
+    monkeypatch.setenv("YRWI_J5", j5[0])
+    if j5[1]:
+        monkeypatch.setenv("YRWI_J5_GB", j5[1])
+    cfg, df, big, idx, _ = long_lists
+    ix = RWIIndex(0)
+    try:
+        for t in big:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+        d = idx.as_dict()
+        rng = np.random.default_rng(8)
+        for n in (2, 2, 3, 4):
+            pick = [int(x) for x in rng.permutation(big)[:n]]
+            ih = [idx.hashes[t] for t in pick]
+            for md in (2147483647, 60):
+                assert np.array_equal(ix.term_search(ih, [], md, NOW), orc.term_search(d, ih, [], md, NOW)), (pick, md)
+        batch = [Query([idx.hashes[t] for t in rng.permutation(big)[:int(rng.integers(2, 5))]], [], now_ms=NOW)
+                 for _ in range(8)]
+        for q, g in zip(batch, ix.search_batch(batch)):
+            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == orc.search(d, q.include, q.exclude, now_ms=NOW, k=100)
+    finally:
+        ix.close()
+
+
 @pytest.mark.parametrize("ratio", ["1", "1000000000"])
 def test_forced_join_algorithm(corpus, ratio, monkeypatch):
     """Every join/exclusion step through the probe kernel (ratio 1) or through

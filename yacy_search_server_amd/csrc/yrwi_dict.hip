@@ -589,13 +589,15 @@ int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
 // Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 64) of the url
 // ids (and 4096 postings): nurls/4 bytes each, so at most 16x the list's own ids
 // (at 1/64 density); total capped by YRWI_BM_GB (default 8).  YRWI_BM_DIV=0: none.
-// The same lists get DList::j5 (16 B per posting) unless YRWI_J5=0: they are the
-// dense ones, where an enumeration's matches sit a few postings apart.
+// The same lists, largest first, get DList::j5 (16 B per posting; total capped by
+// YRWI_J5_GB, default 16, apart from the bitmaps' cap; YRWI_J5=0: none): they are
+// the dense ones, where an enumeration's matches sit a few postings apart.
 int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   hipStream_t st = ctx->stream;
   for (ListRec* L : lists) L->bm = L->j5 = nullptr;
   const char* ej = getenv("YRWI_J5");
-  const bool j5 = !ej || atoi(ej) != 0;
+  const char* gj = getenv("YRWI_J5_GB");
+  const int64_t j5_cap = (ej && atoi(ej) == 0) ? 0 : (int64_t)((gj ? atof(gj) : 16.0) * (double)(1ll << 30));
   const char* e = getenv("YRWI_BM_DIV");
   const int64_t div = e ? atoll(e) : 64;
   const char* g = getenv("YRWI_BM_GB");
@@ -608,15 +610,13 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   for (ListRec* L : lists)
     if (L->n >= thr) big.push_back(L);
   std::sort(big.begin(), big.end(), [](const ListRec* a, const ListRec* b) { return a->n > b->n; });
-  int64_t nbig = 0;  // their postings
-  for (const ListRec* L : big) nbig += L->n;
-  auto bytes = [&]() { return ((int64_t)big.size() * per + (j5 ? 2 * nbig : 0)) * 8; };
-  while (!big.empty() && bytes() > cap_bytes) {  // the largest lists first
-    nbig -= big.back()->n;
-    big.pop_back();
-  }
+  while (!big.empty() && (int64_t)big.size() * per * 8 > cap_bytes) big.pop_back();  // the largest lists first
   if (big.empty()) return 0;
-  const size_t need = (size_t)(bytes() / 8);
+  size_t nj5 = 0;  // lists with a J5 array (the first nj5 of big)
+  int64_t j5_words = 0;
+  while (nj5 < big.size() && (j5_words + 2 * big[nj5]->n) * 8 <= j5_cap) j5_words += 2 * big[nj5++]->n;
+  const size_t bm_words = big.size() * (size_t)per;
+  const size_t need = bm_words + (size_t)j5_words;
   if (need > ctx->bm_cap) {
     if (ctx->bm_all) hipFree(ctx->bm_all);
     ctx->bm_all = nullptr;
@@ -625,13 +625,16 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
       return 0;  // no bitmaps: the joins search the lists instead
     ctx->bm_cap = need;
   }
-  HIPCHK(ctx, hipMemsetAsync(ctx->bm_all, 0, need * 8, st));
+  HIPCHK(ctx, hipMemsetAsync(ctx->bm_all, 0, bm_words * 8, st));  // the J5 arrays are written whole
   std::vector<BmSeg> segs;
   std::vector<int64_t> off;
-  int64_t n = 0;
+  int64_t n = 0, jw = 0;
   for (size_t k = 0; k < big.size(); k++) {
-    big[k]->bm = ctx->bm_all + (size_t)k * (size_t)per;
-    if (j5) big[k]->j5 = ctx->bm_all + big.size() * (size_t)per + 2 * (size_t)n;
+    big[k]->bm = ctx->bm_all + k * (size_t)per;
+    if (k < nj5) {
+      big[k]->j5 = ctx->bm_all + bm_words + (size_t)jw;
+      jw += 2 * big[k]->n;
+    }
     segs.push_back({big[k]->uid, big[k]->bm, big[k]->n, big[k]->feat, big[k]->j5});
     off.push_back(n);
     n += big[k]->n;
