@@ -18,10 +18,14 @@ for nv in "$@"; do
   python3 - $n <<'PY'
 import json, sys
 n = sys.argv[1]
-k = {}
+k, c = {}, {}
 for l in open(f"gpurun_out/kvar/kv_{n}_kstats.txt"):
     f = l.split()
-    if len(f) >= 4: k[f[0].split("::")[-1]] = float(f[-2])
+    if len(f) >= 4:  # template instances (k_probe<true> / <false>) pool: mean per dispatch
+        name = " ".join(f[:-3]).split("::")[-1].split("<")[0]
+        k[name] = k.get(name, 0.0) + float(f[-2]) * int(f[-3])
+        c[name] = c.get(name, 0) + int(f[-3])
+k = {x: k[x] / c[x] for x in k if c[x]}
 d = json.load(open(f"gpurun_out/kvar/{n}.json"))
 print(n, "ms/step %.4f" % d["ms_per_step"], " ".join("%s %.1f" % (x, k.get(x, 0)) for x in ("k_compact", "k_probe", "k_tile_order", "k_join", "k_score", "k_reduce")))
 PY
