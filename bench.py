@@ -65,7 +65,13 @@ def parse_args(argv=None):
                     help="extra BASELINE configs after the headline ('C3,C4,C5'), or 'none'; "
                          "auto: C3,C4,C5 on one GPU, none for N > 1 (the scaling runs time the headline only)")
     ap.add_argument("--leg-steps", type=int, default=20)
-    ap.add_argument("--leg-check", type=int, default=16, help="queries of each leg's timed batch checked against the oracle")
+    ap.add_argument("--leg-check", type=int, default=4,
+                    help="queries of each distinct batch of a leg's timed region checked against the oracle")
+    ap.add_argument("--check", type=int, default=16,
+                    help="queries of each distinct batch of the headline's timed region checked against the oracle")
+    ap.add_argument("--batches", type=int, default=8,
+                    help="distinct query batches cycled over the timed steps (one per in-flight slot; "
+                         "capped at --inflight and made to divide it)")
     ap.add_argument("--leg-latency", type=int, default=50, help="single-query latency samples per leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -189,6 +195,17 @@ def cpu_baseline(idx, qs, now_ms, k, budget_s, threads, prof, label, min_s=10.0)
                       f"oracle/yrwi_oracle.cpp, {threads} host thread(s), one query per thread"}
 
 
+def draws(cfg, nq, min_incl, max_incl, n_excl, qseed, n):
+    """n distinct query batches of one stream shape: batch 0 with `qseed` (None: the
+    config's default), batch b > 0 with a seed of its own (the same df-proportional
+    term sampling)."""
+    from yacy_search_server_amd import synth
+    base = qseed if qseed is not None else cfg.seed ^ 0x51
+    return [synth.queries(cfg, nq, min_incl, max_incl, n_excl,
+                          qseed=base if b == 0 else (base + 0x9E3779B97F4A7C15 * b) & 0xFFFFFFFFFFFFFFFF)
+            for b in range(max(1, n))]
+
+
 def load_pmc(config):
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if os.path.exists(path):
@@ -242,162 +259,214 @@ class Runner:
             self.ix.close()
             self.ix = None
 
-    def measure(self, qs, hashes, prof, nq, k, steps, warmup, inflight, isolated=True):
-        """warmup + `steps` timed batches (max over ranks), then an isolated pass
-        (one batch in flight) whose library statistics give the per-kernel times."""
+    def measure(self, batches, hashes, prof, k, steps, warmup, inflight, isolated=True, identical=True):
+        """`batches`: D distinct query batches of the same shape (draws of one query
+        stream).  Untimed: every batch once with statistics (its postings and bytes),
+        then `warmup` steps.  Timed: `steps` batches, step i = batch i % D in the
+        in-flight slot i % inflight (D divides inflight), max over ranks; the timed
+        region's own output buffers are copied out right after it (the parity
+        sample checks them).  Then, untimed against the headline: the same region
+        with one batch every step (`identical`), and an isolated pass (one batch
+        in flight) whose library statistics give the per-kernel times."""
         import ctypes
         import torch
         from yacy_search_server_amd import _lib
         from yacy_search_server_amd._lib import CHit, CQuery, CStats
         ix = self.ix
-        arr = (CQuery * nq)()
-        keep = [prof]
-        for i, (inc, exc) in enumerate(qs):
-            ib = ctypes.create_string_buffer(b"".join(hashes[t] for t in inc), 12 * max(1, len(inc)))
-            eb = ctypes.create_string_buffer(b"".join(hashes[t] for t in exc), 12 * max(1, len(exc)))
-            keep += [ib, eb]
-            arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
-            arr[i].nincl = len(inc)
-            arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
-            arr[i].nexcl = len(exc)
-            arr[i].max_distance = 2147483647
-            arr[i].k = k
-            arr[i].profile = ctypes.pointer(prof.c)
-            arr[i].language = b"en"
-            arr[i].now_ms = NOW_MS
+        nq = len(batches[0])
         depth = max(1, inflight)
+        D = max(1, min(len(batches), depth))
+        while depth % D:
+            D -= 1
+        batches = batches[:D]
+        keep = [prof]
+        arrs = []
+        for qs in batches:
+            arr = (CQuery * nq)()
+            for i, (inc, exc) in enumerate(qs):
+                ib = ctypes.create_string_buffer(b"".join(hashes[t] for t in inc), 12 * max(1, len(inc)))
+                eb = ctypes.create_string_buffer(b"".join(hashes[t] for t in exc), 12 * max(1, len(exc)))
+                keep += [ib, eb]
+                arr[i].incl = ctypes.cast(ib, ctypes.c_void_p)
+                arr[i].nincl = len(inc)
+                arr[i].excl = ctypes.cast(eb, ctypes.c_void_p)
+                arr[i].nexcl = len(exc)
+                arr[i].max_distance = 2147483647
+                arr[i].k = k
+                arr[i].profile = ctypes.pointer(prof.c)
+                arr[i].language = b"en"
+                arr[i].now_ms = NOW_MS
+            arrs.append(arr)
         bufs = [(ix.host_array(CHit, nq * k), ix.host_array(ctypes.c_int32, nq), CStats()) for _ in range(depth)]
         fields = [f for f, _ in CStats._fields_ if f != "reserved"]
         agg = {f: 0 for f in fields}
+        per_batch = [None] * D
         state = {"depth": depth}
 
-        def collect(st):
+        def collect(st, bi):
             for f in fields:
                 agg[f] += getattr(st, f)
+            per_batch[bi] = {f: getattr(st, f) for f in fields}
 
         trace = os.environ.get("YRWI_BENCH_TRACE")  # per-batch completion times to stderr
 
-        def run_steps(n, stats=True):
+        def run_steps(n, stats=True, batch_of=lambda i: i % D):
             d = state["depth"]
             pending = []
             tl = [time.perf_counter()]
             for i in range(n):
                 b = bufs[i % d]
                 if len(pending) == d:
-                    t, bst = pending.pop(0)
+                    t, bst, bi = pending.pop(0)
                     ix.wait(t)
                     if bst is not None:
-                        collect(bst)
+                        collect(bst, bi)
                     tl.append(time.perf_counter())
                 st = b[2] if stats else None
-                pending.append((ix.submit_raw(arr, nq, k, b[0], b[1], st), st))
-            for t, bst in pending:
+                bi = batch_of(i)
+                pending.append((ix.submit_raw(arrs[bi], nq, k, b[0], b[1], st), st, bi))
+            for t, bst, bi in pending:
                 ix.wait(t)
                 if bst is not None:
-                    collect(bst)
+                    collect(bst, bi)
                 tl.append(time.perf_counter())
             if trace:
                 log("batch done at ms: " + " ".join(f"{(x - tl[0]) * 1e3:.2f}" for x in tl[1:]))
 
-        # timed region without per-batch statistics (no HIP events, as a production
-        # caller runs): every batch is the same query batch, so its counts are the
-        # warm-up's per batch; YRWI_BENCH_STATS=1 collects them in the timed region
-        timed_stats = os.environ.get("YRWI_BENCH_STATS", "0") == "1"
-        run_steps(warmup)
-        per_batch = {f: agg[f] / max(1, warmup) for f in agg}
-        for f in agg:
-            agg[f] = 0
-        self.barrier()
-        torch.cuda.synchronize()
-        gap = float(os.environ.get("YRWI_BENCH_GAP_MS", "0"))  # diagnosis: idle time before the timed region
-        if gap > 0:
-            time.sleep(gap / 1e3)
-        r0 = _lib.lib().yrwi_realloc_events()
-        cs0 = cgroup_cpu_stat()
-        t0 = time.perf_counter()
-        run_steps(steps, stats=timed_stats)
-        torch.cuda.synchronize()  # every batch was waited for; this brackets the device too
-        self.barrier()
-        dt = time.perf_counter() - t0
-        realloc_timed = int(_lib.lib().yrwi_realloc_events() - r0)  # process-wide, no HIP events needed
-        cs1 = cgroup_cpu_stat()
-        throttle = {k: cs1[k] - cs0[k] for k in cs0 if k in cs1} if cs0 and cs1 else None
-        if not timed_stats:
+        def timed_region(n, stats, batch_of):
             for f in agg:
-                agg[f] = per_batch[f] * steps if f != "n_realloc" else 0
-        agg["n_realloc"] = realloc_timed
-        total_post = float(agg["postings_in"])
-        if self.dist is not None:
-            tt = torch.tensor([dt, total_post], dtype=torch.float64, device="cuda")
+                agg[f] = 0
+            self.barrier()
+            torch.cuda.synchronize()
+            r0 = _lib.lib().yrwi_realloc_events()
+            cs0 = cgroup_cpu_stat()
+            t0 = time.perf_counter()
+            run_steps(n, stats=stats, batch_of=batch_of)
+            torch.cuda.synchronize()  # every batch was waited for; this brackets the device too
+            self.barrier()
+            dt = time.perf_counter() - t0
+            realloc = int(_lib.lib().yrwi_realloc_events() - r0)  # process-wide, no HIP events needed
+            cs1 = cgroup_cpu_stat()
+            throttle = {x: cs1[x] - cs0[x] for x in cs0 if x in cs1} if cs0 and cs1 else None
+            if not stats:  # the batches' counts from their statistics run
+                for f in agg:
+                    agg[f] = sum(per_batch[batch_of(i)][f] for i in range(n)) if f != "n_realloc" else 0
+            agg["n_realloc"] = realloc
+            return dt, dict(agg), throttle
+
+        def over_ranks(dt, post):
+            if self.dist is None:
+                return dt, post
+            tt = torch.tensor([dt, post], dtype=torch.float64, device="cuda")
             tmax = tt[:1].clone()
             self.dist.all_reduce(tmax, op=self.dist.ReduceOp.MAX)
             self.dist.all_reduce(tt)
-            dt = float(tmax.item())
-            total_post = float(tt[1].item())
-        timed = dict(agg)
+            return float(tmax.item()), float(tt[1].item())
+
+        # every distinct batch once with statistics (in flight like the timed steps), then the warm-up
+        run_steps(D)
+        run_steps(warmup)
+        # timed region without per-batch statistics (no HIP events, as a production
+        # caller runs); YRWI_BENCH_STATS=1 collects them in the timed region
+        timed_stats = os.environ.get("YRWI_BENCH_STATS", "0") == "1"
+        gap = float(os.environ.get("YRWI_BENCH_GAP_MS", "0"))  # diagnosis: idle time before the timed region
+        if gap > 0:
+            time.sleep(gap / 1e3)
+        dt, timed, throttle = timed_region(steps, timed_stats, lambda i: i % D)
+        dt, total_post = over_ranks(dt, float(timed["postings_in"]))
+        # the timed region's own results: slot s last ran step i_s (batch i_s % D)
+        out = {}
+        for s in range(min(depth, steps)):
+            i_last = max(i for i in range(steps) if i % depth == s)
+            bi = i_last % D
+            if bi not in out:
+                out[bi] = (bytes(memoryview(bufs[s][0]).cast("B")), list(bufs[s][1]))
+        timed["stats_in_timed_region"] = timed_stats
+        timed["cgroup_cpu_stat"] = throttle
+        ident = None
+        if identical and D > 1:
+            dt1, t1, _ = timed_region(steps, timed_stats, lambda i: 0)
+            dt1, post1 = over_ranks(dt1, float(t1["postings_in"]))
+            ident = {"ms_per_step": dt1 / steps * 1e3, "value": post1 / dt1,
+                     "what": f"the same timed region with batch 0 at every step ({steps} steps, "
+                             f"{depth} in flight): eight lanes run identical batches at once"}
         iso = None
         if isolated:
-            # the same batch with one in flight: the library's HIP-event times are
-            # then each kernel's alone (in the timed region two lanes share the GPU)
-            # five single batches; the one with the median kernel time stands for all
-            # (a host stall inside a group of launches would inflate a mean)
+            # batch 0 with one in flight: the library's HIP-event times are then each
+            # kernel's alone (in the timed region several lanes share the GPU); five
+            # single batches, the one with the median kernel time stands for all (a
+            # host stall inside a group of launches would inflate a mean)
             state["depth"] = 1
             runs = []
             for _ in range(max(1, min(steps, 5))):
                 for f in agg:
                     agg[f] = 0
-                run_steps(1)
+                run_steps(1, batch_of=lambda i: 0)
                 runs.append(dict(agg))
             runs.sort(key=lambda r: r["t_kernels_ns"])
             iso = runs[len(runs) // 2]
             iso["batches"] = 1
             iso["isolated_runs_t_kernels_us"] = [round(r["t_kernels_ns"] / 1e3, 1) for r in runs]
-        timed["stats_in_timed_region"] = timed_stats
-        timed["cgroup_cpu_stat"] = throttle
         return {"dt": dt, "steps": steps, "total_post": total_post, "timed": timed, "iso": iso, "bufs": bufs,
-                "arr": arr, "keep": keep}
+                "arrs": arrs, "keep": keep, "timed_out": out, "batches": batches, "D": D, "identical": ident,
+                "per_batch_postings": [pb["postings_in"] for pb in per_batch]}
 
 
-def check_and_latency(R, M, qs, hashes, idx, prof, k, nchk, nlat, label):
-    """Outside the timed region: (a) the isolated pass's results (bufs[0], the last
-    batch run) of `nchk` queries spread over the batch against the oracle (checker
-    only, oracle/yrwi_oracle.cpp); (b) host-call -> top-k-in-host-memory latency of
-    `nlat` single queries of the same set."""
+def check_and_latency(R, M, hashes, idx, prof, k, nchk, nlat, label, threads=1):
+    """Outside the timed region: (a) `nchk` queries (evenly spaced) of EVERY distinct
+    batch, read from the timed region's own output buffers (copied right after
+    it), against the oracle (checker only, oracle/yrwi_oracle.cpp; `threads`
+    queries at a time, ctypes releases the GIL); (b) host-call ->
+    top-k-in-host-memory latency of `nlat` single queries of batch 0, no
+    statistics (the production call)."""
     import ctypes
     import numpy as np
-    from yacy_search_server_amd._lib import CHit, CStats
-    nq = len(qs)
+    from concurrent.futures import ThreadPoolExecutor
+    from yacy_search_server_amd._lib import CHit
     parity = None
     if nchk > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
         oprof = orc.profile_from(prof)
-        hits, nout = M["bufs"][0][0], M["bufs"][0][1]
-        picks = sorted({i * nq // min(nchk, nq) for i in range(min(nchk, nq))})
-        bad = []
-        for qi in picks:
-            inc, exc = qs[qi]
+        hsz = ctypes.sizeof(CHit)
+        jobs = []
+        for bi, qs in enumerate(M["batches"]):
+            nq = len(qs)
+            if bi not in M["timed_out"]:
+                continue
+            raw, nout = M["timed_out"][bi]
+            hits = (CHit * (nq * k)).from_buffer_copy(raw)
+            for qi in sorted({i * nq // min(nchk, nq) for i in range(min(nchk, nq))}):
+                got = [(bytes(hits[qi * k + j].urlhash), hits[qi * k + j].score) for j in range(nout[qi])]
+                jobs.append((bi, qi, qs[qi], got))
+
+        def one(job):
+            bi, qi, (inc, exc), got = job
             d = {hashes[t]: idx.list_rows(t) for t in inc + exc if idx.sizes[t]}
             exp = orc.search(d, [hashes[t] for t in inc], [hashes[t] for t in exc], profile=oprof,
                              now_ms=NOW_MS, k=k)
-            got = [(bytes(hits[qi * k + j].urlhash), hits[qi * k + j].score) for j in range(nout[qi])]
-            if got != [(h, sc) for h, sc, _ in exp]:
-                bad.append(qi)
-        parity = {"queries_checked": len(picks), "mismatches": len(bad), "checker": "oracle/yrwi_oracle.cpp",
-                  "queries": f"{len(picks)} of the {nq} queries of the timed batch, evenly spaced"}
+            return None if got == [(h, sc) for h, sc, _ in exp] else (bi, qi)
+
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            bad = [r for r in ex.map(one, jobs) if r is not None]
+        parity = {"queries_checked": len(jobs), "mismatches": len(bad), "checker": "oracle/yrwi_oracle.cpp",
+                  "distinct_batches_checked": len(M["timed_out"]),
+                  "queries": f"{nchk} evenly spaced queries of each of the {len(M['timed_out'])} distinct batches, "
+                             f"read from the timed region's own output buffers (no statistics, the production call)"}
         if bad:
-            log(f"{label}: PARITY MISMATCH on queries {bad[:10]}")
+            log(f"{label}: PARITY MISMATCH on (batch, query) {bad[:10]}")
     lat = None
     if nlat > 0:
-        one = (CHit * k)()
+        one_h = (CHit * k)()
         n1 = (ctypes.c_int32 * 1)()
+        arr = M["arrs"][0]
         ts = []
-        for i in range(min(nlat, nq)):
+        for i in range(min(nlat, len(M["batches"][0]))):
             t1 = time.perf_counter()
-            R.ix.search_batch_raw(ctypes.byref(M["arr"][i]), 1, k, one, n1, CStats())
+            R.ix.search_batch_raw(ctypes.byref(arr[i]), 1, k, one_h, n1, None)
             ts.append((time.perf_counter() - t1) * 1e3)
         lat = {"p50": float(np.percentile(ts, 50)), "p99": float(np.percentile(ts, 99)), "n": len(ts),
-               "what": "one query per call (yrwi_query_batch, nq = 1): host call -> top-k in host memory"}
+               "what": "one query per call (yrwi_query_batch, nq = 1, no statistics): host call -> top-k in host memory"}
     return parity, lat
 
 
@@ -408,50 +477,60 @@ def _frac(gbps):
 
 
 def kernel_lines(iso, pmc):
-    """The join-phase kernels, each on its SURVEY.md §8(d) share of the bytes over
-    its mean launch time (library HIP events around each launch, isolated pass):
-      k_join    sum of min(K, 4-B ids of both sides) over the merge-executed steps;
-      k_probe   sum of min(K, bytes the probe loads) over the probe-executed steps
-                (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id);
-                K as the reference dispatches the step (J3);
-      k_compact 23 B per include term and joined posting (23 t m_out).
-    traffic = rocprofv3 PMC HBM bytes per launch (profiles/pmc_<config>.json)."""
+    """Every path kernel that moves the batch's postings, each on its bytes over its
+    mean launch time (library HIP events around each launch, isolated pass):
+      k_join    SURVEY.md §8(d): sum of min(K, 4-B ids of both sides) over the merge-executed steps;
+      k_probe   §8(d): sum of min(K, bytes the probe loads) over the probe-executed include steps
+                (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id); K as the reference
+                dispatches the step (J3);
+      k_compact §8(d): 23 B per include term and joined posting (23 t m_out);
+      k_reduce  the 32-B ranking record of every joined posting (+ 1-B exclusion mark), k_shard_fin included;
+      k_score   the same records (an upper bound: chunks the threshold prunes read 16 of the 32 B).
+    traffic = rocprofv3 PMC HBM bytes per launch (profiles/pmc_<config>.json) and
+    hbm_frac = traffic / the profile's own mean launch time / peak (the same dispatches)."""
     n = max(1, iso["n_join_launches"])
+    nr = max(1, iso.get("n_rank_passes", 0))
     pk = (pmc or {}).get("kernels", {})
     out = {}
-    for name, t_ns, alg, extra in (
-            ("k_join", iso["t_join_ns"], iso["bytes_join_capped"], {"alg_bytes_model_K": int(iso["bytes_join"] / n)}),
-            ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"],
+    for name, t_ns, alg, nl, extra in (
+            ("k_join", iso["t_join_ns"], iso["bytes_join_capped"], n,
+             {"alg_bytes_model_K": int(iso["bytes_join"] / n)}),
+            ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"], n,
              {"alg_bytes_model_K": int(iso["bytes_probe"] / n), "loaded_bytes": int(iso["bytes_probe_loaded"] / n)}),
-            ("k_compact", iso["t_compact_ns"], iso["bytes_features"], {})):
-        t = t_ns / n * 1e-9
+            ("k_compact", iso["t_compact_ns"], iso["bytes_features"], n, {}),
+            ("k_reduce", iso.get("t_reduce_ns", 0), iso.get("bytes_reduce", 0), nr, {}),
+            ("k_score", iso.get("t_scorek_ns", 0), iso.get("bytes_score", 0), nr, {})):
+        t = t_ns / nl * 1e-9
         if t <= 0:
             continue
-        gbps = alg / n / t / 1e9
-        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / n), "achieved": round(gbps, 1),
+        gbps = alg / nl / t / 1e9
+        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / nl), "achieved": round(gbps, 1),
              "frac": _frac(gbps)}
         e.update(extra)
         if name == "k_probe" and iso.get("n_probe_dispatches"):
-            # rocprofv3 averages every k_probe dispatch, exclusion steps' too: the
-            # library's mean over the same dispatches is the figure to hold it against
+            # every k_probe dispatch, the exclusion steps' too (profiles key those as k_probe_excl)
             e["mean_dispatch_us_all_steps"] = round(iso["t_probe_all_ns"] / iso["n_probe_dispatches"] / 1e3, 2)
         kd = pk.get(name, {})
         if kd.get("hbm_bytes_per_launch"):
             e["traffic"] = kd["hbm_bytes_per_launch"]
             e["traffic_GBps"] = round(kd["hbm_bytes_per_launch"] / t / 1e9, 1)
-            if kd.get("avg_ns"):
-                e["rocprof_mean_launch_us"] = round(kd["avg_ns"] / 1e3, 2)
+            tp = kd.get("avg_ns", 0) * 1e-9
+            if tp > 0:
+                e["rocprof_mean_launch_us"] = round(tp * 1e6, 2)
+                e["hbm_frac"] = round(kd["hbm_bytes_per_launch"] / tp / 1e9 / HBM_PEAK_GBS, 4)
+            if kd.get("read_requests_dram_per_launch") is not None:
+                e["dram_read_bytes"] = round(128 * kd["read_requests_dram_per_launch"])
         out[name] = e
     return out
 
 
 def roofline_block(iso, timed, steps, ms_per_step, pmc):
     """`roofline` of the bench line: the dominant kernel (longest mean launch among
-    k_join / k_probe / k_compact) with its §8(d) bytes (kernel_lines), plus the
-    path: B = sum K + 12 sum n_excl + 23 t m_out per batch with every join and
-    exclusion step charged min(K, the bytes its kernel loads), over (a) the
-    batch's kernel time in the isolated pass and (b) the timed region's time per
-    batch (batches in flight overlap)."""
+    every path kernel of kernel_lines) with its bytes, plus the path: B = sum K +
+    12 sum n_excl + 23 t m_out per batch with every join and exclusion step
+    charged min(K, the bytes its kernel loads), over (a) the batch's kernel time in
+    the isolated pass and (b) the timed region's time per batch (batches in flight
+    overlap)."""
     kern = kernel_lines(iso, pmc)
     nb = max(1, iso["batches"])
     if not kern:
@@ -460,7 +539,7 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
     dom = max(kern, key=lambda k: kern[k]["mean_launch_us"])
     d = kern[dom]
     r = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": d["frac"], "traffic": d.get("traffic"),
+         "frac": d["frac"], "traffic": d.get("traffic"), "hbm_frac": d.get("hbm_frac"),
          "alg_bytes_per_launch": d["alg_bytes"], "mean_launch_us": d["mean_launch_us"],
          "measured": "HIP events around each launch on the lane's stream (library statistics), isolated pass "
                      "(one batch in flight, median of five batches)"}
@@ -470,7 +549,8 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
         r["mean_dispatch_us_all_steps"] = d["mean_dispatch_us_all_steps"]
     if pmc:
         r["traffic_source"] = (f"{pmc['_file']} (rocprofv3 --pmc: TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B "
-                               f"by request size; tag {pmc.get('tag')}, commit {pmc.get('head')})")
+                               f"by request size, each pass its own run; hbm_frac over the same profile's "
+                               f"kernel-trace mean; tag {pmc.get('tag')}, commit {pmc.get('head')})")
     b_iso = iso["bytes_alg_capped"] / nb
     t_iso = iso["t_kernels_ns"] / nb * 1e-9
     path = {"bytes_per_batch": int(b_iso),
@@ -488,6 +568,11 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
                                    "time": "ms_per_step (timed region, batches in flight)"}
     if pmc and pmc.get("path_hbm_bytes_per_batch"):
         path["traffic_per_batch"] = pmc["path_hbm_bytes_per_batch"]
+        if t_iso > 0:
+            path["isolated"]["hbm_frac"] = round(pmc["path_hbm_bytes_per_batch"] / t_iso / 1e9 / HBM_PEAK_GBS, 4)
+        if ms_per_step > 0:
+            path["throughput_mode"]["hbm_frac"] = round(
+                pmc["path_hbm_bytes_per_batch"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     r["path"] = path
     return r, kern
 
@@ -524,13 +609,14 @@ def run(args, rank, world, local):
         cfg = full.shard(rank, world) if world > 1 else full
     idx, t_dict = R.open_index(cfg)
 
-    qs = synth.queries(full, args.nq, args.terms, max_terms, args.exclude, qseed=args.qseed)
+    bats = draws(full, args.nq, args.terms, max_terms, args.exclude, args.qseed, args.batches)
+    qs = [q for b in bats for q in b]  # the CPU baseline cycles every distinct batch's queries
     prof = RankingProfile()
     if args.profile == "custom":  # exercises the authority path (coeff > 12)
         prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
     elif args.profile == "date":
         prof = RankingProfile.date()
-    M = R.measure(qs, idx.hashes, prof, args.nq, args.k, args.steps, args.warmup, args.inflight)
+    M = R.measure(bats, idx.hashes, prof, args.k, args.steps, args.warmup, args.inflight)
     value = M["total_post"] / M["dt"]
     ms_per_step = M["dt"] / args.steps * 1e3
     iso, timed = M["iso"], M["timed"]
@@ -540,8 +626,8 @@ def run(args, rank, world, local):
     # parity of this very workload and single-query latency (outside the timed region)
     parity = lat = None
     if rank == 0 and world == 1:
-        parity, lat = check_and_latency(R, M, qs, idx.hashes, idx, prof, args.k, 0 if args.no_cpu else 64,
-                                        args.latency, args.config)
+        parity, lat = check_and_latency(R, M, idx.hashes, idx, prof, args.k, 0 if args.no_cpu else args.check,
+                                        args.latency, args.config, threads=host_cores()[0])
 
     cpu = cpu1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -605,7 +691,11 @@ def run(args, rank, world, local):
             "timed_region": ("batches submitted with per-batch statistics (YRWI_BENCH_STATS=1)"
                              if timed["stats_in_timed_region"] else
                              "batches submitted without statistics (no HIP events: the production call); "
-                             "postings and bytes per batch from the warm-up's statistics (the same batch every step)"),
+                             "postings and bytes of each distinct batch from its statistics run before the warm-up"),
+            "distinct_batches": M["D"],
+            "batch_schedule": f"step i runs distinct batch i % {M['D']} in in-flight slot i % {args.inflight}",
+            "postings_per_batch": M["per_batch_postings"],
+            "identical_batch": M["identical"],
             "inflight": args.inflight,
             # per batch, from the library's own HIP events (isolated pass): join+probe kernels,
             # normalisation (reduce..combine), scoring (score..emit), all kernels; host = call to results
@@ -652,17 +742,17 @@ def run_leg(R, leg, args, rank, world):
             R.leg_idx, _ = R.open_index(cfg)
             R.leg_cfg = ("C3", rank, world)
         if leg == "C3":
-            qs = synth.queries(full, 1000, 3, 3, 1)
+            bats = draws(full, 1000, 3, 3, 1, None, args.batches)
         else:
-            qs = synth.queries(full, 4096, 2, 4, 0, qseed=full.seed ^ 0xC4)
+            bats = draws(full, 4096, 2, 4, 0, full.seed ^ 0xC4, args.batches)
         hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
         prof = RankingProfile()
-        M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
+        M = R.measure(bats, hashes, prof, 100, args.leg_steps, 2 * args.inflight, args.inflight,
                       isolated=True)
-        res[leg] = _leg_line(M, leg, len(qs), world, "strong", load_pmc(leg) if world == 1 else None)
+        res[leg] = _leg_line(M, leg, len(bats[0]), world, "strong", load_pmc(leg) if world == 1 else None)
         if check:
             res[leg]["parity_sample"], res[leg]["latency_ms"] = check_and_latency(
-                R, M, qs, hashes, R.leg_idx, prof, 100, nchk, nlat, leg)
+                R, M, hashes, R.leg_idx, prof, 100, nchk, nlat, leg, threads=host_cores()[0])
     elif leg == "C5":
         full = synth.preset("C5")
         parts = max(8, world)
@@ -670,17 +760,17 @@ def run_leg(R, leg, args, rank, world):
         R.leg_cfg = None
         R.leg_idx = None
         idx, _ = R.open_index(full.shard(rank, parts))
-        qs = synth.queries(full, 1000, 2, 4, 0)
+        bats = draws(full, 1000, 2, 4, 0, None, args.batches)
         hashes = [synth.term_hash(full, t) for t in range(full.n_terms)]
         custom = RankingProfile()
         custom.coeff_date, custom.coeff_domlength, custom.coeff_authority, custom.coeff_termfrequency = 15, 15, 13, 10
         for name, prof in (("C5_custom", custom), ("C5_date", RankingProfile.date())):
-            M = R.measure(qs, hashes, prof, len(qs), 100, args.leg_steps, 2 * args.inflight, args.inflight,
+            M = R.measure(bats, hashes, prof, 100, args.leg_steps, 2 * args.inflight, args.inflight,
                           isolated=True)
-            res[name] = _leg_line(M, "C5", len(qs), world, "weak")
+            res[name] = _leg_line(M, "C5", len(bats[0]), world, "weak", load_pmc(name) if world == 1 else None)
             if check:
                 res[name]["parity_sample"], res[name]["latency_ms"] = check_and_latency(
-                    R, M, qs, hashes, idx, prof, 100, nchk, nlat, name)
+                    R, M, hashes, idx, prof, 100, nchk, nlat, name, threads=host_cores()[0])
         del idx
         R.close()
     else:
@@ -692,7 +782,8 @@ def _leg_line(M, leg, nq, world, scaling, pmc=None):
     ms = M["dt"] / M["steps"] * 1e3
     roof, kern = roofline_block(M["iso"], M["timed"], M["steps"], ms, pmc)
     return {"workload": LEG_DESC[leg], "value": M["total_post"] / M["dt"], "unit": "postings/s", "n_gpus": world,
-            "scaling": scaling, "steps": M["steps"], "ms_per_step": ms,
+            "scaling": scaling, "steps": M["steps"], "ms_per_step": ms, "distinct_batches": M["D"],
+            "identical_batch": M["identical"],
             "postings_per_step": M["total_post"] / M["steps"], "queries_per_step": nq,
             "roofline": roof, "roofline_kernels": kern, "joined_per_step": M["timed"]["joined"] / M["steps"],
             "realloc_events_timed": M["timed"]["n_realloc"]}

@@ -140,6 +140,15 @@ typedef struct yrwi_stats {
      their number and device time (HIP events around each) */
   int64_t n_probe_dispatches;
   int64_t t_probe_all_ns;
+  /* rank phase, per pass: k_reduce + k_shard_fin (one launch each) and the k_score launches, HIP events
+     around each group; the bytes their kernels must read: k_reduce the 32-B ranking record of every
+     joined row (+ its 1-B exclusion mark), k_score the same records (an upper bound: chunks pruned by
+     the per-query threshold read only words 2-3) */
+  int64_t n_rank_passes;
+  int64_t t_reduce_ns;
+  int64_t t_scorek_ns;
+  int64_t bytes_reduce;
+  int64_t bytes_score;
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

@@ -342,9 +342,15 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_getList(JNIEnv* e
   if (yrwi_list_size(x, (const uint8_t*)t, &n) != 0) return NULL;
   jbyteArray res = (*env)->NewByteArray(env, (jsize)(n * 40));
   if (n == 0) return res;
-  void* p = (*env)->GetPrimitiveArrayCritical(env, res, NULL);  /* the device copy lands in the Java array */
-  int rc = yrwi_get_list(x, (const uint8_t*)t, (uint8_t*)p, n, &m);
-  (*env)->ReleasePrimitiveArrayCritical(env, res, p, 0);
+  /* the device copy lands in a native buffer first: no GC-blocking critical region
+   * around the copy and its stream synchronisation.  yrwi_get_list drains the
+   * context's batches; it must not run concurrently with yrwi_put_list (one
+   * context per host thread, include/yrwi.h). */
+  uint8_t* buf = (uint8_t*)malloc((size_t)n * 40);
+  if (!buf) return NULL;
+  int rc = yrwi_get_list(x, (const uint8_t*)t, buf, n, &m);
+  if (rc == 0 && m == n) (*env)->SetByteArrayRegion(env, res, 0, (jsize)(n * 40), (const jbyte*)buf);
+  free(buf);
   return rc == 0 && m == n ? res : NULL;
 }
 

@@ -528,3 +528,36 @@ def test_stats_compact_accounting(corpus):
         assert st.bytes_compact in (96 * st.joined, 80 * st.joined), (st.bytes_compact, st.joined)
         assert st.t_compact_ns > 0
     assert seen > 0
+
+
+def test_null_stats_production_path(corpus):
+    """The production call passes no yrwi_stats (NULL: no HIP events around the
+    kernel groups) -- the path bench.py times and a JNI caller runs.  Batches of
+    mixed shapes, eight in flight on the lanes through yrwi_query_batch_submit
+    with st == NULL, and synchronous yrwi_query_batch calls with st == NULL:
+    every result equals the oracle's."""
+    import ctypes
+    from yacy_search_server_amd._lib import CHit
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    kmax = 100
+    pend = []
+    for s in range(10):
+        qs = synth.queries(cfg, 6 + s, 1 + s % 3, 2 + s % 3, s % 2, qseed=900 + s)
+        b = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=kmax, now_ms=NOW) for inc, exc in qs]
+        arr, keep = _cqueries(b)
+        hits, nout = ix.host_array(CHit, len(b) * kmax), ix.host_array(ctypes.c_int32, len(b))
+        pend.append((ix.submit_raw(arr, len(b), kmax, hits, nout, None), b, hits, nout, keep, arr))
+    for t, b, hits, nout, keep, arr in pend:
+        ix.wait(t)
+        for i, q in enumerate(b):
+            got = [(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score) for j in range(nout[i])]
+            exp = orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)
+            assert got == [(h, s) for h, s, _ in exp]
+    # synchronous, NULL statistics
+    t, b, _, _, keep, arr = pend[3]
+    hits, nout = (CHit * (len(b) * kmax))(), (ctypes.c_int32 * len(b))()
+    ix.search_batch_raw(arr, len(b), kmax, hits, nout, None)
+    for i, q in enumerate(b):
+        got = [(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score) for j in range(nout[i])]
+        assert got == [(h, s) for h, s, _ in orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)]

@@ -23,6 +23,12 @@ def find(pattern):
 
 
 def short(name):
+    # k_probe<LONG, MARK>: the exclusion steps' dispatches (MARK) are keyed apart from the include steps'
+    if "k_probe<" in name and "k_probe_part" not in name:
+        args = name.split("k_probe<", 1)[1].split(">", 1)[0].replace(" ", "").split(",")
+        return "k_probe_excl" if len(args) > 1 and args[1] in ("true", "1") else "k_probe"
+    if "k_probeILb" in name:
+        return "k_probe_excl" if "ELb1E" in name.split("k_probeILb", 1)[1][:8] else "k_probe"
     for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
               "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
               "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
@@ -60,6 +66,16 @@ def main(tag, config):
             d["total_ns"] += float(row["AverageNs"]) * int(row["Calls"])
             d["avg_ns"] = d["total_ns"] / d["calls"]
             d["pct"] += float(row.get("Percentage", 0))
+    # per-dispatch durations of the query path's kernels (the kernel trace of the same run)
+    traces = find(os.path.join(base, "kt", "**", "*kernel_trace.csv"))
+    if traces:
+        with open(os.path.join(pout, f"{tag}_dispatches.csv"), "w") as o:
+            o.write("kernel,grid,duration_ns\n")
+            for row in csv.DictReader(open(traces[0])):
+                k = short(row.get("Kernel_Name", ""))
+                if k.startswith("k_") and k not in ("k_validate", "k_features"):
+                    g = row.get("Grid_Size_X") or row.get("Grid_Size") or 0
+                    o.write(f"{k},{g},{int(row['End_Timestamp']) - int(row['Start_Timestamp'])}\n")
     rd, nr = counters(os.path.join(base, "rd"))
     wr, nw = counters(os.path.join(base, "wr"))
     for k in set(rd) | set(wr):
@@ -79,7 +95,7 @@ def main(tag, config):
     # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
     # (k_combine runs once per batch pass); index build, uploads and fills excluded
     path = ("k_partition", "k_probe_part", "k_scan_bounds", "k_order_hist", "k_order_scatter", "k_join", "k_probe",
-            "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
+            "k_probe_excl", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
             "k_emit")
     nb = out["kernels"].get("k_combine", {}).get("calls")
     if nb:
@@ -97,7 +113,7 @@ def main(tag, config):
             out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
         except Exception:
             pass
-    for name in ("k_compact", "k_join", "k_probe"):
+    for name in ("k_compact", "k_join", "k_probe", "k_probe_excl", "k_reduce", "k_score"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
         out[name + "_avg_ns"] = kd.get("avg_ns")

@@ -67,7 +67,9 @@ class CStats(ctypes.Structure):
                 ("t_kernels_ns", ctypes.c_int64), ("bytes_probe_loaded", ctypes.c_int64),
                 ("bytes_probe_capped", ctypes.c_int64), ("bytes_features", ctypes.c_int64),
                 ("bytes_join_capped", ctypes.c_int64), ("bytes_alg_capped", ctypes.c_int64),
-                ("n_probe_dispatches", ctypes.c_int64), ("t_probe_all_ns", ctypes.c_int64)]
+                ("n_probe_dispatches", ctypes.c_int64), ("t_probe_all_ns", ctypes.c_int64),
+                ("n_rank_passes", ctypes.c_int64), ("t_reduce_ns", ctypes.c_int64), ("t_scorek_ns", ctypes.c_int64),
+                ("bytes_reduce", ctypes.c_int64), ("bytes_score", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):

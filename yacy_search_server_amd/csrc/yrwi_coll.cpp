@@ -152,24 +152,32 @@ void turn_release(Lane* L) {
 // every rank and freed by the last reader.  Longer vectors, unordered callers
 // and a missing mailbox fall back to the device all-gather.
 namespace {
-constexpr int HX_SLOTS = 64, HX_MAXN = 4096, HX_CALLS = 8, HX_MAXW = 16;
+constexpr int HX_SLOTS = 64, HX_MAXN = 4096, HX_CALLS = 8, HX_MAXW = 16, HX_ABORTS = 64;
 struct HxEntry {
   int64_t n;
   int64_t v[HX_MAXN];
 };
+// One slot's whole state in one word, every transition a compare-and-swap:
+// (key + 1) << 16 | writers << 8 | leavers (0: free).  A rank joins the slot of
+// its key, writes its entry, counts itself among the writers, waits for all
+// `world` writers, reads, and leaves; the last to leave frees the slot.  A rank
+// that gives up (its part's sequence was aborted) leaves as well, so the slot of
+// an aborted exchange is freed once every rank that wrote to it has left.
 struct HxSlot {
-  std::atomic<int64_t> owner;  // key + 1 of the exchange using the slot, 0: free
-  std::atomic<int32_t> nwritten, nread;
-  char pad[48];
+  std::atomic<uint64_t> state;
+  char pad[56];
 };
 }  // namespace
 
 // segment header: ranks that mapped it (the last of `world` unlinks the name);
-// aborted: a rank's batch part failed, every wait of every rank gives up at once
-// (its peers would otherwise each hold a core for the whole timeout per exchange)
+// aborted[seq % HX_ABORTS] = seq + 1: that batch part failed on some rank, and
+// every rank's waits on that part's exchanges give up at once (its peers would
+// otherwise each hold a core for the whole timeout per exchange).  Only that
+// part: the exchanges of every later part run as usual.
 struct HxHead {
   std::atomic<int32_t> attached;
-  std::atomic<int32_t> aborted;
+  int32_t pad0;
+  std::atomic<int64_t> aborted[HX_ABORTS];
   char pad[56];
 };
 
@@ -185,6 +193,9 @@ struct HostX {
   HxEntry* entry(int i, int r) const {
     char* e0 = static_cast<char*>(base) + sizeof(HxHead) + (size_t)HX_SLOTS * sizeof(HxSlot);
     return reinterpret_cast<HxEntry*>(e0 + ((size_t)i * world + r) * sizeof(HxEntry));
+  }
+  bool aborted(int64_t seq) const {
+    return seq >= 0 && head()->aborted[seq % HX_ABORTS].load(std::memory_order_acquire) == seq + 1;
   }
 };
 
@@ -220,8 +231,8 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank) {
 
 int hostx_attached(const HostX* x) { return x ? x->head()->attached.load(std::memory_order_acquire) : 0; }
 
-void hostx_abort(HostX* x) {
-  if (x) x->head()->aborted.store(1, std::memory_order_release);
+void hostx_abort(HostX* x, int64_t seq) {
+  if (x && seq >= 0) x->head()->aborted[seq % HX_ABORTS].store(seq + 1, std::memory_order_release);
 }
 
 void hostx_close(HostX* x, bool unlink_name) {
@@ -231,15 +242,16 @@ void hostx_close(HostX* x, bool unlink_name) {
   delete x;
 }
 
-// spin, then yield; false after YRWI_HOSTX_TIMEOUT_S (default 60 s: a peer that
-// never arrives fails the batch instead of hanging it)
+// spin, then yield; false once batch part `seq` is aborted, or after
+// YRWI_HOSTX_TIMEOUT_S (default 300 s: a peer that never arrives fails the batch
+// instead of hanging it; a peer busy rebuilding its url dictionary arrives late)
 template <class F>
-static bool hx_wait(const HostX* x, F ready) {
-  static const double limit_s = getenv("YRWI_HOSTX_TIMEOUT_S") ? atof(getenv("YRWI_HOSTX_TIMEOUT_S")) : 60.0;
+static bool hx_wait(const HostX* x, int64_t seq, F ready) {
+  static const double limit_s = getenv("YRWI_HOSTX_TIMEOUT_S") ? atof(getenv("YRWI_HOSTX_TIMEOUT_S")) : 300.0;
   const auto t0 = std::chrono::steady_clock::now();
   for (int64_t i = 0;; i++) {
     if (ready()) return true;
-    if (x->head()->aborted.load(std::memory_order_acquire)) return false;
+    if (x->aborted(seq)) return false;
     if (i < 2000) {
       __builtin_ia32_pause();
       continue;
@@ -251,41 +263,62 @@ static bool hx_wait(const HostX* x, F ready) {
   }
 }
 
+// leave the slot of `key` (read it, or gave up after writing to it); the last
+// leaver frees it: all `world` ranks read it, or its part was aborted and every
+// rank that wrote to it has left
+static void hx_leave(const HostX* x, HxSlot* S, int64_t key, int64_t seq) {
+  uint64_t cur = S->state.load(std::memory_order_acquire);
+  while ((int64_t)(cur >> 16) == key + 1) {
+    const uint64_t nw = (cur >> 8) & 0xFF, nr = (cur & 0xFF) + 1;
+    const bool free_it = nr == (uint64_t)x->world || (nr >= nw && x->aborted(seq));
+    if (S->state.compare_exchange_weak(cur, free_it ? 0 : cur + 1, std::memory_order_acq_rel)) return;
+  }
+}
+
 // 1: not handled here (caller falls back to the device all-gather); <0: error
 int hostx_allsum(Lane* L, std::vector<int64_t>& v) {
   HostX* x = L->hostx;
   if (!x || L->seq < 0 || L->xcall >= HX_CALLS || v.size() > (size_t)HX_MAXN) return 1;
-  const int64_t key = L->seq * HX_CALLS + L->xcall++;
+  const int64_t seq = L->seq, key = seq * HX_CALLS + L->xcall++;
+  const uint64_t tag = (uint64_t)(key + 1) << 16;
   const int si = (int)(key % HX_SLOTS);
   HxSlot* S = x->slot(si);
+  auto gave_up = [&](const char* why) {
+    return L->fail(YRWI_E_RCCL, x->aborted(seq) ? "host exchange: a peer's batch part failed" : why);
+  };
   // claim (or join) the slot for this key
-  if (!hx_wait(x, [&] {
-        int64_t cur = S->owner.load(std::memory_order_acquire);
-        if (cur == key + 1) return true;
+  if (!hx_wait(x, seq, [&] {
+        uint64_t cur = S->state.load(std::memory_order_acquire);
+        if ((cur >> 16) == tag >> 16) return true;
         if (cur != 0) return false;
-        return S->owner.compare_exchange_strong(cur, key + 1, std::memory_order_acq_rel) || cur == key + 1;
+        return S->state.compare_exchange_strong(cur, tag, std::memory_order_acq_rel) || (cur >> 16) == tag >> 16;
       }))
-    return L->fail(YRWI_E_RCCL, x->head()->aborted.load() ? "host exchange: a peer's batch failed"
-                                                          : "host exchange: slot never freed");
+    return gave_up("host exchange: slot never freed");
   HxEntry* me = x->entry(si, x->rank);
   me->n = (int64_t)v.size();
   std::memcpy(me->v, v.data(), v.size() * sizeof(int64_t));
-  S->nwritten.fetch_add(1, std::memory_order_acq_rel);
-  if (!hx_wait(x, [&] { return S->nwritten.load(std::memory_order_acquire) == x->world; }))
-    return L->fail(YRWI_E_RCCL, x->head()->aborted.load() ? "host exchange: a peer's batch failed"
-                                                          : "host exchange: a rank never arrived");
+  // count this write, unless the slot was freed meanwhile (the part was aborted)
+  uint64_t cur = S->state.load(std::memory_order_acquire);
+  do {
+    if ((cur >> 16) != tag >> 16) return gave_up("host exchange: slot lost");
+  } while (!S->state.compare_exchange_weak(cur, cur + (1u << 8), std::memory_order_acq_rel));
+  if (!hx_wait(x, seq, [&] {
+        const uint64_t s = S->state.load(std::memory_order_acquire);
+        return (s >> 16) == tag >> 16 && ((s >> 8) & 0xFF) == (uint64_t)x->world;
+      })) {
+    hx_leave(x, S, key, seq);
+    return gave_up("host exchange: a rank never arrived");
+  }
   std::vector<int64_t> sum(v.size(), 0);
-  for (int r = 0; r < x->world; r++) {
+  int rc = 0;
+  for (int r = 0; r < x->world && !rc; r++) {
     const HxEntry* e = x->entry(si, r);
-    if (e->n != (int64_t)v.size()) return L->fail(YRWI_E_RCCL, "host exchange: size mismatch");
-    for (size_t i = 0; i < v.size(); i++) sum[i] += e->v[i];
+    if (e->n != (int64_t)v.size()) rc = L->fail(YRWI_E_RCCL, "host exchange: size mismatch");
+    for (size_t i = 0; i < v.size() && !rc; i++) sum[i] += e->v[i];
   }
+  hx_leave(x, S, key, seq);
+  if (rc) return rc;
   v.swap(sum);
-  if (S->nread.fetch_add(1, std::memory_order_acq_rel) + 1 == x->world) {  // the last reader frees the slot
-    S->nwritten.store(0, std::memory_order_relaxed);
-    S->nread.store(0, std::memory_order_relaxed);
-    S->owner.store(0, std::memory_order_release);
-  }
   return 0;
 }
 
@@ -297,31 +330,43 @@ extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, i
   HostX* x = hostx_open(id, world, rank);
   if (!x) return 1;
   // n < 0: the last rank's first batch part fails before its exchanges (it aborts
-  // the mailbox, as run_batch_part does); every other rank must fail fast
+  // that part, as run_batch_part does): every other rank's part 0 must fail fast,
+  // and every later part must then run normally on every rank.  Returns part 0's
+  // status when the later parts all succeed, 1000 + the failing part otherwise.
   const bool fail_last = n < 0;
   if (fail_last) n = -n;
   Lane L;  // host-side state only: no stream, no worker thread
   L.world = world;
   L.rank = rank;
   L.hostx = x;
-  int rc = 0;
-  for (int64_t p = 0; p < nparts && rc == 0; p++) {
+  int rc = 0, rc0 = 0;
+  for (int64_t p = 0; p < nparts; p++) {
     L.seq = p;
     L.xcall = 0;
-    if (fail_last && rank == world - 1) {
-      hostx_abort(x);
-      rc = YRWI_E_RCCL;
-      break;
+    int prc = 0;
+    if (fail_last && p == 0 && rank == world - 1) {
+      hostx_abort(x, p);
+      prc = YRWI_E_RCCL;
     }
-    for (int32_t c = 0; c < ncalls && rc == 0; c++) {
+    for (int32_t c = 0; c < ncalls && prc == 0; c++) {
       std::vector<int64_t> v((size_t)n);
       for (int64_t i = 0; i < n; i++) v[(size_t)i] = rank + p + c + i;
       const int r = hostx_allsum(&L, v);
-      if (r != 0) { rc = r < 0 ? r : YRWI_E_RCCL; break; }
+      if (r != 0) { prc = r < 0 ? r : YRWI_E_RCCL; break; }
       for (int64_t i = 0; i < n; i++)
-        if (v[(size_t)i] != (int64_t)world * (p + c + i) + (int64_t)world * (world - 1) / 2) { rc = YRWI_E_RCCL; break; }
+        if (v[(size_t)i] != (int64_t)world * (p + c + i) + (int64_t)world * (world - 1) / 2) { prc = YRWI_E_RCCL; break; }
+    }
+    if (prc && fail_last && p == 0) {
+      hostx_abort(x, p);
+      rc0 = prc;
+      continue;
+    }
+    if (prc) {
+      rc = fail_last ? 1000 + (int)p : prc;
+      break;
     }
   }
+  if (!rc && fail_last) rc = rc0;
   hostx_close(x, rank == 0);
   return rc;
 }

@@ -616,13 +616,25 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   int64_t j5_words = 0;
   while (nj5 < big.size() && (j5_words + 2 * big[nj5]->n) * 8 <= j5_cap) j5_words += 2 * big[nj5++]->n;
   const size_t bm_words = big.size() * (size_t)per;
-  const size_t need = bm_words + (size_t)j5_words;
+  size_t need = bm_words + (size_t)j5_words;
   if (need > ctx->bm_cap) {
     if (ctx->bm_all) hipFree(ctx->bm_all);
     ctx->bm_all = nullptr;
     ctx->bm_cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&ctx->bm_all), need * 8) != hipSuccess)
-      return 0;  // no bitmaps: the joins search the lists instead
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->bm_all), need * 8) != hipSuccess) {
+      // the J5 arrays are an optimisation of the compaction, the bitmaps replace
+      // whole searches: without room for both, drop the J5 arrays first
+      (void)hipGetLastError();
+      nj5 = 0;
+      j5_words = 0;
+      need = bm_words;
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->bm_all), need * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->bm_all = nullptr;
+        return 0;  // no bitmaps: the joins search the lists instead
+      }
+      fprintf(stderr, "[yrwi] url-id bitmaps without J5 arrays: no device memory for both\n");
+    }
     ctx->bm_cap = need;
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->bm_all, 0, bm_words * 8, st));  // the J5 arrays are written whole
@@ -677,7 +689,12 @@ int repack_index(CtxBase* ctx, bool force) {
   const char* e = getenv("YRWI_REPACK_MIN_MB");  // read per call: tests lower it
   const size_t min_dead = (size_t)((e ? atof(e) : 256.0) * (double)(1 << 20));
   if (!force && (dead <= live || dead < min_dead)) return 0;
+  // a repack that failed for want of memory is not retried until the index changes
+  if (!force && ctx->repack_blocked_at == used) return 0;
   hipStream_t st = ctx->stream;
+  // Transactional: every live list is copied into `fresh` while its new pointers
+  // collect in a side table; they replace the lists' pointers only once every copy
+  // is enqueued.  On failure `fresh` is freed and the old layout stays in use.
   Arena fresh(ctx->index_mem.min_chunk);
   if (live > 0) fresh.reserve(live);
   auto move = [&](auto*& ptr, size_t bytes) -> bool {
@@ -689,20 +706,28 @@ int repack_index(CtxBase* ctx, bool force) {
     ptr = reinterpret_cast<T*>(q);
     return true;
   };
+  std::vector<std::pair<ListRec*, ListRec>> moved;
+  moved.reserve(ctx->lists.size());
+  bool ok = true;
   for (auto& kv : ctx->lists) {
     ListRec& L = kv.second;
     if (L.n == 0) continue;
     const size_t n = (size_t)L.n;
-    bool ok = move(L.rows, n * 40) && move(L.khi, n * 8) && move(L.klo, n) &&
-              (L.feat ? move(L.feat, n * FEAT_BYTES) : true) && (L.uid && !in_uid_all(L) ? move(L.uid, n * 4) : true);
-    if (!ok) {  // the lists moved so far live in `fresh`, the others in the old chunks: keep both
-      HIPCHK(ctx, hipStreamSynchronize(st));
-      for (auto& c : fresh.chunks) ctx->index_mem.chunks.push_back(c);
-      fresh.chunks.clear();
-      ctx->index_mem.cur = ctx->index_mem.chunks.size();  // the next allocation opens a new chunk
-      return ctx->fail(YRWI_E_NOMEM, "index repack");
-    }
+    ListRec N = L;
+    ok = move(N.rows, n * 40) && move(N.khi, n * 8) && move(N.klo, n) &&
+         (N.feat ? move(N.feat, n * FEAT_BYTES) : true) && (N.uid && !in_uid_all(N) ? move(N.uid, n * 4) : true);
+    if (!ok) break;
+    moved.emplace_back(&L, N);
   }
+  if (!ok) {
+    hipStreamSynchronize(st);  // copies into `fresh` may be in flight
+    fresh.release();
+    ctx->repack_blocked_at = used;
+    fprintf(stderr, "[yrwi] index repack skipped: no device memory for %.1f MB of live lists (old layout kept)\n",
+            live / 1e6);
+    return 0;
+  }
+  for (auto& m : moved) *m.first = m.second;
   HIPCHK(ctx, hipStreamSynchronize(st));
   ctx->index_mem.release();
   ctx->index_mem.chunks.swap(fresh.chunks);

@@ -278,7 +278,7 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
       ok = ok && hipStreamSynchronize(ctx->stream) == hipSuccess;
       if (d_flag) hipFree(d_flag);
       if (ok && !flag && ctx->hostx) {
-        hostx_close(ctx->hostx, false);
+        hostx_close(ctx->hostx, rank == 0);  // some rank never mapped it: nobody else unlinks the name
         ctx->hostx = nullptr;
         for (Lane* L : ctx->lanes) L->hostx = nullptr;
       }
@@ -308,7 +308,9 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   close_lanes(ctx);
-  hostx_close(ctx->hostx, false);  // unlinked once every rank mapped it (hostx_open)
+  // unlinked once every rank mapped it (hostx_open); rank 0 unlinks it again in
+  // case some rank never did (ENOENT is harmless)
+  hostx_close(ctx->hostx, ctx->rank == 0);
   ctx->hostx = nullptr;
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
@@ -410,6 +412,8 @@ extern "C" int yrwi_get_list(yrwi_ctx* ctx, const uint8_t term[12], uint8_t* row
   KeyT tk;
   if (!ctx || !n || cap < 0 || (cap > 0 && !rows40)) return YRWI_E_ARG;
   if (!key_of(term, &tk)) return ctx->fail(YRWI_E_HASH, "term hash is not well-formed Base64");
+  // like put_list: no batch in flight (the copy below runs on lane 0's stream)
+  drain(ctx);
   auto it = ctx->lists.find(tk);
   *n = it == ctx->lists.end() ? 0 : it->second.n;
   if (*n == 0) return 0;
@@ -684,6 +688,8 @@ struct Timing {
   std::vector<std::array<hipEvent_t, 3>> kjoin;
   std::vector<std::array<hipEvent_t, 2>> kexcl;  // around each exclusion step's k_probe
   std::vector<std::array<hipEvent_t, 2>> kcompact;  // around each k_compact launch
+  std::vector<std::array<hipEvent_t, 2>> kreduce;   // around each k_reduce + k_shard_fin
+  std::vector<std::array<hipEvent_t, 2>> kscore;    // around each pass's k_score launches
   // around every group of back-to-back kernel launches of the batch (no host
   // synchronisation inside a span): their sum is the batch's kernel time
   std::vector<std::array<hipEvent_t, 2>> spans;
@@ -1256,6 +1262,15 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   hipEvent_t sp = span_open(ctx, tm);
   if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
+  if (tm) tm->kreduce.push_back(tm->spans.back());
+  if (st) {
+    st->n_rank_passes++;
+    for (int qi = 0; qi < nq; qi++) {
+      const int64_t n = rq[(size_t)qi].n;
+      st->bytes_reduce += (int64_t)FEAT_BYTES * n + (rq[(size_t)qi].removed ? n : 0);
+      st->bytes_score += (int64_t)FEAT_BYTES * n + (rq[(size_t)qi].removed ? n : 0);
+    }
+  }
   if (shx && any_auth) {
     int rc2 = exchange_host_counts(ctx, nq, nslots, slot_base, d_hkeys, d_hcnt, d_ss);
     if (rc2) return rc2;
@@ -1325,6 +1340,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
                    ctx->stream))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
+  if (tm) tm->kscore.push_back(tm->spans.back());
   mark(4);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
@@ -1518,8 +1534,10 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
 static int run_batch_part(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
                           yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   L->enter();
+  const int64_t seq = L->seq;  // (passing the turn after the final collective clears L->seq)
   const int rc = run_batch_part_(ix, L, q, nq, kmax, out, nout, st);
-  if (rc && L->hostx) hostx_abort(L->hostx);  // peers waiting on this part's exchanges fail fast
+  // peers waiting on this part's exchanges fail fast; later parts are unaffected
+  if (rc && L->hostx) hostx_abort(L->hostx, seq);
   turn_release(L);  // error paths, parts without collectives: the turn still passes in order
   L->release_after_final = false;
   L->leave();
@@ -1592,6 +1610,10 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_compact_ns += (int64_t)(ms * 1e6);
       for (auto& ev : tm.spans)
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_kernels_ns += (int64_t)(ms * 1e6);
+      for (auto& ev : tm.kreduce)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_reduce_ns += (int64_t)(ms * 1e6);
+      for (auto& ev : tm.kscore)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_scorek_ns += (int64_t)(ms * 1e6);
       if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
       if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
     }
@@ -1699,6 +1721,11 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->n_realloc += p.n_realloc;
       st->n_probe_dispatches += p.n_probe_dispatches;
       st->t_probe_all_ns += p.t_probe_all_ns;
+      st->n_rank_passes += p.n_rank_passes;
+      st->t_reduce_ns += p.t_reduce_ns;
+      st->t_scorek_ns += p.t_scorek_ns;
+      st->bytes_reduce += p.bytes_reduce;
+      st->bytes_score += p.bytes_score;
     }
     st->t_total_ns = now_ns() - t0;
   }

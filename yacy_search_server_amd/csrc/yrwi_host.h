@@ -393,6 +393,7 @@ struct CtxBase {
   bool dict_valid = false;   // every list outside dict_pending has url ids in the dictionary
   int64_t dict_churn = 0;    // postings removed or replaced since the last full rebuild
   int64_t index_repacks = 0; // index memory compactions (yrwi_dict.hip repack_index)
+  size_t repack_blocked_at = SIZE_MAX;  // index_mem.total_used when a repack last failed (not retried until it changes)
   int64_t dict_full_builds = 0, dict_incremental = 0;
   std::string err;
   int64_t npostings = 0;
@@ -576,7 +577,7 @@ int check_url_ids(CtxBase* ctx, int64_t* bad);
 
 HostX* hostx_open(const uint8_t id[128], int world, int rank);  // nullptr: not available (device fallback)
 void hostx_close(HostX* x, bool unlink_name);
-void hostx_abort(HostX* x);  // a batch part failed: every rank's pending and later exchanges fail at once
+void hostx_abort(HostX* x, int64_t seq);  // batch part `seq` failed: every rank's exchanges of that part fail at once
 int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)

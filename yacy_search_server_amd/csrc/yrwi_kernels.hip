@@ -960,13 +960,16 @@ __device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, co
   }
 }
 
-template <bool LONG>
+// MARK: an exclusion step (its own instantiation, so kernel traces tell the
+// include steps' dispatches from the exclusion steps')
+template <bool LONG, bool MARK>
 __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
-                                                     int mark, const int2* __restrict__ perm) {
+                                                     const int2* __restrict__ perm) {
+  constexpr int mark = MARK ? 1 : 0;
   __shared__ int32_t sScan[4];
   __shared__ uint64_t sScan64[4];
 #if PROBE_LDS > 0
@@ -3346,14 +3349,10 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (probe_tiles > 0) {
-    if (long_tiles)
-      hipLaunchKernelGGL(k_probe<true>, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base,
-                         d_pdesc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0,
-                         (const int2*)pperm);
-    else
-      hipLaunchKernelGGL(k_probe<false>, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base,
-                         d_pdesc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0,
-                         (const int2*)pperm);
+    auto kp = long_tiles ? (mark ? k_probe<true, true> : k_probe<true, false>)
+                         : (mark ? k_probe<false, true> : k_probe<false, false>);
+    hipLaunchKernelGGL(kp, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm);
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {

@@ -483,8 +483,10 @@ class RWIIndex:
         return PendingBatch(self, ticket, nq, kmax, (arr, keep, hits, nout, st))
 
     def search_batch_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> None:
-        """Zero-marshalling batch call for benchmarks (pre-built ctypes arrays)."""
-        _check(self._h, _lib.lib().yrwi_query_batch(self._h, cq, nq, kmax, hits, nout, ctypes.byref(st)))
+        """Zero-marshalling batch call for benchmarks (pre-built ctypes arrays).
+        st None: no statistics (yrwi_stats* NULL, no HIP events: the production call)."""
+        _check(self._h, _lib.lib().yrwi_query_batch(self._h, cq, nq, kmax, hits, nout,
+                                                    ctypes.byref(st) if st is not None else None))
 
     # ---- asynchronous batches (yrwi_query_batch_submit / _wait) ----
     def submit_raw(self, cq, nq: int, kmax: int, hits, nout, st) -> int:
