@@ -317,6 +317,22 @@ typedef struct yrwi_arrival {
 /* Applies arrivals in array order (per event); arrivals of different events run
  * in parallel, one workgroup per event.  Returns the first nonzero rc. */
 int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr);
+/* ReferenceOrder.normalizeWith(container, local) + cardinal of each of its rows
+ * for a drop-in ReferenceOrder whose SearchEvent.addRWIs stays in Java
+ * (ReferenceOrder.java:70-79,163-265; GpuReferenceOrder): the container continues
+ * the event's ReferenceOrder exactly as an arrival does -- min/max and the
+ * max-distance fold accumulate over every container given so far, the host counts
+ * (doms, maxdomcount) too -- and scores[i] = cardinal(row i) under the state after
+ * this container (settled over it).  The event's doublecheck set,
+ * flag counts and stack are not touched (addRWIs keeps its own).  Do not mix
+ * with yrwi_event_add on one event. */
+int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* rows40, int64_t n, int32_t local,
+                     int64_t* scores);
+/* ReferenceOrder.authority(hostHash) (ReferenceOrder.java:213-216) against the
+ * event's accumulated host counts: out[i] = (doms(h_i) << 8) / (1 + maxdomcount),
+ * h_i the 6-character host hash at hosts6 + 6 i (url-hash chars 6..11).  The
+ * counts exist when the event's profile has coeff_authority > 12 (else 0). */
+int yrwi_event_authority(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* hosts6, int32_t n, int32_t* out);
 typedef struct yrwi_event_info {
   int32_t flagcount[32];        /* SearchEvent.flagcount */
   int64_t postings_in;          /* rows received */

@@ -250,6 +250,44 @@ JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAdd(JNIEnv* env, j
   return rc;
 }
 
+/* ReferenceOrder.normalizeWith + cardinal continuing the event's ReferenceOrder
+ * (yrwi_event_order): one score per row of the container, in its order */
+JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOrder(JNIEnv* env, jclass c, jlong ctx, jlong ev,
+                                                                         jbyteArray rows, jint n, jboolean local) {
+  jlong* sc = (jlong*)malloc(sizeof(jlong) * (size_t)(n > 0 ? n : 1));
+  if (!sc) return NULL;
+  /* the rows are staged by the library before any device work: a short critical region */
+  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
+  int rc = yrwi_event_order((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, (const uint8_t*)p, n,
+                            local ? 1 : 0, (int64_t*)sc);
+  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  jlongArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewLongArray(env, n);
+    (*env)->SetLongArrayRegion(env, res, 0, n, sc);
+  }
+  free(sc);
+  return res;
+}
+
+/* ReferenceOrder.authority of n 6-byte host hashes against the event's host counts */
+JNIEXPORT jintArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAuthority(JNIEnv* env, jclass c, jlong ctx,
+                                                                            jlong ev, jbyteArray hosts6, jint n) {
+  jbyte* h = (*env)->GetByteArrayElements(env, hosts6, NULL);
+  jint* out = (jint*)malloc(sizeof(jint) * (size_t)(n > 0 ? n : 1));
+  int rc = out ? yrwi_event_authority((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, (const uint8_t*)h, n,
+                                      (int32_t*)out)
+               : YRWI_E_NOMEM;
+  (*env)->ReleaseByteArrayElements(env, hosts6, h, JNI_ABORT);
+  jintArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewIntArray(env, n);
+    (*env)->SetIntArrayRegion(env, res, 0, n, out);
+  }
+  free(out);
+  return res;
+}
+
 /* rwiStack contents (yrwi_hit records) */
 JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventResult(JNIEnv* env, jclass c, jlong ctx, jlong ev,
                                                                           jint maxn) {

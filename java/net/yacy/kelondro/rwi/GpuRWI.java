@@ -8,7 +8,7 @@
 //   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.listSizes(...) + joinExclude(...) (GpuTermSearch)
 //   kelondro/rwi/AbstractIndex.java:116        -> GpuRWI.getList(...) (TermSearch.inclusion, on demand)
 //   kelondro/rwi/ReferenceContainer.java:310   -> GpuRWI.joinExclude(...)
-//   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.normalizeScore(...)
+//   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.eventOrder(...) (GpuReferenceOrder: one event per SearchEvent)
 //   search/query/SearchEvent.java:612-631      -> GpuRWI.query(...) (whole local RWI path)
 //   search/query/SearchEvent.java:736-806,1297 -> GpuRWI.queryFiltered(...) (constraints, doubledom)
 //   kelondro/rwi/IndexCell.java:353-386        -> GpuRWI.loadHeaps(...) (BLOB heaps into HBM)
@@ -116,6 +116,23 @@ public final class GpuRWI implements AutoCloseable {
         check(eventAdd(this.ctx, event, containerRows, n, local));
     }
 
+    /** ReferenceOrder.normalizeWith(container, local) + cardinal of every row, continuing
+     *  the event's ReferenceOrder (yrwi_event_order): min/max, the max-distance fold and
+     *  the host counts accumulate over every container given to the event; the scores
+     *  are under the state after this one.  The event's stack is not touched. */
+    public long[] eventOrder(final long event, final byte[] containerRows, final int n, final boolean local) {
+        final long[] sc = eventOrder(this.ctx, event, containerRows, n, local);
+        if (sc == null) throw new IllegalStateException("yrwi_event_order failed");
+        return sc;
+    }
+
+    /** ReferenceOrder.authority(hostHash) against the event's accumulated host counts. */
+    public int eventAuthority(final long event, final byte[] hostHash6) {
+        final int[] a = eventAuthority(this.ctx, event, hostHash6, 1);
+        if (a == null) throw new IllegalStateException("yrwi_event_authority failed");
+        return a[0];
+    }
+
     public byte[] eventResult(final long event, final int maxn) {
         return eventResult(this.ctx, event, maxn);
     }
@@ -199,6 +216,8 @@ public final class GpuRWI implements AutoCloseable {
                                          long maxPostings);
     private static native int eventAdd(long ctx, long event, byte[] rows, int n, boolean local);
     private static native byte[] eventResult(long ctx, long event, int maxn);
+    private static native long[] eventOrder(long ctx, long event, byte[] rows, int n, boolean local);
+    private static native int[] eventAuthority(long ctx, long event, byte[] hosts6, int n);
     private static native byte[] eventPull(long ctx, long event, boolean skipDoubleDom, int maxn);
     private static native void eventClose(long ctx, long event);
     private static native String[] indexAbstracts(long ctx, byte[] words, int nwords, long capacity);

@@ -2,29 +2,36 @@
 // libyrwi on the GPU (SURVEY.md §8b drop-in; UNVERIFIED: no JDK in this image).
 //
 // Replaces (paths relative to source/net/yacy):
-//   search/ranking/ReferenceOrder.java:70-79   normalizeWith -> one yrwi_normalize_score call
-//   search/ranking/ReferenceOrder.java:213-216 authority     -> host counts of the last container
-//   search/ranking/ReferenceOrder.java:223-265 cardinal      -> the settled score of that posting
+//   search/ranking/ReferenceOrder.java:70-79,163-210  normalizeWith -> yrwi_event_order on the order's event
+//   search/ranking/ReferenceOrder.java:213-216        authority     -> yrwi_event_authority (accumulated doms)
+//   search/ranking/ReferenceOrder.java:223-265        cardinal      -> the posting's score from that call
 // Wiring: SearchEvent.<init> (SearchEvent.java:436) constructs
 //   new GpuReferenceOrder(query.ranking, query.targetlang, gpu)
-// instead of new ReferenceOrder(...); SearchEvent.addRWIs is unchanged.
+// instead of new ReferenceOrder(...), and SearchEvent.cleanup() closes it;
+// SearchEvent.addRWIs is unchanged.
 //
-// Semantics: every container handed to normalizeWith is normalised over itself
-// with settled min/max (DESIGN.md §2: the canonical, deterministic reading of
-// the racy reference), then each posting's cardinal is read back.  The queue is
+// Semantics: YaCy keeps ONE ReferenceOrder per SearchEvent, and every container
+// handed to normalizeWith continues it: min/max are cloned from the first posting
+// ever seen and only folded afterwards (ReferenceOrder.java:173-174), the host
+// counts accumulate in doms / maxdomcount (:196-198).  The local container
+// (SearchEvent.java:631), a sitehost retry (:651), every remote peer's container
+// (Protocol.java:802) and heuristic injections (Segment.java:758) are all scored
+// against that accumulated state.  This class holds one libyrwi search event for
+// the order's lifetime and hands it each container (yrwi_event_order): the same
+// accumulation on the GPU, each posting scored under the state after its own
+// container has been folded in (the settled reading of DESIGN.md §2; the
+// reference races the workers' min/max updates against cardinal()).  The queue is
 // returned complete and ends with WordReferenceVars.poison, as addRWIs expects.
 //
 // Per container this class makes no copy of the rows (the RowSet's own byte[]
 // goes to JNI, GpuRows), keeps the scores in one long[] in container order, and
 // each queued entry carries its position in it (Entry), so cardinal(e) is an
-// array read: no per-posting key String and no map.  The host counts behind
-// authority() are built only if something asks for them (the inherited
-// cardinal(URIMetadataNode)); the GPU scores already include authority.
+// array read: no per-posting key String and no map.  authority() asks the GPU's
+// accumulated host counts (they exist when coeff_authority > 12, the only case in
+// which cardinal uses them).
 package net.yacy.search.ranking;
 
-import java.util.HashMap;
 import java.util.Iterator;
-import java.util.Map;
 import java.util.concurrent.BlockingQueue;
 import java.util.concurrent.LinkedBlockingQueue;
 
@@ -35,9 +42,10 @@ import net.yacy.kelondro.index.GpuRows;
 import net.yacy.kelondro.rwi.GpuRWI;
 import net.yacy.kelondro.rwi.ReferenceContainer;
 
-public class GpuReferenceOrder extends ReferenceOrder {
+public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
-    private static final int ROW = 40;  // WordReferenceRow.urlEntryRow.objectsize
+    /** Postings one SearchEvent's order may receive in all (sizes the event's host table). */
+    public static final long DEFAULT_MAX_POSTINGS = 1L << 22;
 
     /** A queued posting with its position in the container's score array. */
     public static final class Entry extends WordReferenceVars {
@@ -56,19 +64,19 @@ public class GpuReferenceOrder extends ReferenceOrder {
     }
 
     private final GpuRWI gpu;
-    private final int[] profile32;
-    private final String language;
-    // the last normalised container's rows (authority() counts its hosts on demand)
-    private volatile byte[] lastRows = null;
-    private volatile int lastCount = 0;
-    private Map<String, Integer> doms = null;
-    private int maxdomcount = 0;
+    private long event;  // yrwi_event*: this order's ReferenceOrder state on the GPU
 
     public GpuReferenceOrder(final RankingProfile profile, final String language, final GpuRWI gpu) {
+        this(profile, language, gpu, DEFAULT_MAX_POSTINGS);
+    }
+
+    public GpuReferenceOrder(final RankingProfile profile, final String language, final GpuRWI gpu,
+                             final long maxPostings) {
         super(profile, language);
         this.gpu = gpu;
-        this.profile32 = GpuRWI.profile32(profile);
-        this.language = language;
+        // "now" is fixed for the event's lifetime (the clone's virtualAge clamp, J6)
+        this.event = gpu.eventOpen(GpuRWI.profile32(profile), language, System.currentTimeMillis(), 1, maxPostings);
+        if (this.event == 0) throw new IllegalStateException("yrwi_event_open failed");
     }
 
     @Override
@@ -77,17 +85,15 @@ public class GpuReferenceOrder extends ReferenceOrder {
         final LinkedBlockingQueue<WordReferenceVars> out = new LinkedBlockingQueue<WordReferenceVars>();
         final int m = container.size();
         if (m > 0) {
-            // RowSet.chunkcache: the sorted 40-byte WordReferenceRow rows, handed over as they are
+            // RowSet.chunkcache: the container's 40-byte WordReferenceRow rows in its order
             final byte[] rows = GpuRows.sortedRows(container);
-            final long[] sc = this.gpu.normalizeScore(rows, m, this.profile32, this.language, System.currentTimeMillis());
-            final Iterator<WordReference> i = container.entries();  // the same (sorted) row order
+            final long[] sc;
+            synchronized (this) {  // containers fold into the order one after another
+                sc = this.gpu.eventOrder(this.event, rows, m, local);
+            }
+            final Iterator<WordReference> i = container.entries();  // the same row order
             int p = 0;
             while (i.hasNext()) out.add(new Entry(i.next(), local, sc, p++));
-            synchronized (this) {
-                this.lastRows = rows;
-                this.lastCount = m;
-                this.doms = null;
-            }
         }
         out.add(WordReferenceVars.poison);
         return out;
@@ -95,27 +101,20 @@ public class GpuReferenceOrder extends ReferenceOrder {
 
     @Override
     public synchronized int authority(final String hostHash) {
-        if (this.doms == null) {  // host counts of the last container (ReferenceOrder.java:176-182)
-            final Map<String, Integer> d = new HashMap<String, Integer>();
-            int maxd = 0;
-            final byte[] rows = this.lastRows;
-            for (int r = 0; rows != null && r < this.lastCount; r++) {
-                final String h = ASCII.String(rows, r * ROW + 6, 6);  // url-hash chars 6..11
-                final Integer c0 = d.get(h);
-                final int c = c0 == null ? 1 : c0 + 1;
-                d.put(h, c);
-                if (c > maxd) maxd = c;
-            }
-            this.doms = d;
-            this.maxdomcount = maxd;
-        }
-        final Integer c = this.doms.get(hostHash);
-        return ((c == null ? 0 : c) << 8) / (1 + this.maxdomcount);
+        return this.gpu.eventAuthority(this.event, ASCII.getBytes(hostHash));
     }
 
     @Override
     public long cardinal(final WordReference t) {
         if (t instanceof Entry) return ((Entry) t).score();
         throw new IllegalStateException("cardinal of a posting that was not normalised by this order");
+    }
+
+    @Override
+    public synchronized void close() {
+        if (this.event != 0) {
+            this.gpu.eventClose(this.event);
+            this.event = 0;
+        }
     }
 }

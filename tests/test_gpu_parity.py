@@ -561,3 +561,53 @@ def test_null_stats_production_path(corpus):
     for i, q in enumerate(b):
         got = [(bytes(hits[i * kmax + j].urlhash), hits[i * kmax + j].score) for j in range(nout[i])]
         assert got == [(h, s) for h, s, _ in orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)]
+
+
+@pytest.mark.parametrize("chain", ["1", "0"], ids=["chained", "stepwise"])
+def test_chained_folds_corpus(corpus, chain, monkeypatch):
+    """Chained folds (ChainQ: one join step, then k_chain tests each match against
+    the later include lists and the exclusion lists) and the step-by-step fold
+    (YRWI_NO_CHAIN=1): 2-4 include terms with 0-2 excluded terms, plus quoted
+    queries (maxDistance: never chained); results equal the oracle's, tie-breaks
+    included."""
+    monkeypatch.setenv("YRWI_NO_CHAIN", "0" if chain == "1" else "1")
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    qs = synth.queries(cfg, 40, 2, 4, 2, qseed=2024) + synth.queries(cfg, 20, 3, 4, 0, qseed=2025)
+    batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], now_ms=NOW,
+                   max_distance=(len(inc) - 1 if i % 7 == 3 else 2147483647)) for i, (inc, exc) in enumerate(qs)]
+    got = ix.search_batch(batch)
+    for q, g in zip(batch, got):
+        exp = orc.search(d, q.include, q.exclude, max_distance=q.max_distance, now_ms=NOW, k=100)
+        assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp
+    for q in batch[:10]:
+        assert np.array_equal(ix.term_search(q.include, q.exclude, q.max_distance, NOW),
+                              orc.term_search(d, q.include, q.exclude, q.max_distance, NOW))
+
+
+@pytest.mark.parametrize("bm", ["64", "0"], ids=["bitmaps", "no_bitmaps"])
+def test_chained_folds_long_lists(long_lists, bm, monkeypatch):
+    """Chained folds over C2's eight longest lists: with url-id bitmaps every later
+    list is tested by one bitmap word per match; without (YRWI_BM_DIV=0) by the
+    list's ids staged around the tile's range in LDS, or -- ranges longer than the
+    LDS stage -- through the line heads (k_chain_part / k_chain)."""
+    monkeypatch.setenv("YRWI_BM_DIV", bm)
+    cfg, df, big, idx, _ = long_lists
+    ix = RWIIndex(0)
+    try:
+        for t in big:
+            ix.add(idx.hashes[t], idx.list_rows(t))
+        d = idx.as_dict()
+        rng = np.random.default_rng(11)
+        batch = []
+        for i in range(16):
+            pick = [int(x) for x in rng.permutation(big)]
+            ni = 2 + i % 3
+            ne = (i // 3) % 3
+            batch.append(Query([idx.hashes[t] for t in pick[:ni]], [idx.hashes[t] for t in pick[ni:ni + ne]],
+                               now_ms=NOW))
+        for q, g in zip(batch, ix.search_batch(batch)):
+            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == orc.search(d, q.include, q.exclude, now_ms=NOW,
+                                                                               k=100)
+    finally:
+        ix.close()

@@ -126,3 +126,73 @@ def test_inclusion_sizes_and_abstracts(corpus):
         done += 1
     assert done > 0
     assert ix.index_abstracts([idx.hashes[inc[0]], b"AAAAAAAAAAAA"]) == []
+
+
+def _jl_profile(name):
+    import java_literal as jl
+    if name == "default":
+        return jl.RankingProfile()
+    if name == "c5":
+        return jl.RankingProfile.parse("", "date=15,domlength=15,authority=13,tf=10")
+    p = jl.RankingProfile()
+    p.all_zero()
+    p.coeff_date = 15
+    return p
+
+
+@pytest.mark.parametrize("profile", ["default", "c5", "date"])
+def test_reference_order_accumulates_across_arrivals(corpus, profile):
+    """GpuReferenceOrder over one SearchEvent's arrivals (yrwi_event_order): the
+    local container (RWIProcess.run, SearchEvent.java:631), a sitehost retry's
+    container (:651), two remote peers' containers (Protocol.java:802; unsorted,
+    duplicates inside and across) and a heuristic injection (Segment.java:758).
+    One ReferenceOrder per SearchEvent: min/max, the max-distance fold and the host
+    counts accumulate over every container (ReferenceOrder.java:163-216), and each
+    container's postings are scored under the state after it -- equal, score for
+    score, to the oracle's persistent ReferenceOrder (java_literal.ReferenceOrder).
+    SearchEvent.addRWIs stays in Java: its doublecheck and rwiStack fed with those
+    scores give the stack the GPU event path (yrwi_event_add) keeps; authority()
+    reads the accumulated host counts."""
+    import java_literal as jl
+    cfg, idx, ix = corpus
+    gp = {"default": RankingProfile(), "c5": RankingProfile("", "date=15,domlength=15,authority=13,tf=10"),
+          "date": RankingProfile.date()}[profile]
+    lp = _jl_profile(profile)
+    whole = idx.as_dict()
+    rng = np.random.default_rng({"default": 1, "c5": 2, "date": 3}[profile])
+    qs = synth.queries(cfg, 6, 2, 3, 0, qseed=777)
+    local = orc.term_search(whole, [idx.hashes[t] for t in qs[0][0]], [], 2147483647, NOW)
+    retry = orc.term_search(whole, [idx.hashes[t] for t in qs[1][0]], [], 2147483647, NOW)
+    allrows = np.asarray(idx.rows, dtype=np.uint8)
+    remote = []
+    for _ in range(3):
+        take = rng.integers(0, len(allrows), 400)
+        take[:80] = take[rng.integers(0, 400, 80)]  # duplicates inside the container
+        r = allrows[take].copy()
+        d = rng.random(400) < 0.5
+        r[d, 38] = rng.integers(0, 40, int(d.sum()))  # word distances: the max-distance fold has work
+        remote.append(r)
+    arrivals = [(local, True), (retry, True), (remote[0], False), (remote[1], False), (remote[2], False)]
+    total = sum(len(r) for r, _ in arrivals)
+    order = jl.ReferenceOrder(lp, "en")
+    stack = jl.ReverseQueue(3000)
+    urls = set()
+    with ix.event(gp, "en", NOW, k=3000, max_postings=total + 16) as ev, \
+            ix.event(gp, "en", NOW, k=3000, max_postings=total + 16) as ev_add:
+        for rows, loc in arrivals:
+            got = ev.order(rows, loc)                                   # GpuReferenceOrder.normalizeWith
+            entries = order.normalize_with([bytes(x) for x in rows], NOW)
+            assert got.tolist() == [order.cardinal(e) for e in entries]  # cardinal(e) of every posting
+            for r, sc in zip(rows, got.tolist()):                       # SearchEvent.addRWIs (unchanged Java)
+                h = bytes(r[:12])
+                if h in urls:
+                    continue
+                urls.add(h)
+                stack.put(sc, h)
+            ev_add.add_rwis(rows, loc)
+        hits, info = ev_add.results()
+        assert [(h.urlhash, h.score) for h in hits] == [(h, w) for (w, _, h) in stack.items]
+        hosts = sorted({bytes(r[6:12]) for r in allrows[rng.integers(0, len(allrows), 50)]})
+        if lp.coeff_authority > 12:  # the host counts exist (and enter cardinal) only then
+            assert ev.authority(hosts) == [order.authority(h) for h in hosts]
+            assert info.maxdomcount == order.maxdomcount

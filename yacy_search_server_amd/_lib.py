@@ -156,6 +156,8 @@ SIGNATURES = {
     "yrwi_event_pull": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, ctypes.POINTER(CHit), ctypes.c_int32,
                                        ctypes.POINTER(ctypes.c_int32)]),
     "yrwi_event_close": (None, [_VP, _VP]),
+    "yrwi_event_order": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int64, ctypes.c_int32, _VP]),
+    "yrwi_event_authority": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int32, _VP]),
     "yrwi_index_abstracts": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _VP,
                                             ctypes.c_int64, _VP, ctypes.POINTER(ctypes.c_int32)]),
     "yrwi_secondary_search": (ctypes.c_int, [_VP, ctypes.POINTER(CAbstract), ctypes.c_int32, ctypes.c_int32,

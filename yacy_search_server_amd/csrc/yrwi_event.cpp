@@ -205,6 +205,76 @@ extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
   return first;
 }
 
+extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* rows40, int64_t n, int32_t local,
+                                int64_t* scores) {
+  if (!ctx || !ev || n < 0 || n >= ((int64_t)1 << 31) || (n > 0 && (!rows40 || !scores))) return YRWI_E_ARG;
+  if (n == 0) return 0;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  uint8_t* d_rows = arena_alloc<uint8_t>(L, n * YRWI_ROW_BYTES);
+  int64_t* d_sc = arena_alloc<int64_t>(L, n);
+  EvDev* d_ev = arena_alloc<EvDev>(L, 1);
+  EvJob* d_job = arena_alloc<EvJob>(L, 1);
+  int32_t* d_jb = arena_alloc<int32_t>(L, 2);
+  int32_t* d_status = arena_alloc<int32_t>(L, 1);
+  if (!d_rows || !d_sc || !d_ev || !d_job || !d_jb || !d_status) return ctx->fail(YRWI_E_NOMEM, "arena");
+  uint8_t* stg = stage_reserve(L, &L->out_stage, (size_t)n * YRWI_ROW_BYTES, true);
+  if (!stg) return ctx->take(L, YRWI_E_HIP);
+  std::memcpy(stg, rows40, (size_t)n * YRWI_ROW_BYTES);
+  hipStream_t s = L->stream;
+  HIPCHK(ctx, hipMemcpyAsync(d_rows, stg, (size_t)n * YRWI_ROW_BYTES, hipMemcpyHostToDevice, s));
+  EvJob J{};
+  J.ev = 0;
+  J.local = local != 0;
+  J.rows = d_rows;
+  J.n = n;
+  J.scores = d_sc;
+  std::vector<EvDev> hev{ev->h};
+  std::vector<EvJob> jobs{J};
+  std::vector<int32_t> jb{0, 1};
+  if (upload(L, d_ev, hev, d_job, jobs, d_jb, jb)) return ctx->take(L, YRWI_E_HIP);
+  if (launch_event_add(d_ev, d_job, d_jb, 1, d_status, s)) return ctx->fail(YRWI_E_HIP, "event_order launch");
+  int32_t st = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&st, d_status, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipMemcpyAsync(scores, d_sc, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, lane_sync(L));
+  if (st == YRWI_E_HASH) return ctx->fail(st, "container: url hash is not well-formed Base64");
+  if (st == YRWI_E_NULL_LANGUAGE) return ctx->fail(st, "container: row with empty language cell (reference NPE)");
+  if (st == YRWI_E_CAPACITY) return ctx->fail(st, "event tables full: max_postings too small");
+  return st;
+}
+
+extern "C" int yrwi_event_authority(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* hosts6, int32_t n, int32_t* out) {
+  if (!ctx || !ev || n < 0 || (n > 0 && (!hosts6 || !out))) return YRWI_E_ARG;
+  if (n == 0) return 0;
+  std::vector<uint64_t> keys((size_t)n);
+  for (int32_t i = 0; i < n; i++) {
+    uint64_t h = 0;
+    for (int j = 0; j < 6; j++) {
+      const int a = AHP[hosts6[6 * (size_t)i + (size_t)j]];
+      if (a < 0) return ctx->fail(YRWI_E_HASH, "host hash is not well-formed Base64");
+      h = (h << 6) | (uint64_t)a;
+    }
+    keys[(size_t)i] = h + 1;  // the host tables' key (host36 + 1)
+  }
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  uint64_t* d_keys = arena_alloc<uint64_t>(L, n);
+  int32_t* d_out = arena_alloc<int32_t>(L, n);
+  EvDev* d_ev = arena_alloc<EvDev>(L, 1);
+  if (!d_keys || !d_out || !d_ev) return ctx->fail(YRWI_E_NOMEM, "arena");
+  std::vector<EvDev> hev{ev->h};
+  if (upload(L, d_ev, hev, d_keys, keys)) return ctx->take(L, YRWI_E_HIP);
+  if (launch_event_authority(d_ev, d_keys, n, d_out, L->stream)) return ctx->fail(YRWI_E_HIP, "authority launch");
+  HIPCHK(ctx, hipMemcpyAsync(out, d_out, (size_t)n * 4, hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  return 0;
+}
+
 extern "C" int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
                                  yrwi_event_info* info) {
   if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out)) return YRWI_E_ARG;

@@ -569,6 +569,7 @@ static void plan_finish(Plan* P, const int64_t* ng_inc, const int64_t* ng_exc) {
   bool use_excl = P->nexc > 0;
   for (int i = 0; i < P->nexc; i++)
     if (ng_exc[i] == 0) use_excl = false;
+  P->nexcl_g = use_excl ? P->nexc : 0;
   if (use_excl)
     for (int i = 0; i < P->nexc; i++)
       if (P->lexc[i]) P->excl.push_back(P->lexc[i]);
@@ -793,9 +794,29 @@ static BandOrder band_order(Lane* ctx, int64_t tiles, int64_t merge_tiles, bool 
   return bo;
 }
 
+// A chained step whose compaction waits for the fold's dispatch modes (k_chain
+// counts the intersections they depend on): what launch_compact needs.
+struct PendingCompact {
+  bool active = false;
+  JoinQ* d_jobs = nullptr;
+  int64_t* d_tb = nullptr;
+  int nj = 0;
+  int64_t tiles = 0;
+  uint2* d_pairs = nullptr;
+  uint32_t* d_puid = nullptr;
+  int64_t* d_src = nullptr;
+  int32_t* d_cnt = nullptr;
+  int64_t* d_off = nullptr;
+  BandOrder bo;
+  std::vector<std::array<int64_t, CHAIN_LVL>> level;  // per job (layout order): k_chain's level counts
+};
+
 // One fold step's join jobs: layout, launch, joined sizes back to the plans.
+// chq (indexed by plan): the ChainQ of every chained query; a step with chained
+// jobs runs k_chain and leaves its compaction to the caller (pend).
 static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>& jobs, std::vector<int>& owner,
-                         yrwi_stats* st, Timing* tm) {
+                         yrwi_stats* st, Timing* tm, const std::vector<ChainQ>* chq = nullptr,
+                         PendingCompact* pend = nullptr) {
   std::vector<int64_t> tile_base;
   int nmerge;
   int64_t merge_tiles, tiles;
@@ -813,9 +834,14 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       if (J.algo != JA_MERGE) st->bytes_probe_loaded += loaded;
       st->bytes_alg_capped += std::min(K, loaded);
     }
-  // joined sizes land in pinned host memory: k_scan_tiles writes them through its
-  // device address (no copy engine), the host reads them after the step's sync
-  uint8_t* land = stage_reserve(ctx, &ctx->down_stage, (size_t)nj * sizeof(int64_t), true);
+  bool chain = false;
+  if (chq)
+    for (int j = 0; j < nj; j++) chain |= plans[(size_t)owner[(size_t)j]].chain;
+  // joined sizes (and chained jobs' level counts) land in pinned host memory:
+  // k_scan_tiles writes them through its device address (no copy engine), the host
+  // reads them after the step's sync
+  const size_t land_words = (size_t)nj * (chain ? 1 + CHAIN_LVL : 1);
+  uint8_t* land = stage_reserve(ctx, &ctx->down_stage, land_words * sizeof(int64_t), true);
   if (!land) return YRWI_E_HIP;
   int64_t* d_mout = nullptr;
   HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_mout), land, 0));
@@ -839,20 +865,53 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   int64_t* d_off = arena_alloc<int64_t>(ctx, tiles);
   if (!d_jobs || !d_tb || !d_split || !d_pdesc || !d_pairs || !d_puid || !d_src || !d_cnt || !d_off)
     return ctx->fail(YRWI_E_NOMEM, "arena");
+  // chained jobs: their ChainQ (level counts into the landing buffer, the later
+  // include lists' rows in slot-indexed arrays beside the pairs), per-tile level
+  // counts and the list ranges of k_chain_part
+  int32_t* d_lvl = nullptr;
+  ProbeDesc* d_crange = nullptr;
+  std::vector<ChainQ> cq;
+  ChainQ* d_cq = nullptr;
+  if (chain) {
+    d_lvl = arena_alloc<int32_t>(ctx, tiles * CHAIN_LVL);
+    d_crange = arena_alloc<ProbeDesc>(ctx, tiles * CHAIN_MAXL);
+    d_cq = arena_alloc<ChainQ>(ctx, nj);
+    if (!d_lvl || !d_crange || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
+    int maxi = 0;
+    for (int j = 0; j < nj; j++)
+      if (plans[(size_t)owner[(size_t)j]].chain) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].ninc);
+    int32_t* d_tup[CHAIN_MAXI] = {nullptr, nullptr};  // rows in the later include lists, indexed like d_pairs
+    for (int l = 0; l < maxi; l++)
+      if (!(d_tup[l] = arena_alloc<int32_t>(ctx, npairs))) return ctx->fail(YRWI_E_NOMEM, "arena");
+    for (int j = 0; j < nj; j++) {
+      JoinQ& J = jobs[(size_t)j];
+      const int pq = owner[(size_t)j];
+      if (!plans[(size_t)pq].chain) continue;
+      ChainQ C = (*chq)[(size_t)pq];
+      C.level = d_mout + nj + (int64_t)j * CHAIN_LVL;
+      for (int l = 0; l < CHAIN_MAXI; l++) C.tup[l] = l < C.ninc ? d_tup[l] : nullptr;
+      J.chain = d_cq + (int64_t)cq.size();
+      cq.push_back(C);
+    }
+  }
   const int64_t h2 = hprof ? now_ns() : 0;
-  if (upload(ctx, d_jobs, jobs, d_tb, tile_base)) return YRWI_E_HIP;
+  if (chain ? upload(ctx, d_jobs, jobs, d_tb, tile_base, d_cq, cq) : upload(ctx, d_jobs, jobs, d_tb, tile_base))
+    return YRWI_E_HIP;
   const int64_t h3 = hprof ? now_ns() : 0;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
-                       false, long_tiles, bo,
-                       ctx->stream, e0, em, e1, c0, c1))
+                       false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
-    tm->kcompact.push_back({c0, c1});
+    if (chain) {
+      hipEventRecord(c1, ctx->stream);  // the span ends after k_chain / k_scan_tiles; compaction comes later
+    } else {
+      tm->kcompact.push_back({c0, c1});
+    }
     tm->spans.push_back({sp, c1});
   }
   if (st) {
@@ -870,10 +929,16 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
             (now_ns() - h5) / 1e6);
   if (st)  // k_compact per joined row: pair + id read, the records it gathers (32 B, + 16 B of the joined
            // side for enumeration steps, + the deferred rows' sources and records), record + id written;
-           // deferred output: A's sources read, sources + id written
+           // deferred output: A's sources read, sources + id written; chained: the rows of every list of
+           // the fold (4 B each beyond the pair), the records of the fold (32 B + 16 B per enumeration step)
     for (int j = 0; j < nj; j++) {
       const JoinQ& J = jobs[(size_t)j];
       const int64_t atw = J.A.tup ? J.A.tw : 0;
+      if (J.chain) {
+        const int64_t t = 2 + (*chq)[(size_t)owner[(size_t)j]].ninc;
+        st->bytes_compact += mh[(size_t)j] * (12 + 4 * (t - 2) + 32 + 24 * (t - 1) + 36);
+        continue;
+      }
       st->bytes_compact += mh[(size_t)j] * (J.out_tup ? 12 + 4 * atw + 4 + 4 * (int64_t)J.out_tw
                                                       : (J.mode == JM_ENUM ? 96 : 80) + 4 * atw +
                                                             (atw > 1 ? 24 * (atw - 1) : 0));
@@ -883,6 +948,24 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     const JoinQ& J = jobs[(size_t)j];
     P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
                    J.out_tup ? J.out_tw : 0};
+  }
+  if (chain && pend) {
+    pend->active = true;
+    pend->d_jobs = d_jobs;
+    pend->d_tb = d_tb;
+    pend->nj = nj;
+    pend->tiles = tiles;
+    pend->d_pairs = d_pairs;
+    pend->d_puid = d_puid;
+    pend->d_src = d_src;
+    pend->d_cnt = d_cnt;
+    pend->d_off = d_off;
+    pend->bo = bo;
+    pend->level.assign((size_t)nj, {0, 0, 0, 0});
+    const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
+    for (int j = 0; j < nj; j++)
+      if (jobs[(size_t)j].chain)
+        for (int l = 0; l < CHAIN_LVL; l++) pend->level[(size_t)j][(size_t)l] = hl[(int64_t)j * CHAIN_LVL + l];
   }
   return 0;
 }
@@ -941,6 +1024,8 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
 // containers: the next list's (Plan.seq_ng) and the accumulated container's,
 // which after the first step is the sum over the shards of their joined rows
 // (one exchange per step that some query continues past; none on one context).
+static ChainList chain_list(const ListRec* L) { return ChainList{L->uid, L->head, L->bm, L->n}; }
+
 static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   const size_t nq = plans.size();
   std::vector<int64_t> acc_g(nq, 0);  // global size of each query's accumulated container
@@ -950,24 +1035,52 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     P.cont = P.seq[0]->dl();
     acc_g[qi] = P.seq_ng[0];
   }
+  static const bool defer = !(getenv("YRWI_NO_DEFER") && atoi(getenv("YRWI_NO_DEFER")));
+  // Chained folds (ChainQ): every query with lists after its first join step --
+  // later includes (t <= 4) and / or exclusions -- and no maxDistance filter.  The
+  // decision rests on global facts only (fold length, exclusion terms in effect),
+  // so every shard takes it alike.  YRWI_NO_CHAIN=1: the step-by-step fold.
+  const char* nc = getenv("YRWI_NO_CHAIN");  // read per call: tests compare both paths in one process
+  const bool chain_on = !(nc && atoi(nc));
+  std::vector<ChainQ> chq(nq);
+  bool any_chain = false;
+  for (size_t qi = 0; qi < nq; qi++) {
+    Plan& P = plans[qi];
+    P.chain = false;
+    if (!chain_on || !defer || P.empty || P.maxd < 65535 || acc_g[qi] == 0) continue;
+    const int t = (int)P.seq.size(), ni = t - 2;
+    if (t < 2 || ni > CHAIN_MAXI || ni + P.nexcl_g == 0 || ni + P.nexcl_g > CHAIN_MAXL) continue;
+    ChainQ& C = chq[qi];
+    std::memset(&C, 0, sizeof(C));
+    C.ninc = ni;
+    for (int l = 0; l < ni; l++) C.l[l] = chain_list(P.seq[(size_t)l + 2]);
+    C.nl = ni;
+    for (const ListRec* E : P.excl) C.l[C.nl++] = chain_list(E);  // this shard's lists of the exclusion terms
+    if (st)
+      for (const ListRec* E : P.excl) st->bytes_alg += 12 * E->n;
+    P.excl.clear();  // excluded inside k_chain: no marks, no exclusion step
+    P.chain = true;
+    any_chain = true;
+  }
   // a query steps at s while it has a list left and its global container is not empty
   auto steps = [&](size_t qi, size_t s) {
     const Plan& P = plans[qi];
-    return !P.empty && P.seq.size() > s + 1 && acc_g[qi] > 0;
+    return !P.empty && P.seq.size() > s + 1 && acc_g[qi] > 0 && !(P.chain && s > 0);
   };
-  static const bool defer = !(getenv("YRWI_NO_DEFER") && atoi(getenv("YRWI_NO_DEFER")));
   for (size_t s = 0;; s++) {
     std::vector<JoinQ> jobs;
     std::vector<int> owner;
     std::vector<FoldSrc> fold;
     std::vector<int> fold_job;
+    std::vector<int> chain_q;  // chained queries with a job in this step (plan index)
     bool any = false, more = false;  // some query steps now / after this step (global decisions)
     for (size_t qi = 0; qi < nq; qi++) {
       if (!steps(qi, s)) continue;
       any = true;
       Plan& P = plans[qi];
-      if (P.seq.size() > s + 2) more = true;
+      if (P.seq.size() > s + 2 && !P.chain) more = true;
       const DList B = P.seq[s + 1]->dl();
+      if (P.chain) P.step_mode[s] = dispatch_mode(acc_g[qi], P.seq_ng[s + 1]);
       if (P.cont.n == 0 || B.n == 0) {  // nothing of this shard survives the step
         P.cont = DList{nullptr, nullptr, nullptr, 0};
         continue;
@@ -985,7 +1098,8 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       // 0..s+1 they join, no records): the next step joins on url ids alone, and
       // only the last step gathers and folds the records of the rows that survive.
       // A maxDistance filter needs every step's joined features: materialised.
-      const bool last = P.seq.size() == s + 2;
+      // A chained query's first step is its only one.
+      const bool last = P.seq.size() == s + 2 || P.chain;
       if (!last && defer && P.maxd >= 65535) {
         J.out_tw = (int32_t)s + 2;
         J.out_tup = arena_alloc<int32_t>(ctx, cap * J.out_tw);
@@ -993,7 +1107,9 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       } else {
         J.out_feat = arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
         if (!J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
-        if (J.A.tup) {
+        if (P.chain) {
+          chain_q.push_back((int)qi);
+        } else if (J.A.tup) {
           FoldSrc F{};
           for (int l = 0; l < J.A.tw; l++) {
             F.feat[l] = P.seq[(size_t)l]->feat;
@@ -1019,8 +1135,92 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       if (upload(ctx, d_fold, fold)) return YRWI_E_HIP;
       for (size_t f = 0; f < fold.size(); f++) jobs[(size_t)fold_job[f]].fold = d_fold + f;
     }
+    // chained queries: their fold programs are written once the modes are known
+    FoldSrc* d_cfold = nullptr;
+    std::vector<int> cfold_of(nq, -1);
+    if (!chain_q.empty()) {
+      d_cfold = arena_alloc<FoldSrc>(ctx, (int64_t)chain_q.size());
+      if (!d_cfold) return ctx->fail(YRWI_E_NOMEM, "arena");
+      for (size_t k = 0; k < chain_q.size(); k++) cfold_of[(size_t)chain_q[k]] = (int)k;
+      for (size_t j = 0; j < jobs.size(); j++)
+        if (cfold_of[(size_t)owner[j]] >= 0) jobs[j].fold = d_cfold + cfold_of[(size_t)owner[j]];
+    }
+    PendingCompact pend;
     if (!jobs.empty())
-      if (int rc = run_join_jobs(ctx, plans, jobs, owner, st, tm)) return rc;
+      if (int rc = run_join_jobs(ctx, plans, jobs, owner, st, tm, any_chain ? &chq : nullptr, &pend)) return rc;
+    if (s == 0 && any_chain) {
+      // the fold's later steps: their dispatch (J3) from the GLOBAL intersection
+      // sizes (k_chain's level counts summed over the shards), then the records
+      std::vector<int> cqs;
+      for (size_t qi = 0; qi < nq; qi++)
+        if (plans[qi].chain && steps(qi, 0)) cqs.push_back((int)qi);
+      std::vector<int> job_of(nq, -1);
+      for (size_t j = 0; j < jobs.size(); j++) job_of[(size_t)owner[j]] = (int)j;
+      std::vector<int64_t> v(cqs.size() * 2, 0);
+      for (size_t k = 0; k < cqs.size(); k++) {
+        const int j = job_of[(size_t)cqs[k]];
+        if (j >= 0 && pend.active) {
+          v[2 * k] = pend.level[(size_t)j][0];
+          v[2 * k + 1] = pend.level[(size_t)j][1];
+        }
+      }
+      std::vector<int64_t> loc = v;
+      if (int rc = allsum_host(ctx, v)) return rc;
+      std::vector<FoldSrc> cf(chain_q.size());
+      for (size_t k = 0; k < cqs.size(); k++) {
+        Plan& P = plans[(size_t)cqs[k]];
+        const int t = (int)P.seq.size();
+        if (t >= 3) P.step_mode[1] = dispatch_mode(v[2 * k], P.seq_ng[2]);
+        if (t >= 4) P.step_mode[2] = dispatch_mode(v[2 * k + 1], P.seq_ng[3]);
+        if (st) {  // the later steps' K (local sizes), charged min(K, the bytes k_chain loads for them)
+          for (int l = 2; l < t; l++) {
+            const int64_t acc = loc[2 * k + (size_t)(l - 2)], n = P.seq[(size_t)l]->n;
+            const int32_t m = P.step_mode[l - 1];
+            const int64_t K = step_bytes(m, acc, n);
+            const int64_t loaded = P.seq[(size_t)l]->bm ? 20 * acc : 4 * acc + std::min(4 * n, 128 * acc);
+            st->bytes_alg += K;
+            st->bytes_probe += K;
+            st->bytes_probe_capped += std::min(K, loaded);
+            st->bytes_probe_loaded += loaded;
+            st->bytes_alg_capped += std::min(K, loaded);
+            if (m == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
+          }
+        }
+        const int f = cfold_of[(size_t)cqs[k]];
+        if (f < 0) continue;  // no job of this query on this shard
+        FoldSrc& F = cf[(size_t)f];
+        for (int l = 0; l < t; l++) {
+          F.feat[l] = P.seq[(size_t)l]->feat;
+          F.j5[l] = P.seq[(size_t)l]->j5;
+        }
+        for (int l = 0; l + 1 < t; l++) F.mode[l] = P.step_mode[l];
+      }
+      if (!cf.empty() && upload(ctx, d_cfold, cf)) return YRWI_E_HIP;
+      if (pend.active) {
+        hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
+        if (c0) hipEventRecord(c0, ctx->stream);
+        if (launch_compact(pend.d_jobs, pend.d_tb, pend.nj, pend.tiles, pend.d_pairs, pend.d_puid, pend.d_src,
+                           pend.d_cnt, pend.d_off, pend.bo, true, ctx->stream))
+          return ctx->fail(YRWI_E_HIP, "compact launch");
+        if (c1) {
+          hipEventRecord(c1, ctx->stream);
+          tm->kcompact.push_back({c0, c1});
+          tm->spans.push_back({c0, c1});
+        }
+      }
+      if (st) {  // exclusions of chained queries: the bytes k_chain loads for them
+        for (size_t k = 0; k < cqs.size(); k++) {
+          const int j = job_of[(size_t)cqs[k]];
+          const ChainQ& C = chq[(size_t)cqs[k]];
+          const int64_t pre = (j >= 0 && pend.active) ? pend.level[(size_t)j][2] : 0;
+          for (int l = C.ninc; l < C.nl; l++)
+            st->bytes_alg_capped += std::min<int64_t>(12 * C.l[l].n, C.l[l].bm ? 20 * pre
+                                                                               : 4 * pre + std::min(4 * C.l[l].n, 128 * pre));
+        }
+      }
+    } else if (pend.active) {
+      return ctx->fail(YRWI_E_HIP, "chained step outside the first fold step");
+    }
     if (!more) break;
     // the accumulated containers' global sizes decide the next step's dispatch
     std::vector<int64_t> v(nq, 0);

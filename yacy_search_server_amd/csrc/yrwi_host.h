@@ -183,6 +183,8 @@ struct Plan {
   DList cont{nullptr, nullptr, nullptr, 0};
   int32_t step_mode[YRWI_MAX_TERMS] = {0};  // JoinMode of every fold step taken
   uint8_t* removed = nullptr;
+  int nexcl_g = 0;      // exclusion terms in effect (J1 on global sizes; excl holds this shard's lists of them)
+  bool chain = false;   // chained fold (ChainQ, yrwi_internal.h): one join step, k_chain does the rest
 };
 
 

@@ -107,6 +107,32 @@ struct FoldSrc {
   int32_t mode[YRWI_MAX_TERMS];          // JoinMode of step s (lists 0..s with list s+1)
 };
 
+// Chained fold (a query of t >= 2 include lists with more lists after its first
+// join step: more includes and / or exclusions; no maxDistance filter).  The
+// first step (lists 0 and 1) joins as usual; k_chain then tests each of its
+// matched pairs against the fold's later include lists and the exclusion lists
+// (url-id bitmap: one 16-B word; otherwise the list's ids or line heads around the
+// tile's range), keeps only the survivors -- the rows the whole fold and
+// exclusion keep, which do not depend on the fold order -- with their rows in the
+// later include lists, and k_compact folds their records over all t lists (J5/J6
+// step by step, each step's dispatch from the intersection sizes k_chain counts).
+// No intermediate container is written.  ReferenceContainer.java:328-388.
+constexpr int CHAIN_MAXL = 6;  // lists tested per pair (later includes, then exclusions)
+constexpr int CHAIN_MAXI = 2;  // later include lists (t <= 4)
+constexpr int CHAIN_LVL = 4;   // per-tile counts: matches, after include 2, after include 3, after exclusion
+struct ChainList {
+  const uint32_t* uid;
+  const uint32_t* head;  // line heads (DList::head) or nullptr
+  const uint64_t* bm;    // url-id bitmap (DList::bm) or nullptr
+  int64_t n;
+};
+struct ChainQ {
+  ChainList l[CHAIN_MAXL];   // includes 2..t-1 of the fold (in fold order), then the exclusion lists
+  int32_t ninc, nl;
+  int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
+  int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
+};
+
 struct JoinQ {
   DList A, B;
   int64_t tile_base;   // first global tile of this job
@@ -131,6 +157,7 @@ struct JoinQ {
   // arrays; every tile writes its run at tile_src[tile] (merge tiles: the prefix
   // of their bounds min(na, nb + 1); probe tiles: ptile per tile)
   int64_t pair_base;
+  const ChainQ* chain;  // chained fold (k_chain, k_compact<true>) or nullptr
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
@@ -314,13 +341,20 @@ struct OrderArgs {
 };
 
 // jobs [0, nmerge) are JA_MERGE with tiles [0, merge_tiles); the rest are JA_PROBE
+// chain: the step has chained jobs (JoinQ::chain): k_chain and k_scan_tiles run
+// (d_tile_lvl: CHAIN_LVL counts per tile), k_compact does not -- the caller
+// launches it with launch_compact once the fold's dispatch modes are known
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src,
                      int32_t* d_tile_cnt, int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* stream,
                      void* ev_begin,
-                     void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr);
+                     void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
+                     bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr);
+int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
+                   const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
+                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
@@ -397,11 +431,19 @@ struct EvJob {
   int32_t local;
   const uint8_t* rows;
   int64_t n;
+  // yrwi_event_order: the arrival only continues the event's ReferenceOrder
+  // (min/max, max-distance fold, host counts) and every row's cardinal under the
+  // state after it lands here; no doublecheck, flag counts or stack (the caller's
+  // SearchEvent.addRWIs keeps those).  nullptr: a full addRWIs arrival.
+  int64_t* scores;
 };
 
 // one workgroup per event: jobs [jb[b], jb[b+1]) of the same event, in arrival order; status[j] = 0 / YRWI_E_*
 int launch_event_add(const EvDev* d_ev, const EvJob* d_jobs, const int32_t* d_jb, int32_t nblocks, int32_t* d_status,
                      void* stream);
+// ReferenceOrder.authority (ReferenceOrder.java:213-216) of n host keys (host36 + 1)
+// against an event's accumulated host counts
+int launch_event_authority(const EvDev* d_ev, const uint64_t* d_keys, int32_t n, int32_t* d_out, void* stream);
 // seeds the url set with the doublecheck urls of the filter (epoch 0)
 int launch_event_seed(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, void* stream);
 

@@ -146,6 +146,13 @@ __device__ __forceinline__ uint2 ldg(const uint2* p) {
   return make_uint2(v.x, v.y);
 }
 template <>
+__device__ __forceinline__ void stg(uint2* p, const uint2& v) {
+  u32x2_t w;
+  w.x = v.x;
+  w.y = v.y;
+  *(__attribute__((address_space(1))) u32x2_t*)p = w;
+}
+template <>
 __device__ __forceinline__ void stg(ulonglong2* p, const ulonglong2& v) {
   u64x2_t w;
   w.x = v.x;
@@ -1046,11 +1053,15 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
 }
 
 // ============================================================ join: scan
+// tile_lvl (chained steps): a chained job's level counts (k_chain) summed into
+// its ChainQ::level (pinned host memory, read after the step's synchronisation)
 __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jobs,
                                                     const int64_t* __restrict__ tile_base,
                                                     const int32_t* __restrict__ tile_cnt,
-                                                    int64_t* __restrict__ tile_off) {
+                                                    int64_t* __restrict__ tile_off,
+                                                    const int32_t* __restrict__ tile_lvl) {
   __shared__ int32_t sScan[4];
+  __shared__ uint64_t sScan64[4];
   const JoinQ& J = jobs[blockIdx.x];
   const int64_t base = tile_base[blockIdx.x];
   int64_t running = 0;
@@ -1063,6 +1074,20 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
     running += tot;
   }
   if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
+  if (tile_lvl && J.chain) {  // workgroup-uniform
+    int64_t* level = ldg(&J.chain->level);
+    for (int l = 0; l < CHAIN_LVL; l++) {
+      uint64_t acc = 0;
+      for (int64_t t0 = 0; t0 < J.ntiles; t0 += 256) {
+        const int64_t t = t0 + threadIdx.x;
+        const uint64_t c = t < J.ntiles ? (uint64_t)tile_lvl[(base + t) * CHAIN_LVL + l] : 0;
+        uint64_t tot;
+        block_excl_sum256_u64(c, sScan64, &tot);
+        acc += tot;
+      }
+      if (threadIdx.x == 0) level[l] = (int64_t)acc;
+    }
+  }
 }
 
 // Merge jobs: tile_src[t] = the job's pair_base + the exclusive prefix of its
@@ -1081,6 +1106,212 @@ __global__ __launch_bounds__(256) void k_scan_bounds(const JoinQ* __restrict__ j
     const int32_t ex = block_excl_sum256(c, sScan, &tot);
     if (t < J.ntiles) tile_src[base + t] = running + ex;
     running += tot;
+  }
+}
+
+// ============================================================ join: chain
+// Chained folds (ChainQ, yrwi_internal.h): after a chained job's first step has
+// written its matched pairs (tile slots), each pair is tested against the fold's
+// later include lists and the exclusion lists; only the survivors stay in the
+// tile's slots, with their rows in the later include lists.
+
+// the ChainList of device memory through global loads (the struct reaches the
+// kernel through a pointer held in device memory)
+__device__ __forceinline__ ChainList load_cl(const ChainList* p) {
+  ChainList L;
+  L.uid = ldg(&p->uid);
+  L.head = ldg(&p->head);
+  L.bm = ldg(&p->bm);
+  L.n = ldg(&p->n);
+  return L;
+}
+__device__ __forceinline__ int64_t lower_bound_cl(const ChainList& L, uint32_t key) {
+  if (!L.head) return lower_bound_uid(L.uid, 0, L.n, key);
+  DList d{};
+  d.uid = L.uid;
+  d.head = L.head;
+  d.n = L.n;
+  return lower_bound_list(d, key);
+}
+
+// the range [lo, hi) of a list without a bitmap that holds the ids of a tile's
+// matches: one thread per (tile, list), all tiles in parallel (as k_probe_part)
+__global__ void k_chain_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
+                             int64_t ntiles, const int32_t* __restrict__ tile_job, const uint32_t* __restrict__ pair_uid,
+                             const int64_t* __restrict__ tile_src, const int32_t* __restrict__ tile_cnt,
+                             ProbeDesc* __restrict__ crange) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ntiles * CHAIN_MAXL) return;
+  const int64_t t = i / CHAIN_MAXL;
+  const int l = (int)(i % CHAIN_MAXL);
+  const int j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+  const ChainQ* C = jobs[j].chain;
+  if (!C || l >= ldg(&C->nl)) return;
+  const ChainList L = load_cl(&C->l[l]);
+  const int32_t cnt = tile_cnt[t];
+  if (L.bm || cnt == 0) return;
+  const int64_t src = tile_src[t];
+  ProbeDesc D;
+  D.lo = lower_bound_cl(L, ldg(pair_uid + src));
+  D.hi = lower_bound_cl(L, ldg(pair_uid + src + cnt - 1) + 1u);  // ids < 2^32 - 1: no wrap
+  D.job = j;
+  D.pad = 0;
+  crange[i] = D;
+}
+
+constexpr int CHAIN_KPT = 9;  // matches per thread: a tile's matches in one pass
+static_assert(CHAIN_KPT * 256 >= JOIN_MAXM && CHAIN_KPT * 256 >= BM_TILE, "k_chain: one pass per tile");
+
+// One workgroup per tile of the step: a chained job's matches (slot k*256 + tid
+// of the tile's run, in url-id order) are tested list by list, only the live ones
+// (the loads of a bitmap list all in flight at once); the survivors are written
+// back to the front of the tile's run, in order, with their rows in the later
+// include lists; tile_lvl gets the tile's counts at each level (the fold's
+// dispatch modes come from their sums).
+__global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
+                                               int njobs, const int32_t* __restrict__ tile_job,
+                                               uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
+                                               const int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
+                                               int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ crange) {
+  __shared__ uint32_t sL[PROBE_LDS];
+  __shared__ uint64_t sScan64[4];
+  const int64_t t = blockIdx.x;
+  const int j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+  const ChainQ* C = jobs[j].chain;
+  if (!C) return;
+  const int32_t cnt = tile_cnt[t];
+  int32_t* lv = tile_lvl + t * CHAIN_LVL;
+  if (cnt == 0) {
+    if (threadIdx.x < CHAIN_LVL) lv[threadIdx.x] = 0;
+    return;
+  }
+  const int64_t src = tile_src[t];
+  const int ninc = ldg(&C->ninc), nl = ldg(&C->nl);
+  uint32_t key[CHAIN_KPT];
+  uint2 pr[CHAIN_KPT];
+  int32_t pos[CHAIN_MAXI][CHAIN_KPT];
+  uint32_t alive = 0;
+#pragma unroll
+  for (int k = 0; k < CHAIN_KPT; k++) {
+    const int i = k * 256 + (int)threadIdx.x;
+    key[k] = 0;
+    pr[k] = make_uint2(0, 0);
+    pos[0][k] = pos[1][k] = 0;
+    if (i < cnt) {
+      key[k] = ldg(pair_uid + src + i);
+      pr[k] = ldg(reinterpret_cast<const uint2*>(pairs) + src + i);
+      alive |= 1u << k;
+    }
+  }
+  uint32_t after1 = alive, after2 = alive;  // live matches of this thread after include 2 / include 3
+  for (int l = 0; l < nl; l++) {
+    const ChainList L = load_cl(&C->l[l]);
+    const bool inc = l < ninc;
+    uint32_t hit = 0;
+    int32_t p[CHAIN_KPT];
+    if (L.bm) {
+      const __amdgpu_buffer_rsrc_t rbm =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
+      uint4 E[CHAIN_KPT];
+#pragma unroll
+      for (int k = 0; k < CHAIN_KPT; k++) {
+        E[k] = make_uint4(0, 0, 0, 0);
+        if ((alive >> k) & 1u)
+          E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
+      }
+#pragma unroll
+      for (int k = 0; k < CHAIN_KPT; k++) {
+        const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
+        const uint64_t bit = 1ull << (key[k] & 63u);
+        p[k] = (int32_t)(ey + __popcll(ex & (bit - 1ull)));
+        if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
+      }
+    } else {
+      const ProbeDesc D = crange[t * CHAIN_MAXL + l];  // workgroup-uniform
+      const int64_t R = D.hi - D.lo;
+      if (R <= PROBE_LDS) {
+        __syncthreads();  // the previous list's range is no longer read
+        for (int x = threadIdx.x; x < (int)R; x += 256) sL[x] = ldg(L.uid + D.lo + x);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CHAIN_KPT; k++) {
+          p[k] = 0;
+          if (!((alive >> k) & 1u)) continue;
+          int lo = 0, hi = (int)R;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sL[mid] < key[k]) lo = mid + 1; else hi = mid;
+          }
+          p[k] = (int32_t)(D.lo + lo);
+          if (lo < (int)R && sL[lo] == key[k]) hit |= 1u << k;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < CHAIN_KPT; k++) {
+          p[k] = 0;
+          if (!((alive >> k) & 1u)) continue;
+          const int64_t q = lower_bound_cl(L, key[k]);
+          p[k] = (int32_t)q;
+          if (q < L.n && ldg(L.uid + q) == key[k]) hit |= 1u << k;
+        }
+      }
+    }
+    if (inc) {
+      alive &= hit;
+#pragma unroll
+      for (int k = 0; k < CHAIN_KPT; k++) {
+        if (l == 0) pos[0][k] = p[k];
+        else if (l == 1) pos[1][k] = p[k];
+      }
+      if (l == 0) after1 = alive;
+      if (l == 1) after2 = alive;
+    } else {
+      alive &= ~hit;
+    }
+  }
+  if (ninc < 2) after2 = after1;
+  // survivors leave in slot order (slot k's 256 matches, then slot k+1's): per-slot
+  // counts packed four to a 64-bit scan, as in probe_bitmap; the level counts ride
+  // along in the last scan's spare fields
+  constexpr int NSC = (CHAIN_KPT + 3) / 4;
+  uint64_t ex[NSC], tot64[NSC];
+#pragma unroll
+  for (int q = 0; q < NSC; q++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 4 * q; k < CHAIN_KPT && k < 4 * q + 4; k++) c |= (uint64_t)((alive >> k) & 1u) << (16 * (k - 4 * q));
+    if (q == NSC - 1) {
+      static_assert(CHAIN_KPT % 4 == 1, "two spare 16-bit fields in the last scan");
+      c |= (uint64_t)__popc(after1) << 16 | (uint64_t)__popc(after2) << 32;
+    }
+    ex[q] = block_excl_sum256_u64(c, sScan64, &tot64[q]);
+  }
+  int32_t base[CHAIN_KPT];
+  int32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < CHAIN_KPT; k++) {
+    base[k] = run;
+    run += (int32_t)((tot64[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+  }
+  // every read of the tile's run happened before the scans' barriers: write in place
+  int32_t* tup0 = ninc > 0 ? ldg(&C->tup[0]) : nullptr;
+  int32_t* tup1 = ninc > 1 ? ldg(&C->tup[1]) : nullptr;
+#pragma unroll
+  for (int k = 0; k < CHAIN_KPT; k++) {
+    if (!((alive >> k) & 1u)) continue;
+    const int64_t o = src + base[k] + (int64_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+    stg(reinterpret_cast<uint2*>(pairs) + o, pr[k]);
+    stg(pair_uid + o, key[k]);
+    if (tup0) stg(tup0 + o, pos[0][k]);
+    if (tup1) stg(tup1 + o, pos[1][k]);
+  }
+  if (threadIdx.x == 0) {
+    tile_cnt[t] = run;
+    const uint64_t lt = tot64[NSC - 1];
+    lv[0] = cnt;
+    lv[1] = (int32_t)((lt >> 16) & 0xFFFFu);
+    lv[2] = (int32_t)((lt >> 32) & 0xFFFFu);
+    lv[3] = run;
   }
 }
 
@@ -1153,6 +1384,9 @@ struct CompactJob {
   const FoldSrc* fold;   // A deferred, this the last step: the fold's lists and modes
   int32_t otw;
   int32_t bw;            // words per posting of bf (FEAT_WORDS, or 2 for an enumeration's DList::j5)
+  int32_t ctw;           // chained job: lists of the fold (0: not chained)
+  const int32_t* ctup0;  // chained job: rows in the fold's lists 2 and 3 (ChainQ::tup)
+  const int32_t* ctup1;
 };
 
 // the record of a deferred row (sources r[0..tw-1] in the fold's lists): J5/J6
@@ -1172,6 +1406,32 @@ __device__ __forceinline__ Rec fold_deferred(const FoldSrc& F, const int32_t* __
   return acc;
 }
 
+// the record of a chained fold's survivor (rows r0..r3 in the fold's lists 0..tw-1):
+// J5/J6 step by step over all tw lists, with each step's dispatch mode
+__device__ __forceinline__ Rec fold_chain(const FoldSrc* F, int32_t r0, int32_t r1, int32_t r2, int32_t r3, int tw,
+                                          int64_t now_ms) {
+  Rec acc = load_rec(ldg(&F->feat[0]), r0);
+#pragma unroll
+  for (int s = 0; s < 2 + CHAIN_MAXI - 1; s++) {
+    if (s + 1 >= tw) break;
+    const int32_t m = ldg(&F->mode[s]);
+    const int64_t e = s == 0 ? r1 : s == 1 ? r2 : r3;
+    ulonglong2 b = make_ulonglong2(0, 0);
+    if (m == JM_TEST_LARGE_B) {
+      acc = load_rec(ldg(&F->feat[s + 1]), e);  // self-join of the larger side
+    } else if (m == JM_ENUM) {
+      const uint64_t* j5 = ldg(&F->j5[s + 1]);
+      b = j5 ? ldg(reinterpret_cast<const ulonglong2*>(j5) + e)
+             : ldg(reinterpret_cast<const ulonglong2*>(ldg(&F->feat[s + 1]) + e * FEAT_WORDS));
+    }
+    acc = joined_rec(acc, b.x, b.y, m, now_ms);
+  }
+  return acc;
+}
+
+// CHAIN: the step has chained jobs (k_chain ran): their matches fold the records
+// of all the fold's lists (fold_chain) instead of joining A's record with B's
+template <bool CHAIN>
 __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
                                                  int njobs, int64_t ntiles, const uint2* __restrict__ pairs,
                                                  const uint32_t* __restrict__ pair_uid,
@@ -1216,6 +1476,13 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         X.otup = J.out_tup;
         X.otw = J.out_tup ? J.out_tw : 0;
         X.fold = J.fold;
+        X.ctw = 0;
+        if (CHAIN && J.chain) {
+          const int ni = ldg(&J.chain->ninc);
+          X.ctw = 2 + ni;
+          X.ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
+          X.ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
+        }
       }
     }
     const int32_t inc = wave_incl_sum(c);
@@ -1277,6 +1544,11 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       B[u] = make_ulonglong2(0, 0);
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
+      if (CHAIN && X.ctw) {
+        A[u] = fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0,
+                          X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
+        continue;
+      }
       if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
       else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
       else A[u] = load_rec(X.af, pr[u].x);
@@ -1287,7 +1559,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
       const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
-      store_rec(X.ofeat, o, joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
+      store_rec(X.ofeat, o, (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
       stg(X.ouid + o, uid[u]);
     }
   }
@@ -3296,7 +3568,8 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
                      int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* st, void* ev0,
-                     void* evm, void* ev1, void* evc0, void* evc1) {
+                     void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
+                     ProbeDesc* d_crange) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -3356,14 +3629,36 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
+    if (chain) {
+      const int64_t nr = total_tiles * CHAIN_MAXL;
+      hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
+                         total_tiles, (const int32_t*)tjob, d_pair_uid, d_tile_src, d_tile_cnt, d_crange);
+      hipLaunchKernelGGL(k_chain, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
+                         (const int32_t*)tjob, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl,
+                         (const ProbeDesc*)d_crange);
+    }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
-                       d_tile_off);
-    if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0,
-                       S(st), d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
-                       d_tile_off, (const int2*)perm, (const int32_t*)tjob);
-    if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
+                       d_tile_off, (const int32_t*)(chain ? d_tile_lvl : nullptr));
+    if (!chain) {  // chained steps compact once the fold's dispatch modes are known (launch_compact)
+      if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
+      if (int r = launch_compact(d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
+                                 d_tile_off, bo, false, st))
+        return r;
+      if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
+    }
   }
+  return rc(hipGetLastError());
+}
+
+int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
+                   const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
+                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* st) {
+  if (total_tiles <= 0) return 0;
+  const int2* perm = bo.key && bo.tile_job ? bo.perm : nullptr;
+  auto kc = chain ? k_compact<true> : k_compact<false>;
+  hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
+                     d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
+                     perm, (const int32_t*)bo.tile_job);
   return rc(hipGetLastError());
 }
 
@@ -3861,6 +4156,26 @@ __global__ __launch_bounds__(EV_THREADS) void k_event_add(const EvDev* __restric
       N.rcp[NF] = N.va_mx != N.va_mn ? 1.0 / (double)(N.va_mx - N.va_mn) : 0.0;
       N.rcp[NF + 1] = N.D != 0 ? 1.0 / (double)N.D : 0.0;
     }
+    if (J.scores) {  // yrwi_event_order: cardinal of every row under the state after this container
+      __syncthreads();
+      if (sMisc[4]) {
+        if (tid == 0) { S.err = YRWI_E_CAPACITY; status[j] = YRWI_E_CAPACITY; }
+        __syncthreads();
+        continue;
+      }
+      for (int64_t i = tid; i < n; i += EV_THREADS) {
+        const Row R = load_row(rows + i * YRWI_ROW_BYTES);
+        const int32_t hc = Q.want_authority ? htab_count(Q.hkeys, Q.hcnt, Q.hmask, host36(R) + 1) : 0;
+        J.scores[i] = cardinal(decode(R), N, Q, hc);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        S.nin += n;
+        status[j] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
     // ---- doublecheck: the first occurrence of a url passing the constraints is admitted (:736-805)
     const uint32_t ep = (uint32_t)S.epoch + 1;
     {
@@ -4009,6 +4324,21 @@ __global__ __launch_bounds__(EV_THREADS) void k_event_add(const EvDev* __restric
     __syncthreads();
   }
   if (tid == 0) *E.st = S;
+}
+
+__global__ void k_event_authority(const EvDev* __restrict__ ev, const uint64_t* __restrict__ keys, int32_t n,
+                                  int32_t* __restrict__ out) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const RankQ& Q = ev->q;
+  const int32_t c = Q.want_authority ? htab_count(Q.hkeys, Q.hcnt, Q.hmask, keys[i]) : 0;
+  out[i] = div32(shl32(c, 8), add32(1, ev->st->maxdom));  // (doms.get(h) << 8) / (1 + maxdomcount)
+}
+
+int launch_event_authority(const EvDev* d_ev, const uint64_t* d_keys, int32_t n, int32_t* d_out, void* st) {
+  if (n > 0) hipLaunchKernelGGL(k_event_authority, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), d_ev, d_keys, n,
+                                d_out);
+  return rc(hipGetLastError());
 }
 
 int launch_event_add(const EvDev* d_ev, const EvJob* d_jobs, const int32_t* d_jb, int32_t nblocks, int32_t* d_status,

@@ -163,6 +163,27 @@ class SearchEvent:
     def add_rwis(self, rows: np.ndarray, local: bool = False) -> int:
         return self._ix.add_rwis([(self, rows, local)])[0]
 
+    def order(self, rows: np.ndarray, local: bool = False) -> np.ndarray:
+        """ReferenceOrder.normalizeWith(container, local) + cardinal of every row
+        (yrwi_event_order): the container continues the event's ReferenceOrder
+        (min/max, max-distance fold, host counts over every container so far); the
+        scores are under the state after it.  The stack is not touched: the
+        drop-in's SearchEvent.addRWIs keeps its own (GpuReferenceOrder)."""
+        r = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, 40)
+        out = np.zeros(len(r), dtype=np.int64)
+        if len(r):
+            _check(self._ix._h, _lib.lib().yrwi_event_order(self._ix._h, self._e, r.ctypes.data, len(r),
+                                                            int(bool(local)), out.ctypes.data))
+        return out
+
+    def authority(self, hosthashes: Sequence[bytes]) -> List[int]:
+        """ReferenceOrder.authority(hostHash) against the accumulated host counts."""
+        buf = b"".join(bytes(h)[:6] for h in hosthashes)
+        out = (ctypes.c_int32 * max(1, len(hosthashes)))()
+        if hosthashes:
+            _check(self._ix._h, _lib.lib().yrwi_event_authority(self._ix._h, self._e, buf, len(hosthashes), out))
+        return [int(out[i]) for i in range(len(hosthashes))]
+
     def results(self) -> Tuple[List["Hit"], "CEventInfo"]:
         out = (_lib.CHit * max(1, self.k))()
         n = ctypes.c_int32()
