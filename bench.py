@@ -485,7 +485,9 @@ def kernel_lines(iso, pmc):
                 dispatches the step (J3);
       k_compact §8(d): 23 B per include term and joined posting (23 t m_out);
       k_reduce  the 32-B ranking record of every joined posting (+ 1-B exclusion mark), k_shard_fin included;
-      k_score   the same records (an upper bound: chunks the threshold prunes read 16 of the 32 B).
+      k_score   the same records (an upper bound: chunks the threshold prunes read 16 of the 32 B);
+      k_chain   §8(d): the chained folds' later steps' K and the exclusions' 12 n_e, each charged
+                min(K, the bytes k_chain loads for it) (k_chain_part and k_scan_tiles included).
     traffic = rocprofv3 PMC HBM bytes per launch (profiles/pmc_<config>.json) and
     hbm_frac = traffic / the profile's own mean launch time / peak (the same dispatches)."""
     n = max(1, iso["n_join_launches"])
@@ -499,7 +501,9 @@ def kernel_lines(iso, pmc):
              {"alg_bytes_model_K": int(iso["bytes_probe"] / n), "loaded_bytes": int(iso["bytes_probe_loaded"] / n)}),
             ("k_compact", iso["t_compact_ns"], iso["bytes_features"], n, {}),
             ("k_reduce", iso.get("t_reduce_ns", 0), iso.get("bytes_reduce", 0), nr, {}),
-            ("k_score", iso.get("t_scorek_ns", 0), iso.get("bytes_score", 0), nr, {})):
+            ("k_score", iso.get("t_scorek_ns", 0), iso.get("bytes_score", 0), nr, {}),
+            ("k_chain", iso.get("t_chain_ns", 0), iso.get("bytes_chain", 0), max(1, iso.get("n_chain_launches", 0)),
+             {})):
         t = t_ns / nl * 1e-9
         if t <= 0:
             continue

@@ -103,6 +103,17 @@ typedef struct yrwi_query_desc {
   char language[8];           /* ReferenceOrder.language, NUL terminated (any length) */
   int64_t now_ms;             /* System.currentTimeMillis() of the request; 0 = now */
   const yrwi_filter* filter;  /* NULL: unconstrained query */
+  /* TermSearch's urlselection (TermSearch.java:42-62 -> AbstractIndex.searchConjunction :96-128):
+   * nurlselection url hashes (12 bytes each; NULL / 0: none).  Every include and exclude
+   * container is restricted to these urls before the conjunction, as
+   * ReferenceContainerCache.get(key, urlselection) does (ReferenceContainerCache.java:448-470):
+   * J1, the J2 fold order and every J3 dispatch then see the restricted sizes.  (IndexCell.get,
+   * YaCy's segment index, ignores the argument (IndexCell.java:353-386) and the local search
+   * passes null (SearchEvent.java:619).)  A selection with two or more include terms runs as a
+   * chained fold: more than four include terms, or a maxDistance filter (quoted query), with a
+   * selection: YRWI_E_UNSUPPORTED. */
+  const uint8_t* urlselection;
+  int32_t nurlselection;
 } yrwi_query_desc;
 
 typedef struct yrwi_stats {
@@ -149,6 +160,12 @@ typedef struct yrwi_stats {
   int64_t t_scorek_ns;
   int64_t bytes_reduce;
   int64_t bytes_score;
+  /* chained folds (k_chain_part + k_chain + k_scan_tiles of a chained step, HIP events around them): the
+     launches, their device time and their SURVEY.md §8(d) bytes -- the later fold steps' K and the
+     exclusions' 12 n_e, each charged min(K, the bytes k_chain loads for it) */
+  int64_t n_chain_launches;
+  int64_t t_chain_ns;
+  int64_t bytes_chain;
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */
@@ -410,6 +427,11 @@ int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nincl, const u
 /* == ReferenceOrder.normalizeWith + cardinal (ReferenceOrder.java:70,223) on one
  *    container (rows sorted by url hash), with settled min/max: score_out[i] =
  *    cardinal(row i). */
+/* TermSearch(index, include, exclude, urlselection, ...).joined() for one query
+ * descriptor (the urlselection of yrwi_query_desc honoured; k, profile, language
+ * and filter unused): the joined and excluded container's rows, as
+ * yrwi_join_exclude writes them. */
+int yrwi_term_search(yrwi_ctx* ctx, const yrwi_query_desc* q, uint8_t* rows40_out, int64_t cap_rows, int64_t* m);
 int yrwi_normalize_score(yrwi_ctx* ctx, const uint8_t* rows40, int64_t m, const yrwi_profile* prof,
                          const char* language, int64_t now_ms, int64_t* score_out);
 

@@ -29,7 +29,7 @@ def short(name):
         return "k_probe_excl" if len(args) > 1 and args[1] in ("true", "1") else "k_probe"
     if "k_probeILb" in name:
         return "k_probe_excl" if "ELb1E" in name.split("k_probeILb", 1)[1][:8] else "k_probe"
-    for k in ("k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
+    for k in ("k_chain_part", "k_chain", "k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
               "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
               "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
@@ -95,7 +95,7 @@ def main(tag, config):
     # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
     # (k_combine runs once per batch pass); index build, uploads and fills excluded
     path = ("k_partition", "k_probe_part", "k_scan_bounds", "k_order_hist", "k_order_scatter", "k_join", "k_probe",
-            "k_probe_excl", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
+            "k_probe_excl", "k_chain_part", "k_chain", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
             "k_emit")
     nb = out["kernels"].get("k_combine", {}).get("calls")
     if nb:
@@ -113,7 +113,7 @@ def main(tag, config):
             out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
         except Exception:
             pass
-    for name in ("k_compact", "k_join", "k_probe", "k_probe_excl", "k_reduce", "k_score"):
+    for name in ("k_compact", "k_join", "k_probe", "k_probe_excl", "k_chain", "k_reduce", "k_score"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
         out[name + "_avg_ns"] = kd.get("avg_ns")

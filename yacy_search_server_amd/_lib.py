@@ -53,7 +53,8 @@ class CQuery(ctypes.Structure):
                 ("excl", ctypes.c_void_p), ("nexcl", ctypes.c_int32),
                 ("max_distance", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("profile", ctypes.POINTER(CProfile)), ("language", ctypes.c_char * 8),
-                ("now_ms", ctypes.c_int64), ("filter", ctypes.POINTER(CFilter))]
+                ("now_ms", ctypes.c_int64), ("filter", ctypes.POINTER(CFilter)),
+                ("urlselection", ctypes.c_void_p), ("nurlselection", ctypes.c_int32)]
 
 
 class CStats(ctypes.Structure):
@@ -69,7 +70,8 @@ class CStats(ctypes.Structure):
                 ("bytes_join_capped", ctypes.c_int64), ("bytes_alg_capped", ctypes.c_int64),
                 ("n_probe_dispatches", ctypes.c_int64), ("t_probe_all_ns", ctypes.c_int64),
                 ("n_rank_passes", ctypes.c_int64), ("t_reduce_ns", ctypes.c_int64), ("t_scorek_ns", ctypes.c_int64),
-                ("bytes_reduce", ctypes.c_int64), ("bytes_score", ctypes.c_int64)]
+                ("bytes_reduce", ctypes.c_int64), ("bytes_score", ctypes.c_int64),
+                ("n_chain_launches", ctypes.c_int64), ("t_chain_ns", ctypes.c_int64), ("bytes_chain", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):
@@ -169,6 +171,8 @@ SIGNATURES = {
     "yrwi_join_exclude": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]),
+    "yrwi_term_search": (ctypes.c_int, [_VP, ctypes.POINTER(CQuery), _VP, ctypes.c_int64,
+                                        ctypes.POINTER(ctypes.c_int64)]),
     "yrwi_normalize_score": (ctypes.c_int, [_VP, _VP, ctypes.c_int64, ctypes.POINTER(CProfile), ctypes.c_char_p,
                                             ctypes.c_int64, _VP]),
 }

@@ -586,12 +586,15 @@ int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   return 0;
 }
 
-// Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 64) of the url
-// ids (and 4096 postings): nurls/4 bytes each, so at most 16x the list's own ids
-// (at 1/64 density); total capped by YRWI_BM_GB (default 8).  YRWI_BM_DIV=0: none.
-// The same lists, largest first, get DList::j5 (16 B per posting; total capped by
-// YRWI_J5_GB, default 16, apart from the bitmaps' cap; YRWI_J5=0: none): they are
-// the dense ones, where an enumeration's matches sit a few postings apart.
+// Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 256) of the url
+// ids (and 4096 postings): nurls/4 bytes each, so at most 64x the list's own ids
+// (at 1/256 density); total capped by YRWI_BM_GB (default 8), largest lists first.
+// YRWI_BM_DIV=0: none.  The joins probe only the dense ones (>= 1/64, layout_jobs);
+// the sparser ones answer k_chain's tests of a chained fold's later lists and the
+// url selections (one word per match instead of a search of the list).
+// The dense lists, largest first, get DList::j5 (16 B per posting; total capped by
+// YRWI_J5_GB, default 16, apart from the bitmaps' cap; YRWI_J5=0: none): where an
+// enumeration's matches sit a few postings apart.
 int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   hipStream_t st = ctx->stream;
   for (ListRec* L : lists) L->bm = L->j5 = nullptr;
@@ -599,7 +602,7 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   const char* gj = getenv("YRWI_J5_GB");
   const int64_t j5_cap = (ej && atoi(ej) == 0) ? 0 : (int64_t)((gj ? atof(gj) : 16.0) * (double)(1ll << 30));
   const char* e = getenv("YRWI_BM_DIV");
-  const int64_t div = e ? atoll(e) : 64;
+  const int64_t div = e ? atoll(e) : 256;
   const char* g = getenv("YRWI_BM_GB");
   const int64_t cap_bytes = (int64_t)((g ? atof(g) : 8.0) * (double)(1ll << 30));
   if (div <= 0 || ctx->nurls <= 0) return 0;
@@ -614,7 +617,9 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   if (big.empty()) return 0;
   size_t nj5 = 0;  // lists with a J5 array (the first nj5 of big)
   int64_t j5_words = 0;
-  while (nj5 < big.size() && (j5_words + 2 * big[nj5]->n) * 8 <= j5_cap) j5_words += 2 * big[nj5++]->n;
+  // (the dense lists only, >= 1/64 of the url ids: where an enumeration's matches sit a few postings apart)
+  while (nj5 < big.size() && big[nj5]->n * 64 >= ctx->nurls && (j5_words + 2 * big[nj5]->n) * 8 <= j5_cap)
+    j5_words += 2 * big[nj5++]->n;
   const size_t bm_words = big.size() * (size_t)per;
   size_t need = bm_words + (size_t)j5_words;
   if (need > ctx->bm_cap) {

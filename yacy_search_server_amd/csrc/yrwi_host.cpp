@@ -527,6 +527,19 @@ static int plan_query(const yrwi_ctx* ix, Lane* ctx, const yrwi_query_desc& d, P
     if (!key_of(d.incl + 12 * i, &P->inc[ninc++])) return ctx->fail(YRWI_E_HASH, "include term hash not well-formed");
   for (int i = 0; i < d.nexcl; i++)
     if (!key_of(d.excl + 12 * i, &P->exc[nexc++])) return ctx->fail(YRWI_E_HASH, "exclude term hash not well-formed");
+  P->has_sel = d.urlselection != nullptr && d.nurlselection > 0;
+  P->sel.clear();
+  P->sel_uid.clear();
+  if (d.nurlselection < 0 || (d.nurlselection > 0 && !d.urlselection))
+    return ctx->fail(YRWI_E_ARG, "bad urlselection");
+  if (P->has_sel) {  // HandleSet urlselection: a sorted set of url hashes
+    P->sel.resize((size_t)d.nurlselection);
+    for (int32_t i = 0; i < d.nurlselection; i++)
+      if (!key_of(d.urlselection + 12 * (size_t)i, &P->sel[(size_t)i]))
+        return ctx->fail(YRWI_E_HASH, "urlselection hash not well-formed");
+    std::sort(P->sel.begin(), P->sel.end());
+    P->sel.erase(std::unique(P->sel.begin(), P->sel.end()), P->sel.end());
+  }
   std::sort(P->inc, P->inc + ninc);
   ninc = (int)(std::unique(P->inc, P->inc + ninc) - P->inc);
   std::sort(P->exc, P->exc + nexc);
@@ -582,6 +595,7 @@ static void plan_finish(Plan* P, const int64_t* ng_inc, const int64_t* ng_exc) {
   for (int i = 0; i < P->ninc; i++) {
     if (i + 1 < P->ninc && tm[i + 1].first == tm[i].first) continue;  // the later put wins
     const int c = tm[i].second;
+    P->seq_term[P->seq.size()] = c;
     P->seq.push_back(P->linc[c] ? P->linc[c] : &kAbsentList);
     P->seq_ng.push_back(ng_inc[c]);
   }
@@ -613,14 +627,102 @@ static int allsum_host(Lane* L, std::vector<int64_t>& v) {
   return 0;
 }
 
+static ChainList chain_list(const ListRec* L) { return ChainList{L->uid, L->head, L->bm, L->n}; }
+
+// TermSearch's urlselection (yrwi_query_desc.urlselection): every selection
+// query's url ids on this shard (from the url dictionary; urls it does not hold
+// can match nothing) and the local sizes of its include and exclude lists
+// restricted to them -- the sizes ReferenceContainerCache.get(key, urlselection)
+// gives (ReferenceContainerCache.java:448-470), on which J1 / J2 / J3 decide.
+static int resolve_selections(Lane* L, std::vector<Plan>& plans) {
+  std::vector<size_t> qs;
+  for (size_t q = 0; q < plans.size(); q++)
+    if (plans[q].has_sel) qs.push_back(q);
+  if (qs.empty()) return 0;
+  if (begin_pass(L)) return YRWI_E_HIP;
+  std::vector<uint64_t> hi;
+  std::vector<uint8_t> lo;
+  std::vector<size_t> off{0};
+  for (size_t q : qs) {
+    for (const KeyT& k : plans[q].sel) {
+      hi.push_back(k.hi);
+      lo.push_back((uint8_t)k.lo);
+    }
+    off.push_back(hi.size());
+  }
+  const int64_t n = (int64_t)hi.size();
+  uint64_t* d_hi = arena_alloc<uint64_t>(L, n);
+  uint8_t* d_lo = arena_alloc<uint8_t>(L, n);
+  uint32_t* d_uid = arena_alloc<uint32_t>(L, n);
+  if (!d_hi || !d_lo || !d_uid) return L->fail(YRWI_E_NOMEM, "arena");
+  if (upload(L, d_hi, hi, d_lo, lo)) return YRWI_E_HIP;
+  if (launch_sel_lookup(d_hi, d_lo, n, L->dkhi, L->dklo, L->dkhi ? L->nurls : 0, d_uid, L->stream))
+    return L->fail(YRWI_E_HIP, "selection lookup launch");
+  const uint8_t* hb = readback(L, &L->down_stage, d_uid, n, 4, 4);
+  if (!hb) return YRWI_E_HIP;
+  HIPCHK(L, lane_sync(L));
+  std::vector<uint32_t> uids((size_t)n);
+  std::memcpy(uids.data(), hb, (size_t)n * 4);
+  std::vector<uint32_t> all;  // every query's ids, concatenated (ascending per query: ids keep key order)
+  std::vector<int64_t> aoff;
+  for (size_t i = 0; i < qs.size(); i++) {
+    Plan& P = plans[qs[i]];
+    P.sel_uid.clear();
+    for (size_t j = off[i]; j < off[i + 1]; j++)
+      if (uids[j] != 0xFFFFFFFFu) P.sel_uid.push_back(uids[j]);
+    aoff.push_back((int64_t)all.size());
+    all.insert(all.end(), P.sel_uid.begin(), P.sel_uid.end());
+  }
+  uint32_t* d_all = arena_alloc<uint32_t>(L, (int64_t)all.size());
+  if (!d_all) return L->fail(YRWI_E_NOMEM, "arena");
+  std::vector<SelCount> jobs;
+  std::vector<std::pair<size_t, int>> who;  // (plan, list: include i or YRWI_MAX_TERMS + exclude i)
+  int64_t* d_cnt = arena_alloc<int64_t>(L, (int64_t)qs.size() * 2 * YRWI_MAX_TERMS);
+  if (!d_cnt) return L->fail(YRWI_E_NOMEM, "arena");
+  for (size_t i = 0; i < qs.size(); i++) {
+    Plan& P = plans[qs[i]];
+    for (int t = 0; t < YRWI_MAX_TERMS; t++) P.sel_ninc[t] = P.sel_nexc[t] = 0;
+    for (int li = 0; li < P.ninc + P.nexc; li++) {
+      const ListRec* R = li < P.ninc ? P.linc[li] : P.lexc[li - P.ninc];
+      if (!R || P.sel_uid.empty()) continue;
+      SelCount c{};
+      c.L = chain_list(R);
+      c.sel = d_all + aoff[i];
+      c.nsel = (int64_t)P.sel_uid.size();
+      c.out = d_cnt + (int64_t)jobs.size();
+      jobs.push_back(c);
+      who.push_back({qs[i], li < P.ninc ? li : YRWI_MAX_TERMS + (li - P.ninc)});
+    }
+  }
+  if (jobs.empty()) return 0;
+  SelCount* d_jobs = arena_alloc<SelCount>(L, (int64_t)jobs.size());
+  if (!d_jobs) return L->fail(YRWI_E_NOMEM, "arena");
+  if (upload(L, d_all, all, d_jobs, jobs)) return YRWI_E_HIP;
+  if (launch_sel_count(d_jobs, (int32_t)jobs.size(), L->stream)) return L->fail(YRWI_E_HIP, "selection count launch");
+  const uint8_t* cb = readback(L, &L->down_stage, d_cnt, (int64_t)jobs.size(), 8, 8);
+  if (!cb) return YRWI_E_HIP;
+  HIPCHK(L, lane_sync(L));
+  for (size_t j = 0; j < jobs.size(); j++) {
+    int64_t c;
+    std::memcpy(&c, cb + 8 * j, 8);
+    Plan& P = plans[who[j].first];
+    if (who[j].second < YRWI_MAX_TERMS) P.sel_ninc[who[j].second] = c;
+    else P.sel_nexc[who[j].second - YRWI_MAX_TERMS] = c;
+  }
+  return 0;
+}
+
 // plan_finish for a batch: global term sizes from one exchange of the local
 // sizes of the batch's distinct terms (sharded), or the local sizes (one context).
 static int plan_batch(Lane* L, std::vector<Plan>& plans) {
+  // a query with a url selection sees its lists restricted to it (resolve_selections)
+  auto inc_n = [](const Plan& P, int i) -> int64_t { return P.has_sel ? P.sel_ninc[i] : P.linc[i] ? P.linc[i]->n : 0; };
+  auto exc_n = [](const Plan& P, int i) -> int64_t { return P.has_sel ? P.sel_nexc[i] : P.lexc[i] ? P.lexc[i]->n : 0; };
   if (!L->sharded) {  // one context: its own sizes are the global ones
     for (Plan& P : plans) {
       int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
-      for (int i = 0; i < P.ninc; i++) gi[i] = P.linc[i] ? P.linc[i]->n : 0;
-      for (int i = 0; i < P.nexc; i++) ge[i] = P.lexc[i] ? P.lexc[i]->n : 0;
+      for (int i = 0; i < P.ninc; i++) gi[i] = inc_n(P, i);
+      for (int i = 0; i < P.nexc; i++) ge[i] = exc_n(P, i);
       plan_finish(&P, gi, ge);
     }
     return 0;
@@ -634,12 +736,18 @@ static int plan_batch(Lane* L, std::vector<Plan>& plans) {
     sz.push_back(l ? l->n : 0);
     return sz.size() - 1;
   };
+  auto own_slot = [&](int64_t n) {  // a selection query's restricted size: a slot of its own
+    sz.push_back(n);
+    return sz.size() - 1;
+  };
   // first-appearance order over the batch's queries: identical on every rank
   std::vector<std::array<size_t, 2 * YRWI_MAX_TERMS>> idx(plans.size());
   for (size_t q = 0; q < plans.size(); q++) {
     Plan& P = plans[q];
-    for (int i = 0; i < P.ninc; i++) idx[q][(size_t)i] = slot_of(P.inc[i], P.linc[i]);
-    for (int i = 0; i < P.nexc; i++) idx[q][(size_t)(YRWI_MAX_TERMS + i)] = slot_of(P.exc[i], P.lexc[i]);
+    for (int i = 0; i < P.ninc; i++)
+      idx[q][(size_t)i] = P.has_sel ? own_slot(inc_n(P, i)) : slot_of(P.inc[i], P.linc[i]);
+    for (int i = 0; i < P.nexc; i++)
+      idx[q][(size_t)(YRWI_MAX_TERMS + i)] = P.has_sel ? own_slot(exc_n(P, i)) : slot_of(P.exc[i], P.lexc[i]);
   }
   if (int rc = allsum_host(L, sz)) return rc;
   for (size_t q = 0; q < plans.size(); q++) {
@@ -668,6 +776,7 @@ static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
   if (mode == JM_ENUM) return 12 * (na + nb);
   int64_t ns = std::min(na, nb), nl = std::max(na, nb);
+  if (ns <= 0) return 0;  // by test with an empty smaller side: nothing is probed
   int64_t lg = 0;
   while ((ns << lg) < nl) lg++;  // ceil(log2(nl/ns))
   return 12 * (ns + std::min(nl, ns * (lg + 1)));
@@ -691,6 +800,7 @@ struct Timing {
   std::vector<std::array<hipEvent_t, 2>> kcompact;  // around each k_compact launch
   std::vector<std::array<hipEvent_t, 2>> kreduce;   // around each k_reduce + k_shard_fin
   std::vector<std::array<hipEvent_t, 2>> kscore;    // around each pass's k_score launches
+  std::vector<std::array<hipEvent_t, 2>> kchain;    // around each chained step's k_chain_part .. k_scan_tiles
   // around every group of back-to-back kernel launches of the batch (no host
   // synchronisation inside a span): their sum is the batch's kernel time
   std::vector<std::array<hipEvent_t, 2>> spans;
@@ -712,12 +822,18 @@ static void span_close(Lane* L, Timing* tm, hipEvent_t b) {
 
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
-static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vector<int>& owner, std::vector<int64_t>& tile_base,
-                        int* nmerge, int64_t* merge_tiles, int64_t* tiles, bool* long_tiles) {
+static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& jobs, std::vector<int>& owner,
+                        std::vector<int64_t>& tile_base, int* nmerge, int64_t* merge_tiles, int64_t* tiles,
+                        bool* long_tiles) {
   *long_tiles = false;
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
     JoinQ& J = jobs[i];
+    // a sparse list's bitmap (below 1/64 of the url ids: k_chain's tests and the
+    // selections use it) does not take a join: its probes search the list, where
+    // a tile's staged range costs less than a bitmap line per key
+    if (J.A.bm && J.A.n * 64 < nurls) J.A.bm = nullptr;
+    if (J.B.bm && J.B.n * 64 < nurls) J.B.bm = nullptr;
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
     J.small_is_A = J.A.n <= J.B.n;
     // skewed sizes: probe the large list; a large list with a url-id bitmap is
@@ -727,7 +843,7 @@ static void layout_jobs(int64_t probe_ratio, std::vector<JoinQ>& jobs, std::vect
     // long bitmap tiles only where no record is gathered per match (a deferred
     // step writes sources, an exclusion marks): a final step's compaction keeps
     // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
-    const bool light = J.out_tup != nullptr || J.mode == JM_MARK;
+    const bool light = J.out_tup != nullptr || J.mode == JM_MARK || J.chained;  // chained: only survivors gather
     J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
     if (J.ptile == KPT_LARGE * PROBE_TILE) *long_tiles = true;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
@@ -823,7 +939,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
   const int64_t h0 = hprof ? now_ns() : 0;
   bool long_tiles;
-  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
@@ -879,7 +995,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     if (!d_lvl || !d_crange || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
     int maxi = 0;
     for (int j = 0; j < nj; j++)
-      if (plans[(size_t)owner[(size_t)j]].chain) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].ninc);
+      if (plans[(size_t)owner[(size_t)j]].chain) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].npos);
     int32_t* d_tup[CHAIN_MAXI] = {nullptr, nullptr};  // rows in the later include lists, indexed like d_pairs
     for (int l = 0; l < maxi; l++)
       if (!(d_tup[l] = arena_alloc<int32_t>(ctx, npairs))) return ctx->fail(YRWI_E_NOMEM, "arena");
@@ -889,7 +1005,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       if (!plans[(size_t)pq].chain) continue;
       ChainQ C = (*chq)[(size_t)pq];
       C.level = d_mout + nj + (int64_t)j * CHAIN_LVL;
-      for (int l = 0; l < CHAIN_MAXI; l++) C.tup[l] = l < C.ninc ? d_tup[l] : nullptr;
+      for (int l = 0; l < CHAIN_MAXI; l++) C.tup[l] = l < C.npos ? d_tup[l] : nullptr;
       J.chain = d_cq + (int64_t)cq.size();
       cq.push_back(C);
     }
@@ -909,6 +1025,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     tm->kjoin.push_back({e0, em, e1});
     if (chain) {
       hipEventRecord(c1, ctx->stream);  // the span ends after k_chain / k_scan_tiles; compaction comes later
+      tm->kchain.push_back({e1, c1});
     } else {
       tm->kcompact.push_back({c0, c1});
     }
@@ -917,6 +1034,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (st) {
     st->n_join_launches++;
     st->n_probe_dispatches += tiles > merge_tiles;
+    st->n_chain_launches += chain ? 1 : 0;
   }
   const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
@@ -935,7 +1053,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       const JoinQ& J = jobs[(size_t)j];
       const int64_t atw = J.A.tup ? J.A.tw : 0;
       if (J.chain) {
-        const int64_t t = 2 + (*chq)[(size_t)owner[(size_t)j]].ninc;
+        const int64_t t = 2 + (*chq)[(size_t)owner[(size_t)j]].npos;
         st->bytes_compact += mh[(size_t)j] * (12 + 4 * (t - 2) + 32 + 24 * (t - 1) + 36);
         continue;
       }
@@ -943,6 +1061,16 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
                                                       : (J.mode == JM_ENUM ? 96 : 80) + 4 * atw +
                                                             (atw > 1 ? 24 * (atw - 1) : 0));
     }
+  if (chain) {  // chained jobs' containers, sized by their survivors; the job table again for k_compact
+    for (int j = 0; j < nj; j++) {
+      JoinQ& J = jobs[(size_t)j];
+      if (!J.chain) continue;
+      J.out_uid = arena_alloc<uint32_t>(ctx, mh[(size_t)j]);
+      J.out_feat = arena_alloc<uint64_t>(ctx, mh[(size_t)j] * FEAT_WORDS);
+      if (!J.out_uid || !J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
+    }
+    if (upload(ctx, d_jobs, jobs)) return YRWI_E_HIP;
+  }
   for (int j = 0; j < nj; j++) {
     Plan& P = plans[(size_t)owner[(size_t)j]];
     const JoinQ& J = jobs[(size_t)j];
@@ -961,7 +1089,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     pend->d_cnt = d_cnt;
     pend->d_off = d_off;
     pend->bo = bo;
-    pend->level.assign((size_t)nj, {0, 0, 0, 0});
+    pend->level.assign((size_t)nj, {0, 0, 0, 0, 0});
     const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
     for (int j = 0; j < nj; j++)
       if (jobs[(size_t)j].chain)
@@ -996,7 +1124,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   int nmerge;
   int64_t merge_tiles, tiles;
   bool long_tiles;
-  layout_jobs(ctx->probe_ratio, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   if (st)
     for (const JoinQ& J : jobs) st->bytes_alg_capped += std::min<int64_t>(12 * J.B.n, loaded_bytes(J));
@@ -1024,15 +1152,13 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
 // containers: the next list's (Plan.seq_ng) and the accumulated container's,
 // which after the first step is the sum over the shards of their joined rows
 // (one exchange per step that some query continues past; none on one context).
-static ChainList chain_list(const ListRec* L) { return ChainList{L->uid, L->head, L->bm, L->n}; }
-
 static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   const size_t nq = plans.size();
   std::vector<int64_t> acc_g(nq, 0);  // global size of each query's accumulated container
   for (size_t qi = 0; qi < nq; qi++) {
     Plan& P = plans[qi];
     if (P.empty) { P.cont = DList{nullptr, nullptr, nullptr, 0}; continue; }
-    P.cont = P.seq[0]->dl();
+    P.cont = P.seq[0]->dl();  // (a single list under a url selection: restricted below)
     acc_g[qi] = P.seq_ng[0];
   }
   static const bool defer = !(getenv("YRWI_NO_DEFER") && atoi(getenv("YRWI_NO_DEFER")));
@@ -1044,17 +1170,61 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
   const bool chain_on = !(nc && atoi(nc));
   std::vector<ChainQ> chq(nq);
   bool any_chain = false;
+  // url selections (resolve_selections): their ids for this pass's kernels; a
+  // single include list is restricted right here (k_sel_pick), a fold of two or
+  // more chains the selection as its first test (ChainQ)
+  std::vector<uint32_t*> dsel(nq, nullptr);
+  std::vector<SelPick> picks;
+  for (size_t qi = 0; qi < nq; qi++) {
+    Plan& P = plans[qi];
+    if (!P.has_sel || P.empty) continue;
+    if (!P.sel_uid.empty()) {
+      if (!(dsel[qi] = arena_alloc<uint32_t>(ctx, (int64_t)P.sel_uid.size()))) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (upload(ctx, dsel[qi], P.sel_uid)) return YRWI_E_HIP;
+    }
+    if (P.seq.size() == 1) {  // ReferenceContainer.java:355-370: the one (restricted) container, rows as stored
+      const int64_t m = P.sel_ninc[P.seq_term[0]];
+      P.cont = DList{nullptr, nullptr, nullptr, 0};
+      if (m == 0 || P.seq[0]->n == 0) continue;
+      SelPick k{};
+      k.L = chain_list(P.seq[0]);
+      k.feat = P.seq[0]->feat;
+      k.rows = P.seq[0]->rows;
+      k.sel = dsel[qi];
+      k.nsel = (int64_t)P.sel_uid.size();
+      k.out_uid = arena_alloc<uint32_t>(ctx, m);
+      k.out_feat = arena_alloc<uint64_t>(ctx, m * FEAT_WORDS);
+      k.out_rows = arena_alloc<uint8_t>(ctx, m * YRWI_ROW_BYTES);
+      if (!k.out_uid || !k.out_feat || !k.out_rows) return ctx->fail(YRWI_E_NOMEM, "arena");
+      P.cont = DList{nullptr, nullptr, k.out_rows, m, k.out_uid, k.out_feat, nullptr, nullptr, 0};
+      picks.push_back(k);
+    }
+  }
+  if (!picks.empty()) {
+    SelPick* d_pk = arena_alloc<SelPick>(ctx, (int64_t)picks.size());
+    if (!d_pk) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (upload(ctx, d_pk, picks)) return YRWI_E_HIP;
+    if (launch_sel_pick(d_pk, (int32_t)picks.size(), ctx->stream)) return ctx->fail(YRWI_E_HIP, "selection launch");
+  }
   for (size_t qi = 0; qi < nq; qi++) {
     Plan& P = plans[qi];
     P.chain = false;
-    if (!chain_on || !defer || P.empty || P.maxd < 65535 || acc_g[qi] == 0) continue;
-    const int t = (int)P.seq.size(), ni = t - 2;
-    if (t < 2 || ni > CHAIN_MAXI || ni + P.nexcl_g == 0 || ni + P.nexcl_g > CHAIN_MAXL) continue;
+    const int t = (int)P.seq.size(), ni = t - 2, ns = P.has_sel ? 1 : 0;
+    const bool can = chain_on && defer && !P.empty && P.maxd >= 65535 && acc_g[qi] > 0 && t >= 2 &&
+                     ni <= CHAIN_MAXI && ns + ni + P.nexcl_g > 0 && ns + ni + P.nexcl_g <= CHAIN_MAXL;
+    if (P.has_sel && !P.empty && t >= 2 && !can)
+      return ctx->fail(YRWI_E_UNSUPPORTED, "urlselection: a fold of more than four include terms or with a "
+                                           "maxDistance filter");
+    if (!can) continue;
     ChainQ& C = chq[qi];
     std::memset(&C, 0, sizeof(C));
-    C.ninc = ni;
-    for (int l = 0; l < ni; l++) C.l[l] = chain_list(P.seq[(size_t)l + 2]);
-    C.nl = ni;
+    C.nl = 0;
+    if (ns)  // the selection first: its ids, no heads, no bitmap
+      C.l[C.nl++] = ChainList{dsel[qi], nullptr, nullptr, (int64_t)P.sel_uid.size()};
+    for (int l = 0; l < ni; l++) C.l[C.nl++] = chain_list(P.seq[(size_t)l + 2]);
+    C.ninc = C.nl;
+    C.pos0 = ns;
+    C.npos = ni;
     for (const ListRec* E : P.excl) C.l[C.nl++] = chain_list(E);  // this shard's lists of the exclusion terms
     if (st)
       for (const ListRec* E : P.excl) st->bytes_alg += 12 * E->n;
@@ -1091,9 +1261,12 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.mode = dispatch_mode(acc_g[qi], P.seq_ng[s + 1]);
       J.maxd = P.maxd;
       J.now_ms = P.now_ms;
+      J.chained = P.chain ? 1 : 0;
       P.step_mode[s] = J.mode;
       int64_t cap = std::min(J.A.n, J.B.n);
-      J.out_uid = arena_alloc<uint32_t>(ctx, cap);
+      // a chained job's output is allocated once k_chain has counted its survivors
+      // (run_join_jobs): its capacity bound min(nA, nB) is far above them
+      J.out_uid = P.chain ? nullptr : arena_alloc<uint32_t>(ctx, cap);
       // A step before the fold's last keeps its rows deferred (the rows of lists
       // 0..s+1 they join, no records): the next step joins on url ids alone, and
       // only the last step gathers and folds the records of the rows that survive.
@@ -1105,8 +1278,8 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         J.out_tup = arena_alloc<int32_t>(ctx, cap * J.out_tw);
         if (!J.out_tup) return ctx->fail(YRWI_E_NOMEM, "arena");
       } else {
-        J.out_feat = arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
-        if (!J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
+        J.out_feat = P.chain ? nullptr : arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
+        if (!J.out_feat && !P.chain) return ctx->fail(YRWI_E_NOMEM, "arena");
         if (P.chain) {
           chain_q.push_back((int)qi);
         } else if (J.A.tup) {
@@ -1120,7 +1293,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
           fold_job.push_back((int)jobs.size());
         }
       }
-      if (!J.out_uid) return ctx->fail(YRWI_E_NOMEM, "arena");
+      if (!J.out_uid && !P.chain) return ctx->fail(YRWI_E_NOMEM, "arena");
       if (st) {
         st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
@@ -1159,9 +1332,10 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       std::vector<int64_t> v(cqs.size() * 2, 0);
       for (size_t k = 0; k < cqs.size(); k++) {
         const int j = job_of[(size_t)cqs[k]];
-        if (j >= 0 && pend.active) {
-          v[2 * k] = pend.level[(size_t)j][0];
-          v[2 * k + 1] = pend.level[(size_t)j][1];
+        if (j >= 0 && pend.active) {  // the intersection sizes after the selection (if any) and include 2
+          const int o = chq[(size_t)cqs[k]].pos0;
+          v[2 * k] = pend.level[(size_t)j][(size_t)o];
+          v[2 * k + 1] = pend.level[(size_t)j][(size_t)o + 1];
         }
       }
       std::vector<int64_t> loc = v;
@@ -1179,9 +1353,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
             const int64_t K = step_bytes(m, acc, n);
             const int64_t loaded = P.seq[(size_t)l]->bm ? 20 * acc : 4 * acc + std::min(4 * n, 128 * acc);
             st->bytes_alg += K;
-            st->bytes_probe += K;
-            st->bytes_probe_capped += std::min(K, loaded);
-            st->bytes_probe_loaded += loaded;
+            st->bytes_chain += std::min(K, loaded);
             st->bytes_alg_capped += std::min(K, loaded);
             if (m == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
           }
@@ -1212,10 +1384,13 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         for (size_t k = 0; k < cqs.size(); k++) {
           const int j = job_of[(size_t)cqs[k]];
           const ChainQ& C = chq[(size_t)cqs[k]];
-          const int64_t pre = (j >= 0 && pend.active) ? pend.level[(size_t)j][2] : 0;
-          for (int l = C.ninc; l < C.nl; l++)
-            st->bytes_alg_capped += std::min<int64_t>(12 * C.l[l].n, C.l[l].bm ? 20 * pre
-                                                                               : 4 * pre + std::min(4 * C.l[l].n, 128 * pre));
+          const int64_t pre = (j >= 0 && pend.active) ? pend.level[(size_t)j][(size_t)C.ninc] : 0;
+          for (int l = C.ninc; l < C.nl; l++) {
+            const int64_t b = std::min<int64_t>(12 * C.l[l].n, C.l[l].bm ? 20 * pre
+                                                                         : 4 * pre + std::min(4 * C.l[l].n, 128 * pre));
+            st->bytes_alg_capped += b;
+            st->bytes_chain += b;
+          }
         }
       }
     } else if (pend.active) {
@@ -1756,6 +1931,8 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
     if (rc) return rc;
     if (st) st->postings_in += all[(size_t)i].postings_in;
   }
+  // url selections: restricted list sizes first (J1/J2/J3 decide on them)
+  if (int rc = resolve_selections(L, all)) return rc;
   // J1/J2 on global list sizes (one exchange of the batch's term sizes when sharded,
   // through this lane's arena and staging)
   if (L->sharded && begin_pass(L)) return YRWI_E_HIP;
@@ -1814,6 +1991,8 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_reduce_ns += (int64_t)(ms * 1e6);
       for (auto& ev : tm.kscore)
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_scorek_ns += (int64_t)(ms * 1e6);
+      for (auto& ev : tm.kchain)
+        if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_chain_ns += (int64_t)(ms * 1e6);
       if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
       if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
     }
@@ -1926,6 +2105,9 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->t_scorek_ns += p.t_scorek_ns;
       st->bytes_reduce += p.bytes_reduce;
       st->bytes_score += p.bytes_score;
+      st->n_chain_launches += p.n_chain_launches;
+      st->t_chain_ns += p.t_chain_ns;
+      st->bytes_chain += p.bytes_chain;
     }
     st->t_total_ns = now_ns() - t0;
   }
@@ -2034,9 +2216,6 @@ extern "C" int yrwi_score_nodes(yrwi_ctx* ctx, const yrwi_node* nodes, int64_t n
 extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nincl, const uint8_t* excl,
                                  int32_t nexcl, int32_t max_distance, int64_t now_ms, uint8_t* rows_out,
                                  int64_t cap_rows, int64_t* m) {
-  if (!ctx || !m) return YRWI_E_ARG;
-  *m = 0;
-  hipSetDevice(ctx->device);
   yrwi_query_desc d{};
   d.incl = incl;
   d.nincl = nincl;
@@ -2045,12 +2224,24 @@ extern "C" int yrwi_join_exclude(yrwi_ctx* ctx, const uint8_t* incl, int32_t nin
   d.max_distance = max_distance;
   d.k = 1;
   d.now_ms = now_ms;
+  return yrwi_term_search(ctx, &d, rows_out, cap_rows, m);
+}
+
+extern "C" int yrwi_term_search(yrwi_ctx* ctx, const yrwi_query_desc* q, uint8_t* rows_out, int64_t cap_rows,
+                                int64_t* m) {
+  if (!ctx || !m || !q) return YRWI_E_ARG;
+  *m = 0;
+  hipSetDevice(ctx->device);
+  yrwi_query_desc d = *q;
+  d.k = 1;
+  d.filter = nullptr;
   drain(ctx);
   if (int rc0 = ensure_url_ids(ctx)) return rc0;
   Lane* L = ctx->lanes[0];
   std::vector<Plan> plans(1);
   int rc = ctx->take(L, plan_query(ctx, L, d, &plans[0]));
   if (rc) return rc;
+  if ((rc = ctx->take(L, resolve_selections(L, plans)))) return rc;
   if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
   if ((rc = ctx->take(L, plan_batch(L, plans)))) return rc;
   rc = ctx->take(L, run_join_phase(L, plans, nullptr, nullptr));

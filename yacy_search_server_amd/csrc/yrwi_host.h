@@ -185,6 +185,14 @@ struct Plan {
   uint8_t* removed = nullptr;
   int nexcl_g = 0;      // exclusion terms in effect (J1 on global sizes; excl holds this shard's lists of them)
   bool chain = false;   // chained fold (ChainQ, yrwi_internal.h): one join step, k_chain does the rest
+  int seq_term[YRWI_MAX_TERMS] = {0};  // include term (linc index) of every seq list
+  // TermSearch's urlselection (yrwi_query_desc.urlselection): its keys (sorted,
+  // unique), their url ids on this shard (ascending; urls the dictionary does not
+  // hold dropped), and the local sizes of the query's lists restricted to it
+  bool has_sel = false;
+  std::vector<KeyT> sel;
+  std::vector<uint32_t> sel_uid;
+  int64_t sel_ninc[YRWI_MAX_TERMS] = {0}, sel_nexc[YRWI_MAX_TERMS] = {0};
 };
 
 

@@ -117,9 +117,9 @@ struct FoldSrc {
 // later include lists, and k_compact folds their records over all t lists (J5/J6
 // step by step, each step's dispatch from the intersection sizes k_chain counts).
 // No intermediate container is written.  ReferenceContainer.java:328-388.
-constexpr int CHAIN_MAXL = 6;  // lists tested per pair (later includes, then exclusions)
+constexpr int CHAIN_MAXL = 6;  // lists tested per pair (the url selection, later includes, then exclusions)
 constexpr int CHAIN_MAXI = 2;  // later include lists (t <= 4)
-constexpr int CHAIN_LVL = 4;   // per-tile counts: matches, after include 2, after include 3, after exclusion
+constexpr int CHAIN_LVL = 5;   // per-tile counts: matches, after include tests 1, 2, 3, after exclusion
 struct ChainList {
   const uint32_t* uid;
   const uint32_t* head;  // line heads (DList::head) or nullptr
@@ -127,8 +127,12 @@ struct ChainList {
   int64_t n;
 };
 struct ChainQ {
-  ChainList l[CHAIN_MAXL];   // includes 2..t-1 of the fold (in fold order), then the exclusion lists
-  int32_t ninc, nl;
+  // include tests first -- the query's url selection (if any: uid = its url ids, no
+  // heads, no bitmap), then includes 2..t-1 of the fold (in fold order) -- then
+  // the exclusion lists
+  ChainList l[CHAIN_MAXL];
+  int32_t ninc, nl;          // include tests; all lists
+  int32_t pos0, npos;        // the include tests whose row is kept: [pos0, pos0 + npos) (lists 2..t-1)
   int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
   int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
 };
@@ -142,7 +146,7 @@ struct JoinQ {
   int32_t algo;        // JoinAlgo
   int32_t small_is_A;  // JA_PROBE: which side is probed into the other
   int32_t ptile;       // JA_PROBE: small-list elements per tile (PROBE_TILE, BM_TILE with a bitmap)
-  int32_t pad_;
+  int32_t chained;     // a chained fold's first step (set before layout; JoinQ::chain points at its ChainQ)
   uint8_t* removed;    // JM_MARK target (indexed like A)
   uint32_t* out_uid;   // compacted output container (capacity min(nA, nB))
   uint64_t* out_feat;  // its ranking records (FEAT_WORDS per row)
@@ -441,6 +445,31 @@ struct EvJob {
 // one workgroup per event: jobs [jb[b], jb[b+1]) of the same event, in arrival order; status[j] = 0 / YRWI_E_*
 int launch_event_add(const EvDev* d_ev, const EvJob* d_jobs, const int32_t* d_jb, int32_t nblocks, int32_t* d_status,
                      void* stream);
+// ---- TermSearch's urlselection (yrwi_query_desc.urlselection)
+// url id of each of n url keys (0xFFFFFFFF: not in the url dictionary)
+int launch_sel_lookup(const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, const uint64_t* dkhi, const uint8_t* dklo,
+                      int64_t nurls, uint32_t* d_uid, void* stream);
+struct SelCount {
+  ChainList L;           // an include or exclude list of the query
+  const uint32_t* sel;   // the query's url ids (ascending)
+  int64_t nsel;
+  int64_t* out;          // |L restricted to the selection|
+};
+int launch_sel_count(const SelCount* d_jobs, int32_t njobs, void* stream);
+// a single include list restricted to the selection, rows as they are stored
+// (ReferenceContainerCache.get + the as-is single container, ReferenceContainer.java:355-370):
+// one workgroup per query
+struct SelPick {
+  ChainList L;
+  const uint64_t* feat;
+  const uint8_t* rows;
+  const uint32_t* sel;
+  int64_t nsel;
+  uint32_t* out_uid;
+  uint64_t* out_feat;
+  uint8_t* out_rows;
+};
+int launch_sel_pick(const SelPick* d_jobs, int32_t njobs, void* stream);
 // ReferenceOrder.authority (ReferenceOrder.java:213-216) of n host keys (host36 + 1)
 // against an event's accumulated host counts
 int launch_event_authority(const EvDev* d_ev, const uint64_t* d_keys, int32_t n, int32_t* d_out, void* stream);

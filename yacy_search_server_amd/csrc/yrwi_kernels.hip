@@ -1159,6 +1159,142 @@ __global__ void k_chain_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   crange[i] = D;
 }
 
+// Lower bounds of up to KPT keys at once, each in its own window a[base, base + n)
+// of at most 32 ids (a line of ids or of line heads): a power-of-two bisection of
+// six rounds (results 0..32), the same for every key, with every live key's load
+// of a round in flight together (the lines a per-key search would wait for one by one)
+template <int KPT>
+__device__ __forceinline__ void lower_bound_multi(const uint32_t* __restrict__ a, int64_t* base, int32_t* n,
+                                                  const uint32_t* key, uint32_t live) {
+  int32_t off[KPT];
+#pragma unroll
+  for (int k = 0; k < KPT; k++) off[k] = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    uint32_t v[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      v[k] = 0xFFFFFFFFu;
+      if (((live >> k) & 1u) && off[k] + step <= n[k]) v[k] = ldg(a + base[k] + off[k] + step - 1);
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; k++)
+      if (v[k] < key[k]) off[k] += step;
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; k++) base[k] += off[k];
+}
+
+// the same in LDS over one array s[0, n) for every key (n <= 8192): the first
+// index with s[i] >= key, no divergence (every key takes the same steps)
+template <int KPT>
+__device__ __forceinline__ void lds_lower_bound_multi(const uint32_t* s, int n, const uint32_t* key, uint32_t live,
+                                                      int* out) {
+#pragma unroll
+  for (int k = 0; k < KPT; k++) out[k] = 0;
+  int top = 1;
+  while (top * 2 <= n) top *= 2;
+  for (int step = n > 0 ? top : 0; step > 0; step >>= 1) {
+#pragma unroll
+    for (int k = 0; k < KPT; k++)
+      if (((live >> k) & 1u) && out[k] + step <= n && s[out[k] + step - 1] < key[k]) out[k] += step;
+  }
+}
+
+// Membership and position of the live keys (ascending, all inside [lo, hi)) in a
+// list without a url-id bitmap, by the whole workgroup (barriers inside; every
+// decision is workgroup-uniform): the range's ids staged in LDS when it fits;
+// otherwise its level-1 line heads (every 32nd id) or, past that, its level-2
+// heads (every 1024th) staged in LDS, an LDS search per key, then (level 2) one
+// line of level-1 heads and one leaf line of ids per key (lower_bound_multi);
+// per-key head searches only beyond both stages.
+template <int KPT>
+__device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int64_t hi, const uint32_t* key,
+                                             uint32_t live, int32_t* pos, uint32_t& hit, uint32_t* sL) {
+  hit = 0;
+  const int64_t R = hi - lo;
+  __syncthreads();  // the previous list's stage is no longer read
+  if (R <= PROBE_LDS) {
+    for (int x = threadIdx.x; x < (int)R; x += 256) sL[x] = ldg(L.uid + lo + x);
+    __syncthreads();
+    int a[KPT];
+    lds_lower_bound_multi<KPT>(sL, (int)R, key, live, a);
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      pos[k] = (int32_t)(lo + a[k]);
+      if (((live >> k) & 1u) && a[k] < (int)R && sL[a[k]] == key[k]) hit |= 1u << k;
+    }
+    return;
+  }
+  if (L.head) {
+    int sh = 5;
+    const uint32_t* __restrict__ hd = L.head;
+    int64_t g0 = (lo + 31) >> 5, g1 = (hi + 31) >> 5;  // heads at positions in [lo, hi)
+    if (g1 - g0 > PROBE_LDS) {
+      sh = 10;
+      hd = L.head + head1_cap(L.n);
+      g0 = (lo + 1023) >> 10;
+      g1 = (hi + 1023) >> 10;
+    }
+    if (g1 - g0 <= PROBE_LDS) {  // workgroup-uniform
+      const int H = (int)(g1 - g0);
+      for (int x = threadIdx.x; x < H; x += 256) sL[x] = ldg(hd + g0 + x);
+      __syncthreads();
+      int64_t wl[KPT];
+      int32_t wn[KPT];
+      int ha[KPT];  // first staged head >= key
+      lds_lower_bound_multi<KPT>(sL, H, key, live, ha);
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int a = ha[k];
+        // the lower bound lies in (position of head a-1, position of head a], within [lo, hi]
+        wl[k] = a > 0 ? ((g0 + a - 1) << sh) + 1 : lo;
+        const int64_t wr = a < H ? ((g0 + a) << sh) : hi;
+        wn[k] = ((live >> k) & 1u) ? (int32_t)(wr - wl[k]) : 0;
+      }
+      if (sh == 10) {  // narrow each window to one leaf line with its <= 32 level-1 heads
+        int64_t f0[KPT], hb[KPT];
+        int32_t hn[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+          f0[k] = (wl[k] + 31) >> 5;
+          hb[k] = f0[k];
+          hn[k] = (int32_t)(((wl[k] + wn[k] + 31) >> 5) - f0[k]);
+        }
+        lower_bound_multi<KPT>(L.head, hb, hn, key, live);
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+          const int64_t c = hb[k], f1 = (wl[k] + wn[k] + 31) >> 5;
+          const int64_t l2 = c > f0[k] ? ((c - 1) << 5) + 1 : wl[k];
+          const int64_t r2 = c < f1 ? (c << 5) : wl[k] + wn[k];
+          wl[k] = l2;
+          wn[k] = (int32_t)(r2 - l2);
+        }
+      }
+      lower_bound_multi<KPT>(L.uid, wl, wn, key, live);
+      uint32_t v[KPT];
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        v[k] = 0xFFFFFFFFu;
+        pos[k] = (int32_t)wl[k];
+        if (((live >> k) & 1u) && wl[k] < hi) v[k] = ldg(L.uid + wl[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < KPT; k++)
+        if (((live >> k) & 1u) && wl[k] < hi && v[k] == key[k]) hit |= 1u << k;
+      return;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; k++) {
+    pos[k] = 0;
+    if (!((live >> k) & 1u)) continue;
+    const int64_t q = lower_bound_cl(L, key[k]);
+    pos[k] = (int32_t)q;
+    if (q < L.n && ldg(L.uid + q) == key[k]) hit |= 1u << k;
+  }
+}
+
 constexpr int CHAIN_KPT = 9;  // matches per thread: a tile's matches in one pass
 static_assert(CHAIN_KPT * 256 >= JOIN_MAXM && CHAIN_KPT * 256 >= BM_TILE, "k_chain: one pass per tile");
 
@@ -1203,7 +1339,8 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
       alive |= 1u << k;
     }
   }
-  uint32_t after1 = alive, after2 = alive;  // live matches of this thread after include 2 / include 3
+  const int pos0 = ldg(&C->pos0);
+  uint32_t after1 = alive, after2 = alive, after3 = alive;  // live matches after include tests 1, 2, 3
   for (int l = 0; l < nl; l++) {
     const ChainList L = load_cl(&C->l[l]);
     const bool inc = l < ninc;
@@ -1228,48 +1365,25 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
       }
     } else {
       const ProbeDesc D = crange[t * CHAIN_MAXL + l];  // workgroup-uniform
-      const int64_t R = D.hi - D.lo;
-      if (R <= PROBE_LDS) {
-        __syncthreads();  // the previous list's range is no longer read
-        for (int x = threadIdx.x; x < (int)R; x += 256) sL[x] = ldg(L.uid + D.lo + x);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < CHAIN_KPT; k++) {
-          p[k] = 0;
-          if (!((alive >> k) & 1u)) continue;
-          int lo = 0, hi = (int)R;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sL[mid] < key[k]) lo = mid + 1; else hi = mid;
-          }
-          p[k] = (int32_t)(D.lo + lo);
-          if (lo < (int)R && sL[lo] == key[k]) hit |= 1u << k;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < CHAIN_KPT; k++) {
-          p[k] = 0;
-          if (!((alive >> k) & 1u)) continue;
-          const int64_t q = lower_bound_cl(L, key[k]);
-          p[k] = (int32_t)q;
-          if (q < L.n && ldg(L.uid + q) == key[k]) hit |= 1u << k;
-        }
-      }
+      chain_search<CHAIN_KPT>(L, D.lo, D.hi, key, alive, p, hit, sL);
     }
     if (inc) {
       alive &= hit;
+      const int pi = l - pos0;  // the selection keeps no row
 #pragma unroll
       for (int k = 0; k < CHAIN_KPT; k++) {
-        if (l == 0) pos[0][k] = p[k];
-        else if (l == 1) pos[1][k] = p[k];
+        if (pi == 0) pos[0][k] = p[k];
+        else if (pi == 1) pos[1][k] = p[k];
       }
       if (l == 0) after1 = alive;
       if (l == 1) after2 = alive;
+      if (l == 2) after3 = alive;
     } else {
       alive &= ~hit;
     }
   }
   if (ninc < 2) after2 = after1;
+  if (ninc < 3) after3 = after2;
   // survivors leave in slot order (slot k's 256 matches, then slot k+1's): per-slot
   // counts packed four to a 64-bit scan, as in probe_bitmap; the level counts ride
   // along in the last scan's spare fields
@@ -1281,8 +1395,8 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
 #pragma unroll
     for (int k = 4 * q; k < CHAIN_KPT && k < 4 * q + 4; k++) c |= (uint64_t)((alive >> k) & 1u) << (16 * (k - 4 * q));
     if (q == NSC - 1) {
-      static_assert(CHAIN_KPT % 4 == 1, "two spare 16-bit fields in the last scan");
-      c |= (uint64_t)__popc(after1) << 16 | (uint64_t)__popc(after2) << 32;
+      static_assert(CHAIN_KPT % 4 == 1, "three spare 16-bit fields in the last scan");
+      c |= (uint64_t)__popc(after1) << 16 | (uint64_t)__popc(after2) << 32 | (uint64_t)__popc(after3) << 48;
     }
     ex[q] = block_excl_sum256_u64(c, sScan64, &tot64[q]);
   }
@@ -1294,8 +1408,9 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
     run += (int32_t)((tot64[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
   }
   // every read of the tile's run happened before the scans' barriers: write in place
-  int32_t* tup0 = ninc > 0 ? ldg(&C->tup[0]) : nullptr;
-  int32_t* tup1 = ninc > 1 ? ldg(&C->tup[1]) : nullptr;
+  const int npos = ldg(&C->npos);
+  int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
+  int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
 #pragma unroll
   for (int k = 0; k < CHAIN_KPT; k++) {
     if (!((alive >> k) & 1u)) continue;
@@ -1311,7 +1426,78 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
     lv[0] = cnt;
     lv[1] = (int32_t)((lt >> 16) & 0xFFFFu);
     lv[2] = (int32_t)((lt >> 32) & 0xFFFFu);
-    lv[3] = run;
+    lv[3] = (int32_t)((lt >> 48) & 0xFFFFu);
+    lv[4] = run;
+  }
+}
+
+// ============================================================ url selection
+// TermSearch's urlselection (yrwi_query_desc.urlselection): the selection's url
+// ids from the dictionary, the size of every list of the query restricted to it,
+// and (single include list) the restricted list itself.
+__global__ void k_sel_lookup(const uint64_t* __restrict__ hi, const uint8_t* __restrict__ lo, int64_t n,
+                             const uint64_t* __restrict__ dkhi, const uint8_t* __restrict__ dklo, int64_t nurls,
+                             uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = hi[i];
+  const uint8_t l = lo[i];
+  int64_t a = 0, b = nurls;  // first dictionary key >= (h, l)
+  while (a < b) {
+    const int64_t mid = (a + b) >> 1;
+    const uint64_t mh = ldg(dkhi + mid);
+    if (mh < h || (mh == h && ldg(dklo + mid) < l)) a = mid + 1; else b = mid;
+  }
+  out[i] = (a < nurls && ldg(dkhi + a) == h && ldg(dklo + a) == l) ? (uint32_t)a : 0xFFFFFFFFu;
+}
+
+// membership (and position) of url id u in a list: its bitmap word, or its line heads
+__device__ __forceinline__ bool list_has(const ChainList& L, uint32_t u, int64_t* pos) {
+  if (L.n <= 0) return false;
+  if (L.bm) {
+    const ulonglong2 w = ldg(reinterpret_cast<const ulonglong2*>(L.bm) + (u >> 6));
+    const uint64_t bit = 1ull << (u & 63u);
+    *pos = (int64_t)w.y + __popcll(w.x & (bit - 1ull));
+    return (w.x & bit) != 0;
+  }
+  const int64_t q = lower_bound_cl(L, u);
+  *pos = q;
+  return q < L.n && ldg(L.uid + q) == u;
+}
+
+__global__ __launch_bounds__(256) void k_sel_count(const SelCount* __restrict__ jobs) {
+  __shared__ int32_t sScan[4];
+  const SelCount& J = jobs[blockIdx.x];
+  int32_t c = 0;
+  for (int64_t i = threadIdx.x; i < J.nsel; i += 256) {
+    int64_t p;
+    c += list_has(J.L, ldg(J.sel + i), &p) ? 1 : 0;
+  }
+  int32_t tot;
+  block_excl_sum256(c, sScan, &tot);
+  if (threadIdx.x == 0) *J.out = tot;
+}
+
+__global__ __launch_bounds__(256) void k_sel_pick(const SelPick* __restrict__ jobs) {
+  __shared__ int32_t sScan[4];
+  const SelPick& J = jobs[blockIdx.x];
+  int64_t run = 0;
+  for (int64_t i0 = 0; i0 < J.nsel; i0 += 256) {  // the selection in url-id order: the list's order
+    const int64_t i = i0 + threadIdx.x;
+    int64_t p = 0;
+    const bool h = i < J.nsel && list_has(J.L, ldg(J.sel + i), &p);
+    int32_t tot;
+    const int32_t off = block_excl_sum256(h ? 1 : 0, sScan, &tot);
+    if (h) {
+      const int64_t o = run + off;
+      stg(J.out_uid + o, ldg(J.sel + i));
+      store_rec(J.out_feat, o, load_rec(J.feat, p));
+      // 40-B rows, 8-B aligned (index memory and arena allocations start on 256 B)
+      const uint2* s2 = reinterpret_cast<const uint2*>(J.rows + p * YRWI_ROW_BYTES);
+      uint2* d2 = reinterpret_cast<uint2*>(J.out_rows + o * YRWI_ROW_BYTES);
+      for (int w = 0; w < YRWI_ROW_BYTES / 8; w++) stg(d2 + w, ldg(s2 + w));
+    }
+    run += tot;
   }
 }
 
@@ -1478,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         X.fold = J.fold;
         X.ctw = 0;
         if (CHAIN && J.chain) {
-          const int ni = ldg(&J.chain->ninc);
+          const int ni = ldg(&J.chain->npos);
           X.ctw = 2 + ni;
           X.ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
           X.ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
@@ -3563,6 +3749,17 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
   return rc(hipGetLastError());
 }
 
+// YRWI_SYNC_DEBUG=1: synchronise after every launch of a join step and name it on
+// stderr (a kernel that never finishes is the last one named)
+static void dbg_sync(const char* what, void* st) {
+  static const bool on = getenv("YRWI_SYNC_DEBUG") && atoi(getenv("YRWI_SYNC_DEBUG"));
+  if (!on) return;
+  fprintf(stderr, "[yrwi sync] %s ...", what);
+  fflush(stderr);
+  const hipError_t e = hipStreamSynchronize(reinterpret_cast<hipStream_t>(st));
+  fprintf(stderr, " done (%s)\n", hipGetErrorString(e));
+}
+
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
@@ -3591,11 +3788,13 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (merge_tiles > 0) {
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src, tkey, tjob);
+    dbg_sync("k_partition", st);
     if (!mark) hipLaunchKernelGGL(k_scan_bounds, dim3((unsigned)nmerge), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_src);
   }
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc, tkey, tjob, pkey, bo.pshift);
+  if (probe_tiles > 0) dbg_sync("k_probe_part", st);
   if (perm || pperm) {
     OrderArgs oa{};
     int nb = 0;
@@ -3615,17 +3814,20 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     if (pperm) prob(perm ? 1 : 0, pkey, probe_tiles, 0, tjob + merge_tiles, pperm);
     hipLaunchKernelGGL(k_order_hist, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
     hipLaunchKernelGGL(k_order_scatter, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
+    dbg_sync("k_order", st);
   }
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
+  if (merge_tiles > 0) dbg_sync("k_join", st);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
   if (probe_tiles > 0) {
     auto kp = long_tiles ? (mark ? k_probe<true, true> : k_probe<true, false>)
                          : (mark ? k_probe<false, true> : k_probe<false, false>);
     hipLaunchKernelGGL(kp, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
                        merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm);
+    dbg_sync(mark ? "k_probe (exclusion)" : "k_probe", st);
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
@@ -3633,12 +3835,15 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
       const int64_t nr = total_tiles * CHAIN_MAXL;
       hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
                          total_tiles, (const int32_t*)tjob, d_pair_uid, d_tile_src, d_tile_cnt, d_crange);
+      dbg_sync("k_chain_part", st);
       hipLaunchKernelGGL(k_chain, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
                          (const int32_t*)tjob, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl,
                          (const ProbeDesc*)d_crange);
+      dbg_sync("k_chain", st);
     }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off, (const int32_t*)(chain ? d_tile_lvl : nullptr));
+    dbg_sync("k_scan_tiles", st);
     if (!chain) {  // chained steps compact once the fold's dispatch modes are known (launch_compact)
       if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       if (int r = launch_compact(d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
@@ -3659,6 +3864,7 @@ int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njob
   hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
                      d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
                      perm, (const int32_t*)bo.tile_job);
+  dbg_sync(chain ? "k_compact<chain>" : "k_compact", st);
   return rc(hipGetLastError());
 }
 
@@ -4333,6 +4539,22 @@ __global__ void k_event_authority(const EvDev* __restrict__ ev, const uint64_t* 
   const RankQ& Q = ev->q;
   const int32_t c = Q.want_authority ? htab_count(Q.hkeys, Q.hcnt, Q.hmask, keys[i]) : 0;
   out[i] = div32(shl32(c, 8), add32(1, ev->st->maxdom));  // (doms.get(h) << 8) / (1 + maxdomcount)
+}
+
+int launch_sel_lookup(const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, const uint64_t* dkhi, const uint8_t* dklo,
+                      int64_t nurls, uint32_t* d_uid, void* st) {
+  if (n > 0)
+    hipLaunchKernelGGL(k_sel_lookup, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), d_hi, d_lo, n, dkhi, dklo,
+                       nurls, d_uid);
+  return rc(hipGetLastError());
+}
+int launch_sel_count(const SelCount* d_jobs, int32_t njobs, void* st) {
+  if (njobs > 0) hipLaunchKernelGGL(k_sel_count, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs);
+  return rc(hipGetLastError());
+}
+int launch_sel_pick(const SelPick* d_jobs, int32_t njobs, void* st) {
+  if (njobs > 0) hipLaunchKernelGGL(k_sel_pick, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs);
+  return rc(hipGetLastError());
 }
 
 int launch_event_authority(const EvDev* d_ev, const uint64_t* d_keys, int32_t n, int32_t* d_out, void* st) {

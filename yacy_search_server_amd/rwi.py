@@ -223,6 +223,7 @@ class Query:
     language: str = "en"
     now_ms: int = 0
     filter: Optional[QueryFilter] = None
+    urlselection: Optional[Sequence[bytes]] = None  # TermSearch's urlselection (url hashes)
 
 
 def _check(ctx, rc: int):
@@ -322,16 +323,23 @@ class RWIIndex:
 
     # ---- TermSearch / joinExcludeContainers ----
     def term_search(self, include: Sequence[bytes], exclude: Sequence[bytes] = (),
-                    max_distance: int = INTEGER_MAX, now_ms: int = 0) -> np.ndarray:
-        """The joined (and excluded) ReferenceContainer as (m, 40) uint8 rows."""
+                    max_distance: int = INTEGER_MAX, now_ms: int = 0,
+                    urlselection: Optional[Sequence[bytes]] = None) -> np.ndarray:
+        """The joined (and excluded) ReferenceContainer as (m, 40) uint8 rows
+        (TermSearch.joined(); with `urlselection`, every list restricted to those urls)."""
         cap = 0
         for t in include:
             cap = max(cap, self.get_size(t))
         out = np.zeros((max(cap, 1), 40), dtype=np.uint8)
         m = ctypes.c_int64()
-        _check(self._h, _lib.lib().yrwi_join_exclude(self._h, _hashes(include), len(include), _hashes(exclude),
-                                                     len(exclude), max_distance, now_ms, out.ctypes.data, cap,
-                                                     ctypes.byref(m)))
+        if urlselection is None:
+            _check(self._h, _lib.lib().yrwi_join_exclude(self._h, _hashes(include), len(include), _hashes(exclude),
+                                                         len(exclude), max_distance, now_ms, out.ctypes.data, cap,
+                                                         ctypes.byref(m)))
+        else:
+            arr, keep, _, _, _ = self._marshal([Query(include, exclude, max_distance, 1, None, "en", now_ms, None,
+                                                      urlselection)], 1)
+            _check(self._h, _lib.lib().yrwi_term_search(self._h, arr, out.ctypes.data, cap, ctypes.byref(m)))
         return out[:m.value].copy()
 
     # ---- ReferenceOrder.normalizeWith + cardinal ----
@@ -474,6 +482,11 @@ class RWIIndex:
             if q.filter is not None:
                 keep.append(q.filter)
                 arr[i].filter = ctypes.pointer(q.filter.c)
+            if q.urlselection is not None:
+                sb = ctypes.create_string_buffer(_hashes(q.urlselection), max(1, 12 * len(q.urlselection)))
+                keep.append(sb)
+                arr[i].urlselection = ctypes.cast(sb, ctypes.c_void_p)
+                arr[i].nurlselection = len(q.urlselection)
         hits = (CHit * (nq * kmax))()
         nout = (ctypes.c_int32 * nq)()
         return arr, keep, hits, nout, kmax
