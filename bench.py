@@ -387,7 +387,7 @@ class Runner:
         if identical and D > 1:
             dt1, t1, _ = timed_region(steps, timed_stats, lambda i: 0)
             dt1, post1 = over_ranks(dt1, float(t1["postings_in"]))
-            ident = {"ms_per_step": dt1 / steps * 1e3, "value": post1 / dt1,
+            ident = {"ms_per_step": dt1 / steps * 1e3, "value": post1 / dt1, "realloc_events": t1["n_realloc"],
                      "what": f"the same timed region with batch 0 at every step ({steps} steps, "
                              f"{depth} in flight): eight lanes run identical batches at once"}
         iso = None

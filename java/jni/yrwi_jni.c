@@ -58,6 +58,41 @@ JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_joinExclude(JNIEn
   return res;  /* null on error (caller: yrwi_last_error) */
 }
 
+/* TermSearch(..., urlselection, ...).joined(): every list restricted to the url
+ * selection (n * 12 bytes) before the conjunction (yrwi_term_search) */
+JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_termSearch(JNIEnv* env, jclass c, jlong ctx,
+                                                                         jbyteArray incl, jint nincl, jbyteArray excl,
+                                                                         jint nexcl, jbyteArray sel, jint nsel,
+                                                                         jint maxd, jlong now) {
+  yrwi_ctx* x = (yrwi_ctx*)(intptr_t)ctx;
+  jbyte* ib = (*env)->GetByteArrayElements(env, incl, NULL);
+  jbyte* eb = (*env)->GetByteArrayElements(env, excl, NULL);
+  jbyte* sb = sel ? (*env)->GetByteArrayElements(env, sel, NULL) : NULL;
+  int64_t cap = 0, n;
+  for (int i = 0; i < nincl; i++) {
+    if (yrwi_list_size(x, (const uint8_t*)ib + 12 * i, &n) == 0 && n > cap) cap = n;
+  }
+  uint8_t* out = (uint8_t*)malloc((size_t)(cap > 0 ? cap : 1) * 40);
+  yrwi_query_desc q;
+  memset(&q, 0, sizeof(q));
+  q.incl = (const uint8_t*)ib; q.nincl = nincl;
+  q.excl = (const uint8_t*)eb; q.nexcl = nexcl;
+  q.max_distance = maxd; q.k = 1; q.now_ms = now;
+  q.urlselection = (const uint8_t*)sb; q.nurlselection = sb ? nsel : 0;
+  int64_t m = 0;
+  int rc = out ? yrwi_term_search(x, &q, out, cap, &m) : YRWI_E_NOMEM;
+  (*env)->ReleaseByteArrayElements(env, incl, ib, JNI_ABORT);
+  (*env)->ReleaseByteArrayElements(env, excl, eb, JNI_ABORT);
+  if (sb) (*env)->ReleaseByteArrayElements(env, sel, sb, JNI_ABORT);
+  jbyteArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewByteArray(env, (jsize)(m * 40));
+    (*env)->SetByteArrayRegion(env, res, 0, (jsize)(m * 40), (const jbyte*)out);
+  }
+  free(out);
+  return res;
+}
+
 /* joinExclude into a direct ByteBuffer the caller owns and reuses (no JNI array copy
  * of the joined container): returns m (rows written, 40 bytes each) or the (negative)
  * error code -- YRWI_E_ARG when the container holds more rows than capacity / 40. */

@@ -5,7 +5,7 @@
 // they have not been compiled here.  See INTEGRATION.md.
 //
 // Drop-in points (paths relative to source/net/yacy):
-//   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.listSizes(...) + joinExclude(...) (GpuTermSearch)
+//   kelondro/rwi/TermSearch.java:42-70         -> GpuRWI.listSizes(...) + joinExclude(...) / termSearch(...) (GpuTermSearch)
 //   kelondro/rwi/AbstractIndex.java:116        -> GpuRWI.getList(...) (TermSearch.inclusion, on demand)
 //   kelondro/rwi/ReferenceContainer.java:310   -> GpuRWI.joinExclude(...)
 //   search/ranking/ReferenceOrder.java:70,223  -> GpuRWI.eventOrder(...) (GpuReferenceOrder: one event per SearchEvent)
@@ -47,6 +47,18 @@ public final class GpuRWI implements AutoCloseable {
                               final long nowMillis) {
         return joinExclude(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
                            maxDistance, nowMillis);
+    }
+
+    /** TermSearch(..., urlselection, ...).joined(): every include and exclude list restricted
+     *  to the url selection (url hashes) before the conjunction, as
+     *  ReferenceContainerCache.get(key, urlselection) restricts it (yrwi_term_search). */
+    public byte[] termSearch(final byte[][] include, final byte[][] exclude, final byte[][] urlselection,
+                             final int maxDistance, final long nowMillis) {
+        final byte[] rows = termSearch(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
+                                       urlselection == null ? null : flatten(urlselection),
+                                       urlselection == null ? 0 : urlselection.length, maxDistance, nowMillis);
+        if (rows == null) throw new IllegalStateException("yrwi_term_search failed");
+        return rows;
     }
 
     /** joinExclude into a caller-owned direct buffer (ByteBuffer.allocateDirect, reused
@@ -201,6 +213,8 @@ public final class GpuRWI implements AutoCloseable {
                                              int maxDistance, long nowMillis);
     private static native long[] normalizeScore(long ctx, byte[] rows, int m, int[] profile32, String language,
                                                 long nowMillis);
+    private static native byte[] termSearch(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl, byte[] sel,
+                                            int nsel, int maxDistance, long nowMillis);
     private static native long joinExcludeInto(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl,
                                                int maxDistance, long nowMillis, java.nio.ByteBuffer out);
     private static native byte[] query(long ctx, byte[] incl, int nincl, byte[] excl, int nexcl, int maxDistance,

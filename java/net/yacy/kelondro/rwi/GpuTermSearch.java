@@ -41,8 +41,10 @@ public class GpuTermSearch<ReferenceType extends Reference> extends TermSearch<R
     private TreeMap<byte[], ReferenceContainer<ReferenceType>> inclusionContainers = null;
 
     /** TermSearch(base, queryHashes, excludeHashes, urlselection, termFactory, maxDistance)
-     *  on the GPU index.  urlselection must be null (the local search passes null,
-     *  SearchEvent.java:619; the GPU index has no url-set restriction). */
+     *  on the GPU index.  A non-null urlselection restricts every include and exclude
+     *  list to those urls before the conjunction, as ReferenceContainerCache.get(key,
+     *  urlselection) does (the local search passes null, SearchEvent.java:619; IndexCell
+     *  ignores the argument).  inclusion() / sizes stay the unrestricted lists'. */
     public GpuTermSearch(final GpuRWI gpu, final HandleSet queryHashes, final HandleSet excludeHashes,
                          final HandleSet urlselection, final ReferenceFactory<ReferenceType> termFactory,
                          final int maxDistance) {
@@ -62,8 +64,10 @@ public class GpuTermSearch<ReferenceType extends Reference> extends TermSearch<R
     private static <R extends Reference> ReferenceContainer<R> join(
             final GpuRWI gpu, final HandleSet queryHashes, final HandleSet excludeHashes, final HandleSet urlselection,
             final ReferenceFactory<R> termFactory, final int maxDistance) {
-        if (urlselection != null) throw new UnsupportedOperationException("urlselection on the GPU index");
         if (queryHashes == null || queryHashes.isEmpty()) return ReferenceContainer.emptyContainer(termFactory, null);
+        if (urlselection != null)
+            return wrap(termFactory, gpu.termSearch(toArray(queryHashes), toArray(excludeHashes), toArray(urlselection),
+                                                    maxDistance, System.currentTimeMillis()));
         return wrap(termFactory, gpu.joinExclude(toArray(queryHashes), toArray(excludeHashes), maxDistance,
                                                  System.currentTimeMillis()));
     }

@@ -593,20 +593,31 @@ def exclude_containers(pivot: List[bytes], containers: Sequence[List[bytes]]) ->
 
 
 def term_search(index: Dict[bytes, List[bytes]], include: Iterable[bytes], exclude: Iterable[bytes],
-                max_distance: int, now_ms: int, trace: Optional[list] = None) -> List[bytes]:
+                max_distance: int, now_ms: int, trace: Optional[list] = None,
+                urlselection: Optional[Iterable[bytes]] = None) -> List[bytes]:
     """TermSearch.<init> (TermSearch.java:42-70) + AbstractIndex.searchConjunction
     (AbstractIndex.java:96-128) + joinExcludeContainers (:310-326).
 
     HandleSet semantics: term hashes are a sorted set (duplicates collapse).
     Returns a *new* list (the reference mutates the index container for
-    one-term queries; we never mutate the index)."""
+    one-term queries; we never mutate the index).  `urlselection` (url hashes):
+    every container as ReferenceContainerCache.get(key, urlselection) returns it
+    (ReferenceContainerCache.java:448-470): its entries whose url hash is in the
+    selection, in order -- an empty one counts as missing in searchConjunction."""
     inc = sorted(set(include), key=lambda h: key72(h))
     exc = sorted(set(exclude), key=lambda h: key72(h))
+    sel = None if urlselection is None else set(bytes(u) for u in urlselection)
+
+    def get(h):
+        c = index.get(h)
+        if c is None or sel is None:
+            return c
+        return [r for r in c if bytes(r[:12]) in sel]
 
     def conjunction(hashes):
         out = []
         for h in hashes:
-            c = index.get(h)
+            c = get(h)
             if c is None or len(c) == 0:
                 return []  # any missing term -> empty map
             out.append(list(c))

@@ -172,3 +172,34 @@ def test_literal_vs_cpp_random(preset, nq, minq, maxq, nexcl, today):
             assert a == b, (qi, name)
             nonempty += bool(a)
     assert nonempty > 0
+
+
+@pytest.mark.parametrize("frac", [0.01, 0.3])
+def test_urlselection_restriction_is_the_literal_get(frac):
+    """TermSearch's urlselection: the literal restatement of searchConjunction over
+    ReferenceContainerCache.get(key, urlselection) (java_literal.term_search with a
+    selection) equals the C++ oracle run over the lists restricted beforehand -- the
+    restriction the GPU test (test_gpu_parity.test_urlselection_restricts_every_list)
+    checks libyrwi against."""
+    cfg = synth.preset("dense")
+    idx = synth.build_index(cfg)
+    d = idx.as_dict()
+    dl = {h: [bytes(r) for r in rows] for h, rows in d.items()}
+    urls = sorted({bytes(r[:12]) for r in np.asarray(idx.rows)})
+    rng = np.random.default_rng(17)
+    sel = {urls[i] for i in rng.choice(len(urls), max(1, int(frac * len(urls))), replace=False)}
+    rd = {}
+    for h, rows in d.items():
+        keep = np.fromiter((bytes(r[:12]) in sel for r in rows), dtype=bool, count=len(rows))
+        if keep.any():
+            rd[h] = rows[keep]
+    now = 20741 * jl.DAY + 5
+    nonempty = 0
+    for inc, exc in synth.queries(cfg, 16, 1, 4, 2, qseed=99):
+        ih = [idx.hashes[t] for t in inc]
+        eh = [idx.hashes[t] for t in exc]
+        rows_l = jl.term_search(dl, ih, eh, 2147483647, now, urlselection=sel)
+        rows_c = orc.term_search(rd, ih, eh, 2147483647, now)
+        assert b"".join(rows_l) == rows_c.tobytes()
+        nonempty += bool(rows_l)
+    assert nonempty > 0
