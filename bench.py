@@ -703,13 +703,7 @@ def run(args, rank, world, local):
             "inflight": args.inflight,
             # per batch, from the library's own HIP events (isolated pass): join+probe kernels,
             # normalisation (reduce..combine), scoring (score..emit), all kernels; host = call to results
-            "phase_ms": {"join": round(iso["t_join_ns"] / 1e6 / nbi, 3),
-                         "probe": round(iso["t_probe_ns"] / 1e6 / nbi, 3),
-                         "compact": round(iso["t_compact_ns"] / 1e6 / nbi, 3),
-                         "norm": round(iso["t_norm_ns"] / 1e6 / nbi, 3),
-                         "score": round(iso["t_score_ns"] / 1e6 / nbi, 3),
-                         "kernels": round(iso["t_kernels_ns"] / 1e6 / nbi, 3),
-                         "host_total": round(iso["t_total_ns"] / 1e6 / nbi, 3)},
+            "phase_ms": phase_ms(iso),
             "url_dictionary_build_s": round(t_dict, 3),
             "legs": legs or None,
         }
@@ -790,7 +784,22 @@ def _leg_line(M, leg, nq, world, scaling, pmc=None):
             "identical_batch": M["identical"],
             "postings_per_step": M["total_post"] / M["steps"], "queries_per_step": nq,
             "roofline": roof, "roofline_kernels": kern, "joined_per_step": M["timed"]["joined"] / M["steps"],
-            "realloc_events_timed": M["timed"]["n_realloc"]}
+            "realloc_events_timed": M["timed"]["n_realloc"], "phase_ms": phase_ms(M["iso"])}
+
+
+def phase_ms(iso):
+    """Per batch, from the library's own HIP events (isolated pass): join+probe
+    kernels, compaction, normalisation (reduce..combine), scoring (score..emit),
+    all kernels; host = call to results."""
+    nbi = max(1, iso["batches"])
+    return {"join": round(iso["t_join_ns"] / 1e6 / nbi, 3),
+            "probe": round(iso["t_probe_ns"] / 1e6 / nbi, 3),
+            "compact": round(iso["t_compact_ns"] / 1e6 / nbi, 3),
+            "chain": round(iso.get("t_chain_ns", 0) / 1e6 / nbi, 3),
+            "norm": round(iso["t_norm_ns"] / 1e6 / nbi, 3),
+            "score": round(iso["t_score_ns"] / 1e6 / nbi, 3),
+            "kernels": round(iso["t_kernels_ns"] / 1e6 / nbi, 3),
+            "host_total": round(iso["t_total_ns"] / 1e6 / nbi, 3)}
 
 
 def dry_run(args, rank, world):

@@ -925,6 +925,7 @@ struct PendingCompact {
   int64_t* d_off = nullptr;
   BandOrder bo;
   std::vector<std::array<int64_t, CHAIN_LVL>> level;  // per job (layout order): k_chain's level counts
+  std::vector<char> probed;  // per job: a probe job, whose chain tests ran inside k_probe (else k_chain)
 };
 
 // One fold step's join jobs: layout, launch, joined sizes back to the plans.
@@ -988,11 +989,25 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   ProbeDesc* d_crange = nullptr;
   std::vector<ChainQ> cq;
   ChainQ* d_cq = nullptr;
+  std::vector<int2> cgrp;  // chain groups: runs of up to CHAIN_GMAX tiles of one chained job (k_chain)
+  int2* d_cgrp = nullptr;
   if (chain) {
+    // a group holds about 640 expected matches (independent lists: nA nB / nurls
+    // per job), so a workgroup tests close to one round of 768
+    for (int j = 0; j < nj; j++) {
+      const JoinQ& J = jobs[(size_t)j];
+      if (!plans[(size_t)owner[(size_t)j]].chain || J.ntiles <= 0) continue;
+      const double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
+                              (double)J.ntiles;
+      const int G = (int)std::max(1.0, std::min((double)CHAIN_GMAX, 640.0 / std::max(1.0, per_tile)));
+      for (int64_t t = 0; t < J.ntiles; t += G)
+        cgrp.push_back(make_int2((int32_t)(tile_base[(size_t)j] + t), (int32_t)std::min<int64_t>(G, J.ntiles - t)));
+    }
     d_lvl = arena_alloc<int32_t>(ctx, tiles * CHAIN_LVL);
-    d_crange = arena_alloc<ProbeDesc>(ctx, tiles * CHAIN_MAXL);
+    d_crange = arena_alloc<ProbeDesc>(ctx, (int64_t)cgrp.size() * CHAIN_MAXL);
+    d_cgrp = arena_alloc<int2>(ctx, (int64_t)cgrp.size());
     d_cq = arena_alloc<ChainQ>(ctx, nj);
-    if (!d_lvl || !d_crange || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
+    if (!d_lvl || !d_crange || !d_cgrp || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
     int maxi = 0;
     for (int j = 0; j < nj; j++)
       if (plans[(size_t)owner[(size_t)j]].chain) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].npos);
@@ -1011,7 +1026,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
   }
   const int64_t h2 = hprof ? now_ns() : 0;
-  if (chain ? upload(ctx, d_jobs, jobs, d_tb, tile_base, d_cq, cq) : upload(ctx, d_jobs, jobs, d_tb, tile_base))
+  if (chain ? upload(ctx, d_jobs, jobs, d_tb, tile_base, d_cq, cq, d_cgrp, cgrp)
+            : upload(ctx, d_jobs, jobs, d_tb, tile_base))
     return YRWI_E_HIP;
   const int64_t h3 = hprof ? now_ns() : 0;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
@@ -1019,7 +1035,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   hipEvent_t sp = span_open(ctx, tm);
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
-                       false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange))
+                       false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange, d_cgrp,
+                       (int64_t)cgrp.size()))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
@@ -1090,6 +1107,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     pend->d_off = d_off;
     pend->bo = bo;
     pend->level.assign((size_t)nj, {0, 0, 0, 0, 0});
+    pend->probed.assign((size_t)nj, 0);
+    for (int j = 0; j < nj; j++) pend->probed[(size_t)j] = jobs[(size_t)j].algo != JA_MERGE;
     const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
     for (int j = 0; j < nj; j++)
       if (jobs[(size_t)j].chain)
@@ -1346,14 +1365,23 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         const int t = (int)P.seq.size();
         if (t >= 3) P.step_mode[1] = dispatch_mode(v[2 * k], P.seq_ng[2]);
         if (t >= 4) P.step_mode[2] = dispatch_mode(v[2 * k + 1], P.seq_ng[3]);
-        if (st) {  // the later steps' K (local sizes), charged min(K, the bytes k_chain loads for them)
+        // the chain tests of a probe job ran inside k_probe: their bytes are k_probe's
+        const int jk = job_of[(size_t)cqs[k]];
+        const bool in_probe = jk >= 0 && pend.active && pend.probed[(size_t)jk];
+        if (st) {  // the later steps' K (local sizes), charged min(K, the bytes the chain tests load for them)
           for (int l = 2; l < t; l++) {
             const int64_t acc = loc[2 * k + (size_t)(l - 2)], n = P.seq[(size_t)l]->n;
             const int32_t m = P.step_mode[l - 1];
             const int64_t K = step_bytes(m, acc, n);
             const int64_t loaded = P.seq[(size_t)l]->bm ? 20 * acc : 4 * acc + std::min(4 * n, 128 * acc);
             st->bytes_alg += K;
-            st->bytes_chain += std::min(K, loaded);
+            if (in_probe) {
+              st->bytes_probe += K;
+              st->bytes_probe_capped += std::min(K, loaded);
+              st->bytes_probe_loaded += loaded;
+            } else {
+              st->bytes_chain += std::min(K, loaded);
+            }
             st->bytes_alg_capped += std::min(K, loaded);
             if (m == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
           }
@@ -1385,11 +1413,17 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
           const int j = job_of[(size_t)cqs[k]];
           const ChainQ& C = chq[(size_t)cqs[k]];
           const int64_t pre = (j >= 0 && pend.active) ? pend.level[(size_t)j][(size_t)C.ninc] : 0;
+          const bool in_probe = j >= 0 && pend.active && pend.probed[(size_t)j];
           for (int l = C.ninc; l < C.nl; l++) {
             const int64_t b = std::min<int64_t>(12 * C.l[l].n, C.l[l].bm ? 20 * pre
                                                                          : 4 * pre + std::min(4 * C.l[l].n, 128 * pre));
             st->bytes_alg_capped += b;
-            st->bytes_chain += b;
+            if (in_probe) {
+              st->bytes_probe_capped += b;
+              st->bytes_probe_loaded += b;
+            } else {
+              st->bytes_chain += b;
+            }
           }
         }
       }
@@ -1881,7 +1915,15 @@ static int64_t now_ns() {
 // each, at most the smaller side) and the joined container (url id + 32-byte
 // record: 36 B per row, at most the smallest list), then the rank phase over
 // that container (exclusion marks, chunk summaries, candidates: ~48 B per row).
-static int64_t scratch_estimate(const Plan& P) {
+// Scratch bytes a query is expected to take in a pass.  Step by step, every join
+// step allocates its container at its bound min(nA, nB) before it runs: 48 B per
+// slot and step, plus the ranked container.  A chained fold (the same eligibility
+// rule as run_join_phase, without the data-dependent empty check) takes its pair
+// slots (12 B), its later-list rows (4 B per later include) and tile arrays once;
+// its output container is allocated at the exact survivor count after the chain
+// test, estimated here from the lists' url-id densities (independent terms, four
+// times over, at most the bound): the arena grows past the estimate if needed.
+static int64_t scratch_estimate(const Plan& P, int64_t nurls) {
   if (P.empty || P.seq.empty()) return 4096;
   int64_t sum = 0, nmin = INT64_MAX;
   for (const ListRec* l : P.seq) {
@@ -1889,7 +1931,19 @@ static int64_t scratch_estimate(const Plan& P) {
     nmin = std::min(nmin, l->n);
   }
   for (const ListRec* l : P.excl) sum += l->n;
-  return sum / 64 + (48 * (int64_t)(P.seq.size() - 1) + 48) * nmin + 65536;
+  const int t = (int)P.seq.size(), ni = t - 2, ns = P.has_sel ? 1 : 0;
+  const char* nc = getenv("YRWI_NO_CHAIN");
+  const bool chain = !(nc && atoi(nc)) && P.maxd >= 65535 && t >= 2 && ni <= CHAIN_MAXI &&
+                     ns + ni + P.nexcl_g > 0 && ns + ni + P.nexcl_g <= CHAIN_MAXL && nurls > 0;
+  if (!chain) return sum / 64 + (48 * (int64_t)(t - 1) + 48) * nmin + 65536;
+  double out = 4.0 * (double)nmin;
+  bool skipped = false;
+  for (const ListRec* l : P.seq) {
+    if (!skipped && l->n == nmin) { skipped = true; continue; }
+    out *= std::min(1.0, (double)l->n / (double)nurls);
+  }
+  const int64_t est = std::min<int64_t>(nmin, (int64_t)out);
+  return sum / 64 + (16 + 4 * (int64_t)std::max(ni, 0)) * nmin + 48 * est + 65536;
 }
 
 // Scratch budget of one pass (YRWI_SCRATCH_GB, default 32 GiB per lane).  A
@@ -1939,11 +1993,13 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   if (int rc = plan_batch(L, all)) return rc;
   tp = now_ns() - t0;
   const int64_t budget = scratch_budget(L);
+  int npass = 0;
   for (int g0 = 0; g0 < nq;) {
+    npass++;
     int g1 = g0;
     int64_t need = 0;
     while (g1 < nq) {
-      const int64_t e = scratch_estimate(all[(size_t)g1]);
+      const int64_t e = scratch_estimate(all[(size_t)g1], L->nurls);
       if (g1 > g0 && need + e > budget) break;
       need += e;
       g1++;
@@ -2020,8 +2076,9 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   }
   if (hprof) {
     const int64_t wall = now_ns() - t0, wait = L->wait_ns - w0;
-    fprintf(stderr, "[yrwi host] nq %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms, scratch %.1f MB\n",
-            nq, wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6, L->arena.capacity() / 1e6);
+    fprintf(stderr, "[yrwi host] nq %d passes %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms, "
+            "scratch %.1f MB\n", nq, npass, wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6,
+            L->arena.capacity() / 1e6);
   }
   return 0;
 }

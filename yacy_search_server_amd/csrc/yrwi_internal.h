@@ -73,9 +73,16 @@ __host__ __device__ constexpr int64_t heads_cap(int64_t n) { return head1_cap(n)
 //   w1 = r | o << 8 | i << 16 | x << 24 | y << 32 | m << 40 | n << 48 | d << 56
 //        posinphrase, posofphrase, worddistance, llocal, lother, urllength, urlcomps, doctype
 //   w2 = a | l << 16 | z << 32          lastModified days, language (byte 22 low), flags (byte 29 low)
-//   w3 = h | dl << 32                   ByteArray.hashCode(urlhash), domLengthEstimation key (ahpla[urlhash[11]] & 3)
-// The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.
+//   w3 = host | dl << 36                the url's host hash (url-hash chars 6..11 as 36 bits,
+//                                       DigestURL :229-296), domLengthEstimation key (ahpla[urlhash[11]] & 3)
+// The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.  The host
+// hash is what ReferenceOrder's host counts key on (:196-198, authority :213-216):
+// the rank phase counts and looks up hosts from the record it streams anyway,
+// without gathering the url's key from the dictionary.  ByteArray.hashCode of the
+// url hash (the top-k tie-break) is computed from the key for candidates only.
 constexpr int FEAT_WORDS = 4;
+constexpr int REC_DL_SHIFT = 36;
+constexpr uint64_t REC_HOST_MASK = (1ull << 36) - 1;
 constexpr int FEAT_BYTES = 8 * FEAT_WORDS;
 
 // Feature rule of a join step (ReferenceContainer.joinConstructive :406-416).
@@ -120,6 +127,7 @@ struct FoldSrc {
 constexpr int CHAIN_MAXL = 6;  // lists tested per pair (the url selection, later includes, then exclusions)
 constexpr int CHAIN_MAXI = 2;  // later include lists (t <= 4)
 constexpr int CHAIN_LVL = 5;   // per-tile counts: matches, after include tests 1, 2, 3, after exclusion
+constexpr int CHAIN_GMAX = 32; // tiles of one job per k_chain workgroup (a chain group: int2 {first tile, tiles})
 struct ChainList {
   const uint32_t* uid;
   const uint32_t* head;  // line heads (DList::head) or nullptr
@@ -355,7 +363,8 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* stream,
                      void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
-                     bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr);
+                     bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
+                     const int2* d_cgrp = nullptr, int64_t ngroups = 0);
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);

@@ -367,6 +367,7 @@ struct Rec {
   uint64_t w[FEAT_WORDS];
 };
 
+__device__ __forceinline__ uint64_t host36(const Row& r);
 __device__ __forceinline__ Rec rec_of_row(const Row& r) {
   Rec q;
   q.w[0] = (uint64_t)r.u16(O_T) | (uint64_t)r.u16(O_W) << 16 | (uint64_t)r.u16(O_P) << 32 | (uint64_t)r.b(O_U) << 48 |
@@ -375,7 +376,7 @@ __device__ __forceinline__ Rec rec_of_row(const Row& r) {
            (uint64_t)r.b(O_Y) << 32 | (uint64_t)r.b(O_M) << 40 | (uint64_t)r.b(O_N) << 48 | (uint64_t)r.b(O_D) << 56;
   const uint64_t z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | ((uint64_t)r.b(O_Z + 3) << 24);
   q.w[2] = (uint64_t)r.u16(O_A) | (uint64_t)(r.b(O_L) | (r.b(O_L + 1) << 8)) << 16 | z << 32;
-  q.w[3] = (uint64_t)(uint32_t)url_hashcode(r) | (uint64_t)(ahpla(r.b(11)) & 3) << 32;
+  q.w[3] = host36(r) | (uint64_t)(ahpla(r.b(11)) & 3) << REC_DL_SHIFT;
   return q;
 }
 
@@ -417,7 +418,7 @@ __device__ __forceinline__ Feat decode_rec(const Rec& q) {
   x.z = (uint32_t)(w2 >> 32);
   x.lang = (uint32_t)((w2 >> 16) & 0xFFFF);
   x.d = (uint32_t)(w1 >> 56);
-  x.dl = (int32_t)((q.w[3] >> 32) & 3);
+  x.dl = (int32_t)((q.w[3] >> REC_DL_SHIFT) & 3);
   return x;
 }
 
@@ -967,6 +968,7 @@ __device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, co
   }
 }
 
+
 // MARK: an exclusion step (its own instantiation, so kernel traces tell the
 // include steps' dispatches from the exclusion steps')
 template <bool LONG, bool MARK>
@@ -1076,16 +1078,14 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
   if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
   if (tile_lvl && J.chain) {  // workgroup-uniform
     int64_t* level = ldg(&J.chain->level);
+    uint64_t acc[CHAIN_LVL] = {};
+    for (int64_t t = threadIdx.x; t < J.ntiles; t += 256)
+#pragma unroll
+      for (int l = 0; l < CHAIN_LVL; l++) acc[l] += (uint64_t)tile_lvl[(base + t) * CHAIN_LVL + l];
     for (int l = 0; l < CHAIN_LVL; l++) {
-      uint64_t acc = 0;
-      for (int64_t t0 = 0; t0 < J.ntiles; t0 += 256) {
-        const int64_t t = t0 + threadIdx.x;
-        const uint64_t c = t < J.ntiles ? (uint64_t)tile_lvl[(base + t) * CHAIN_LVL + l] : 0;
-        uint64_t tot;
-        block_excl_sum256_u64(c, sScan64, &tot);
-        acc += tot;
-      }
-      if (threadIdx.x == 0) level[l] = (int64_t)acc;
+      uint64_t tot;
+      block_excl_sum256_u64(acc[l], sScan64, &tot);
+      if (threadIdx.x == 0) level[l] = (int64_t)tot;
     }
   }
 }
@@ -1134,29 +1134,38 @@ __device__ __forceinline__ int64_t lower_bound_cl(const ChainList& L, uint32_t k
   return lower_bound_list(d, key);
 }
 
-// the range [lo, hi) of a list without a bitmap that holds the ids of a tile's
-// matches: one thread per (tile, list), all tiles in parallel (as k_probe_part)
+// the range [lo, hi) of a list without a bitmap that holds the ids of a chain
+// group's matches (from its first match to its last): one thread per (group,
+// list), all groups in parallel (as k_probe_part)
 __global__ void k_chain_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                             int64_t ntiles, const int32_t* __restrict__ tile_job, const uint32_t* __restrict__ pair_uid,
+                             const int2* __restrict__ grp, int64_t ngroups, const uint32_t* __restrict__ pair_uid,
                              const int64_t* __restrict__ tile_src, const int32_t* __restrict__ tile_cnt,
                              ProbeDesc* __restrict__ crange) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ntiles * CHAIN_MAXL) return;
-  const int64_t t = i / CHAIN_MAXL;
+  if (i >= ngroups * CHAIN_MAXL) return;
+  const int64_t g = i / CHAIN_MAXL;
   const int l = (int)(i % CHAIN_MAXL);
-  const int j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+  const int2 G = grp[g];
+  const int j = find_job(tile_base, njobs, G.x);
   const ChainQ* C = jobs[j].chain;
   if (!C || l >= ldg(&C->nl)) return;
   const ChainList L = load_cl(&C->l[l]);
-  const int32_t cnt = tile_cnt[t];
-  if (L.bm || cnt == 0) return;
-  const int64_t src = tile_src[t];
+  if (L.bm) return;
+  int f = -1, e = -1;
+  for (int k = 0; k < G.y; k++)
+    if (tile_cnt[G.x + k] > 0) {
+      if (f < 0) f = k;
+      e = k;
+    }
+  if (f < 0) return;
+  const uint32_t k0 = ldg(pair_uid + tile_src[G.x + f]);
+  const uint32_t k1 = ldg(pair_uid + tile_src[G.x + e] + tile_cnt[G.x + e] - 1);
   ProbeDesc D;
-  D.lo = lower_bound_cl(L, ldg(pair_uid + src));
-  D.hi = lower_bound_cl(L, ldg(pair_uid + src + cnt - 1) + 1u);  // ids < 2^32 - 1: no wrap
+  D.lo = lower_bound_cl(L, k0);
+  D.hi = lower_bound_cl(L, k1 + 1u);  // ids < 2^32 - 1: no wrap
   D.job = j;
   D.pad = 0;
-  crange[i] = D;
+  crange[g * CHAIN_MAXL + l] = D;
 }
 
 // Lower bounds of up to KPT keys at once, each in its own window a[base, base + n)
@@ -1295,139 +1304,175 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
   }
 }
 
-constexpr int CHAIN_KPT = 9;  // matches per thread: a tile's matches in one pass
-static_assert(CHAIN_KPT * 256 >= JOIN_MAXM && CHAIN_KPT * 256 >= BM_TILE, "k_chain: one pass per tile");
+constexpr int CHAIN_KPT = 3;  // matches per thread and round: 768 a round, few registers
+static_assert(CHAIN_KPT * 256 <= 1023, "k_chain: 10-bit count fields");
 
-// One workgroup per tile of the step: a chained job's matches (slot k*256 + tid
-// of the tile's run, in url-id order) are tested list by list, only the live ones
+// One workgroup per chain group (up to CHAIN_GMAX consecutive tiles of one chained
+// job, sized by the host to about one round of matches): the group's matches, in
+// url-id order across its tiles (tile t's run, then tile t+1's), are tested in
+// rounds of 768 (slot k*256 + tid of the round), list by list, only the live ones
 // (the loads of a bitmap list all in flight at once); the survivors are written
-// back to the front of the tile's run, in order, with their rows in the later
-// include lists; tile_lvl gets the tile's counts at each level (the fold's
-// dispatch modes come from their sums).
+// back to the front of their own tile's run, in order, with their rows in the
+// later include lists.  A round reads only slots at or past every slot an earlier
+// round wrote, and writes only slots it has read: in place.  The group's level
+// counts (the fold's dispatch modes come from their sums per job) go to its first
+// tile's tile_lvl, zeros to the others.  Few keys per thread keep the kernel at a
+// high occupancy; whole groups of tiles per workgroup keep a probe step's sparse
+// tiles (C3: ~90 matches per 2048-key tile) from costing a workgroup's dependent
+// loads each.
 __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base,
-                                               int njobs, const int32_t* __restrict__ tile_job,
+                                               int njobs, const int2* __restrict__ grp,
                                                uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                const int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
                                                int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ crange) {
   __shared__ uint32_t sL[PROBE_LDS];
   __shared__ uint64_t sScan64[4];
-  const int64_t t = blockIdx.x;
-  const int j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+  __shared__ int32_t sOff[CHAIN_GMAX + 1];  // exclusive prefix of the tiles' match counts
+  __shared__ int64_t sSrc[CHAIN_GMAX];
+  __shared__ int32_t sRun[CHAIN_GMAX];      // survivors written so far, per tile
+  __shared__ int32_t sCnt[CHAIN_GMAX];      // survivors of the round, per tile
+  __shared__ int32_t sBase[CHAIN_GMAX];     // their exclusive prefix
+  const int64_t g = blockIdx.x;
+  const int2 G = grp[g];
+  const int j = find_job(tile_base, njobs, G.x);
   const ChainQ* C = jobs[j].chain;
-  if (!C) return;
-  const int32_t cnt = tile_cnt[t];
-  int32_t* lv = tile_lvl + t * CHAIN_LVL;
-  if (cnt == 0) {
-    if (threadIdx.x < CHAIN_LVL) lv[threadIdx.x] = 0;
-    return;
-  }
-  const int64_t src = tile_src[t];
-  const int ninc = ldg(&C->ninc), nl = ldg(&C->nl);
-  uint32_t key[CHAIN_KPT];
-  uint2 pr[CHAIN_KPT];
-  int32_t pos[CHAIN_MAXI][CHAIN_KPT];
-  uint32_t alive = 0;
-#pragma unroll
-  for (int k = 0; k < CHAIN_KPT; k++) {
-    const int i = k * 256 + (int)threadIdx.x;
-    key[k] = 0;
-    pr[k] = make_uint2(0, 0);
-    pos[0][k] = pos[1][k] = 0;
-    if (i < cnt) {
-      key[k] = ldg(pair_uid + src + i);
-      pr[k] = ldg(reinterpret_cast<const uint2*>(pairs) + src + i);
-      alive |= 1u << k;
+  const int tid = (int)threadIdx.x, n = G.y;
+  if (tid < 64) {
+    const int32_t c = tid < n ? tile_cnt[G.x + tid] : 0;
+    const int32_t inc = wave_incl_sum(c);
+    if (tid < n) {
+      sOff[tid + 1] = inc;
+      sSrc[tid] = tile_src[G.x + tid];
+      sRun[tid] = 0;
     }
+    if (tid == 0) sOff[0] = 0;
   }
-  const int pos0 = ldg(&C->pos0);
-  uint32_t after1 = alive, after2 = alive, after3 = alive;  // live matches after include tests 1, 2, 3
-  for (int l = 0; l < nl; l++) {
-    const ChainList L = load_cl(&C->l[l]);
-    const bool inc = l < ninc;
-    uint32_t hit = 0;
-    int32_t p[CHAIN_KPT];
-    if (L.bm) {
-      const __amdgpu_buffer_rsrc_t rbm =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
-      uint4 E[CHAIN_KPT];
-#pragma unroll
-      for (int k = 0; k < CHAIN_KPT; k++) {
-        E[k] = make_uint4(0, 0, 0, 0);
-        if ((alive >> k) & 1u)
-          E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
-      }
-#pragma unroll
-      for (int k = 0; k < CHAIN_KPT; k++) {
-        const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
-        const uint64_t bit = 1ull << (key[k] & 63u);
-        p[k] = (int32_t)(ey + __popcll(ex & (bit - 1ull)));
-        if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
-      }
-    } else {
-      const ProbeDesc D = crange[t * CHAIN_MAXL + l];  // workgroup-uniform
-      chain_search<CHAIN_KPT>(L, D.lo, D.hi, key, alive, p, hit, sL);
-    }
-    if (inc) {
-      alive &= hit;
-      const int pi = l - pos0;  // the selection keeps no row
-#pragma unroll
-      for (int k = 0; k < CHAIN_KPT; k++) {
-        if (pi == 0) pos[0][k] = p[k];
-        else if (pi == 1) pos[1][k] = p[k];
-      }
-      if (l == 0) after1 = alive;
-      if (l == 1) after2 = alive;
-      if (l == 2) after3 = alive;
-    } else {
-      alive &= ~hit;
-    }
-  }
-  if (ninc < 2) after2 = after1;
-  if (ninc < 3) after3 = after2;
-  // survivors leave in slot order (slot k's 256 matches, then slot k+1's): per-slot
-  // counts packed four to a 64-bit scan, as in probe_bitmap; the level counts ride
-  // along in the last scan's spare fields
-  constexpr int NSC = (CHAIN_KPT + 3) / 4;
-  uint64_t ex[NSC], tot64[NSC];
-#pragma unroll
-  for (int q = 0; q < NSC; q++) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int k = 4 * q; k < CHAIN_KPT && k < 4 * q + 4; k++) c |= (uint64_t)((alive >> k) & 1u) << (16 * (k - 4 * q));
-    if (q == NSC - 1) {
-      static_assert(CHAIN_KPT % 4 == 1, "three spare 16-bit fields in the last scan");
-      c |= (uint64_t)__popc(after1) << 16 | (uint64_t)__popc(after2) << 32 | (uint64_t)__popc(after3) << 48;
-    }
-    ex[q] = block_excl_sum256_u64(c, sScan64, &tot64[q]);
-  }
-  int32_t base[CHAIN_KPT];
-  int32_t run = 0;
-#pragma unroll
-  for (int k = 0; k < CHAIN_KPT; k++) {
-    base[k] = run;
-    run += (int32_t)((tot64[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-  }
-  // every read of the tile's run happened before the scans' barriers: write in place
-  const int npos = ldg(&C->npos);
+  __syncthreads();
+  const int32_t M = sOff[n];
+  const int ninc = ldg(&C->ninc), nl = ldg(&C->nl), pos0 = ldg(&C->pos0), npos = ldg(&C->npos);
   int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
   int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
+  int32_t n1 = 0, n2 = 0, n3 = 0, nsurv = 0;  // live after include tests 1, 2, 3; survivors
+  for (int r0 = 0; r0 < M; r0 += CHAIN_KPT * 256) {  // workgroup-uniform
+    uint32_t key[CHAIN_KPT];
+    uint2 pr[CHAIN_KPT];
+    int32_t pos[CHAIN_MAXI][CHAIN_KPT];
+    int32_t tk[CHAIN_KPT];  // the match's tile in the group
+    uint32_t alive = 0;
 #pragma unroll
-  for (int k = 0; k < CHAIN_KPT; k++) {
-    if (!((alive >> k) & 1u)) continue;
-    const int64_t o = src + base[k] + (int64_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-    stg(reinterpret_cast<uint2*>(pairs) + o, pr[k]);
-    stg(pair_uid + o, key[k]);
-    if (tup0) stg(tup0 + o, pos[0][k]);
-    if (tup1) stg(tup1 + o, pos[1][k]);
+    for (int k = 0; k < CHAIN_KPT; k++) {
+      const int i = r0 + k * 256 + tid;
+      key[k] = 0;
+      pr[k] = make_uint2(0, 0);
+      pos[0][k] = pos[1][k] = 0;
+      tk[k] = 0;
+      if (i < M) {
+        int a = 0, b = n;  // last tile whose first match is at or before i
+        while (b - a > 1) {
+          const int m = (a + b) >> 1;
+          if (sOff[m] <= i) a = m; else b = m;
+        }
+        tk[k] = a;
+        const int64_t slot = sSrc[a] + (i - sOff[a]);
+        key[k] = ldg(pair_uid + slot);
+        pr[k] = ldg(reinterpret_cast<const uint2*>(pairs) + slot);
+        alive |= 1u << k;
+      }
+    }
+    uint32_t after1 = alive, after2 = alive, after3 = alive;
+    for (int l = 0; l < nl; l++) {
+      const ChainList L = load_cl(&C->l[l]);
+      uint32_t hit = 0;
+      int32_t p[CHAIN_KPT];
+      if (L.bm) {
+        const __amdgpu_buffer_rsrc_t rbm =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
+        uint4 E[CHAIN_KPT];
+#pragma unroll
+        for (int k = 0; k < CHAIN_KPT; k++) {
+          E[k] = make_uint4(0, 0, 0, 0);
+          if ((alive >> k) & 1u)
+            E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
+        }
+#pragma unroll
+        for (int k = 0; k < CHAIN_KPT; k++) {
+          const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x;
+          const uint64_t bit = 1ull << (key[k] & 63u);
+          p[k] = (int32_t)(E[k].z + __popcll(ex & (bit - 1ull)));  // list positions < 2^31
+          if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
+        }
+      } else {
+        const ProbeDesc D = crange[g * CHAIN_MAXL + l];  // workgroup-uniform
+        chain_search<CHAIN_KPT>(L, D.lo, D.hi, key, alive, p, hit, sL);
+      }
+      if (l < ninc) {
+        alive &= hit;
+        const int pi = l - pos0;  // the selection keeps no row
+#pragma unroll
+        for (int k = 0; k < CHAIN_KPT; k++) {
+          if (pi == 0) pos[0][k] = p[k];
+          else if (pi == 1) pos[1][k] = p[k];
+        }
+        if (l == 0) after1 = alive;
+        if (l == 1) after2 = alive;
+        if (l == 2) after3 = alive;
+      } else {
+        alive &= ~hit;
+      }
+    }
+    if (ninc < 2) after2 = after1;
+    if (ninc < 3) after3 = after2;
+    if (tid < n) sCnt[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CHAIN_KPT; k++)
+      if ((alive >> k) & 1u) atomicAdd(&sCnt[tk[k]], 1);
+    // each survivor's rank in the round (slot order = the group's match order) and
+    // the level counts, in 10-bit fields of one 64-bit scan (its barriers also
+    // complete the LDS counts above)
+    uint64_t c = (uint64_t)__popc(after1) << 30 | (uint64_t)__popc(after2) << 40 | (uint64_t)__popc(after3) << 50;
+#pragma unroll
+    for (int k = 0; k < CHAIN_KPT; k++) c |= (uint64_t)((alive >> k) & 1u) << (10 * k);
+    uint64_t tot;
+    const uint64_t ex = block_excl_sum256_u64(c, sScan64, &tot);
+    if (tid == 0) {
+      int32_t acc = 0;
+      for (int x = 0; x < n; x++) {
+        sBase[x] = acc;
+        acc += sCnt[x];
+      }
+    }
+    __syncthreads();
+    int32_t before = 0;  // survivors of the round in earlier slots
+#pragma unroll
+    for (int k = 0; k < CHAIN_KPT; k++) {
+      if ((alive >> k) & 1u) {
+        const int x = tk[k];
+        const int32_t rank = before + (int32_t)((ex >> (10 * k)) & 0x3FFu);
+        const int64_t o = sSrc[x] + sRun[x] + (rank - sBase[x]);
+        stg(reinterpret_cast<uint2*>(pairs) + o, pr[k]);
+        stg(pair_uid + o, key[k]);
+        if (tup0) stg(tup0 + o, pos[0][k]);
+        if (tup1) stg(tup1 + o, pos[1][k]);
+      }
+      before += (int32_t)((tot >> (10 * k)) & 0x3FFu);
+    }
+    nsurv += before;
+    n1 += (int32_t)((tot >> 30) & 0x3FFu);
+    n2 += (int32_t)((tot >> 40) & 0x3FFu);
+    n3 += (int32_t)((tot >> 50) & 0x3FFu);
+    __syncthreads();  // every write of the round read sRun / sBase
+    if (tid < n) sRun[tid] += sCnt[tid];
+    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    tile_cnt[t] = run;
-    const uint64_t lt = tot64[NSC - 1];
-    lv[0] = cnt;
-    lv[1] = (int32_t)((lt >> 16) & 0xFFFFu);
-    lv[2] = (int32_t)((lt >> 32) & 0xFFFFu);
-    lv[3] = (int32_t)((lt >> 48) & 0xFFFFu);
-    lv[4] = run;
+  if (tid < n) {
+    tile_cnt[G.x + tid] = sRun[tid];
+    int32_t* lv = tile_lvl + (G.x + tid) * CHAIN_LVL;
+    lv[0] = tid == 0 ? M : 0;
+    lv[1] = tid == 0 ? n1 : 0;
+    lv[2] = tid == 0 ? n2 : 0;
+    lv[3] = tid == 0 ? n3 : 0;
+    lv[4] = tid == 0 ? nsurv : 0;
   }
 }
 
@@ -1950,10 +1995,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
       if (Q.want_authority) {
-        uint64_t khi;
-        uint32_t klo;
-        key_at(Q, e, khi, klo);
-        uint64_t key = key_host36(khi, klo) + 1;
+        uint64_t key = (rg[s % RED_GROUP].w[3] & REC_HOST_MASK) + 1;  // the record's host hash: no key gather
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
           unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
@@ -2655,6 +2697,20 @@ __device__ __forceinline__ int32_t url_hashcode(const Row& r) {
   return h;
 }
 
+// ByteArray.hashCode (ByteArray.java:80-84) of element e's url hash, from its key
+// (the top-k tie-break: computed for candidates only)
+__device__ __forceinline__ uint32_t elem_hashcode(const RankQ& Q, int64_t e) {
+  uint64_t khi;
+  uint32_t klo;
+  key_at(Q, e, khi, klo);
+  uint8_t h[12];
+  key_chars(khi, klo, h);
+  int32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) x = add32(mul32(31, x), (int32_t)h[j]);
+  return (uint32_t)x;
+}
+
 __device__ __forceinline__ int32_t host_count(const RankQ& Q, uint64_t host) {
   uint64_t key = host + 1;
   uint64_t slot = mix64(key) & Q.hmask;
@@ -2918,7 +2974,7 @@ __device__ __forceinline__ PruneP prune_params(const NormState& N, const RankQ& 
 __device__ __forceinline__ int64_t score_bound(const Rec& q, const NormState& N, const RankQ& Q, const PruneP& P,
                                                bool* valid, const CardTab* tab = nullptr) {
   const yrwi_profile& rk = Q.prof;
-  const int dl = (int)((q.w[3] >> 32) & 3);
+  const int dl = (int)((q.w[3] >> REC_DL_SHIFT) & 3);
   const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
   int64_t ex = (int64_t)shl32(256 - dln, rk.coeff_domlength);
   if (N.va_mx != N.va_mn)
@@ -2979,15 +3035,14 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
       const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
       if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
     }
-    if (!F && Q.want_authority) key_at(Q, e, khi, klo);
     const Feat t = decode_rec(q);
-    const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
+    const int32_t hc = Q.want_authority ? host_count(Q, q.w[3] & REC_HOST_MASK) : 0;
     a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
     if (a[s] < T) {
       a[s] = 0;
       continue;
     }
-    if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+    if (z) z[s] = ((uint64_t)(elem_hashcode(Q, e) ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
     vm |= 1u << s;
   }
   return vm;
@@ -3154,7 +3209,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
       if ((vm >> s) & 1u) {
         const int i = s * CHUNK_THREADS + tid;
         const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-        const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
+        const uint32_t h = elem_hashcode(Q, e);
         out[voff].k1 = a[s];
         out[voff].k2 = ((uint64_t)(h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
         voff++;
@@ -3178,7 +3233,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (((vm >> s) & 1u) && a[s] >= T) {
       const int i = s * CHUNK_THREADS + tid;
       const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-      const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
+      const uint32_t h = elem_hashcode(Q, e);
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       off++;
@@ -3636,13 +3691,7 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
     const int64_t e = c * CHUNK + s;
     if (e >= Q.n) break;
     const Feat t = decode_rec(load_rec(Q.feat, e));
-    int32_t hc = 0;
-    if (Q.want_authority) {
-      uint64_t khi;
-      uint32_t klo;
-      key_at(Q, e, khi, klo);
-      hc = host_count(Q, key_host36(khi, klo));
-    }
+    const int32_t hc = Q.want_authority ? host_count(Q, ldg(Q.feat + e * FEAT_WORDS + 3) & REC_HOST_MASK) : 0;
     out[e] = cardinal(t, N, Q, hc);
   }
 }
@@ -3766,7 +3815,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
-                     ProbeDesc* d_crange) {
+                     ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -3831,14 +3880,14 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
-    if (chain) {
-      const int64_t nr = total_tiles * CHAIN_MAXL;
-      hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
-                         total_tiles, (const int32_t*)tjob, d_pair_uid, d_tile_src, d_tile_cnt, d_crange);
+    if (chain && ngroups > 0) {
+      const int64_t nr = ngroups * CHAIN_MAXL;
+      hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs, d_tile_base,
+                         njobs, d_cgrp, ngroups, (const uint32_t*)d_pair_uid, (const int64_t*)d_tile_src,
+                         (const int32_t*)d_tile_cnt, d_crange);
       dbg_sync("k_chain_part", st);
-      hipLaunchKernelGGL(k_chain, dim3((unsigned)total_tiles), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs,
-                         (const int32_t*)tjob, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl,
-                         (const ProbeDesc*)d_crange);
+      hipLaunchKernelGGL(k_chain, dim3((unsigned)ngroups), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs, d_cgrp,
+                         d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl, (const ProbeDesc*)d_crange);
       dbg_sync("k_chain", st);
     }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
