@@ -1,6 +1,7 @@
-# Kernel stats of the C5 custom (authority) leg and of C3 with the fused chain.
+# C5 legs (authority k_reduce) and the whole GPU suite.
 set -o pipefail
-mkdir -p gpurun_out/kst
-KARGS="--config C5 --shard-of 8 --terms 2 --max-terms 4 --profile custom" bash tools/kstats.sh c5c || exit 1
-KARGS="--config C3 --terms 3 --exclude 1" bash tools/kstats.sh c3fused || exit 1
-mv gpurun_out/c5c_kstats.txt gpurun_out/c3fused_kstats.txt gpurun_out/kst/
+mkdir -p gpurun_out/c5
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > gpurun_out/c5/t.log 2>&1 || exit $?
+timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --legs C5,C4 --latency 0 --leg-latency 0 \
+  --no-cpu > gpurun_out/c5/legs.json 2> gpurun_out/c5/legs.err || exit $?

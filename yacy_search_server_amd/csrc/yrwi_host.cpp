@@ -822,6 +822,16 @@ static void span_close(Lane* L, Timing* tm, hipEvent_t b) {
 
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
+// YRWI_CHAIN_FUSED=1: a chained job's probe tiles keep their matches in LDS and
+// test them in the same workgroup (k_probe<.., CHAIN>, BM_TILE tiles) instead of
+// writing them for k_chain.  Measured slower on C3 (3.62 against 3.22-3.30 ms per
+// step: the probe workgroups lose occupancy and the long tiles), kept as the
+// experiment's switch.
+static bool chain_fused() {
+  static const bool on = getenv("YRWI_CHAIN_FUSED") && atoi(getenv("YRWI_CHAIN_FUSED"));
+  return on;
+}
+
 static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& jobs, std::vector<int>& owner,
                         std::vector<int64_t>& tile_base, int* nmerge, int64_t* merge_tiles, int64_t* tiles,
                         bool* long_tiles) {
@@ -843,7 +853,10 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     // long bitmap tiles only where no record is gathered per match (a deferred
     // step writes sources, an exclusion marks): a final step's compaction keeps
     // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
-    const bool light = J.out_tup != nullptr || J.mode == JM_MARK || J.chained;  // chained: only survivors gather
+    // (a fused chained job's tiles keep their matches in LDS for the chain tests:
+    // BM_TILE, whose registers leave room for them)
+    const bool light = chain_fused() ? (J.out_tup != nullptr || J.mode == JM_MARK) && !J.chained
+                                     : J.out_tup != nullptr || J.mode == JM_MARK || J.chained;
     J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
     if (J.ptile == KPT_LARGE * PROBE_TILE) *long_tiles = true;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
@@ -989,14 +1002,15 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   ProbeDesc* d_crange = nullptr;
   std::vector<ChainQ> cq;
   ChainQ* d_cq = nullptr;
-  std::vector<int2> cgrp;  // chain groups: runs of up to CHAIN_GMAX tiles of one chained job (k_chain)
+  std::vector<int2> cgrp;  // chain groups: runs of up to CHAIN_GMAX merge tiles of one chained job (k_chain)
   int2* d_cgrp = nullptr;
+  ProbeDesc* d_prange = nullptr;  // later-list ranges of every probe tile (k_probe<.., CHAIN>)
   if (chain) {
     // a group holds about 640 expected matches (independent lists: nA nB / nurls
     // per job), so a workgroup tests close to one round of 768
-    for (int j = 0; j < nj; j++) {
+    for (int j = 0; j < nj; j++) {  // (fused: a probe job's tiles test their matches inside k_probe)
       const JoinQ& J = jobs[(size_t)j];
-      if (!plans[(size_t)owner[(size_t)j]].chain || J.ntiles <= 0) continue;
+      if (!plans[(size_t)owner[(size_t)j]].chain || J.ntiles <= 0 || (chain_fused() && J.algo != JA_MERGE)) continue;
       const double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
                               (double)J.ntiles;
       const int G = (int)std::max(1.0, std::min((double)CHAIN_GMAX, 640.0 / std::max(1.0, per_tile)));
@@ -1005,6 +1019,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
     d_lvl = arena_alloc<int32_t>(ctx, tiles * CHAIN_LVL);
     d_crange = arena_alloc<ProbeDesc>(ctx, (int64_t)cgrp.size() * CHAIN_MAXL);
+    if (chain_fused() && !(d_prange = arena_alloc<ProbeDesc>(ctx, (tiles - merge_tiles) * CHAIN_MAXL)))
+      return ctx->fail(YRWI_E_NOMEM, "arena");
     d_cgrp = arena_alloc<int2>(ctx, (int64_t)cgrp.size());
     d_cq = arena_alloc<ChainQ>(ctx, nj);
     if (!d_lvl || !d_crange || !d_cgrp || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
@@ -1036,7 +1052,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
                        false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange, d_cgrp,
-                       (int64_t)cgrp.size()))
+                       (int64_t)cgrp.size(), d_prange))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
@@ -1108,7 +1124,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     pend->bo = bo;
     pend->level.assign((size_t)nj, {0, 0, 0, 0, 0});
     pend->probed.assign((size_t)nj, 0);
-    for (int j = 0; j < nj; j++) pend->probed[(size_t)j] = jobs[(size_t)j].algo != JA_MERGE;
+    for (int j = 0; j < nj; j++) pend->probed[(size_t)j] = chain_fused() && jobs[(size_t)j].algo != JA_MERGE;
     const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
     for (int j = 0; j < nj; j++)
       if (jobs[(size_t)j].chain)
@@ -1669,7 +1685,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, any_auth)) return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kreduce.push_back(tm->spans.back());
   if (st) {
@@ -1915,15 +1931,13 @@ static int64_t now_ns() {
 // each, at most the smaller side) and the joined container (url id + 32-byte
 // record: 36 B per row, at most the smallest list), then the rank phase over
 // that container (exclusion marks, chunk summaries, candidates: ~48 B per row).
-// Scratch bytes a query is expected to take in a pass.  Step by step, every join
-// step allocates its container at its bound min(nA, nB) before it runs: 48 B per
-// slot and step, plus the ranked container.  A chained fold (the same eligibility
-// rule as run_join_phase, without the data-dependent empty check) takes its pair
-// slots (12 B), its later-list rows (4 B per later include) and tile arrays once;
-// its output container is allocated at the exact survivor count after the chain
-// test, estimated here from the lists' url-id densities (independent terms, four
-// times over, at most the bound): the arena grows past the estimate if needed.
-static int64_t scratch_estimate(const Plan& P, int64_t nurls) {
+// Scratch bytes a query is expected to take in a pass: 48 B per slot of its
+// smallest list and fold step (a step-by-step container at its bound min(nA, nB);
+// a chained fold's pair slots, later-list rows, tile arrays and output), plus the
+// ranked container.  (A tighter estimate for chained folds -- pairs and rows
+// once, the output from the lists' densities -- put C4's eight lanes past the
+// device's memory as their outputs grew the arenas: profiles/r04_c4_host.txt.)
+static int64_t scratch_estimate(const Plan& P) {
   if (P.empty || P.seq.empty()) return 4096;
   int64_t sum = 0, nmin = INT64_MAX;
   for (const ListRec* l : P.seq) {
@@ -1931,19 +1945,7 @@ static int64_t scratch_estimate(const Plan& P, int64_t nurls) {
     nmin = std::min(nmin, l->n);
   }
   for (const ListRec* l : P.excl) sum += l->n;
-  const int t = (int)P.seq.size(), ni = t - 2, ns = P.has_sel ? 1 : 0;
-  const char* nc = getenv("YRWI_NO_CHAIN");
-  const bool chain = !(nc && atoi(nc)) && P.maxd >= 65535 && t >= 2 && ni <= CHAIN_MAXI &&
-                     ns + ni + P.nexcl_g > 0 && ns + ni + P.nexcl_g <= CHAIN_MAXL && nurls > 0;
-  if (!chain) return sum / 64 + (48 * (int64_t)(t - 1) + 48) * nmin + 65536;
-  double out = 4.0 * (double)nmin;
-  bool skipped = false;
-  for (const ListRec* l : P.seq) {
-    if (!skipped && l->n == nmin) { skipped = true; continue; }
-    out *= std::min(1.0, (double)l->n / (double)nurls);
-  }
-  const int64_t est = std::min<int64_t>(nmin, (int64_t)out);
-  return sum / 64 + (16 + 4 * (int64_t)std::max(ni, 0)) * nmin + 48 * est + 65536;
+  return sum / 64 + (48 * (int64_t)(P.seq.size() - 1) + 48) * nmin + 65536;
 }
 
 // Scratch budget of one pass (YRWI_SCRATCH_GB, default 32 GiB per lane).  A
@@ -1999,7 +2001,7 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
     int g1 = g0;
     int64_t need = 0;
     while (g1 < nq) {
-      const int64_t e = scratch_estimate(all[(size_t)g1], L->nurls);
+      const int64_t e = scratch_estimate(all[(size_t)g1]);
       if (g1 > g0 && need + e > budget) break;
       need += e;
       g1++;

@@ -364,7 +364,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
                      bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
-                     const int2* d_cgrp = nullptr, int64_t ngroups = 0);
+                     const int2* d_cgrp = nullptr, int64_t ngroups = 0, ProbeDesc* d_prange = nullptr);
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);
@@ -372,7 +372,7 @@ int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, bool authority);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip

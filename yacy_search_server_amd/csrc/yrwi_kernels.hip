@@ -884,10 +884,12 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
 // long job at 8), the others KPT = 4 (a final step's compaction keeps its band
 // order per tile: C2 at 8 took k_probe 111 -> 116 and k_compact 220 -> 237 us).
 template <int KPT>
-__device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, const DList& Lg, int64_t b,
-                                             int64_t tile_base0, uint2* __restrict__ pairs,
-                                             uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
-                                             int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64) {
+__device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm, const DList& Lg, int64_t b,
+                                                int64_t tile_base0, uint2* __restrict__ pairs,
+                                                uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
+                                                int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64,
+                                                uint16_t* sLoc = nullptr, uint32_t* sPos = nullptr,
+                                                int64_t* src_out = nullptr) {
   // url-id bitmap of the large list: one 16-B load per key gives membership and,
   // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
   // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
@@ -933,7 +935,7 @@ __device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, co
       hm &= ~(1u << k);
     }
   }
-  if (mark) return;
+  if (mark) return 0;
   // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
   // of four 16-bit per-slot counts gives every hit's place in its slot
   constexpr int NSC = (KPT + 3) / 4;  // 64-bit scans of four slot counts each
@@ -957,28 +959,50 @@ __device__ __forceinline__ void probe_bitmap(const JoinQ& J, const DList& Sm, co
     tile_src[b] = src;
     tile_cnt[b] = run;
   }
+  if (src_out) *src_out = src;
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     if (!((hm >> k) & 1u)) continue;
     const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
     const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
-    const int64_t o = src + base[k] + (int64_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-    pairs[o] = make_uint2((uint32_t)ia, (uint32_t)ib);
-    pair_uid[o] = keys[k];
+    const int32_t lo = base[k] + (int32_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+    if (sLoc) {  // a chained job's tile: its matches stay in LDS for the chain tests
+      sLoc[lo] = (uint16_t)(k * PROBE_TILE + (int)threadIdx.x);
+      sPos[lo] = (uint32_t)jls[k];
+    } else {
+      pairs[src + lo] = make_uint2((uint32_t)ia, (uint32_t)ib);
+      pair_uid[src + lo] = keys[k];
+    }
   }
+  return run;
 }
 
 
+__device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t src, int32_t cnt,
+                               const uint16_t* sLoc, const uint32_t* sPos, const uint32_t* __restrict__ small_uid,
+                               int64_t s0, bool small_is_A, uint2* __restrict__ pairs,
+                               uint32_t* __restrict__ pair_uid, int32_t* __restrict__ tile_cnt,
+                               int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ cr, uint32_t* sL,
+                               uint64_t* sScan64);
+
 // MARK: an exclusion step (its own instantiation, so kernel traces tell the
-// include steps' dispatches from the exclusion steps')
-template <bool LONG, bool MARK>
+// include steps' dispatches from the exclusion steps').  CHAIN: the first step of
+// chained folds: a chained job's tile keeps its matches in LDS and tests them
+// against the fold's later lists in the same workgroup (chain_lds_tile, with the
+// ranges k_chain_part<true> found for the tile): only survivors reach HBM.
+template <bool LONG, bool MARK, bool CHAIN>
 __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
-                                                     const int2* __restrict__ perm) {
+                                                     const int2* __restrict__ perm, int32_t* __restrict__ tile_lvl,
+                                                     const ProbeDesc* __restrict__ prange) {
+  static_assert(!(MARK && CHAIN), "an exclusion step chains nothing");
   constexpr int mark = MARK ? 1 : 0;
+  constexpr int CAP = CHAIN ? BM_TILE : 1;  // a chained tile's matches at most (BM_TILE >= PROBE_TILE)
+  __shared__ uint16_t sLoc[CAP];  // a chained tile's matches: small-list index in the tile,
+  __shared__ uint32_t sPos[CAP];  // and the large list's position
   __shared__ int32_t sScan[4];
   __shared__ uint64_t sScan64[4];
 #if PROBE_LDS > 0
@@ -990,14 +1014,24 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const JoinQ& J = jobs[D.job];
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
+  const bool chained = CHAIN && J.chain != nullptr;  // workgroup-uniform
   if (Lg.bm) {
     // a launch without long tiles does not carry the KPT_LARGE code (its registers
     // cost C2 a wave per SIMD: k_probe 111 -> 119 us)
-    if (LONG && J.ptile == KPT_LARGE * PROBE_TILE)
+    // (a chained job's tiles are BM_TILE: layout_jobs)
+    if (LONG && !chained && J.ptile == KPT_LARGE * PROBE_TILE) {
       probe_bitmap<KPT_LARGE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark, sScan64);
-    else
-      probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark,
-                                         sScan64);
+      return;
+    }
+    int64_t src = 0;
+    const int32_t cnt = probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src,
+                                                           tile_cnt, mark, sScan64, chained ? sLoc : nullptr, sPos,
+                                                           &src);
+    if (CHAIN && chained) {
+      __syncthreads();  // the tile's matches in LDS
+      chain_lds_tile(J.chain, b, src, cnt, sLoc, sPos, Sm.uid, (b - tile_base[D.job]) * J.ptile, J.small_is_A, pairs,
+                     pair_uid, tile_cnt, tile_lvl, prange + t * CHAIN_MAXL, sL, sScan64);
+    }
     return;
   }
   const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
@@ -1047,6 +1081,16 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   if (threadIdx.x == 0) {
     tile_src[b] = src;
     tile_cnt[b] = tot;
+  }
+  if (CHAIN && chained) {  // the matches in LDS, then the chain tests
+    if (hit) {
+      sLoc[off] = (uint16_t)threadIdx.x;
+      sPos[off] = (uint32_t)jl;
+    }
+    __syncthreads();
+    chain_lds_tile(J.chain, b, src, tot, sLoc, sPos, Sm.uid, s0, J.small_is_A, pairs, pair_uid, tile_cnt, tile_lvl,
+                   prange + t * CHAIN_MAXL, sL, sScan64);
+    return;
   }
   if (hit) {
     pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
@@ -1134,39 +1178,62 @@ __device__ __forceinline__ int64_t lower_bound_cl(const ChainList& L, uint32_t k
   return lower_bound_list(d, key);
 }
 
-// the range [lo, hi) of a list without a bitmap that holds the ids of a chain
-// group's matches (from its first match to its last): one thread per (group,
-// list), all groups in parallel (as k_probe_part)
+// the range [lo, hi) of a list without a bitmap that holds the ids of a unit's
+// matches: one thread per (unit, list), all units in parallel (as k_probe_part).
+// PRE: the units are the probe tiles [tile0, tile0 + n) of the step (k_probe<..,
+// CHAIN> tests their matches), the range spans the tile's small-list ids, which
+// hold its matches.  Otherwise the units are chain groups of merge tiles (grp),
+// after k_join: the range spans the group's matches.
+template <bool PRE>
 __global__ void k_chain_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                             const int2* __restrict__ grp, int64_t ngroups, const uint32_t* __restrict__ pair_uid,
-                             const int64_t* __restrict__ tile_src, const int32_t* __restrict__ tile_cnt,
-                             ProbeDesc* __restrict__ crange) {
+                             const int2* __restrict__ grp, int64_t tile0, int64_t n,
+                             const uint32_t* __restrict__ pair_uid, const int64_t* __restrict__ tile_src,
+                             const int32_t* __restrict__ tile_cnt, ProbeDesc* __restrict__ crange) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ngroups * CHAIN_MAXL) return;
-  const int64_t g = i / CHAIN_MAXL;
+  if (i >= n * CHAIN_MAXL) return;
+  const int64_t u = i / CHAIN_MAXL;
   const int l = (int)(i % CHAIN_MAXL);
-  const int2 G = grp[g];
-  const int j = find_job(tile_base, njobs, G.x);
-  const ChainQ* C = jobs[j].chain;
+  const int2 G = PRE ? make_int2(0, 0) : grp[u];
+  const int64_t t = PRE ? tile0 + u : G.x;
+  const int j = find_job(tile_base, njobs, t);
+  const JoinQ& J = jobs[j];
+  const ChainQ* C = J.chain;
   if (!C || l >= ldg(&C->nl)) return;
   const ChainList L = load_cl(&C->l[l]);
   if (L.bm) return;
-  int f = -1, e = -1;
-  for (int k = 0; k < G.y; k++)
-    if (tile_cnt[G.x + k] > 0) {
-      if (f < 0) f = k;
-      e = k;
-    }
-  if (f < 0) return;
-  const uint32_t k0 = ldg(pair_uid + tile_src[G.x + f]);
-  const uint32_t k1 = ldg(pair_uid + tile_src[G.x + e] + tile_cnt[G.x + e] - 1);
+  uint32_t k0, k1;
+  if (PRE) {
+    const DList& Sm = J.small_is_A ? J.A : J.B;
+    const int64_t s0 = (t - tile_base[j]) * J.ptile;
+    const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
+    if (s0 >= s1) return;
+    k0 = ldg(Sm.uid + s0);
+    k1 = ldg(Sm.uid + s1 - 1);
+  } else {
+    int f = -1, e = -1;
+    for (int k = 0; k < G.y; k++)
+      if (tile_cnt[G.x + k] > 0) {
+        if (f < 0) f = k;
+        e = k;
+      }
+    if (f < 0) return;
+    k0 = ldg(pair_uid + tile_src[G.x + f]);
+    k1 = ldg(pair_uid + tile_src[G.x + e] + tile_cnt[G.x + e] - 1);
+  }
   ProbeDesc D;
   D.lo = lower_bound_cl(L, k0);
   D.hi = lower_bound_cl(L, k1 + 1u);  // ids < 2^32 - 1: no wrap
   D.job = j;
   D.pad = 0;
-  crange[g * CHAIN_MAXL + l] = D;
+  crange[u * CHAIN_MAXL + l] = D;
 }
+
+#ifdef YRWI_CHAIN_PROF  // profiling build only: k_chain's paths (yrwi_chain_prof reads and clears them)
+__device__ unsigned long long g_cprof[24];
+#define CPROF(i, v) atomicAdd(&g_cprof[i], (unsigned long long)(v))
+#else
+#define CPROF(i, v)
+#endif
 
 // Lower bounds of up to KPT keys at once, each in its own window a[base, base + n)
 // of at most 32 ids (a line of ids or of line heads): a power-of-two bisection of
@@ -1223,7 +1290,10 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
   hit = 0;
   const int64_t R = hi - lo;
   __syncthreads();  // the previous list's stage is no longer read
+  CPROF(20, R);
   if (R <= PROBE_LDS) {
+    CPROF(4, __popc(live));
+    if (threadIdx.x == 0) CPROF(5, 1);
     for (int x = threadIdx.x; x < (int)R; x += 256) sL[x] = ldg(L.uid + lo + x);
     __syncthreads();
     int a[KPT];
@@ -1246,6 +1316,8 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
       g1 = (hi + 1023) >> 10;
     }
     if (g1 - g0 <= PROBE_LDS) {  // workgroup-uniform
+      CPROF(sh == 5 ? 6 : 8, __popc(live));
+      if (threadIdx.x == 0) CPROF(sh == 5 ? 7 : 9, 1);
       const int H = (int)(g1 - g0);
       for (int x = threadIdx.x; x < H; x += 256) sL[x] = ldg(hd + g0 + x);
       __syncthreads();
@@ -1294,6 +1366,8 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
       return;
     }
   }
+  CPROF(10, __popc(live));
+  if (threadIdx.x == 0) CPROF(11, 1);
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     pos[k] = 0;
@@ -1304,7 +1378,65 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
   }
 }
 
-constexpr int CHAIN_KPT = 3;  // matches per thread and round: 768 a round, few registers
+// The fold's later include lists and its exclusion lists, in order, against the
+// live keys of a round (bitmap list: every live key's 16-B word in flight at once;
+// otherwise chain_search over the range cr[l] staged / headed in LDS; barriers
+// inside, every decision workgroup-uniform).  Returns the keys left alive; pos =
+// their rows in the kept include lists; after1..3 = alive after include test 1..3.
+template <int KPT>
+__device__ __forceinline__ uint32_t chain_tests(const ChainQ* __restrict__ C, int ninc, int nl, int pos0,
+                                                const ProbeDesc* __restrict__ cr, const uint32_t* key,
+                                                uint32_t alive, int32_t (*pos)[KPT], uint32_t& after1,
+                                                uint32_t& after2, uint32_t& after3, uint32_t* sL) {
+  after1 = after2 = after3 = alive;
+  for (int l = 0; l < nl; l++) {
+    const ChainList L = load_cl(&C->l[l]);
+    uint32_t hit = 0;
+    int32_t p[KPT];
+    if (L.bm) {
+      CPROF(2, __popc(alive));
+      if (threadIdx.x == 0) CPROF(3, 1);
+      const __amdgpu_buffer_rsrc_t rbm =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
+      uint4 E[KPT];
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        E[k] = make_uint4(0, 0, 0, 0);
+        if ((alive >> k) & 1u)
+          E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
+      }
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x;
+        const uint64_t bit = 1ull << (key[k] & 63u);
+        p[k] = (int32_t)(E[k].z + __popcll(ex & (bit - 1ull)));  // list positions < 2^31
+        if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
+      }
+    } else {
+      const ProbeDesc D = cr[l];  // workgroup-uniform
+      chain_search<KPT>(L, D.lo, D.hi, key, alive, p, hit, sL);
+    }
+    if (l < ninc) {
+      alive &= hit;
+      const int pi = l - pos0;  // the selection keeps no row
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        if (pi == 0) pos[0][k] = p[k];
+        else if (pi == 1) pos[1][k] = p[k];
+      }
+      if (l == 0) after1 = alive;
+      if (l == 1) after2 = alive;
+      if (l == 2) after3 = alive;
+    } else {
+      alive &= ~hit;
+    }
+  }
+  if (ninc < 2) after2 = after1;
+  if (ninc < 3) after3 = after2;
+  return alive;
+}
+
+constexpr int CHAIN_KPT = 3;  // matches per thread and round: 768 a round (one: 65 VGPRs, 7 waves, but C3 1.69 against 1.43 ms)
 static_assert(CHAIN_KPT * 256 <= 1023, "k_chain: 10-bit count fields");
 
 // One workgroup per chain group (up to CHAIN_GMAX consecutive tiles of one chained
@@ -1349,6 +1481,14 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
   }
   __syncthreads();
   const int32_t M = sOff[n];
+#ifdef YRWI_CHAIN_PROF
+  const unsigned long long ck0 = wall_clock64();
+  if (tid == 0) {
+    CPROF(0, 1);
+    CPROF(1, M);
+    CPROF(12, n);
+  }
+#endif
   const int ninc = ldg(&C->ninc), nl = ldg(&C->nl), pos0 = ldg(&C->pos0), npos = ldg(&C->npos);
   int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
   int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
@@ -1379,49 +1519,9 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
         alive |= 1u << k;
       }
     }
-    uint32_t after1 = alive, after2 = alive, after3 = alive;
-    for (int l = 0; l < nl; l++) {
-      const ChainList L = load_cl(&C->l[l]);
-      uint32_t hit = 0;
-      int32_t p[CHAIN_KPT];
-      if (L.bm) {
-        const __amdgpu_buffer_rsrc_t rbm =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
-        uint4 E[CHAIN_KPT];
-#pragma unroll
-        for (int k = 0; k < CHAIN_KPT; k++) {
-          E[k] = make_uint4(0, 0, 0, 0);
-          if ((alive >> k) & 1u)
-            E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
-        }
-#pragma unroll
-        for (int k = 0; k < CHAIN_KPT; k++) {
-          const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x;
-          const uint64_t bit = 1ull << (key[k] & 63u);
-          p[k] = (int32_t)(E[k].z + __popcll(ex & (bit - 1ull)));  // list positions < 2^31
-          if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
-        }
-      } else {
-        const ProbeDesc D = crange[g * CHAIN_MAXL + l];  // workgroup-uniform
-        chain_search<CHAIN_KPT>(L, D.lo, D.hi, key, alive, p, hit, sL);
-      }
-      if (l < ninc) {
-        alive &= hit;
-        const int pi = l - pos0;  // the selection keeps no row
-#pragma unroll
-        for (int k = 0; k < CHAIN_KPT; k++) {
-          if (pi == 0) pos[0][k] = p[k];
-          else if (pi == 1) pos[1][k] = p[k];
-        }
-        if (l == 0) after1 = alive;
-        if (l == 1) after2 = alive;
-        if (l == 2) after3 = alive;
-      } else {
-        alive &= ~hit;
-      }
-    }
-    if (ninc < 2) after2 = after1;
-    if (ninc < 3) after3 = after2;
+    uint32_t after1, after2, after3;
+    alive = chain_tests<CHAIN_KPT>(C, ninc, nl, pos0, crange + g * CHAIN_MAXL, key, alive, pos, after1, after2, after3,
+                                   sL);
     if (tid < n) sCnt[tid] = 0;
     __syncthreads();
 #pragma unroll
@@ -1465,6 +1565,13 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
     if (tid < n) sRun[tid] += sCnt[tid];
     __syncthreads();
   }
+#ifdef YRWI_CHAIN_PROF
+  if (tid == 0) {
+    CPROF(13, (M + CHAIN_KPT * 256 - 1) / (CHAIN_KPT * 256));
+    CPROF(15, wall_clock64() - ck0);
+    CPROF(16, nsurv);
+  }
+#endif
   if (tid < n) {
     tile_cnt[G.x + tid] = sRun[tid];
     int32_t* lv = tile_lvl + (G.x + tid) * CHAIN_LVL;
@@ -1473,6 +1580,64 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
     lv[2] = tid == 0 ? n2 : 0;
     lv[3] = tid == 0 ? n3 : 0;
     lv[4] = tid == 0 ? nsurv : 0;
+  }
+}
+
+// k_probe<.., CHAIN>: the chain tests of one probe tile of a chained job, on the
+// cnt matches the probe left in LDS (sLoc / sPos, in url-id order) instead of in
+// the tile's slots: rounds of 256 (one per thread); only the survivors are
+// written, at the front of the tile's slots, with their rows in the later include
+// lists; the tile's survivor count and its level counts.  The matches that do
+// not survive are never written to HBM nor read back.
+__device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t src, int32_t cnt,
+                               const uint16_t* sLoc, const uint32_t* sPos, const uint32_t* __restrict__ small_uid,
+                               int64_t s0, bool small_is_A, uint2* __restrict__ pairs,
+                               uint32_t* __restrict__ pair_uid, int32_t* __restrict__ tile_cnt,
+                               int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ cr, uint32_t* sL,
+                               uint64_t* sScan64) {
+  const int tid = (int)threadIdx.x;
+  const int ninc = ldg(&C->ninc), nl = ldg(&C->nl), pos0 = ldg(&C->pos0), npos = ldg(&C->npos);
+  int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
+  int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
+  int32_t n1 = 0, n2 = 0, n3 = 0, run = 0;
+  for (int r0 = 0; r0 < cnt; r0 += 256) {  // workgroup-uniform
+    const int i = r0 + tid;
+    uint32_t key[1] = {0};
+    uint2 pr = make_uint2(0, 0);
+    int32_t pos[CHAIN_MAXI][1] = {{0}, {0}};
+    uint32_t alive = 0;
+    if (i < cnt) {  // the small list's id (the tile just read it: a cache hit) and the pair
+      const int64_t ik = s0 + sLoc[i];
+      const uint32_t jl = sPos[i];
+      key[0] = ldg(small_uid + ik);
+      pr = small_is_A ? make_uint2((uint32_t)ik, jl) : make_uint2(jl, (uint32_t)ik);
+      alive = 1;
+    }
+    uint32_t after1, after2, after3;
+    alive = chain_tests<1>(C, ninc, nl, pos0, cr, key, alive, pos, after1, after2, after3, sL);
+    const uint64_t c = (uint64_t)alive | (uint64_t)after1 << 16 | (uint64_t)after2 << 32 | (uint64_t)after3 << 48;
+    uint64_t tot;
+    const uint64_t ex = block_excl_sum256_u64(c, sScan64, &tot);
+    if (alive) {
+      const int64_t o = src + run + (int64_t)(ex & 0xFFFFu);
+      stg(reinterpret_cast<uint2*>(pairs) + o, pr);
+      stg(pair_uid + o, key[0]);
+      if (tup0) stg(tup0 + o, pos[0][0]);
+      if (tup1) stg(tup1 + o, pos[1][0]);
+    }
+    run += (int32_t)(tot & 0xFFFFu);
+    n1 += (int32_t)((tot >> 16) & 0xFFFFu);
+    n2 += (int32_t)((tot >> 32) & 0xFFFFu);
+    n3 += (int32_t)((tot >> 48) & 0xFFFFu);
+  }
+  if (tid == 0) {
+    tile_cnt[b] = run;
+    int32_t* lv = tile_lvl + b * CHAIN_LVL;
+    lv[0] = cnt;
+    lv[1] = n1;
+    lv[2] = n2;
+    lv[3] = n3;
+    lv[4] = run;
   }
 }
 
@@ -1922,6 +2087,8 @@ __device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int3
 // need (min/max, tf, host counts); the order-dependent fold of posintext /
 // distance works on thread-consecutive elements, so (valid, p, od) of every
 // element are exchanged through LDS.
+//
+// Host counts (authority) are not k_reduce's: k_hostcount runs before it.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
@@ -1947,7 +2114,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 #pragma unroll
   for (int j = 0; j < NP2; j++) { pmn[j] = 0xFFFFFFFFu; pmx[j] = 0u; }
   int32_t pmax = -1, nval = 0, myfirst = BIG;
-  int32_t hmax = 0;  // largest host count this thread saw (one atomicMax per wave below)
   int32_t tcn = -1, tdn = 1, tcx = -1, tdx = 1;  // tf min / max as fractions (-1: none yet)
   int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
   // RED_GROUP elements at a time: their exclusion marks, then their records, all
@@ -1994,25 +2160,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       myfirst = min(myfirst, eo);
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
-      if (Q.want_authority) {
-        uint64_t key = (rg[s % RED_GROUP].w[3] & REC_HOST_MASK) + 1;  // the record's host hash: no key gather
-        uint64_t slot = mix64(key) & Q.hmask;
-        while (true) {
-          unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
-          if (prev == 0ull || prev == key) {
-            uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
-            hmax = max(hmax, (int32_t)cnt);  // the last increment of every host sees its final count
-            break;
-          }
-          slot = (slot + 1) & Q.hmask;
-        }
-      }
     }
     sPO[eo + (eo >> 5)] = po;
-  }
-  if (Q.want_authority) {  // block-uniform: one atomicMax per wave instead of one per posting
-    const int32_t wm = wave_max_i(hmax);
-    if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
   }
   // first valid element of the chunk (element order)
   int32_t firstIdx;
@@ -3815,7 +3964,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
-                     ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups) {
+                     ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups, ProbeDesc* d_prange) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -3871,20 +4020,32 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
   if (merge_tiles > 0) dbg_sync("k_join", st);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
+  const bool fused = chain && d_prange != nullptr;  // YRWI_CHAIN_FUSED (yrwi_host.cpp chain_fused)
   if (probe_tiles > 0) {
-    auto kp = long_tiles ? (mark ? k_probe<true, true> : k_probe<true, false>)
-                         : (mark ? k_probe<false, true> : k_probe<false, false>);
+    if (fused) {  // the chained jobs' later-list ranges of every probe tile, for k_probe<.., true>
+      const int64_t nr = probe_tiles * CHAIN_MAXL;
+      hipLaunchKernelGGL(k_chain_part<true>, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                         d_tile_base, njobs, (const int2*)nullptr, merge_tiles, probe_tiles,
+                         (const uint32_t*)d_pair_uid, (const int64_t*)d_tile_src, (const int32_t*)d_tile_cnt,
+                         d_prange);
+      dbg_sync("k_chain_part<probe tiles>", st);
+    }
+    auto kp = long_tiles ? (mark ? k_probe<true, true, false>
+                                 : fused ? k_probe<true, false, true> : k_probe<true, false, false>)
+                         : (mark ? k_probe<false, true, false>
+                                 : fused ? k_probe<false, false, true> : k_probe<false, false, false>);
     hipLaunchKernelGGL(kp, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm);
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm, d_tile_lvl,
+                       (const ProbeDesc*)d_prange);
     dbg_sync(mark ? "k_probe (exclusion)" : "k_probe", st);
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
-    if (chain && ngroups > 0) {
+    if (chain && ngroups > 0) {  // chain groups (fused: of merge tiles only)
       const int64_t nr = ngroups * CHAIN_MAXL;
-      hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs, d_tile_base,
-                         njobs, d_cgrp, ngroups, (const uint32_t*)d_pair_uid, (const int64_t*)d_tile_src,
-                         (const int32_t*)d_tile_cnt, d_crange);
+      hipLaunchKernelGGL(k_chain_part<false>, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                         d_tile_base, njobs, d_cgrp, (int64_t)0, ngroups, (const uint32_t*)d_pair_uid,
+                         (const int64_t*)d_tile_src, (const int32_t*)d_tile_cnt, d_crange);
       dbg_sync("k_chain_part", st);
       hipLaunchKernelGGL(k_chain, dim3((unsigned)ngroups), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs, d_cgrp,
                          d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl, (const ProbeDesc*)d_crange);
@@ -3950,9 +4111,100 @@ int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n
   return rc(hipGetLastError());
 }
 
+// Host counts of ReferenceOrder (doms / maxdomcount, :176-216), for authority:
+// one workgroup per 2048-posting chunk of an authority query.  The chunk's hosts
+// (the records' word 3: no key gather) are counted in an LDS table (host + 1 and
+// count in one 64-bit word, 4096 slots), then added to the query's global table
+// once per distinct host of the chunk -- every home slot's compare-and-swap in
+// flight at once, then every add.  Hosts are Zipf-distributed (C5: the top host
+// holds ~9% of the urls): one global add per posting serialised thousands of
+// atomics on a few slots inside k_reduce (C5 custom k_reduce 98-121 us against
+// 43 us for the /date profile).
+constexpr int HOST_LDS = 2 * CHUNK;
+constexpr int HOST_PT = HOST_LDS / CHUNK_THREADS;
+__global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __restrict__ qs,
+                                                            const int32_t* __restrict__ chunk_q,
+                                                            ShardSum* __restrict__ shard) {
+  __shared__ unsigned long long sHost[HOST_LDS];
+  const int64_t b = blockIdx.x;
+  const int qi = chunk_q[b];
+  const RankQ& Q = qs[qi];
+  if (!Q.want_authority) return;  // workgroup-uniform
+  const int64_t c = b - Q.chunk_base;
+  const int tid = (int)threadIdx.x;
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++) sHost[x * CHUNK_THREADS + tid] = 0ull;
+  __syncthreads();
+  uint64_t w3[CHUNK_IPT];
+  bool ok[CHUNK_IPT];
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {  // every element's word in flight at once
+    const int64_t e = c * CHUNK + s * CHUNK_THREADS + tid;
+    ok[s] = e < Q.n;
+    const int64_t ee = ok[s] ? e : Q.n - 1;
+    w3[s] = ldg(Q.feat + ee * FEAT_WORDS + 3);
+    if (Q.removed && ldg(Q.removed + ee)) ok[s] = false;
+  }
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    if (!ok[s]) continue;
+    const unsigned long long key = ((w3[s] & REC_HOST_MASK) + 1) << 12;
+    uint32_t slot = (uint32_t)mix64(key) & (HOST_LDS - 1);
+    while (true) {
+      const unsigned long long prev = atomicCAS(&sHost[slot], 0ull, key);
+      if (prev == 0ull || (prev >> 12) == (key >> 12)) {
+        atomicAdd(&sHost[slot], 1ull);
+        break;
+      }
+      slot = (slot + 1) & (HOST_LDS - 1);
+    }
+  }
+  __syncthreads();
+  unsigned long long hk[HOST_PT], prev[HOST_PT];
+  uint64_t gs[HOST_PT];
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++) {  // every home slot's compare-and-swap in flight at once
+    const unsigned long long w = sHost[x * CHUNK_THREADS + tid];
+    hk[x] = w >> 12;
+    gs[x] = mix64(hk[x]) & Q.hmask;
+    prev[x] = w ? atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]) : 0ull;
+  }
+  int32_t hmax = 0;
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++) {
+    if (!hk[x]) continue;
+    while (prev[x] != 0ull && prev[x] != hk[x]) {  // another host holds the home slot: probe on
+      gs[x] = (gs[x] + 1) & Q.hmask;
+      prev[x] = atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]);
+    }
+  }
+  uint32_t cnt[HOST_PT];
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++) {
+    const uint32_t n = (uint32_t)(sHost[x * CHUNK_THREADS + tid] & 0xFFFull);
+    cnt[x] = hk[x] ? atomicAdd(&Q.hcnt[gs[x]], n) + n : 0u;
+  }
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++) hmax = max(hmax, (int32_t)cnt[x]);  // the last add of a host sees its total
+  const int32_t wm = wave_max_i(hmax);
+  if ((tid & 63) == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
+}
+
+#ifdef YRWI_CHAIN_PROF
+extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build only: read and clear
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cprof), sizeof(g_cprof)) != hipSuccess) return -1;
+  unsigned long long z[24] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, bool authority) {
+  if (total_chunks > 0 && authority)
+    hipLaunchKernelGGL(k_hostcount, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
+                       d_shard);
   if (total_chunks > 0)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
