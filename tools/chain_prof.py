@@ -13,7 +13,8 @@ from yacy_search_server_amd import RWIIndex, RankingProfile, Query, synth, _lib 
 
 NAMES = ["groups", "matches", "bm_tests", "bm_lists", "lds_tests", "lds_lists", "h1_tests", "h1_lists",
          "h2_tests", "h2_lists", "key_tests", "key_lists", "tiles", "rounds", "search_cycles", "wg_cycles",
-         "survivors", "", "", "", "range_ids_sum", "", "", ""]
+         "survivors", "hc_groups", "hc_chunks_of_query_sum", "hc_distinct", "hc_collisions", "hc_insert_cycles",
+         "hc_flush_cycles", "hc_elements_of_query_sum"]
 
 
 def main():
@@ -21,6 +22,8 @@ def main():
     nincl = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     nexcl = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     cfg = synth.preset(preset)
+    if len(sys.argv) > 5:  # url-hash shard r of n (C5: shard 0 of 8)
+        cfg = cfg.shard(0, int(sys.argv[5]))
     idx = synth.build_index(cfg)
     ix = RWIIndex(0)
     for t in range(cfg.n_terms):
@@ -28,8 +31,11 @@ def main():
             ix.add(idx.hashes[t], idx.list_rows(t))
     ix.build_url_ids()
     hashes = [synth.term_hash(cfg, t) for t in range(cfg.n_terms)]
-    qs = synth.queries(cfg, 1000, nincl, nincl, nexcl)
+    maxi = int(os.environ.get("CP_MAX_TERMS", nincl))
+    qs = synth.queries(synth.preset(preset), 1000, nincl, maxi, nexcl)
     prof = RankingProfile()
+    if len(sys.argv) > 4 and sys.argv[4] == "custom":
+        prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
     batch = [Query([hashes[t] for t in inc], [hashes[t] for t in exc], k=100, profile=prof) for inc, exc in qs]
     f = _lib.lib().yrwi_chain_prof
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]

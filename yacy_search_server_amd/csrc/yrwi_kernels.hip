@@ -1290,7 +1290,7 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
   hit = 0;
   const int64_t R = hi - lo;
   __syncthreads();  // the previous list's stage is no longer read
-  CPROF(20, R);
+
   if (R <= PROBE_LDS) {
     CPROF(4, __popc(live));
     if (threadIdx.x == 0) CPROF(5, 1);
@@ -4115,11 +4115,13 @@ int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n
 // one workgroup per 2048-posting chunk of an authority query.  The chunk's hosts
 // (the records' word 3: no key gather) are counted in an LDS table (host + 1 and
 // count in one 64-bit word, 4096 slots), then added to the query's global table
-// once per distinct host of the chunk -- every home slot's compare-and-swap in
-// flight at once, then every add.  Hosts are Zipf-distributed (C5: the top host
-// holds ~9% of the urls): one global add per posting serialised thousands of
-// atomics on a few slots inside k_reduce (C5 custom k_reduce 98-121 us against
-// 43 us for the /date profile).
+// once per distinct host of the chunk -- every home slot read at once, a
+// compare-and-swap only where the host is not there yet (the query's other
+// chunks insert its frequent hosts first), then every add.  Device-scope atomics
+// are what this kernel waits on (C5 custom: 0.75 M (chunk, host) pairs, 0.21 M
+// probe steps; 97.6 us with a compare-and-swap per pair), so every one saved
+// counts; inside k_reduce one add per posting took 98-121 us against k_reduce's
+// 43 us for the /date profile.
 constexpr int HOST_LDS = 2 * CHUNK;
 constexpr int HOST_PT = HOST_LDS / CHUNK_THREADS;
 __global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __restrict__ qs,
@@ -4132,6 +4134,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __rest
   if (!Q.want_authority) return;  // workgroup-uniform
   const int64_t c = b - Q.chunk_base;
   const int tid = (int)threadIdx.x;
+#ifdef YRWI_CHAIN_PROF
+  const unsigned long long hc0 = wall_clock64();
+  if (tid == 0) { CPROF(17, 1); CPROF(18, Q.nchunks); }
+#endif
 #pragma unroll
   for (int x = 0; x < HOST_PT; x++) sHost[x * CHUNK_THREADS + tid] = 0ull;
   __syncthreads();
@@ -4160,20 +4166,28 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __rest
     }
   }
   __syncthreads();
+#ifdef YRWI_CHAIN_PROF
+  const unsigned long long hc1 = wall_clock64();
+#endif
   unsigned long long hk[HOST_PT], prev[HOST_PT];
   uint64_t gs[HOST_PT];
 #pragma unroll
-  for (int x = 0; x < HOST_PT; x++) {  // every home slot's compare-and-swap in flight at once
+  for (int x = 0; x < HOST_PT; x++) {  // every home slot read at once (plain loads: a key once set never changes)
     const unsigned long long w = sHost[x * CHUNK_THREADS + tid];
     hk[x] = w >> 12;
     gs[x] = mix64(hk[x]) & Q.hmask;
-    prev[x] = w ? atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]) : 0ull;
+    prev[x] = w ? (unsigned long long)Q.hkeys[gs[x]] : 0ull;
   }
+#pragma unroll
+  for (int x = 0; x < HOST_PT; x++)  // the home slots not yet holding their host: compare-and-swap, all at once
+    if (hk[x] && prev[x] != hk[x])
+      prev[x] = atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]);
   int32_t hmax = 0;
 #pragma unroll
   for (int x = 0; x < HOST_PT; x++) {
     if (!hk[x]) continue;
     while (prev[x] != 0ull && prev[x] != hk[x]) {  // another host holds the home slot: probe on
+      CPROF(20, 1);
       gs[x] = (gs[x] + 1) & Q.hmask;
       prev[x] = atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]);
     }
@@ -4188,6 +4202,16 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __rest
   for (int x = 0; x < HOST_PT; x++) hmax = max(hmax, (int32_t)cnt[x]);  // the last add of a host sees its total
   const int32_t wm = wave_max_i(hmax);
   if ((tid & 63) == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
+#ifdef YRWI_CHAIN_PROF
+  int nd = 0;
+  for (int x = 0; x < HOST_PT; x++) nd += hk[x] ? 1 : 0;
+  CPROF(19, nd);
+  if (tid == 0) {
+    CPROF(21, hc1 - hc0);
+    CPROF(22, wall_clock64() - hc1);
+    CPROF(23, Q.n);
+  }
+#endif
 }
 
 #ifdef YRWI_CHAIN_PROF
