@@ -13,8 +13,7 @@ from yacy_search_server_amd import RWIIndex, RankingProfile, Query, synth, _lib 
 
 NAMES = ["groups", "matches", "bm_tests", "bm_lists", "lds_tests", "lds_lists", "h1_tests", "h1_lists",
          "h2_tests", "h2_lists", "key_tests", "key_lists", "tiles", "rounds", "search_cycles", "wg_cycles",
-         "survivors", "hc_groups", "hc_chunks_of_query_sum", "hc_distinct", "hc_collisions", "hc_insert_cycles",
-         "hc_flush_cycles", "hc_elements_of_query_sum"]
+         "survivors", "", "", "", "", "", "", ""]
 
 
 def main():

@@ -29,7 +29,7 @@ def short(name):
         return "k_probe_excl" if len(args) > 1 and args[1] in ("true", "1") else "k_probe"
     if "k_probeILb" in name:
         return "k_probe_excl" if "ELb1E" in name.split("k_probeILb", 1)[1][:8] else "k_probe"
-    for k in ("k_hostcount", "k_chain_part", "k_chain", "k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
+    for k in ("k_chain_part", "k_chain", "k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
               "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
               "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:

@@ -1685,7 +1685,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, any_auth)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kreduce.push_back(tm->spans.back());
   if (st) {

@@ -372,7 +372,7 @@ int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, bool authority);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip

@@ -2088,7 +2088,13 @@ __device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int3
 // distance works on thread-consecutive elements, so (valid, p, od) of every
 // element are exchanged through LDS.
 //
-// Host counts (authority) are not k_reduce's: k_hostcount runs before it.
+// Authority host counts (ReferenceOrder doms / maxdomcount, :176-216): every
+// valid element adds one to its host's slot in the query's global table, the host
+// hash taken from the record's word 3 (no key gather from the url dictionary:
+// C5 custom k_reduce 121.7 -> 97.9 us).  A separate per-chunk kernel counting in
+// LDS first (k_hostcount, round 4) took 107 + 18 us: its distinct (chunk, host)
+// pairs still cost a device atomic each, and the Zipf hosts of a chunk are mostly
+// distinct.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
@@ -2114,6 +2120,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 #pragma unroll
   for (int j = 0; j < NP2; j++) { pmn[j] = 0xFFFFFFFFu; pmx[j] = 0u; }
   int32_t pmax = -1, nval = 0, myfirst = BIG;
+  int32_t hmax = 0;  // largest host count this thread saw (one atomicMax per wave below)
   int32_t tcn = -1, tdn = 1, tcx = -1, tdx = 1;  // tf min / max as fractions (-1: none yet)
   int32_t av[CHUNK_IPT];  // lastModified days of my elements (-1: invalid)
   // RED_GROUP elements at a time: their exclusion marks, then their records, all
@@ -2160,8 +2167,26 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       myfirst = min(myfirst, eo);
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
+      if (Q.want_authority) {
+        const uint64_t key = (rg[s % RED_GROUP].w[3] & REC_HOST_MASK) + 1;  // the record's host hash
+        uint64_t slot = mix64(key) & Q.hmask;
+        while (true) {
+          const unsigned long long prev =
+              atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
+          if (prev == 0ull || prev == key) {
+            const uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
+            hmax = max(hmax, (int32_t)cnt);  // the last increment of every host sees its final count
+            break;
+          }
+          slot = (slot + 1) & Q.hmask;
+        }
+      }
     }
     sPO[eo + (eo >> 5)] = po;
+  }
+  if (Q.want_authority) {  // block-uniform: one atomicMax per wave instead of one per posting
+    const int32_t wm = wave_max_i(hmax);
+    if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
   }
   // first valid element of the chunk (element order)
   int32_t firstIdx;
@@ -4111,109 +4136,6 @@ int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n
   return rc(hipGetLastError());
 }
 
-// Host counts of ReferenceOrder (doms / maxdomcount, :176-216), for authority:
-// one workgroup per 2048-posting chunk of an authority query.  The chunk's hosts
-// (the records' word 3: no key gather) are counted in an LDS table (host + 1 and
-// count in one 64-bit word, 4096 slots), then added to the query's global table
-// once per distinct host of the chunk -- every home slot read at once, a
-// compare-and-swap only where the host is not there yet (the query's other
-// chunks insert its frequent hosts first), then every add.  Device-scope atomics
-// are what this kernel waits on (C5 custom: 0.75 M (chunk, host) pairs, 0.21 M
-// probe steps; 97.6 us with a compare-and-swap per pair), so every one saved
-// counts; inside k_reduce one add per posting took 98-121 us against k_reduce's
-// 43 us for the /date profile.
-constexpr int HOST_LDS = 2 * CHUNK;
-constexpr int HOST_PT = HOST_LDS / CHUNK_THREADS;
-__global__ __launch_bounds__(CHUNK_THREADS) void k_hostcount(const RankQ* __restrict__ qs,
-                                                            const int32_t* __restrict__ chunk_q,
-                                                            ShardSum* __restrict__ shard) {
-  __shared__ unsigned long long sHost[HOST_LDS];
-  const int64_t b = blockIdx.x;
-  const int qi = chunk_q[b];
-  const RankQ& Q = qs[qi];
-  if (!Q.want_authority) return;  // workgroup-uniform
-  const int64_t c = b - Q.chunk_base;
-  const int tid = (int)threadIdx.x;
-#ifdef YRWI_CHAIN_PROF
-  const unsigned long long hc0 = wall_clock64();
-  if (tid == 0) { CPROF(17, 1); CPROF(18, Q.nchunks); }
-#endif
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++) sHost[x * CHUNK_THREADS + tid] = 0ull;
-  __syncthreads();
-  uint64_t w3[CHUNK_IPT];
-  bool ok[CHUNK_IPT];
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {  // every element's word in flight at once
-    const int64_t e = c * CHUNK + s * CHUNK_THREADS + tid;
-    ok[s] = e < Q.n;
-    const int64_t ee = ok[s] ? e : Q.n - 1;
-    w3[s] = ldg(Q.feat + ee * FEAT_WORDS + 3);
-    if (Q.removed && ldg(Q.removed + ee)) ok[s] = false;
-  }
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {
-    if (!ok[s]) continue;
-    const unsigned long long key = ((w3[s] & REC_HOST_MASK) + 1) << 12;
-    uint32_t slot = (uint32_t)mix64(key) & (HOST_LDS - 1);
-    while (true) {
-      const unsigned long long prev = atomicCAS(&sHost[slot], 0ull, key);
-      if (prev == 0ull || (prev >> 12) == (key >> 12)) {
-        atomicAdd(&sHost[slot], 1ull);
-        break;
-      }
-      slot = (slot + 1) & (HOST_LDS - 1);
-    }
-  }
-  __syncthreads();
-#ifdef YRWI_CHAIN_PROF
-  const unsigned long long hc1 = wall_clock64();
-#endif
-  unsigned long long hk[HOST_PT], prev[HOST_PT];
-  uint64_t gs[HOST_PT];
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++) {  // every home slot read at once (plain loads: a key once set never changes)
-    const unsigned long long w = sHost[x * CHUNK_THREADS + tid];
-    hk[x] = w >> 12;
-    gs[x] = mix64(hk[x]) & Q.hmask;
-    prev[x] = w ? (unsigned long long)Q.hkeys[gs[x]] : 0ull;
-  }
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++)  // the home slots not yet holding their host: compare-and-swap, all at once
-    if (hk[x] && prev[x] != hk[x])
-      prev[x] = atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]);
-  int32_t hmax = 0;
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++) {
-    if (!hk[x]) continue;
-    while (prev[x] != 0ull && prev[x] != hk[x]) {  // another host holds the home slot: probe on
-      CPROF(20, 1);
-      gs[x] = (gs[x] + 1) & Q.hmask;
-      prev[x] = atomicCAS((unsigned long long*)&Q.hkeys[gs[x]], 0ull, hk[x]);
-    }
-  }
-  uint32_t cnt[HOST_PT];
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++) {
-    const uint32_t n = (uint32_t)(sHost[x * CHUNK_THREADS + tid] & 0xFFFull);
-    cnt[x] = hk[x] ? atomicAdd(&Q.hcnt[gs[x]], n) + n : 0u;
-  }
-#pragma unroll
-  for (int x = 0; x < HOST_PT; x++) hmax = max(hmax, (int32_t)cnt[x]);  // the last add of a host sees its total
-  const int32_t wm = wave_max_i(hmax);
-  if ((tid & 63) == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
-#ifdef YRWI_CHAIN_PROF
-  int nd = 0;
-  for (int x = 0; x < HOST_PT; x++) nd += hk[x] ? 1 : 0;
-  CPROF(19, nd);
-  if (tid == 0) {
-    CPROF(21, hc1 - hc0);
-    CPROF(22, wall_clock64() - hc1);
-    CPROF(23, Q.n);
-  }
-#endif
-}
-
 #ifdef YRWI_CHAIN_PROF
 extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build only: read and clear
   if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -4225,10 +4147,7 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, bool authority) {
-  if (total_chunks > 0 && authority)
-    hipLaunchKernelGGL(k_hostcount, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                       d_shard);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st) {
   if (total_chunks > 0)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
