@@ -73,16 +73,9 @@ __host__ __device__ constexpr int64_t heads_cap(int64_t n) { return head1_cap(n)
 //   w1 = r | o << 8 | i << 16 | x << 24 | y << 32 | m << 40 | n << 48 | d << 56
 //        posinphrase, posofphrase, worddistance, llocal, lother, urllength, urlcomps, doctype
 //   w2 = a | l << 16 | z << 32          lastModified days, language (byte 22 low), flags (byte 29 low)
-//   w3 = host | dl << 36                the url's host hash (url-hash chars 6..11 as 36 bits,
-//                                       DigestURL :229-296), domLengthEstimation key (ahpla[urlhash[11]] & 3)
-// The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.  The host
-// hash is what ReferenceOrder's host counts key on (:196-198, authority :213-216):
-// the rank phase counts and looks up hosts from the record it streams anyway,
-// without gathering the url's key from the dictionary.  ByteArray.hashCode of the
-// url hash (the top-k tie-break) is computed from the key for candidates only.
+//   w3 = h | dl << 32                   ByteArray.hashCode(urlhash), domLengthEstimation key (ahpla[urlhash[11]] & 3)
+// The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.
 constexpr int FEAT_WORDS = 4;
-constexpr int REC_DL_SHIFT = 36;
-constexpr uint64_t REC_HOST_MASK = (1ull << 36) - 1;
 constexpr int FEAT_BYTES = 8 * FEAT_WORDS;
 
 // Feature rule of a join step (ReferenceContainer.joinConstructive :406-416).

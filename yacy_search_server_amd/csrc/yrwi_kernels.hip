@@ -367,7 +367,6 @@ struct Rec {
   uint64_t w[FEAT_WORDS];
 };
 
-__device__ __forceinline__ uint64_t host36(const Row& r);
 __device__ __forceinline__ Rec rec_of_row(const Row& r) {
   Rec q;
   q.w[0] = (uint64_t)r.u16(O_T) | (uint64_t)r.u16(O_W) << 16 | (uint64_t)r.u16(O_P) << 32 | (uint64_t)r.b(O_U) << 48 |
@@ -376,7 +375,7 @@ __device__ __forceinline__ Rec rec_of_row(const Row& r) {
            (uint64_t)r.b(O_Y) << 32 | (uint64_t)r.b(O_M) << 40 | (uint64_t)r.b(O_N) << 48 | (uint64_t)r.b(O_D) << 56;
   const uint64_t z = r.b(O_Z) | (r.b(O_Z + 1) << 8) | (r.b(O_Z + 2) << 16) | ((uint64_t)r.b(O_Z + 3) << 24);
   q.w[2] = (uint64_t)r.u16(O_A) | (uint64_t)(r.b(O_L) | (r.b(O_L + 1) << 8)) << 16 | z << 32;
-  q.w[3] = host36(r) | (uint64_t)(ahpla(r.b(11)) & 3) << REC_DL_SHIFT;
+  q.w[3] = (uint64_t)(uint32_t)url_hashcode(r) | (uint64_t)(ahpla(r.b(11)) & 3) << 32;
   return q;
 }
 
@@ -418,7 +417,7 @@ __device__ __forceinline__ Feat decode_rec(const Rec& q) {
   x.z = (uint32_t)(w2 >> 32);
   x.lang = (uint32_t)((w2 >> 16) & 0xFFFF);
   x.d = (uint32_t)(w1 >> 56);
-  x.dl = (int32_t)((q.w[3] >> REC_DL_SHIFT) & 3);
+  x.dl = (int32_t)((q.w[3] >> 32) & 3);
   return x;
 }
 
@@ -1110,22 +1109,23 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
   __shared__ uint64_t sScan64[4];
   const JoinQ& J = jobs[blockIdx.x];
   const int64_t base = tile_base[blockIdx.x];
+  const bool lvl = tile_lvl && J.chain;  // workgroup-uniform
+  uint64_t acc[CHAIN_LVL] = {};
   int64_t running = 0;
   for (int64_t t0 = 0; t0 < J.ntiles; t0 += 256) {
     int64_t t = t0 + threadIdx.x;
     int32_t c = t < J.ntiles ? tile_cnt[base + t] : 0;
+    if (lvl && t < J.ntiles)  // the level counts ride along (their loads in flight with the count's)
+#pragma unroll
+      for (int l = 0; l < CHAIN_LVL; l++) acc[l] += (uint64_t)tile_lvl[(base + t) * CHAIN_LVL + l];
     int32_t tot;
     int32_t ex = block_excl_sum256(c, sScan, &tot);
     if (t < J.ntiles) tile_off[base + t] = running + ex;
     running += tot;
   }
   if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
-  if (tile_lvl && J.chain) {  // workgroup-uniform
+  if (lvl) {
     int64_t* level = ldg(&J.chain->level);
-    uint64_t acc[CHAIN_LVL] = {};
-    for (int64_t t = threadIdx.x; t < J.ntiles; t += 256)
-#pragma unroll
-      for (int l = 0; l < CHAIN_LVL; l++) acc[l] += (uint64_t)tile_lvl[(base + t) * CHAIN_LVL + l];
     for (int l = 0; l < CHAIN_LVL; l++) {
       uint64_t tot;
       block_excl_sum256_u64(acc[l], sScan64, &tot);
@@ -1280,10 +1280,9 @@ __device__ __forceinline__ void lds_lower_bound_multi(const uint32_t* s, int n, 
 // Membership and position of the live keys (ascending, all inside [lo, hi)) in a
 // list without a url-id bitmap, by the whole workgroup (barriers inside; every
 // decision is workgroup-uniform): the range's ids staged in LDS when it fits;
-// otherwise its level-1 line heads (every 32nd id) or, past that, its level-2
-// heads (every 1024th) staged in LDS, an LDS search per key, then (level 2) one
-// line of level-1 heads and one leaf line of ids per key (lower_bound_multi);
-// per-key head searches only beyond both stages.
+// otherwise its level-1 line heads (every 32nd id) staged in LDS, an LDS search
+// per key, then one leaf line of ids per key (lower_bound_multi); per-key head
+// searches beyond that.
 template <int KPT>
 __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int64_t hi, const uint32_t* key,
                                              uint32_t live, int32_t* pos, uint32_t& hit, uint32_t* sL) {
@@ -1306,20 +1305,12 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
     return;
   }
   if (L.head) {
-    int sh = 5;
-    const uint32_t* __restrict__ hd = L.head;
-    int64_t g0 = (lo + 31) >> 5, g1 = (hi + 31) >> 5;  // heads at positions in [lo, hi)
-    if (g1 - g0 > PROBE_LDS) {
-      sh = 10;
-      hd = L.head + head1_cap(L.n);
-      g0 = (lo + 1023) >> 10;
-      g1 = (hi + 1023) >> 10;
-    }
+    const int64_t g0 = (lo + 31) >> 5, g1 = (hi + 31) >> 5;  // level-1 heads at positions in [lo, hi)
     if (g1 - g0 <= PROBE_LDS) {  // workgroup-uniform
-      CPROF(sh == 5 ? 6 : 8, __popc(live));
-      if (threadIdx.x == 0) CPROF(sh == 5 ? 7 : 9, 1);
+      CPROF(6, __popc(live));
+      if (threadIdx.x == 0) CPROF(7, 1);
       const int H = (int)(g1 - g0);
-      for (int x = threadIdx.x; x < H; x += 256) sL[x] = ldg(hd + g0 + x);
+      for (int x = threadIdx.x; x < H; x += 256) sL[x] = ldg(L.head + g0 + x);
       __syncthreads();
       int64_t wl[KPT];
       int32_t wn[KPT];
@@ -1329,28 +1320,9 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
       for (int k = 0; k < KPT; k++) {
         const int a = ha[k];
         // the lower bound lies in (position of head a-1, position of head a], within [lo, hi]
-        wl[k] = a > 0 ? ((g0 + a - 1) << sh) + 1 : lo;
-        const int64_t wr = a < H ? ((g0 + a) << sh) : hi;
+        wl[k] = a > 0 ? ((g0 + a - 1) << 5) + 1 : lo;
+        const int64_t wr = a < H ? ((g0 + a) << 5) : hi;
         wn[k] = ((live >> k) & 1u) ? (int32_t)(wr - wl[k]) : 0;
-      }
-      if (sh == 10) {  // narrow each window to one leaf line with its <= 32 level-1 heads
-        int64_t f0[KPT], hb[KPT];
-        int32_t hn[KPT];
-#pragma unroll
-        for (int k = 0; k < KPT; k++) {
-          f0[k] = (wl[k] + 31) >> 5;
-          hb[k] = f0[k];
-          hn[k] = (int32_t)(((wl[k] + wn[k] + 31) >> 5) - f0[k]);
-        }
-        lower_bound_multi<KPT>(L.head, hb, hn, key, live);
-#pragma unroll
-        for (int k = 0; k < KPT; k++) {
-          const int64_t c = hb[k], f1 = (wl[k] + wn[k] + 31) >> 5;
-          const int64_t l2 = c > f0[k] ? ((c - 1) << 5) + 1 : wl[k];
-          const int64_t r2 = c < f1 ? (c << 5) : wl[k] + wn[k];
-          wl[k] = l2;
-          wn[k] = (int32_t)(r2 - l2);
-        }
       }
       lower_bound_multi<KPT>(L.uid, wl, wn, key, live);
       uint32_t v[KPT];
@@ -1366,8 +1338,8 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
       return;
     }
   }
-  CPROF(10, __popc(live));
-  if (threadIdx.x == 0) CPROF(11, 1);
+  // ranges past PROBE_LDS line heads (C3: 4 k of 100 M tests; a level-2 stage
+  // here cost k_chain a wave per SIMD, 96 -> 106 VGPRs): per-key head searches
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     pos[k] = 0;
@@ -1384,13 +1356,13 @@ __device__ __forceinline__ void chain_search(const ChainList& L, int64_t lo, int
 // inside, every decision workgroup-uniform).  Returns the keys left alive; pos =
 // their rows in the kept include lists; after1..3 = alive after include test 1..3.
 template <int KPT>
-__device__ __forceinline__ uint32_t chain_tests(const ChainQ* __restrict__ C, int ninc, int nl, int pos0,
-                                                const ProbeDesc* __restrict__ cr, const uint32_t* key,
+__device__ __forceinline__ uint32_t chain_tests(const ChainList* cl, int ninc, int nl, int pos0,
+                                                const ProbeDesc* cr, const uint32_t* key,
                                                 uint32_t alive, int32_t (*pos)[KPT], uint32_t& after1,
                                                 uint32_t& after2, uint32_t& after3, uint32_t* sL) {
   after1 = after2 = after3 = alive;
   for (int l = 0; l < nl; l++) {
-    const ChainList L = load_cl(&C->l[l]);
+    const ChainList L = cl[l];
     uint32_t hit = 0;
     int32_t p[KPT];
     if (L.bm) {
@@ -1469,6 +1441,8 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
   const int j = find_job(tile_base, njobs, G.x);
   const ChainQ* C = jobs[j].chain;
   const int tid = (int)threadIdx.x, n = G.y;
+  __shared__ ChainList sCL[CHAIN_MAXL];  // the fold's lists and this group's ranges, loaded once
+  __shared__ ProbeDesc sCR[CHAIN_MAXL];
   if (tid < 64) {
     const int32_t c = tid < n ? tile_cnt[G.x + tid] : 0;
     const int32_t inc = wave_incl_sum(c);
@@ -1478,6 +1452,9 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
       sRun[tid] = 0;
     }
     if (tid == 0) sOff[0] = 0;
+  } else if (tid < 64 + CHAIN_MAXL) {
+    sCL[tid - 64] = load_cl(&C->l[tid - 64]);
+    sCR[tid - 64] = crange[g * CHAIN_MAXL + tid - 64];  // (unset for bitmap lists: unused)
   }
   __syncthreads();
   const int32_t M = sOff[n];
@@ -1520,8 +1497,7 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
       }
     }
     uint32_t after1, after2, after3;
-    alive = chain_tests<CHAIN_KPT>(C, ninc, nl, pos0, crange + g * CHAIN_MAXL, key, alive, pos, after1, after2, after3,
-                                   sL);
+    alive = chain_tests<CHAIN_KPT>(sCL, ninc, nl, pos0, sCR, key, alive, pos, after1, after2, after3, sL);
     if (tid < n) sCnt[tid] = 0;
     __syncthreads();
 #pragma unroll
@@ -1614,7 +1590,7 @@ __device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t 
       alive = 1;
     }
     uint32_t after1, after2, after3;
-    alive = chain_tests<1>(C, ninc, nl, pos0, cr, key, alive, pos, after1, after2, after3, sL);
+    alive = chain_tests<1>(C->l, ninc, nl, pos0, cr, key, alive, pos, after1, after2, after3, sL);
     const uint64_t c = (uint64_t)alive | (uint64_t)after1 << 16 | (uint64_t)after2 << 32 | (uint64_t)after3 << 48;
     uint64_t tot;
     const uint64_t ex = block_excl_sum256_u64(c, sScan64, &tot);
@@ -2089,12 +2065,12 @@ __device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int3
 // element are exchanged through LDS.
 //
 // Authority host counts (ReferenceOrder doms / maxdomcount, :176-216): every
-// valid element adds one to its host's slot in the query's global table, the host
-// hash taken from the record's word 3 (no key gather from the url dictionary:
-// C5 custom k_reduce 121.7 -> 97.9 us).  A separate per-chunk kernel counting in
-// LDS first (k_hostcount, round 4) took 107 + 18 us: its distinct (chunk, host)
-// pairs still cost a device atomic each, and the Zipf hosts of a chunk are mostly
-// distinct.
+// valid element adds one to its host's slot in the query's global table.  (Round
+// 4 tried the host hash in the record's word 3 instead of ByteArray.hashCode:
+// C5 custom k_reduce 121.7 -> 97.9 us, but the candidates' hashCode then came
+// from the url keys, C2 k_score 94 -> 115 us -- the headline pays for it; and a
+// separate per-chunk kernel counting in LDS first, k_hostcount: 107 + 18 us, its
+// distinct (chunk, host) pairs still cost a device atomic each.)
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
@@ -2168,7 +2144,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
       if (Q.want_authority) {
-        const uint64_t key = (rg[s % RED_GROUP].w[3] & REC_HOST_MASK) + 1;  // the record's host hash
+        uint64_t khi;
+        uint32_t klo;
+        key_at(Q, e, khi, klo);
+        const uint64_t key = key_host36(khi, klo) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
           const unsigned long long prev =
@@ -2871,20 +2850,6 @@ __device__ __forceinline__ int32_t url_hashcode(const Row& r) {
   return h;
 }
 
-// ByteArray.hashCode (ByteArray.java:80-84) of element e's url hash, from its key
-// (the top-k tie-break: computed for candidates only)
-__device__ __forceinline__ uint32_t elem_hashcode(const RankQ& Q, int64_t e) {
-  uint64_t khi;
-  uint32_t klo;
-  key_at(Q, e, khi, klo);
-  uint8_t h[12];
-  key_chars(khi, klo, h);
-  int32_t x = 0;
-#pragma unroll
-  for (int j = 0; j < 12; j++) x = add32(mul32(31, x), (int32_t)h[j]);
-  return (uint32_t)x;
-}
-
 __device__ __forceinline__ int32_t host_count(const RankQ& Q, uint64_t host) {
   uint64_t key = host + 1;
   uint64_t slot = mix64(key) & Q.hmask;
@@ -3148,7 +3113,7 @@ __device__ __forceinline__ PruneP prune_params(const NormState& N, const RankQ& 
 __device__ __forceinline__ int64_t score_bound(const Rec& q, const NormState& N, const RankQ& Q, const PruneP& P,
                                                bool* valid, const CardTab* tab = nullptr) {
   const yrwi_profile& rk = Q.prof;
-  const int dl = (int)((q.w[3] >> REC_DL_SHIFT) & 3);
+  const int dl = (int)((q.w[3] >> 32) & 3);
   const int32_t dln = dl == 0 ? 4 : dl == 1 ? 10 : dl == 2 ? 14 : 20;
   int64_t ex = (int64_t)shl32(256 - dln, rk.coeff_domlength);
   if (N.va_mx != N.va_mn)
@@ -3209,14 +3174,15 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
       const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
       if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
     }
+    if (!F && Q.want_authority) key_at(Q, e, khi, klo);
     const Feat t = decode_rec(q);
-    const int32_t hc = Q.want_authority ? host_count(Q, q.w[3] & REC_HOST_MASK) : 0;
+    const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
     a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
     if (a[s] < T) {
       a[s] = 0;
       continue;
     }
-    if (z) z[s] = ((uint64_t)(elem_hashcode(Q, e) ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
+    if (z) z[s] = ((uint64_t)((uint32_t)q.w[3] ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
     vm |= 1u << s;
   }
   return vm;
@@ -3383,7 +3349,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
       if ((vm >> s) & 1u) {
         const int i = s * CHUNK_THREADS + tid;
         const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-        const uint32_t h = elem_hashcode(Q, e);
+        const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
         out[voff].k1 = a[s];
         out[voff].k2 = ((uint64_t)(h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
         voff++;
@@ -3407,7 +3373,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (((vm >> s) & 1u) && a[s] >= T) {
       const int i = s * CHUNK_THREADS + tid;
       const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
-      const uint32_t h = elem_hashcode(Q, e);
+      const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
       off++;
@@ -3865,7 +3831,13 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
     const int64_t e = c * CHUNK + s;
     if (e >= Q.n) break;
     const Feat t = decode_rec(load_rec(Q.feat, e));
-    const int32_t hc = Q.want_authority ? host_count(Q, ldg(Q.feat + e * FEAT_WORDS + 3) & REC_HOST_MASK) : 0;
+    int32_t hc = 0;
+    if (Q.want_authority) {
+      uint64_t khi;
+      uint32_t klo;
+      key_at(Q, e, khi, klo);
+      hc = host_count(Q, key_host36(khi, klo));
+    }
     out[e] = cardinal(t, N, Q, hc);
   }
 }
