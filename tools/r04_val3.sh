@@ -1,0 +1,7 @@
+# Chain lists staged in LDS: chained-fold GPU tests, then the C3 / C4 legs.
+set -o pipefail
+mkdir -p gpurun_out/val3
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -v --timeout 240 --timeout-method thread \
+  -k "chained or urlselection or long_bitmap or forced_join or c3_shard or c4_batch" > gpurun_out/val3/t.log 2>&1 || exit $?
+timeout -k 10 700 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --legs C3,C4 --latency 0 --leg-latency 0 \
+  --no-cpu > gpurun_out/val3/legs.json 2> gpurun_out/val3/legs.err || exit $?
