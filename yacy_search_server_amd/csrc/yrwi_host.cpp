@@ -855,8 +855,12 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
     // (a fused chained job's tiles keep their matches in LDS for the chain tests:
     // BM_TILE, whose registers leave room for them)
+    // A chained job whose first later include list has a bitmap (J.chain_bm, set by
+    // the caller) tests it inside its bitmap probe, on BM_TILE tiles: the long
+    // tiles' registers leave no room for it.  Otherwise no such test.
+    if (!bm || J.algo == JA_MERGE) J.chain_bm = nullptr;
     const bool light = chain_fused() ? (J.out_tup != nullptr || J.mode == JM_MARK) && !J.chained
-                                     : J.out_tup != nullptr || J.mode == JM_MARK || J.chained;
+                                     : J.out_tup != nullptr || J.mode == JM_MARK || (J.chained && !J.chain_bm);
     J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
     if (J.ptile == KPT_LARGE * PROBE_TILE) *long_tiles = true;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
@@ -953,6 +957,11 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
   const int64_t h0 = hprof ? now_ns() : 0;
   bool long_tiles;
+  if (chq && !chain_fused())  // candidates for the probe's own test of the first later include (layout_jobs)
+    for (size_t j = 0; j < jobs.size(); j++) {
+      const ChainQ& Cq = (*chq)[(size_t)owner[j]];
+      jobs[j].chain_bm = plans[(size_t)owner[j]].chain && Cq.pos0 == 0 && Cq.ninc >= 1 ? Cq.l[0].bm : nullptr;
+    }
   layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   const int64_t h1 = hprof ? now_ns() : 0;
@@ -1011,8 +1020,11 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     for (int j = 0; j < nj; j++) {  // (fused: a probe job's tiles test their matches inside k_probe)
       const JoinQ& J = jobs[(size_t)j];
       if (!plans[(size_t)owner[(size_t)j]].chain || J.ntiles <= 0 || (chain_fused() && J.algo != JA_MERGE)) continue;
-      const double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
-                              (double)J.ntiles;
+      double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
+                        (double)J.ntiles;
+      const ChainQ& Cq = (*chq)[(size_t)owner[(size_t)j]];
+      if (J.chain_bm)  // the probe already thinned the matches by the first later include
+        per_tile *= std::min(1.0, (double)Cq.l[0].n / (double)std::max<int64_t>(1, ctx->nurls));
       const int G = (int)std::max(1.0, std::min((double)CHAIN_GMAX, 640.0 / std::max(1.0, per_tile)));
       for (int64_t t = 0; t < J.ntiles; t += G)
         cgrp.push_back(make_int2((int32_t)(tile_base[(size_t)j] + t), (int32_t)std::min<int64_t>(G, J.ntiles - t)));
@@ -1037,6 +1049,11 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       ChainQ C = (*chq)[(size_t)pq];
       C.level = d_mout + nj + (int64_t)j * CHAIN_LVL;
       for (int l = 0; l < CHAIN_MAXI; l++) C.tup[l] = l < C.npos ? d_tup[l] : nullptr;
+      // a bitmap probe tests the first later include list itself when that list
+      // has a bitmap (no selection before it): only its survivors reach k_chain
+      C.pre = J.chain_bm != nullptr ? 1 : 0;  // (layout_jobs kept it for bitmap probes only)
+      J.chain_tup0 = C.pre ? C.tup[0] : nullptr;
+      J.chain_fill = C.pre && C.ninc == 1 ? 2 : 0;
       J.chain = d_cq + (int64_t)cq.size();
       cq.push_back(C);
     }

@@ -136,6 +136,8 @@ struct ChainQ {
   int32_t pos0, npos;        // the include tests whose row is kept: [pos0, pos0 + npos) (lists 2..t-1)
   int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
   int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
+  int32_t pre;               // leading include tests done by the first step's probe (JoinQ::chain_bm): 0 or 1
+  int32_t pad_;
 };
 
 struct JoinQ {
@@ -163,6 +165,14 @@ struct JoinQ {
   // of their bounds min(na, nb + 1); probe tiles: ptile per tile)
   int64_t pair_base;
   const ChainQ* chain;  // chained fold (k_chain, k_compact<true>) or nullptr
+  // ChainQ::pre = 1: the first later include list's url-id bitmap, tested by the
+  // bitmap probe on its hits before they are written (its rows into chain_tup0,
+  // the tile's first two level counts into tile_lvl); chain_fill: level counts
+  // 2 and 3 that repeat count 1 (no second later include)
+  const uint64_t* chain_bm;
+  int32_t* chain_tup0;
+  int32_t chain_fill;
+  int32_t pad2_;
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A

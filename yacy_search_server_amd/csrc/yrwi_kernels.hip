@@ -888,7 +888,7 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
                                                 uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
                                                 int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64,
                                                 uint16_t* sLoc = nullptr, uint32_t* sPos = nullptr,
-                                                int64_t* src_out = nullptr) {
+                                                int64_t* src_out = nullptr, int32_t* tile_lvl = nullptr) {
   // url-id bitmap of the large list: one 16-B load per key gives membership and,
   // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
   // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
@@ -935,6 +935,31 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
     }
   }
   if (mark) return 0;
+  // a chained job's first later include list with a bitmap (JoinQ::chain_bm):
+  // tested here on the hits, in registers, so that only its survivors are
+  // written (with their rows in it) for k_chain; the tile's counts before and
+  // after it are its first level counts
+  const bool pre = J.chain_bm != nullptr && tile_lvl != nullptr;  // workgroup-uniform
+  int32_t tp[KPT];
+  uint32_t hm0 = hm;
+  if (pre) {
+    const __amdgpu_buffer_rsrc_t r2 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(J.chain_bm), 0, 0x7FFFFFFF, 0x00020000);
+    uint4 E2[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      E2[k] = make_uint4(0, 0, 0, 0);
+      if ((hm >> k) & 1u)
+        E2[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r2, (int)(keys[k] >> 6) * 16, 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint64_t ex2 = (uint64_t)E2[k].y << 32 | E2[k].x;
+      const uint64_t bit = 1ull << (keys[k] & 63u);
+      tp[k] = (int32_t)(E2[k].z + __popcll(ex2 & (bit - 1ull)));  // list positions < 2^31
+      if (!(ex2 & bit)) hm &= ~(1u << k);
+    }
+  }
   // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
   // of four 16-bit per-slot counts gives every hit's place in its slot
   constexpr int NSC = (KPT + 3) / 4;  // 64-bit scans of four slot counts each
@@ -958,6 +983,16 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
     tile_src[b] = src;
     tile_cnt[b] = run;
   }
+  if (pre) {  // the tile's matches and those left after the prefix test
+    uint64_t tot;
+    block_excl_sum256_u64((uint64_t)__popc(hm0) | (uint64_t)__popc(hm) << 32, sScan64, &tot);
+    if (threadIdx.x == 0) {
+      int32_t* lv = tile_lvl + b * CHAIN_LVL;
+      lv[0] = (int32_t)(tot & 0xFFFFFFFFu);
+      lv[1] = (int32_t)(tot >> 32);
+      for (int x = 0; x < J.chain_fill; x++) lv[2 + x] = lv[1];
+    }
+  }
   if (src_out) *src_out = src;
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
@@ -971,6 +1006,7 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
     } else {
       pairs[src + lo] = make_uint2((uint32_t)ia, (uint32_t)ib);
       pair_uid[src + lo] = keys[k];
+      if (pre) stg(J.chain_tup0 + src + lo, tp[k]);
     }
   }
   return run;
@@ -1019,13 +1055,14 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     // cost C2 a wave per SIMD: k_probe 111 -> 119 us)
     // (a chained job's tiles are BM_TILE: layout_jobs)
     if (LONG && !chained && J.ptile == KPT_LARGE * PROBE_TILE) {
+      // (a job whose probe tests a chain list itself has BM_TILE tiles: layout_jobs)
       probe_bitmap<KPT_LARGE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark, sScan64);
       return;
     }
     int64_t src = 0;
     const int32_t cnt = probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src,
                                                            tile_cnt, mark, sScan64, chained ? sLoc : nullptr, sPos,
-                                                           &src);
+                                                           &src, chained ? nullptr : tile_lvl);
     if (CHAIN && chained) {
       __syncthreads();  // the tile's matches in LDS
       chain_lds_tile(J.chain, b, src, cnt, sLoc, sPos, Sm.uid, (b - tile_base[D.job]) * J.ptile, J.small_is_A, pairs,
@@ -1467,6 +1504,7 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
   }
 #endif
   const int ninc = ldg(&C->ninc), nl = ldg(&C->nl), pos0 = ldg(&C->pos0), npos = ldg(&C->npos);
+  const int pre = ldg(&C->pre);  // leading include tests the probe did (their rows in tup0, counts in tile_lvl)
   int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
   int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
   int32_t n1 = 0, n2 = 0, n3 = 0, nsurv = 0;  // live after include tests 1, 2, 3; survivors
@@ -1493,11 +1531,13 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
         const int64_t slot = sSrc[a] + (i - sOff[a]);
         key[k] = ldg(pair_uid + slot);
         pr[k] = ldg(reinterpret_cast<const uint2*>(pairs) + slot);
+        if (pre) pos[0][k] = ldg(tup0 + slot);
         alive |= 1u << k;
       }
     }
     uint32_t after1, after2, after3;
-    alive = chain_tests<CHAIN_KPT>(sCL, ninc, nl, pos0, sCR, key, alive, pos, after1, after2, after3, sL);
+    alive = chain_tests<CHAIN_KPT>(sCL + pre, ninc - pre, nl - pre, pos0 - pre, sCR + pre, key, alive, pos, after1,
+                                   after2, after3, sL);
     if (tid < n) sCnt[tid] = 0;
     __syncthreads();
 #pragma unroll
@@ -1551,10 +1591,15 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
   if (tid < n) {
     tile_cnt[G.x + tid] = sRun[tid];
     int32_t* lv = tile_lvl + (G.x + tid) * CHAIN_LVL;
-    lv[0] = tid == 0 ? M : 0;
-    lv[1] = tid == 0 ? n1 : 0;
-    lv[2] = tid == 0 ? n2 : 0;
-    lv[3] = tid == 0 ? n3 : 0;
+    if (!pre) {
+      lv[0] = tid == 0 ? M : 0;
+      lv[1] = tid == 0 ? n1 : 0;
+      lv[2] = tid == 0 ? n2 : 0;
+      lv[3] = tid == 0 ? n3 : 0;
+    } else if (ninc >= 2) {  // the probe wrote counts 0 and 1 per tile; this group's tests start at include 2
+      lv[2] = tid == 0 ? n1 : 0;
+      lv[3] = tid == 0 ? n2 : 0;
+    }
     lv[4] = tid == 0 ? nsurv : 0;
   }
 }
