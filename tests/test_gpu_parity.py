@@ -563,14 +563,18 @@ def test_null_stats_production_path(corpus):
         assert got == [(h, s) for h, s, _ in orc.search(d, q.include, q.exclude, now_ms=NOW, k=q.k)]
 
 
-@pytest.mark.parametrize("chain", ["1", "0"], ids=["chained", "stepwise"])
+@pytest.mark.parametrize("chain", ["1", "0", "cf"], ids=["chained", "stepwise", "count_first"])
 def test_chained_folds_corpus(corpus, chain, monkeypatch):
     """Chained folds (ChainQ: one join step, then k_chain tests each match against
     the later include lists and the exclusion lists) and the step-by-step fold
     (YRWI_NO_CHAIN=1): 2-4 include terms with 0-2 excluded terms, plus quoted
     queries (maxDistance: never chained); results equal the oracle's, tie-breaks
-    included."""
-    monkeypatch.setenv("YRWI_NO_CHAIN", "0" if chain == "1" else "1")
+    included.  count_first (YRWI_CHAIN_CF=2): every 3-term chained fold counts
+    list 0 x list 1 apart and chains its survivors from list 2 (ChainQ::perm) --
+    in the benchmarks only folds whose list 2 is the smallest, which these small
+    lists (no int-wrapped J2 keys) never produce."""
+    monkeypatch.setenv("YRWI_NO_CHAIN", "1" if chain == "0" else "0")
+    monkeypatch.setenv("YRWI_CHAIN_CF", "2" if chain == "cf" else "1")
     cfg, idx, ix = corpus
     d = idx.as_dict()
     qs = synth.queries(cfg, 40, 2, 4, 2, qseed=2024) + synth.queries(cfg, 20, 3, 4, 0, qseed=2025)
@@ -585,13 +589,15 @@ def test_chained_folds_corpus(corpus, chain, monkeypatch):
                               orc.term_search(d, q.include, q.exclude, q.max_distance, NOW))
 
 
-@pytest.mark.parametrize("bm", ["64", "0"], ids=["bitmaps", "no_bitmaps"])
-def test_chained_folds_long_lists(long_lists, bm, monkeypatch):
+@pytest.mark.parametrize("bm,cf", [("64", "1"), ("0", "1"), ("64", "2"), ("0", "2")],
+                         ids=["bitmaps", "no_bitmaps", "bitmaps_count_first", "no_bitmaps_count_first"])
+def test_chained_folds_long_lists(long_lists, bm, cf, monkeypatch):
     """Chained folds over C2's eight longest lists: with url-id bitmaps every later
     list is tested by one bitmap word per match; without (YRWI_BM_DIV=0) by the
     list's ids staged around the tile's range in LDS, or -- ranges longer than the
     LDS stage -- through the line heads (k_chain_part / k_chain)."""
     monkeypatch.setenv("YRWI_BM_DIV", bm)
+    monkeypatch.setenv("YRWI_CHAIN_CF", cf)
     cfg, df, big, idx, _ = long_lists
     ix = RWIIndex(0)
     try:

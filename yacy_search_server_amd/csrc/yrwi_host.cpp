@@ -855,10 +855,11 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
     // (a fused chained job's tiles keep their matches in LDS for the chain tests:
     // BM_TILE, whose registers leave room for them)
-    // A chained job whose first later include list has a bitmap (J.chain_bm, set by
-    // the caller) tests it inside its bitmap probe, on BM_TILE tiles: the long
-    // tiles' registers leave no room for it.  Otherwise no such test.
-    if (!bm || J.algo == JA_MERGE) J.chain_bm = nullptr;
+    // A chained probe job whose first later include list has a bitmap (J.chain_bm,
+    // set by the caller) tests it inside k_probe -- a bitmap probe on BM_TILE
+    // tiles (the long tiles' registers leave no room for it), a range probe on its
+    // usual tiles; merge jobs leave it to k_chain.
+    if (J.algo == JA_MERGE) J.chain_bm = nullptr;
     const bool light = chain_fused() ? (J.out_tup != nullptr || J.mode == JM_MARK) && !J.chained
                                      : J.out_tup != nullptr || J.mode == JM_MARK || (J.chained && !J.chain_bm);
     J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
@@ -960,7 +961,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (chq && !chain_fused())  // candidates for the probe's own test of the first later include (layout_jobs)
     for (size_t j = 0; j < jobs.size(); j++) {
       const ChainQ& Cq = (*chq)[(size_t)owner[j]];
-      jobs[j].chain_bm = plans[(size_t)owner[j]].chain && Cq.pos0 == 0 && Cq.ninc >= 1 ? Cq.l[0].bm : nullptr;
+      jobs[j].chain_bm = jobs[j].chained && Cq.pos0 == 0 && Cq.ninc >= 1 ? Cq.l[0].bm : nullptr;
     }
   layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
@@ -975,7 +976,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
   bool chain = false;
   if (chq)
-    for (int j = 0; j < nj; j++) chain |= plans[(size_t)owner[(size_t)j]].chain;
+    for (int j = 0; j < nj; j++) chain |= jobs[(size_t)j].chained != 0;
   // joined sizes (and chained jobs' level counts) land in pinned host memory:
   // k_scan_tiles writes them through its device address (no copy engine), the host
   // reads them after the step's sync
@@ -991,7 +992,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     JoinQ& J = jobs[(size_t)j];
     J.m_out = d_mout + j;
     J.pair_base = npairs;
-    npairs += std::min(J.A.n, J.B.n) + (J.algo == JA_MERGE ? J.ntiles : 0);
+    if (!J.count_only) npairs += std::min(J.A.n, J.B.n) + (J.algo == JA_MERGE ? J.ntiles : 0);
   }
   JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
   int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
@@ -1019,7 +1020,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     // per job), so a workgroup tests close to one round of 768
     for (int j = 0; j < nj; j++) {  // (fused: a probe job's tiles test their matches inside k_probe)
       const JoinQ& J = jobs[(size_t)j];
-      if (!plans[(size_t)owner[(size_t)j]].chain || J.ntiles <= 0 || (chain_fused() && J.algo != JA_MERGE)) continue;
+      if (!J.chained || J.ntiles <= 0 || (chain_fused() && J.algo != JA_MERGE)) continue;
       double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
                         (double)J.ntiles;
       const ChainQ& Cq = (*chq)[(size_t)owner[(size_t)j]];
@@ -1038,14 +1039,14 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     if (!d_lvl || !d_crange || !d_cgrp || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
     int maxi = 0;
     for (int j = 0; j < nj; j++)
-      if (plans[(size_t)owner[(size_t)j]].chain) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].npos);
+      if (jobs[(size_t)j].chained) maxi = std::max(maxi, (*chq)[(size_t)owner[(size_t)j]].npos);
     int32_t* d_tup[CHAIN_MAXI] = {nullptr, nullptr};  // rows in the later include lists, indexed like d_pairs
     for (int l = 0; l < maxi; l++)
       if (!(d_tup[l] = arena_alloc<int32_t>(ctx, npairs))) return ctx->fail(YRWI_E_NOMEM, "arena");
     for (int j = 0; j < nj; j++) {
       JoinQ& J = jobs[(size_t)j];
       const int pq = owner[(size_t)j];
-      if (!plans[(size_t)pq].chain) continue;
+      if (!J.chained) continue;  // (a count-first fold's counted job is not)
       ChainQ C = (*chq)[(size_t)pq];
       C.level = d_mout + nj + (int64_t)j * CHAIN_LVL;
       for (int l = 0; l < CHAIN_MAXI; l++) C.tup[l] = l < C.npos ? d_tup[l] : nullptr;
@@ -1102,6 +1103,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     for (int j = 0; j < nj; j++) {
       const JoinQ& J = jobs[(size_t)j];
       const int64_t atw = J.A.tup ? J.A.tw : 0;
+      if (J.count_only) continue;
       if (J.chain) {
         const int64_t t = 2 + (*chq)[(size_t)owner[(size_t)j]].npos;
         st->bytes_compact += mh[(size_t)j] * (12 + 4 * (t - 2) + 32 + 24 * (t - 1) + 36);
@@ -1124,6 +1126,10 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   for (int j = 0; j < nj; j++) {
     Plan& P = plans[(size_t)owner[(size_t)j]];
     const JoinQ& J = jobs[(size_t)j];
+    if (J.count_only) {
+      P.cf_count = mh[(size_t)j];
+      continue;
+    }
     P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
                    J.out_tup ? J.out_tw : 0};
   }
@@ -1220,6 +1226,9 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
   // so every shard takes it alike.  YRWI_NO_CHAIN=1: the step-by-step fold.
   const char* nc = getenv("YRWI_NO_CHAIN");  // read per call: tests compare both paths in one process
   const bool chain_on = !(nc && atoi(nc));
+  // YRWI_CHAIN_CF: 0 never count-first, 2 every 3-term chained fold (tests), default 1 (list 2 the smallest)
+  const char* cfe = getenv("YRWI_CHAIN_CF");
+  const int cf_mode = cfe ? atoi(cfe) : 1;
   std::vector<ChainQ> chq(nq);
   bool any_chain = false;
   // url selections (resolve_selections): their ids for this pass's kernels; a
@@ -1271,12 +1280,21 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     ChainQ& C = chq[qi];
     std::memset(&C, 0, sizeof(C));
     C.nl = 0;
+    // Count-first (t = 3 whose list 2 is the smallest -- J2's int-wrapped keys put
+    // big lists first: C3's 52 such queries make 85 of its 98 M first-step
+    // matches): list 0 x list 1 is only counted (its size is step 1's dispatch),
+    // the survivors are chained from list 2 (probing list 0, then testing list 1)
+    P.cf = cf_mode != 0 && t == 3 && !ns &&
+           (cf_mode == 2 || (P.seq_ng[2] < P.seq_ng[0] && P.seq_ng[2] < P.seq_ng[1]));
     if (ns)  // the selection first: its ids, no heads, no bitmap
       C.l[C.nl++] = ChainList{dsel[qi], nullptr, nullptr, (int64_t)P.sel_uid.size()};
-    for (int l = 0; l < ni; l++) C.l[C.nl++] = chain_list(P.seq[(size_t)l + 2]);
+    if (P.cf) C.l[C.nl++] = chain_list(P.seq[1]);
+    else
+      for (int l = 0; l < ni; l++) C.l[C.nl++] = chain_list(P.seq[(size_t)l + 2]);
     C.ninc = C.nl;
     C.pos0 = ns;
     C.npos = ni;
+    C.perm = P.cf ? 1 : 0;
     for (const ListRec* E : P.excl) C.l[C.nl++] = chain_list(E);  // this shard's lists of the exclusion terms
     if (st)
       for (const ListRec* E : P.excl) st->bytes_alg += 12 * E->n;
@@ -1315,6 +1333,22 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.now_ms = P.now_ms;
       J.chained = P.chain ? 1 : 0;
       P.step_mode[s] = J.mode;
+      if (P.cf) {  // count-first: list 0 x list 1 counted, the chained job probes list 2 into list 0
+        JoinQ K = J;
+        K.chained = 0;
+        K.count_only = 1;
+        if (st) st->bytes_alg += step_bytes(K.mode, K.A.n, K.B.n);
+        jobs.push_back(K);
+        owner.push_back((int)qi);
+        const DList L2 = P.seq[2]->dl();
+        if (L2.n == 0) {  // nothing of this shard survives (its count still goes in)
+          P.cont = DList{nullptr, nullptr, nullptr, 0};
+          continue;
+        }
+        J.A = L2;
+        J.B = P.cont;
+        J.mode = JM_ENUM;  // (the chained job's records are folded by fold_chain with the fold's modes)
+      }
       int64_t cap = std::min(J.A.n, J.B.n);
       // a chained job's output is allocated once k_chain has counted its survivors
       // (run_join_jobs): its capacity bound min(nA, nB) is far above them
@@ -1380,11 +1414,14 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       for (size_t qi = 0; qi < nq; qi++)
         if (plans[qi].chain && steps(qi, 0)) cqs.push_back((int)qi);
       std::vector<int> job_of(nq, -1);
-      for (size_t j = 0; j < jobs.size(); j++) job_of[(size_t)owner[j]] = (int)j;
+      for (size_t j = 0; j < jobs.size(); j++)
+        if (!jobs[j].count_only) job_of[(size_t)owner[j]] = (int)j;
       std::vector<int64_t> v(cqs.size() * 2, 0);
       for (size_t k = 0; k < cqs.size(); k++) {
         const int j = job_of[(size_t)cqs[k]];
-        if (j >= 0 && pend.active) {  // the intersection sizes after the selection (if any) and include 2
+        if (plans[(size_t)cqs[k]].cf) {  // count-first: |list 0 x list 1| counted apart (t = 3: no second)
+          v[2 * k] = plans[(size_t)cqs[k]].cf_count;
+        } else if (j >= 0 && pend.active) {  // the intersection sizes after the selection (if any) and include 2
           const int o = chq[(size_t)cqs[k]].pos0;
           v[2 * k] = pend.level[(size_t)j][(size_t)o];
           v[2 * k + 1] = pend.level[(size_t)j][(size_t)o + 1];

@@ -182,6 +182,10 @@ struct Plan {
   // runtime container (a deferred one between the steps of a multi-term fold)
   DList cont{nullptr, nullptr, nullptr, 0};
   int32_t step_mode[YRWI_MAX_TERMS] = {0};  // JoinMode of every fold step taken
+  // count-first chained fold (t = 3, list 2 the smallest): list 0 x list 1 only
+  // counted (its size decides step 1's dispatch), the survivors chained from list 2
+  bool cf = false;
+  int64_t cf_count = 0;  // this shard's |list 0 x list 1|
   uint8_t* removed = nullptr;
   int nexcl_g = 0;      // exclusion terms in effect (J1 on global sizes; excl holds this shard's lists of them)
   bool chain = false;   // chained fold (ChainQ, yrwi_internal.h): one join step, k_chain does the rest

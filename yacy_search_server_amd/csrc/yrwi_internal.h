@@ -137,7 +137,7 @@ struct ChainQ {
   int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
   int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
   int32_t pre;               // leading include tests done by the first step's probe (JoinQ::chain_bm): 0 or 1
-  int32_t pad_;
+  int32_t perm;              // count-first fold (t = 3): pairs are (row in list 2, row in list 0), tup[0] list 1
 };
 
 struct JoinQ {
@@ -172,7 +172,7 @@ struct JoinQ {
   const uint64_t* chain_bm;
   int32_t* chain_tup0;
   int32_t chain_fill;
-  int32_t pad2_;
+  int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A

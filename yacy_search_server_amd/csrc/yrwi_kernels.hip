@@ -631,6 +631,7 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
       int32_t tot;
       int32_t off = block_excl_sum256(__popc(mbits), sScan, &tot);
       if (threadIdx.x == 0) tile_cnt[b] = tot;
+      if (jobs[jc].count_only) mbits = 0;  // counted only (workgroup-uniform)
       uint2* out = pairs + src;
       uint32_t* outu = pair_uid + src;
       for (uint32_t m = mbits; m; m &= m - 1) {
@@ -1000,7 +1001,8 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
     const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
     const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
     const int32_t lo = base[k] + (int32_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-    if (sLoc) {  // a chained job's tile: its matches stay in LDS for the chain tests
+    if (J.count_only) {  // counted only
+    } else if (sLoc) {  // a chained job's tile: its matches stay in LDS for the chain tests
       sLoc[lo] = (uint16_t)(k * PROBE_TILE + (int)threadIdx.x);
       sPos[lo] = (uint32_t)jls[k];
     } else {
@@ -1111,12 +1113,37 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     if (hit) stg(J.removed + ia, (uint8_t)1);
     return;
   }
+  // a chained job's first later include list with a bitmap: tested here (as in
+  // probe_bitmap), only its survivors written, the tile's first two level counts
+  const bool pre = !CHAIN && J.chain_bm != nullptr && tile_lvl != nullptr;  // workgroup-uniform
+  const bool hit0 = hit;
+  int32_t tp = 0;
+  if (pre && hit) {
+    const __amdgpu_buffer_rsrc_t r2 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(J.chain_bm), 0, 0x7FFFFFFF, 0x00020000);
+    const uint4 E2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r2, (int)(key >> 6) * 16, 0, 0));
+    const uint64_t ex2 = (uint64_t)E2.y << 32 | E2.x;
+    const uint64_t bit = 1ull << (key & 63u);
+    tp = (int32_t)(E2.z + __popcll(ex2 & (bit - 1ull)));
+    if (!(ex2 & bit)) hit = false;
+  }
   int32_t tot;
   const int32_t off = block_excl_sum256(hit ? 1 : 0, sScan, &tot);
   const int64_t src = J.pair_base + s0;  // PROBE_TILE pair slots per tile: the job's run is min(nA, nB) long
   if (threadIdx.x == 0) {
     tile_src[b] = src;
     tile_cnt[b] = tot;
+  }
+  if (pre) {
+    int32_t tot0;
+    block_excl_sum256(hit0 ? 1 : 0, sScan, &tot0);
+    if (threadIdx.x == 0) {
+      int32_t* lv = tile_lvl + b * CHAIN_LVL;
+      lv[0] = tot0;
+      lv[1] = tot;
+      for (int x = 0; x < J.chain_fill; x++) lv[2 + x] = tot;
+    }
+    if (hit) stg(J.chain_tup0 + src + off, tp);
   }
   if (CHAIN && chained) {  // the matches in LDS, then the chain tests
     if (hit) {
@@ -1128,7 +1155,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
                    prange + t * CHAIN_MAXL, sL, sScan64);
     return;
   }
-  if (hit) {
+  if (hit && !J.count_only) {
     pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
     pair_uid[src + off] = key;
   }
@@ -1802,6 +1829,7 @@ struct CompactJob {
   int32_t otw;
   int32_t bw;            // words per posting of bf (FEAT_WORDS, or 2 for an enumeration's DList::j5)
   int32_t ctw;           // chained job: lists of the fold (0: not chained)
+  int32_t cperm;         // count-first fold: pair = (row in list 2, row in list 0), ctup0 = row in list 1
   const int32_t* ctup0;  // chained job: rows in the fold's lists 2 and 3 (ChainQ::tup)
   const int32_t* ctup1;
 };
@@ -1876,6 +1904,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
       }
       c = tile_cnt[t];
+      if (c && jobs[j].count_only) c = 0;  // a count-first fold's counted join: nothing to compact
       if (c) {
         const JoinQ& J = jobs[j];
         CompactJob& X = sJ[threadIdx.x];
@@ -1894,9 +1923,11 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         X.otw = J.out_tup ? J.out_tw : 0;
         X.fold = J.fold;
         X.ctw = 0;
+        X.cperm = 0;
         if (CHAIN && J.chain) {
           const int ni = ldg(&J.chain->npos);
           X.ctw = 2 + ni;
+          X.cperm = ldg(&J.chain->perm);
           X.ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
           X.ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
         }
@@ -1962,8 +1993,10 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       if (tl[u] < 0) continue;
       const CompactJob& X = sJ[tl[u]];
       if (CHAIN && X.ctw) {
-        A[u] = fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0,
-                          X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
+        const int32_t t2 = X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0;
+        A[u] = X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x, 0, X.ctw, X.now_ms)
+                       : fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2,
+                                    X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
         continue;
       }
       if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
