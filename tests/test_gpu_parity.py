@@ -569,7 +569,7 @@ def test_chained_folds_corpus(corpus, chain, monkeypatch):
     the later include lists and the exclusion lists) and the step-by-step fold
     (YRWI_NO_CHAIN=1): 2-4 include terms with 0-2 excluded terms, plus quoted
     queries (maxDistance: never chained); results equal the oracle's, tie-breaks
-    included.  count_first (YRWI_CHAIN_CF=2): every 3-term chained fold counts
+    included.  count_first (YRWI_CHAIN_CF=2): every 3- and 4-term chained fold counts
     list 0 x list 1 apart and chains its survivors from list 2 (ChainQ::perm) --
     in the benchmarks only folds whose list 2 is the smallest, which these small
     lists (no int-wrapped J2 keys) never produce."""

@@ -789,6 +789,7 @@ static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
 static int64_t loaded_bytes(const JoinQ& J) {
   const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
   if (J.algo == JA_MERGE) return 4 * (ns + nl);
+  if (J.algo == JA_BMAND) return 16 * J.bm_words;  // the bits of both bitmaps (8 B of every 16-B word)
   const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
   return bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
 }
@@ -839,6 +840,17 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
     JoinQ& J = jobs[i];
+    // a counted-only join of two lists with bitmaps: popcounts of their words
+    if (J.count_only && J.A.bm && J.B.bm && nurls > 0) {
+      J.algo = JA_BMAND;
+      J.small_is_A = 1;
+      J.ptile = BMAND_WORDS;
+      J.bm_words = (nurls + 63) / 64;
+      J.ntiles = ceil_div(J.bm_words, BMAND_WORDS);
+      J.chain_bm = nullptr;
+      order[i] = i;
+      continue;
+    }
     // a sparse list's bitmap (below 1/64 of the url ids: k_chain's tests and the
     // selections use it) does not take a join: its probes search the list, where
     // a tile's staged range costs less than a bitmap line per key
@@ -1284,13 +1296,18 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     // big lists first: C3's 52 such queries make 85 of its 98 M first-step
     // matches): list 0 x list 1 is only counted (its size is step 1's dispatch),
     // the survivors are chained from list 2 (probing list 0, then testing list 1)
-    P.cf = cf_mode != 0 && t == 3 && !ns &&
+    // (t = 4 too: the chain's first test, list 1, leaves |list 0..2| -- step 2's
+    // dispatch -- and list 3 follows)
+    P.cf = cf_mode != 0 && (t == 3 || t == 4) && !ns &&
            (cf_mode == 2 || (P.seq_ng[2] < P.seq_ng[0] && P.seq_ng[2] < P.seq_ng[1]));
     if (ns)  // the selection first: its ids, no heads, no bitmap
       C.l[C.nl++] = ChainList{dsel[qi], nullptr, nullptr, (int64_t)P.sel_uid.size()};
-    if (P.cf) C.l[C.nl++] = chain_list(P.seq[1]);
-    else
+    if (P.cf) {
+      C.l[C.nl++] = chain_list(P.seq[1]);
+      if (t == 4) C.l[C.nl++] = chain_list(P.seq[3]);
+    } else {
       for (int l = 0; l < ni; l++) C.l[C.nl++] = chain_list(P.seq[(size_t)l + 2]);
+    }
     C.ninc = C.nl;
     C.pos0 = ns;
     C.npos = ni;
@@ -1419,8 +1436,9 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       std::vector<int64_t> v(cqs.size() * 2, 0);
       for (size_t k = 0; k < cqs.size(); k++) {
         const int j = job_of[(size_t)cqs[k]];
-        if (plans[(size_t)cqs[k]].cf) {  // count-first: |list 0 x list 1| counted apart (t = 3: no second)
+        if (plans[(size_t)cqs[k]].cf) {  // count-first: |list 0 x list 1| counted apart, then |list 0..2|
           v[2 * k] = plans[(size_t)cqs[k]].cf_count;
+          if (j >= 0 && pend.active) v[2 * k + 1] = pend.level[(size_t)j][1];
         } else if (j >= 0 && pend.active) {  // the intersection sizes after the selection (if any) and include 2
           const int o = chq[(size_t)cqs[k]].pos0;
           v[2 * k] = pend.level[(size_t)j][(size_t)o];

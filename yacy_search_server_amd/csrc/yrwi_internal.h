@@ -89,7 +89,11 @@ enum JoinMode : int32_t {
 // Intersection algorithm of a job (independent of the reference's feature rule):
 // merge-path tiles for comparable sizes, per-element probing of the large list
 // for skewed ones (the galloping bound of BASELINE.md §4).
-enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1 };
+// JA_BMAND: a counted-only join of two lists that both have url-id bitmaps:
+// popcount(bits A & bits B) over ranges of bitmap words (tiles of BMAND_WORDS),
+// in place of probing one list's ids into the other (k_probe)
+enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2 };
+constexpr int BMAND_WORDS = 4096;
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
 #ifndef YRWI_BM_TILE
 #define YRWI_BM_TILE 1024
@@ -137,7 +141,7 @@ struct ChainQ {
   int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
   int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
   int32_t pre;               // leading include tests done by the first step's probe (JoinQ::chain_bm): 0 or 1
-  int32_t perm;              // count-first fold (t = 3): pairs are (row in list 2, row in list 0), tup[0] list 1
+  int32_t perm;              // count-first fold: pairs are (row in list 2, row in list 0), tup[0] list 1, tup[1] list 3
 };
 
 struct JoinQ {
@@ -173,6 +177,7 @@ struct JoinQ {
   int32_t* chain_tup0;
   int32_t chain_fill;
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
+  int64_t bm_words;    // JA_BMAND: bitmap words of the url-id space
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A

@@ -837,6 +837,18 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
   const JoinQ& J = jobs[j];
+  if (J.algo == JA_BMAND) {  // a range of bitmap words: no ids to read, no range
+    const uint32_t id0 = (uint32_t)min((tile0 + t - tile_base[j]) * (int64_t)J.ptile * 64, (int64_t)0xFFFFFFFF);
+    if (tile_key) tile_key[tile0 + t] = id0;
+    if (tile_job) tile_job[tile0 + t] = j;
+    if (probe_key) probe_key[t] = id0 >> probe_shift;
+    ProbeDesc D;
+    D.job = j;
+    D.pad = 0;
+    D.lo = D.hi = 0;
+    pdesc[t] = D;
+    return;
+  }
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const int64_t s0 = (tile0 + t - tile_base[j]) * J.ptile;
@@ -1049,6 +1061,20 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const int64_t b = tile0 + t;
   const ProbeDesc D = pdesc[t];
   const JoinQ& J = jobs[D.job];
+  if (!MARK && J.algo == JA_BMAND) {  // workgroup-uniform: |A x B| from the bits of both bitmaps
+    const int64_t w0 = (b - tile_base[D.job]) * (int64_t)J.ptile;
+    const int64_t w1 = w0 + J.ptile < J.bm_words ? w0 + J.ptile : J.bm_words;
+    int32_t c = 0;
+    for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
+      c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w));
+    int32_t tot;
+    block_excl_sum256(c, sScan, &tot);
+    if (threadIdx.x == 0) {
+      tile_src[b] = J.pair_base;
+      tile_cnt[b] = tot;
+    }
+    return;
+  }
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
   const bool chained = CHAIN && J.chain != nullptr;  // workgroup-uniform
@@ -1829,7 +1855,7 @@ struct CompactJob {
   int32_t otw;
   int32_t bw;            // words per posting of bf (FEAT_WORDS, or 2 for an enumeration's DList::j5)
   int32_t ctw;           // chained job: lists of the fold (0: not chained)
-  int32_t cperm;         // count-first fold: pair = (row in list 2, row in list 0), ctup0 = row in list 1
+  int32_t cperm;         // count-first fold: pair = (row in list 2, row in list 0), ctup0 / ctup1 = rows in lists 1 / 3
   const int32_t* ctup0;  // chained job: rows in the fold's lists 2 and 3 (ChainQ::tup)
   const int32_t* ctup1;
 };
@@ -1994,7 +2020,8 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       const CompactJob& X = sJ[tl[u]];
       if (CHAIN && X.ctw) {
         const int32_t t2 = X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0;
-        A[u] = X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x, 0, X.ctw, X.now_ms)
+        A[u] = X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x,
+                                    X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms)
                        : fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2,
                                     X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
         continue;
