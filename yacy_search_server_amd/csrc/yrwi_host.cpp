@@ -2020,14 +2020,18 @@ static int64_t scratch_estimate(const Plan& P) {
   return sum / 64 + (48 * (int64_t)(P.seq.size() - 1) + 48) * nmin + 65536;
 }
 
-// Scratch budget of one pass (YRWI_SCRATCH_GB, default 32 GiB per lane).  A
+// Scratch budget of one pass (YRWI_SCRATCH_GB per lane, default 192 GiB / lanes).  A
 // batch whose queries need more runs as consecutive passes over query ranges;
 // sharded contexts never split (every rank must issue the same collectives, and
 // the estimate depends on the local shard), so they keep one pass per batch.
 static int64_t scratch_budget(const Lane* L) {
   if (L->sharded) return INT64_MAX;
-  const char* e = getenv("YRWI_SCRATCH_GB");  // per lane; default 128 GiB shared by the lanes
-  const double gb = e ? atof(e) : 128.0 / (double)std::max(1, L->nlanes);
+  // per lane; default 192 GiB shared by the lanes (C4: 16 GiB per lane ran 7 passes
+  // a batch at 10.3 ms/step, 24 GiB 9.86, 32 GiB 9.73 -- the passes' fixed
+  // kernels and syncs; the arenas stayed inside the 288 GB beside the 1 B-posting
+  // index: profiles/r04_scratch_c4.txt)
+  const char* e = getenv("YRWI_SCRATCH_GB");
+  const double gb = e ? atof(e) : 192.0 / (double)std::max(1, L->nlanes);
   return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
 }
 
