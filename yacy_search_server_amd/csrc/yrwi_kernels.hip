@@ -2255,8 +2255,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
         const uint64_t key = key_host36(khi, klo) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
-          const unsigned long long prev =
-              atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
+          // a plain read first: a key once set never changes, and most postings'
+          // hosts are already in (Zipf): one device atomic instead of two
+          unsigned long long prev = Q.hkeys[slot];
+          if (prev != key) prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
           if (prev == 0ull || prev == key) {
             const uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
             hmax = max(hmax, (int32_t)cnt);  // the last increment of every host sees its final count
