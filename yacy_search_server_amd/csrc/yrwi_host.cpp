@@ -1139,7 +1139,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     Plan& P = plans[(size_t)owner[(size_t)j]];
     const JoinQ& J = jobs[(size_t)j];
     if (J.count_only) {
-      P.cf_count = mh[(size_t)j];
+      (J.bm3 ? P.cf_count2 : P.cf_count) = mh[(size_t)j];
       continue;
     }
     P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
@@ -1298,20 +1298,25 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     // the survivors are chained from list 2 (probing list 0, then testing list 1)
     // (t = 4 too: the chain's first test, list 1, leaves |list 0..2| -- step 2's
     // dispatch -- and list 3 follows)
-    P.cf = cf_mode != 0 && (t == 3 || t == 4) && !ns &&
+    P.cf3 = cf_mode != 0 && t == 4 && !ns && !ctx->sharded && P.seq[0]->bm && P.seq[1]->bm && P.seq[2]->bm &&
+            (cf_mode == 2 || (P.seq_ng[3] < P.seq_ng[0] && P.seq_ng[3] < P.seq_ng[1] && P.seq_ng[3] < P.seq_ng[2]));
+    P.cf = !P.cf3 && cf_mode != 0 && (t == 3 || t == 4) && !ns &&
            (cf_mode == 2 || (P.seq_ng[2] < P.seq_ng[0] && P.seq_ng[2] < P.seq_ng[1]));
     if (ns)  // the selection first: its ids, no heads, no bitmap
       C.l[C.nl++] = ChainList{dsel[qi], nullptr, nullptr, (int64_t)P.sel_uid.size()};
     if (P.cf) {
       C.l[C.nl++] = chain_list(P.seq[1]);
       if (t == 4) C.l[C.nl++] = chain_list(P.seq[3]);
+    } else if (P.cf3) {
+      C.l[C.nl++] = chain_list(P.seq[1]);
+      C.l[C.nl++] = chain_list(P.seq[2]);
     } else {
       for (int l = 0; l < ni; l++) C.l[C.nl++] = chain_list(P.seq[(size_t)l + 2]);
     }
     C.ninc = C.nl;
     C.pos0 = ns;
     C.npos = ni;
-    C.perm = P.cf ? 1 : 0;
+    C.perm = P.cf ? 1 : P.cf3 ? 2 : 0;
     for (const ListRec* E : P.excl) C.l[C.nl++] = chain_list(E);  // this shard's lists of the exclusion terms
     if (st)
       for (const ListRec* E : P.excl) st->bytes_alg += 12 * E->n;
@@ -1350,14 +1355,19 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       J.now_ms = P.now_ms;
       J.chained = P.chain ? 1 : 0;
       P.step_mode[s] = J.mode;
-      if (P.cf) {  // count-first: list 0 x list 1 counted, the chained job probes list 2 into list 0
+      if (P.cf || P.cf3) {  // count-first: list 0 x list 1 counted, the chained job probes list 2 (3) into list 0
         JoinQ K = J;
         K.chained = 0;
         K.count_only = 1;
         if (st) st->bytes_alg += step_bytes(K.mode, K.A.n, K.B.n);
         jobs.push_back(K);
         owner.push_back((int)qi);
-        const DList L2 = P.seq[2]->dl();
+        if (P.cf3) {  // and list 0 x list 1 x list 2 (a three-way popcount)
+          K.bm3 = P.seq[2]->bm;
+          jobs.push_back(K);
+          owner.push_back((int)qi);
+        }
+        const DList L2 = P.seq[P.cf3 ? 3 : 2]->dl();
         if (L2.n == 0) {  // nothing of this shard survives (its count still goes in)
           P.cont = DList{nullptr, nullptr, nullptr, 0};
           continue;
@@ -1436,7 +1446,10 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       std::vector<int64_t> v(cqs.size() * 2, 0);
       for (size_t k = 0; k < cqs.size(); k++) {
         const int j = job_of[(size_t)cqs[k]];
-        if (plans[(size_t)cqs[k]].cf) {  // count-first: |list 0 x list 1| counted apart, then |list 0..2|
+        if (plans[(size_t)cqs[k]].cf3) {  // from list 3: both sizes counted apart
+          v[2 * k] = plans[(size_t)cqs[k]].cf_count;
+          v[2 * k + 1] = plans[(size_t)cqs[k]].cf_count2;
+        } else if (plans[(size_t)cqs[k]].cf) {  // count-first: |list 0 x list 1| counted apart, then |list 0..2|
           v[2 * k] = plans[(size_t)cqs[k]].cf_count;
           if (j >= 0 && pend.active) v[2 * k + 1] = pend.level[(size_t)j][1];
         } else if (j >= 0 && pend.active) {  // the intersection sizes after the selection (if any) and include 2

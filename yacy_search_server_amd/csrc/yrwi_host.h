@@ -186,6 +186,11 @@ struct Plan {
   // counted (its size decides step 1's dispatch), the survivors chained from list 2
   bool cf = false;
   int64_t cf_count = 0;  // this shard's |list 0 x list 1|
+  // from list 3 (t = 4, list 3 the smallest, lists 0..2 with bitmaps, one
+  // context): |list 0 x list 1| and |list 0 x list 1 x list 2| both counted as
+  // bitmap popcounts, the survivors chained from list 3
+  bool cf3 = false;
+  int64_t cf_count2 = 0;
   uint8_t* removed = nullptr;
   int nexcl_g = 0;      // exclusion terms in effect (J1 on global sizes; excl holds this shard's lists of them)
   bool chain = false;   // chained fold (ChainQ, yrwi_internal.h): one join step, k_chain does the rest

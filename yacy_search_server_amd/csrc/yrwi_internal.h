@@ -141,7 +141,8 @@ struct ChainQ {
   int32_t* tup[CHAIN_MAXI];  // each survivor's row in include list 2 + i (slot-indexed like the pairs)
   int64_t* level;            // the job's CHAIN_LVL counts (written by k_scan_tiles; pinned host memory)
   int32_t pre;               // leading include tests done by the first step's probe (JoinQ::chain_bm): 0 or 1
-  int32_t perm;              // count-first fold: pairs are (row in list 2, row in list 0), tup[0] list 1, tup[1] list 3
+  int32_t perm;              // count-first fold: 1: pairs (row in list 2, row in list 0), tup[0] list 1, tup[1] list 3;
+                             // 2 (from list 3): pairs (row in list 3, row in list 0), tup[0] list 1, tup[1] list 2
 };
 
 struct JoinQ {
@@ -178,6 +179,7 @@ struct JoinQ {
   int32_t chain_fill;
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
   int64_t bm_words;    // JA_BMAND: bitmap words of the url-id space
+  const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A

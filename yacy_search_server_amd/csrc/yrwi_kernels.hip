@@ -1065,8 +1065,12 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     const int64_t w0 = (b - tile_base[D.job]) * (int64_t)J.ptile;
     const int64_t w1 = w0 + J.ptile < J.bm_words ? w0 + J.ptile : J.bm_words;
     int32_t c = 0;
-    for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
-      c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w));
+    if (J.bm3)
+      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
+        c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w) & ldg(J.bm3 + 2 * w));
+    else
+      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
+        c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w));
     int32_t tot;
     block_excl_sum256(c, sScan, &tot);
     if (threadIdx.x == 0) {
@@ -2020,8 +2024,10 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       const CompactJob& X = sJ[tl[u]];
       if (CHAIN && X.ctw) {
         const int32_t t2 = X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0;
-        A[u] = X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x,
-                                    X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms)
+        A[u] = X.cperm == 2 ? fold_chain(X.fold, (int32_t)pr[u].y, t2, ldg(X.ctup1 + pi[u]), (int32_t)pr[u].x,
+                                         X.ctw, X.now_ms)
+               : X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x,
+                                      X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms)
                        : fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2,
                                     X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
         continue;
@@ -2255,10 +2261,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
         const uint64_t key = key_host36(khi, klo) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
-          // a plain read first: a key once set never changes, and most postings'
-          // hosts are already in (Zipf): one device atomic instead of two
-          unsigned long long prev = Q.hkeys[slot];
-          if (prev != key) prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
+          // (a plain read before the compare-and-swap, to skip it for hosts already
+          // in: k_reduce 99 -> 158 us on C5 custom, the read's round trip first)
+          const unsigned long long prev =
+              atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
           if (prev == 0ull || prev == key) {
             const uint32_t cnt = atomicAdd(&Q.hcnt[slot], 1u) + 1u;
             hmax = max(hmax, (int32_t)cnt);  // the last increment of every host sees its final count
