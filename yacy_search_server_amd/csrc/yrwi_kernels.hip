@@ -1837,8 +1837,11 @@ __device__ __forceinline__ Rec joined_rec(Rec o, uint64_t b0, uint64_t b1, int m
 #ifndef YRWI_COMPACT_TILES
 #define YRWI_COMPACT_TILES 4
 #endif
+// 2 since the chained folds' fold_chain (round 4): compaction 0.307 -> 0.227 ms
+// on C3, 3.02 -> 2.95 on C4, 0.226 -> 0.213 on C2 against 4; 8 matches per
+// thread 0.629 / 4.41 / 0.238 (profiles/r04_compact_sweep.txt).
 #ifndef YRWI_COMPACT_UNROLL
-#define YRWI_COMPACT_UNROLL 4
+#define YRWI_COMPACT_UNROLL 2
 #endif
 constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
 constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
