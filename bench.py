@@ -103,6 +103,40 @@ def launch_ranks(n: int) -> int:
     return next((rc for rc in rcs if rc), 0)
 
 
+# ------------------------------------------------------------------ provenance
+_IDENT = None
+
+
+def source_identity():
+    """Which build this is: `src` = sha1 (12 hex) of libyrwi's sources (csrc/ and
+    include/yrwi.h) -- the same on the GPU box, which has no .git; `head` = the git
+    commit (here) or the REVISION file a post-commit hook leaves in the tree (box).
+    tools/pmc_summary.py stamps profiles with the same pair, so a bench line can
+    say whether its counter profile measured this very build."""
+    global _IDENT
+    if _IDENT is None:
+        import hashlib
+        h = hashlib.sha1()
+        csrc = os.path.join(ROOT, "yacy_search_server_amd", "csrc")
+        files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                       if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile")
+        for p in files + [os.path.join(ROOT, "include", "yrwi.h")]:
+            h.update(os.path.basename(p).encode())
+            with open(p, "rb") as f:
+                h.update(f.read())
+        head = None
+        try:
+            head = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], text=True,
+                                           stderr=subprocess.DEVNULL).strip() or None
+        except (OSError, subprocess.CalledProcessError):
+            pass
+        if head is None and os.path.exists(os.path.join(ROOT, "REVISION")):
+            with open(os.path.join(ROOT, "REVISION")) as f:
+                head = f.read().strip() or None
+        _IDENT = {"head": head, "src": h.hexdigest()[:12]}
+    return _IDENT
+
+
 # ------------------------------------------------------------------- baselines
 def cpu_model() -> str:
     try:
@@ -507,21 +541,27 @@ def kernel_lines(iso, pmc):
         t = t_ns / nl * 1e-9
         if t <= 0:
             continue
-        gbps = alg / nl / t / 1e9
-        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(alg / nl), "achieved": round(gbps, 1),
-             "frac": _frac(gbps)}
+        a = alg / nl
+        kd = pk.get(name, {})
+        traffic = kd.get("hbm_bytes_per_launch")
+        # bytes credited: the SURVEY 8(d) model, capped at the bytes the counters saw
+        # leave L2 (a model above them credits requests L2 / LDS served)
+        cred = min(a, traffic) if traffic else a
+        gbps = cred / t / 1e9
+        e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(a), "credited_bytes": int(cred),
+             "capped_at_traffic": bool(traffic and a > traffic), "achieved": round(gbps, 1), "frac": _frac(gbps)}
         e.update(extra)
         if name == "k_probe" and iso.get("n_probe_dispatches"):
             # every k_probe dispatch, the exclusion steps' too (profiles key those as k_probe_excl)
             e["mean_dispatch_us_all_steps"] = round(iso["t_probe_all_ns"] / iso["n_probe_dispatches"] / 1e3, 2)
-        kd = pk.get(name, {})
-        if kd.get("hbm_bytes_per_launch"):
-            e["traffic"] = kd["hbm_bytes_per_launch"]
-            e["traffic_GBps"] = round(kd["hbm_bytes_per_launch"] / t / 1e9, 1)
+        if traffic:
+            e["traffic"] = traffic
+            e["traffic_GBps"] = round(traffic / t / 1e9, 1)
             tp = kd.get("avg_ns", 0) * 1e-9
             if tp > 0:
                 e["rocprof_mean_launch_us"] = round(tp * 1e6, 2)
-                e["hbm_frac"] = round(kd["hbm_bytes_per_launch"] / tp / 1e9 / HBM_PEAK_GBS, 4)
+                e["frac_rocprof"] = _frac(cred / tp / 1e9)
+                e["hbm_frac"] = round(traffic / tp / 1e9 / HBM_PEAK_GBS, 4)
             if kd.get("read_requests_dram_per_launch") is not None:
                 e["dram_read_bytes"] = round(128 * kd["read_requests_dram_per_launch"])
         out[name] = e
@@ -544,17 +584,21 @@ def roofline_block(iso, timed, steps, ms_per_step, pmc):
     d = kern[dom]
     r = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": d["frac"], "traffic": d.get("traffic"), "hbm_frac": d.get("hbm_frac"),
-         "alg_bytes_per_launch": d["alg_bytes"], "mean_launch_us": d["mean_launch_us"],
+         "alg_bytes_per_launch": d["alg_bytes"], "credited_bytes_per_launch": d["credited_bytes"],
+         "mean_launch_us": d["mean_launch_us"],
          "measured": "HIP events around each launch on the lane's stream (library statistics), isolated pass "
                      "(one batch in flight, median of five batches)"}
     if d.get("rocprof_mean_launch_us"):
         r["rocprof_mean_launch_us"] = d["rocprof_mean_launch_us"]
+        r["frac_rocprof"] = d.get("frac_rocprof")
     if d.get("mean_dispatch_us_all_steps"):
         r["mean_dispatch_us_all_steps"] = d["mean_dispatch_us_all_steps"]
     if pmc:
         r["traffic_source"] = (f"{pmc['_file']} (rocprofv3 --pmc: TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B "
                                f"by request size, each pass its own run; hbm_frac over the same profile's "
                                f"kernel-trace mean; tag {pmc.get('tag')}, commit {pmc.get('head')})")
+        r["profile"] = {"file": pmc["_file"], "head": pmc.get("head"), "src": pmc.get("src"),
+                        "src_match": pmc.get("src") == source_identity()["src"]}
     b_iso = iso["bytes_alg_capped"] / nb
     t_iso = iso["t_kernels_ns"] / nb * 1e-9
     path = {"bytes_per_batch": int(b_iso),
@@ -707,10 +751,86 @@ def run(args, rank, world, local):
             "url_dictionary_build_s": round(t_dict, 3),
             "legs": legs or None,
         }
-        print(json.dumps(out), flush=True)
+        ident = source_identity()
+        out["build"] = ident
+        detail = write_detail(out, ident)
+        print(json.dumps(compact_line(out, detail)), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def write_detail(out, ident):
+    """The full record (every per-kernel block, the path model, the identical-batch
+    run, per-batch data) goes to profiles/bench_detail_<head or src>.json and, when a
+    gpurun_out/ directory can be made, a copy there (what a GPU call brings back)."""
+    name = f"bench_detail_{ident['head'] or ident['src']}.json"
+    rel = os.path.join("profiles", name)
+    for d in (os.path.join(ROOT, "profiles"), os.path.join(ROOT, "gpurun_out")):
+        try:
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, name), "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError as e:
+            log(f"detail not written to {d}: {e!r}")
+    return rel
+
+
+def _short_roof(r):
+    keep = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "hbm_frac", "alg_bytes_per_launch",
+            "credited_bytes_per_launch", "mean_launch_us", "rocprof_mean_launch_us", "frac_rocprof")
+    o = {k: r.get(k) for k in keep if k in r}
+    if r.get("profile"):
+        o["profile"] = r["profile"]
+    p = r.get("path") or {}
+    if p:
+        o["path"] = {"bytes_per_batch": p.get("bytes_per_batch"), "traffic_per_batch": p.get("traffic_per_batch"),
+                     "isolated_frac": (p.get("isolated") or {}).get("frac"),
+                     "throughput_frac": (p.get("throughput_mode") or {}).get("frac"),
+                     "throughput_hbm_frac": (p.get("throughput_mode") or {}).get("hbm_frac")}
+    return o
+
+
+def _short_leg(leg):
+    if "error" in leg:
+        return {"error": leg["error"][:200]}
+    r = leg.get("roofline") or {}
+    par = leg.get("parity_sample") or {}
+    lat = leg.get("latency_ms") or {}
+    return {"ms_per_step": round(leg["ms_per_step"], 4), "value": leg["value"], "kernel": r.get("kernel"),
+            "frac": r.get("frac"), "frac_rocprof": r.get("frac_rocprof"), "hbm_frac": r.get("hbm_frac"),
+            "checked": par.get("queries_checked"), "mismatches": par.get("mismatches"),
+            "p50_ms": round(lat["p50"], 3) if lat.get("p50") is not None else None,
+            "realloc_events_timed": leg.get("realloc_events_timed")}
+
+
+def compact_line(out, detail):
+    """The one stdout line the driver parses (kept to a few KB: round 4's 20 KB line
+    overflowed the driver's tail).  The full record is in `detail`."""
+    cpu = out.get("cpu_baseline")
+    cpu1 = out.get("cpu_baseline_1thread")
+    par = out.get("parity_sample")
+    lat = out.get("latency_ms")
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    line["roofline"] = _short_roof(out["roofline"])
+    line["cpu_baseline"] = None if cpu is None else {
+        "value": cpu["value"], "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
+        "sample": cpu["sample"], "cpu_model": cpu.get("cpu_model")}
+    line["cpu_baseline_1thread"] = None if cpu1 is None else {"value": cpu1["value"], "cores": cpu1["cores"]}
+    line["parity_sample"] = None if par is None else {
+        "queries_checked": par["queries_checked"], "mismatches": par["mismatches"], "checker": par["checker"],
+        "distinct_batches_checked": par["distinct_batches_checked"]}
+    line["latency_ms"] = None if lat is None else {"p50": round(lat["p50"], 4), "p99": round(lat["p99"], 4),
+                                                   "n": lat["n"]}
+    line["realloc_events_timed"] = out.get("realloc_events_timed")
+    line["distinct_batches"] = out.get("distinct_batches")
+    line["inflight"] = out.get("inflight")
+    if out.get("legs"):
+        line["legs"] = {name: _short_leg(leg) for name, leg in out["legs"].items()}
+    line["build"] = out.get("build")
+    line["detail"] = detail
+    return line
 
 
 LEG_DESC = {

@@ -160,8 +160,8 @@ typedef struct yrwi_stats {
   int64_t t_scorek_ns;
   int64_t bytes_reduce;
   int64_t bytes_score;
-  /* chained folds (k_chain_part + k_chain + k_scan_tiles of a chained step, HIP events around them): the
-     launches, their device time and their SURVEY.md §8(d) bytes -- the later fold steps' K and the
+  /* chained folds: the k_chain launches, their device time (HIP events around k_chain alone, the
+     population rocprofv3 averages) and their SURVEY.md §8(d) bytes -- the later fold steps' K and the
      exclusions' 12 n_e, each charged min(K, the bytes k_chain loads for it) */
   int64_t n_chain_launches;
   int64_t t_chain_ns;

@@ -29,3 +29,26 @@ def test_gpus_1_single_process():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = _run("--dry-run", env=env)
     assert out["n_gpus"] == 1
+
+
+def test_compact_line_fits_the_driver_tail():
+    """The stdout line stays a few KB (round 4's 20 KB line overflowed the driver's
+    tail): rebuilt from round 4's full record, it keeps the contract's fields, the
+    roofline, the CPU baseline, parity, latency and one summary per leg."""
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+        full = json.load(f)
+    full["build"] = bench.source_identity()
+    line = bench.compact_line(full, "profiles/bench_detail_x.json")
+    s = json.dumps(line)
+    assert len(s) <= 6000, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "parity_sample", "latency_ms", "legs", "detail"):
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    assert set(line["legs"]) == {"C3", "C4", "C5_custom", "C5_date"}
+    assert all("ms_per_step" in v and "frac" in v for v in line["legs"].values())

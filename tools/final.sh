@@ -1,4 +1,5 @@
-# Round-4 final check at HEAD: the whole GPU suite, then the driver's bench command.
+# Round check at HEAD (run through gpurun from the repo root): the whole GPU suite,
+# then the driver's bench command.  Output in gpurun_out/final/.
 set -o pipefail
 mkdir -p gpurun_out/final
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \

@@ -106,13 +106,13 @@ def main(tag, config):
                 tot += kd["hbm_bytes_per_launch"] * kd["calls"]
         out["path_hbm_bytes_per_batch"] = tot / nb
         out["batches_profiled"] = nb
-    import subprocess
-    out["head"] = os.environ.get("PROF_HEAD")  # the commit measured (the GPU box has no .git)
-    if not out["head"]:
-        try:
-            out["head"] = subprocess.check_output(["git", "-C", ROOT, "describe", "--always", "--dirty"], text=True).strip()
-        except Exception:
-            pass
+    # the build measured: the same (head, src) pair bench.py stamps on its line (the
+    # GPU box has no .git: head comes from PROF_HEAD or the REVISION file)
+    sys.path.insert(0, ROOT)
+    from bench import source_identity
+    ident = source_identity()
+    out["head"] = os.environ.get("PROF_HEAD") or ident["head"]
+    out["src"] = ident["src"]
     for name in ("k_compact", "k_join", "k_probe", "k_probe_excl", "k_chain", "k_reduce", "k_score"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
