@@ -1086,18 +1086,21 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
+    // the span ends after k_scan_tiles (chained steps: compaction comes later)
+    hipEvent_t se = ctx->event();
+    hipEventRecord(se, ctx->stream);
     if (chain) {
-      hipEventRecord(c1, ctx->stream);  // the span ends after k_chain / k_scan_tiles; compaction comes later
-      tm->kchain.push_back({e1, c1});
+      // c0 / c1 bracket k_chain alone; a step without chain groups launched none
+      if (!cgrp.empty()) tm->kchain.push_back({c0, c1});
     } else {
       tm->kcompact.push_back({c0, c1});
     }
-    tm->spans.push_back({sp, c1});
+    tm->spans.push_back({sp, se});
   }
   if (st) {
     st->n_join_launches++;
     st->n_probe_dispatches += tiles > merge_tiles;
-    st->n_chain_launches += chain ? 1 : 0;
+    st->n_chain_launches += chain && !cgrp.empty() ? 1 : 0;  // k_chain launches (timed in t_chain_ns)
   }
   const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);

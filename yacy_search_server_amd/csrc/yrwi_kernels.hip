@@ -4160,8 +4160,11 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                          d_tile_base, njobs, d_cgrp, (int64_t)0, ngroups, (const uint32_t*)d_pair_uid,
                          (const int64_t*)d_tile_src, (const int32_t*)d_tile_cnt, d_crange);
       dbg_sync("k_chain_part", st);
+      // chained steps: evc0 / evc1 bracket k_chain alone (the population rocprofv3 averages)
+      if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       hipLaunchKernelGGL(k_chain, dim3((unsigned)ngroups), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs, d_cgrp,
                          d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl, (const ProbeDesc*)d_crange);
+      if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
       dbg_sync("k_chain", st);
     }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
