@@ -178,7 +178,12 @@ int yrwi_open(int device, yrwi_ctx** out);
 /* One shard of a URL-hash-range partitioned index (Distribution.java:153-158):
  * rank r of `world` (power of two) owns url hashes whose first character index
  * c satisfies c >> (6 - log2(world)) == r.  `nccl_id` is the 128-byte
- * ncclUniqueId from yrwi_get_unique_id() on rank 0, broadcast by the caller. */
+ * ncclUniqueId from yrwi_get_unique_id() on rank 0, broadcast by the caller.
+ * The shards merge their partial results over RCCL (Protocol.java:802 merges
+ * peers' results); when RCCL cannot form the group -- ranks sharing one device --
+ * and the ranks share a node, the device collectives run host-staged through
+ * shared memory instead (an id starting with "YRWI-HOSTSTAGE " selects that
+ * without trying RCCL). */
 int yrwi_open_shard(int device, int rank, int world, const uint8_t nccl_id[128], yrwi_ctx** out);
 int yrwi_get_unique_id(uint8_t nccl_id[128]);
 void yrwi_close(yrwi_ctx* ctx);
@@ -324,6 +329,13 @@ typedef struct yrwi_event yrwi_event;
  * most postings the event will receive (sizes the url and host tables). */
 int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms, int32_t k,
                     const yrwi_filter* filter, int64_t max_postings, yrwi_event** out);
+/* An event for yrwi_event_order / yrwi_event_authority only (GpuReferenceOrder: the
+ * ReferenceOrder of a SearchEvent whose addRWIs stays in Java): no url set and no
+ * stack, the host table sized for max_hosts distinct hosts (authority profiles;
+ * more: YRWI_E_CAPACITY), device memory reused from closed order-only events.
+ * The event entry points serialise on the context (callers on several threads). */
+int yrwi_event_open_order(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms,
+                          int64_t max_hosts, yrwi_event** out);
 typedef struct yrwi_arrival {
   yrwi_event* ev;
   const uint8_t* rows40;  /* n rows of 40 bytes */

@@ -9,6 +9,20 @@
 
 #include "yrwi.h"
 
+/* A Java byte[] of at least `need` bytes copied into native memory (no critical
+ * region around library calls that synchronise with the GPU: GC stays free);
+ * NULL (IllegalArgumentException pending) when the array is shorter, or on OOM. */
+static uint8_t* copy_in(JNIEnv* env, jbyteArray a, int64_t need) {
+  if (a == NULL || need < 0 || (int64_t)(*env)->GetArrayLength(env, a) < need) {
+    jclass ex = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+    if (ex) (*env)->ThrowNew(env, ex, "array shorter than n rows / hosts");
+    return NULL;
+  }
+  uint8_t* b = (uint8_t*)malloc((size_t)(need > 0 ? need : 1));
+  if (b && need > 0) (*env)->GetByteArrayRegion(env, a, 0, (jsize)need, (jbyte*)b);
+  return b;
+}
+
 static void to_profile(JNIEnv* env, jintArray a, yrwi_profile* p) {
   if (a == NULL) { yrwi_profile_default(p); return; }
   (*env)->GetIntArrayRegion(env, a, 0, 32, (jint*)p);
@@ -27,10 +41,10 @@ JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_putList(JNIEnv* env, jc
                                                                 jbyteArray rows, jint n, jint sorted) {
   jbyte t[12];
   (*env)->GetByteArrayRegion(env, term, 0, 12, t);
-  /* RowSet.chunkcache is pinned only for the H2D copy */
-  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
-  int rc = yrwi_put_list((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)t, (const uint8_t*)p, n, sorted);
-  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  uint8_t* p = copy_in(env, rows, (int64_t)n * 40);
+  if (!p) return YRWI_E_ARG;
+  int rc = yrwi_put_list((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)t, p, n, sorted);
+  free(p);
   return rc;
 }
 
@@ -133,14 +147,19 @@ JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_normalizeScore(JN
   yrwi_profile p;
   to_profile(env, prof, &p);
   const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
-  jlongArray res = (*env)->NewLongArray(env, m);
-  jlong* sc = (*env)->GetLongArrayElements(env, res, NULL);
-  void* r = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
-  int rc = yrwi_normalize_score((yrwi_ctx*)(intptr_t)ctx, (const uint8_t*)r, m, &p, l, now, (int64_t*)sc);
-  (*env)->ReleasePrimitiveArrayCritical(env, rows, r, JNI_ABORT);
-  (*env)->ReleaseLongArrayElements(env, res, sc, 0);
+  uint8_t* r = copy_in(env, rows, (int64_t)m * 40);
+  if (!r) { (*env)->ReleaseStringUTFChars(env, lang, l); return NULL; }
+  jlong* sc = (jlong*)malloc(sizeof(jlong) * (size_t)(m > 0 ? m : 1));
+  int rc = sc ? yrwi_normalize_score((yrwi_ctx*)(intptr_t)ctx, r, m, &p, l, now, (int64_t*)sc) : YRWI_E_NOMEM;
+  free(r);
   (*env)->ReleaseStringUTFChars(env, lang, l);
-  return rc == 0 ? res : NULL;
+  jlongArray res = NULL;
+  if (rc == 0) {
+    res = (*env)->NewLongArray(env, m);
+    (*env)->SetLongArrayRegion(env, res, 0, m, sc);
+  }
+  free(sc);
+  return res;
 }
 
 JNIEXPORT jbyteArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_query(JNIEnv* env, jclass c, jlong ctx,
@@ -270,18 +289,32 @@ JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpen(JNIEnv* env,
   return rc == 0 ? (jlong)(intptr_t)ev : 0;
 }
 
+/* GpuReferenceOrder's event: the ReferenceOrder state and host table only (yrwi_event_open_order) */
+JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpenOrder(JNIEnv* env, jclass c, jlong ctx,
+                                                                        jintArray prof, jstring lang, jlong now,
+                                                                        jlong maxHosts) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  yrwi_event* ev = NULL;
+  int rc = yrwi_event_open_order((yrwi_ctx*)(intptr_t)ctx, &p, l, now, maxHosts, &ev);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  return rc == 0 ? (jlong)(intptr_t)ev : 0;
+}
+
 /* addRWIs(container, local): rows = RowSet.chunkcache bytes of the container in its order */
 JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAdd(JNIEnv* env, jclass c, jlong ctx, jlong ev,
                                                                  jbyteArray rows, jint n, jboolean local) {
   yrwi_arrival a;
   memset(&a, 0, sizeof(a));
-  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
+  uint8_t* p = copy_in(env, rows, (int64_t)n * 40);
+  if (!p) return YRWI_E_ARG;
   a.ev = (yrwi_event*)(intptr_t)ev;
-  a.rows40 = (const uint8_t*)p;
+  a.rows40 = p;
   a.n = n;
   a.local = local ? 1 : 0;
   int rc = yrwi_event_add((yrwi_ctx*)(intptr_t)ctx, &a, 1);
-  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  free(p);
   return rc;
 }
 
@@ -289,13 +322,14 @@ JNIEXPORT jint JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAdd(JNIEnv* env, j
  * (yrwi_event_order): one score per row of the container, in its order */
 JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOrder(JNIEnv* env, jclass c, jlong ctx, jlong ev,
                                                                          jbyteArray rows, jint n, jboolean local) {
+  /* yrwi_event_order drains the context and synchronises with the GPU: the rows are
+   * copied out of the Java heap first (no GC-blocking critical region around it) */
+  uint8_t* p = copy_in(env, rows, (int64_t)n * 40);
+  if (!p) return NULL;
   jlong* sc = (jlong*)malloc(sizeof(jlong) * (size_t)(n > 0 ? n : 1));
-  if (!sc) return NULL;
-  /* the rows are staged by the library before any device work: a short critical region */
-  void* p = (*env)->GetPrimitiveArrayCritical(env, rows, NULL);
-  int rc = yrwi_event_order((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, (const uint8_t*)p, n,
-                            local ? 1 : 0, (int64_t*)sc);
-  (*env)->ReleasePrimitiveArrayCritical(env, rows, p, JNI_ABORT);
+  if (!sc) { free(p); return NULL; }
+  int rc = yrwi_event_order((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, p, n, local ? 1 : 0, (int64_t*)sc);
+  free(p);
   jlongArray res = NULL;
   if (rc == 0) {
     res = (*env)->NewLongArray(env, n);
@@ -308,12 +342,12 @@ JNIEXPORT jlongArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOrder(JNIEnv
 /* ReferenceOrder.authority of n 6-byte host hashes against the event's host counts */
 JNIEXPORT jintArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventAuthority(JNIEnv* env, jclass c, jlong ctx,
                                                                             jlong ev, jbyteArray hosts6, jint n) {
-  jbyte* h = (*env)->GetByteArrayElements(env, hosts6, NULL);
+  uint8_t* h = copy_in(env, hosts6, (int64_t)n * 6);
+  if (!h) return NULL;
   jint* out = (jint*)malloc(sizeof(jint) * (size_t)(n > 0 ? n : 1));
-  int rc = out ? yrwi_event_authority((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, (const uint8_t*)h, n,
-                                      (int32_t*)out)
+  int rc = out ? yrwi_event_authority((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, h, n, (int32_t*)out)
                : YRWI_E_NOMEM;
-  (*env)->ReleaseByteArrayElements(env, hosts6, h, JNI_ABORT);
+  free(h);
   jintArray res = NULL;
   if (rc == 0) {
     res = (*env)->NewIntArray(env, n);

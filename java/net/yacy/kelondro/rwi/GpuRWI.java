@@ -16,6 +16,10 @@ package net.yacy.kelondro.rwi;
 
 public final class GpuRWI implements AutoCloseable {
 
+    // A libyrwi context is not thread-safe (include/yrwi.h): every call on it is
+    // synchronized on this object.  YaCy reaches one GpuRWI from the search threads,
+    // the remote-peer (Protocol) threads and the result workers (authority()).
+
     static { System.loadLibrary("yrwi_jni"); }  // links libyrwi.so
 
     private long ctx;  // yrwi_ctx*
@@ -26,24 +30,24 @@ public final class GpuRWI implements AutoCloseable {
     }
 
     /** IndexCell.add for a whole container: the RowSet chunkcache bytes (n * 40, sorted). */
-    public void putList(final byte[] termHash, final byte[] chunkcache, final int n) {
+    public synchronized void putList(final byte[] termHash, final byte[] chunkcache, final int n) {
         check(putList(this.ctx, termHash, chunkcache, n, 1));
     }
 
     /** Index.size(termHash) of each term on the GPU index (yrwi_list_size; 0: no list). */
-    public long[] listSizes(final byte[][] terms) {
+    public synchronized long[] listSizes(final byte[][] terms) {
         return listSizes(this.ctx, flatten(terms), terms.length);
     }
 
     /** Index.get(termHash) off the query path (yrwi_get_list): the list's sorted rows (n * 40 bytes). */
-    public byte[] getList(final byte[] term) {
+    public synchronized byte[] getList(final byte[] term) {
         final byte[] rows = getList(this.ctx, term);
         if (rows == null) throw new IllegalStateException("yrwi_get_list failed");
         return rows;
     }
 
     /** TermSearch + joinExcludeContainers: returns the joined container's rows (m * 40 bytes). */
-    public byte[] joinExclude(final byte[][] include, final byte[][] exclude, final int maxDistance,
+    public synchronized byte[] joinExclude(final byte[][] include, final byte[][] exclude, final int maxDistance,
                               final long nowMillis) {
         return joinExclude(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
                            maxDistance, nowMillis);
@@ -52,7 +56,7 @@ public final class GpuRWI implements AutoCloseable {
     /** TermSearch(..., urlselection, ...).joined(): every include and exclude list restricted
      *  to the url selection (url hashes) before the conjunction, as
      *  ReferenceContainerCache.get(key, urlselection) restricts it (yrwi_term_search). */
-    public byte[] termSearch(final byte[][] include, final byte[][] exclude, final byte[][] urlselection,
+    public synchronized byte[] termSearch(final byte[][] include, final byte[][] exclude, final byte[][] urlselection,
                              final int maxDistance, final long nowMillis) {
         final byte[] rows = termSearch(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
                                        urlselection == null ? null : flatten(urlselection),
@@ -64,7 +68,7 @@ public final class GpuRWI implements AutoCloseable {
     /** joinExclude into a caller-owned direct buffer (ByteBuffer.allocateDirect, reused
      *  across queries): no copy of the joined container through a Java array.  Returns
      *  the number of 40-byte rows written; throws when the container does not fit. */
-    public long joinExcludeInto(final byte[][] include, final byte[][] exclude, final int maxDistance,
+    public synchronized long joinExcludeInto(final byte[][] include, final byte[][] exclude, final int maxDistance,
                                 final long nowMillis, final java.nio.ByteBuffer out) {
         final long m = joinExcludeInto(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length,
                                        maxDistance, nowMillis, out);
@@ -73,14 +77,14 @@ public final class GpuRWI implements AutoCloseable {
     }
 
     /** ReferenceOrder.normalizeWith + cardinal with settled min/max: one score per row. */
-    public long[] normalizeScore(final byte[] rows, final int m, final int[] profile32, final String language,
+    public synchronized long[] normalizeScore(final byte[] rows, final int m, final int[] profile32, final String language,
                                  final long nowMillis) {
         return normalizeScore(this.ctx, rows, m, profile32, language, nowMillis);
     }
 
     /** SearchEvent local RWI path: top-k (urlhash, cardinal) of one query. Output: k * 24 bytes
      *  (12-byte url hash, int32 ByteArray.hashCode, int64 score), little endian. */
-    public byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+    public synchronized byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
                         final int[] profile32, final String language, final long nowMillis) {
         return query(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length, maxDistance, k,
                      profile32, language, nowMillis, null);
@@ -88,7 +92,7 @@ public final class GpuRWI implements AutoCloseable {
 
     /** query(...) with the call's yrwi_stats (17 longs, order in yrwi_jni.c stats_out):
      *  postings in, joined rows, algorithmic bytes, per-phase device times, launches. */
-    public byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+    public synchronized byte[] query(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
                         final int[] profile32, final String language, final long nowMillis, final long[] stats) {
         return query(this.ctx, flatten(include), include.length, flatten(exclude), exclude.length, maxDistance, k,
                      profile32, language, nowMillis, stats);
@@ -97,14 +101,14 @@ public final class GpuRWI implements AutoCloseable {
     /** IndexCell's BLOB heaps (text.index.*.blob) into the GPU index; lists already
      *  present act as the RAM cache.  Returns {files, records, free, badKeys, terms,
      *  postings, droppedTerms}. */
-    public long[] loadHeaps(final String[] heapFiles, final boolean orderByFileName) {
+    public synchronized long[] loadHeaps(final String[] heapFiles, final boolean orderByFileName) {
         return loadHeaps(this.ctx, heapFiles, orderByFileName ? 1 : 0);
     }
 
     /** query(...) under SearchEvent.addRWIs constraints (SearchEvent.java:736-806) and,
      *  with skipDoubleDom, in pullOneRWI order (:1297-1394).  flagCount (int[32] or null)
      *  receives SearchEvent.flagcount. */
-    public byte[] queryFiltered(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
+    public synchronized byte[] queryFiltered(final byte[][] include, final byte[][] exclude, final int maxDistance, final int k,
                                 final int[] profile32, final String language, final long nowMillis,
                                 final byte[] constraint, final boolean allOfConstraint, final int contentdom,
                                 final boolean strictContentDom, final String modifierLanguage, final byte[] sitehash,
@@ -119,12 +123,20 @@ public final class GpuRWI implements AutoCloseable {
     /** A SearchEvent's rwiStack on the GPU: open once per event, then addRWIs for the
      *  local container and every remote peer's container (Protocol.java:802); the
      *  result is the stack in rwiStack order (24-byte records as query()). */
-    public long eventOpen(final int[] profile32, final String language, final long nowMillis, final int k,
+    public synchronized long eventOpen(final int[] profile32, final String language, final long nowMillis, final int k,
                           final long maxPostings) {
         return eventOpen(this.ctx, profile32, language, nowMillis, k, maxPostings);
     }
 
-    public void addRWIs(final long event, final byte[] containerRows, final int n, final boolean local) {
+    /** An event holding only a SearchEvent's ReferenceOrder (yrwi_event_open_order):
+     *  eventOrder / eventAuthority only, the host table sized for maxHosts hosts; device
+     *  memory comes from closed order-only events (no device-wide allocation per event). */
+    public synchronized long eventOpenOrder(final int[] profile32, final String language, final long nowMillis,
+                                            final long maxHosts) {
+        return eventOpenOrder(this.ctx, profile32, language, nowMillis, maxHosts);
+    }
+
+    public synchronized void addRWIs(final long event, final byte[] containerRows, final int n, final boolean local) {
         check(eventAdd(this.ctx, event, containerRows, n, local));
     }
 
@@ -132,48 +144,55 @@ public final class GpuRWI implements AutoCloseable {
      *  the event's ReferenceOrder (yrwi_event_order): min/max, the max-distance fold and
      *  the host counts accumulate over every container given to the event; the scores
      *  are under the state after this one.  The event's stack is not touched. */
-    public long[] eventOrder(final long event, final byte[] containerRows, final int n, final boolean local) {
+    public synchronized long[] eventOrder(final long event, final byte[] containerRows, final int n, final boolean local) {
         final long[] sc = eventOrder(this.ctx, event, containerRows, n, local);
         if (sc == null) throw new IllegalStateException("yrwi_event_order failed");
         return sc;
     }
 
     /** ReferenceOrder.authority(hostHash) against the event's accumulated host counts. */
-    public int eventAuthority(final long event, final byte[] hostHash6) {
+    public synchronized int eventAuthority(final long event, final byte[] hostHash6) {
         final int[] a = eventAuthority(this.ctx, event, hostHash6, 1);
         if (a == null) throw new IllegalStateException("yrwi_event_authority failed");
         return a[0];
     }
 
-    public byte[] eventResult(final long event, final int maxn) {
+    /** eventAuthority for n host hashes at once (6 bytes each, concatenated): one call. */
+    public synchronized int[] eventAuthorities(final long event, final byte[] hostHashes6, final int n) {
+        final int[] a = eventAuthority(this.ctx, event, hostHashes6, n);
+        if (a == null) throw new IllegalStateException("yrwi_event_authority failed");
+        return a;
+    }
+
+    public synchronized byte[] eventResult(final long event, final int maxn) {
         return eventResult(this.ctx, event, maxn);
     }
 
     /** SearchEvent.pullOneRWI(skipDoubleDom) up to maxn times (SearchEvent.java:1297-1394):
      *  yrwi_hit records (12-byte url hash, int hashCode, long score) in pull order;
      *  the entries leave the event's rwiStack, the doubleDomCache stays with the event. */
-    public byte[] pullRWI(final long event, final boolean skipDoubleDom, final int maxn) {
+    public synchronized byte[] pullRWI(final long event, final boolean skipDoubleDom, final int maxn) {
         return eventPull(this.ctx, event, skipDoubleDom, maxn);
     }
 
-    public void eventClose(final long event) {
+    public synchronized void eventClose(final long event) {
         eventClose(this.ctx, event);
     }
 
     /** WordReferenceFactory.compressIndex of each include word's list (search.java:264-281):
      *  one "{...}" per word; empty when a word has no list (searchConjunction is empty). */
-    public String[] indexAbstracts(final byte[][] words, final long capacity) {
+    public synchronized String[] indexAbstracts(final byte[][] words, final long capacity) {
         return indexAbstracts(this.ctx, flatten(words), words.length, capacity);
     }
 
     /** ReferenceOrder.cardinal(URIMetadataNode) of packed yrwi_node records (60 bytes each). */
-    public long[] scoreNodes(final byte[] nodes, final int n, final int[] profile32, final String language,
+    public synchronized long[] scoreNodes(final byte[] nodes, final int n, final int[] profile32, final String language,
                              final int maxdomcount) {
         return scoreNodes(this.ctx, nodes, n, profile32, language, maxdomcount);
     }
 
     @Override
-    public void close() {
+    public synchronized void close() {
         if (this.ctx != 0) { close(this.ctx); this.ctx = 0; }
     }
 
@@ -228,6 +247,8 @@ public final class GpuRWI implements AutoCloseable {
                                                boolean skipDoubleDom, int[] flagCount);
     private static native long eventOpen(long ctx, int[] profile32, String language, long nowMillis, int k,
                                          long maxPostings);
+    private static native long eventOpenOrder(long ctx, int[] profile32, String language, long nowMillis,
+                                              long maxHosts);
     private static native int eventAdd(long ctx, long event, byte[] rows, int n, boolean local);
     private static native byte[] eventResult(long ctx, long event, int maxn);
     private static native long[] eventOrder(long ctx, long event, byte[] rows, int n, boolean local);

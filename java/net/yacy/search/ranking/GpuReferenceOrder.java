@@ -28,9 +28,20 @@
 // each queued entry carries its position in it (Entry), so cardinal(e) is an
 // array read: no per-posting key String and no map.  authority() asks the GPU's
 // accumulated host counts (they exist when coeff_authority > 12, the only case in
-// which cardinal uses them).
+// which cardinal uses them); its answers are cached until the next container
+// changes the counts, so the result workers' per-node calls (cardinal(
+// URIMetadataNode)) reach the GPU once per distinct host.
+//
+// Resources: the event is order-only (yrwi_event_open_order: the state and a host
+// table sized by expected hosts, no url set or stack), its device block reused
+// from closed orders (no device-wide allocation per SearchEvent).  close() returns
+// it; a SearchEvent that is dropped without cleanup() still returns it through the
+// Cleaner.  Every native call goes through GpuRWI, which serialises them on the
+// shared context (a context is not thread-safe).
 package net.yacy.search.ranking;
 
+import java.lang.ref.Cleaner;
+import java.util.HashMap;
 import java.util.Iterator;
 import java.util.concurrent.BlockingQueue;
 import java.util.concurrent.LinkedBlockingQueue;
@@ -44,8 +55,22 @@ import net.yacy.kelondro.rwi.ReferenceContainer;
 
 public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
-    /** Postings one SearchEvent's order may receive in all (sizes the event's host table). */
-    public static final long DEFAULT_MAX_POSTINGS = 1L << 22;
+    /** Distinct hosts one SearchEvent's order may see (sizes the event's host table,
+     *  12 B per slot, two slots per host: 3 MB). */
+    public static final long DEFAULT_MAX_HOSTS = 1L << 17;
+
+    private static final Cleaner CLEANER = Cleaner.create();
+
+    /** Returns the event to the context if the order was dropped unclosed. */
+    private static final class Release implements Runnable {
+        private final GpuRWI gpu;
+        private long event;
+        Release(final GpuRWI gpu, final long event) { this.gpu = gpu; this.event = event; }
+        @Override
+        public synchronized void run() {
+            if (this.event != 0) { this.gpu.eventClose(this.event); this.event = 0; }
+        }
+    }
 
     /** A queued posting with its position in the container's score array. */
     public static final class Entry extends WordReferenceVars {
@@ -65,18 +90,25 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
     private final GpuRWI gpu;
     private long event;  // yrwi_event*: this order's ReferenceOrder state on the GPU
+    private final Release release;
+    private final Cleaner.Cleanable cleanable;
+    private final boolean authorityProfile;
+    private final HashMap<String, Integer> authorityCache = new HashMap<String, Integer>();
 
     public GpuReferenceOrder(final RankingProfile profile, final String language, final GpuRWI gpu) {
-        this(profile, language, gpu, DEFAULT_MAX_POSTINGS);
+        this(profile, language, gpu, DEFAULT_MAX_HOSTS);
     }
 
     public GpuReferenceOrder(final RankingProfile profile, final String language, final GpuRWI gpu,
-                             final long maxPostings) {
+                             final long maxHosts) {
         super(profile, language);
         this.gpu = gpu;
+        this.authorityProfile = profile.coeff_authority > 12;
         // "now" is fixed for the event's lifetime (the clone's virtualAge clamp, J6)
-        this.event = gpu.eventOpen(GpuRWI.profile32(profile), language, System.currentTimeMillis(), 1, maxPostings);
-        if (this.event == 0) throw new IllegalStateException("yrwi_event_open failed");
+        this.event = gpu.eventOpenOrder(GpuRWI.profile32(profile), language, System.currentTimeMillis(), maxHosts);
+        if (this.event == 0) throw new IllegalStateException("yrwi_event_open_order failed");
+        this.release = new Release(gpu, this.event);
+        this.cleanable = CLEANER.register(this, this.release);
     }
 
     @Override
@@ -90,6 +122,7 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
             final long[] sc;
             synchronized (this) {  // containers fold into the order one after another
                 sc = this.gpu.eventOrder(this.event, rows, m, local);
+                this.authorityCache.clear();  // the host counts changed
             }
             final Iterator<WordReference> i = container.entries();  // the same row order
             int p = 0;
@@ -101,7 +134,12 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
     @Override
     public synchronized int authority(final String hostHash) {
-        return this.gpu.eventAuthority(this.event, ASCII.getBytes(hostHash));
+        if (!this.authorityProfile) return 0;  // no host counts: ReferenceOrder's doms stay empty
+        final Integer a = this.authorityCache.get(hostHash);
+        if (a != null) return a.intValue();
+        final int v = this.gpu.eventAuthority(this.event, ASCII.getBytes(hostHash));
+        this.authorityCache.put(hostHash, v);
+        return v;
     }
 
     @Override
@@ -113,8 +151,8 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
     @Override
     public synchronized void close() {
         if (this.event != 0) {
-            this.gpu.eventClose(this.event);
             this.event = 0;
+            this.cleanable.clean();  // Release.run once: the event back to the context
         }
     }
 }

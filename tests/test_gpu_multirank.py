@@ -1,10 +1,13 @@
 """Sharded (multi-rank) libyrwi path on ONE GPU: world ranks, each a process
-that owns one URL-hash shard on device 0 and talks to the others over RCCL.
-This exercises yrwi_open_shard, the ShardSum all-gather + ordered combine and
-the top-k all-gather merge end to end; the result must be bit-exact against
-the single-container oracle.  If RCCL refuses several ranks on one device the
-test is skipped (the 8-GPU path is then covered only by the driver's runs and
-by tests/test_multi_gloo.py)."""
+that owns one URL-hash shard on device 0.  RCCL refuses several ranks on one
+device, so the ranks' device collectives (ShardSum all-gather, authority
+host-count exchange, top-k all-gather) run host-staged through the node's
+shared memory (yrwi_coll.cpp) -- after RCCL's init fails ("auto", the
+production fallback) or straight away (a YRWI-HOSTSTAGE group id).  The list-size
+planning goes through the host mailbox as on the 8-GPU node.  This runs
+yrwi_open_shard, global-size planning, the ordered combine, the host-count
+exchange and the top-k merge of libyrwi across processes; the result must be
+bit-exact against the single-container oracle (authority profile included)."""
 
 import os
 import sys
@@ -26,19 +29,19 @@ def _rank_main(rank, world, uid, out_q):
         from yacy_search_server_amd import Query, RankingProfile, RWIIndex, synth
         full = synth.preset("small")
         part = synth.build_index(full.shard(rank, world))
-        try:
-            ix = RWIIndex(0, shard=(rank, world, uid))
-        except Exception as e:  # RCCL refused several ranks on one GPU
-            out_q.put((rank, "skip", str(e)))
-            return
+        ix = RWIIndex(0, shard=(rank, world, uid))
         for t in range(full.n_terms):
             if part.sizes[t]:
                 ix.add(part.hashes[t], part.list_rows(t))
-        qs = synth.queries(full, 24, 1, 4, 1, qseed=41)
+        qs = synth.queries(full, 36, 1, 4, 1, qseed=41)
         c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")  # authority -> host-count exchange
         batch = [Query([part.hashes[t] for t in inc], [part.hashes[t] for t in exc], now_ms=NOW, k=100,
                        profile=(c5 if i % 2 else None)) for i, (inc, exc) in enumerate(qs)]
-        got = ix.search_batch(batch)
+        # one synchronous batch (split over the lanes), then two in flight on different lanes
+        got = ix.search_batch(batch[:12])
+        p1 = ix.submit(batch[12:24])
+        p2 = ix.submit(batch[24:])
+        got += p1.result() + p2.result()
         whole = synth.build_index(full).as_dict()
         bad = []
         for qi, (q, g) in enumerate(zip(batch, got)):
@@ -52,11 +55,11 @@ def _rank_main(rank, world, uid, out_q):
         out_q.put((rank, "error", repr(e)))
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_query_on_one_gpu(world):
+@pytest.mark.parametrize("world,transport", [(2, "auto"), (2, "staged"), (4, "staged")])
+def test_sharded_query_on_one_gpu(world, transport):
     import torch.multiprocessing as mp
     from yacy_search_server_amd import unique_id
-    uid = unique_id()
+    uid = unique_id() if transport == "auto" else b"YRWI-HOSTSTAGE\0" + os.urandom(113)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_rank_main, args=(r, world, uid, q)) for r in range(world)]
@@ -69,8 +72,6 @@ def test_sharded_query_on_one_gpu(world):
         p.join(timeout=60)
         if p.is_alive():
             p.kill()
-    if any(r[1] == "skip" for r in res):
-        pytest.skip("RCCL refused %d ranks on one GPU: %s" % (world, [r[2] for r in res if r[1] == "skip"][0]))
     for rank, status, info in res:
         assert status == "ok", (rank, info)
         assert info == [], (rank, info)

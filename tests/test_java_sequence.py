@@ -177,7 +177,9 @@ def test_reference_order_accumulates_across_arrivals(corpus, profile):
     order = jl.ReferenceOrder(lp, "en")
     stack = jl.ReverseQueue(3000)
     urls = set()
-    with ix.event(gp, "en", NOW, k=3000, max_postings=total + 16) as ev, \
+    # GpuReferenceOrder holds an order-only event (yrwi_event_open_order); the full
+    # event beside it runs addRWIs on the GPU (yrwi_event_add) for comparison
+    with ix.reference_order(gp, "en", NOW, max_hosts=total) as ev, \
             ix.event(gp, "en", NOW, k=3000, max_postings=total + 16) as ev_add:
         for rows, loc in arrivals:
             got = ev.order(rows, loc)                                   # GpuReferenceOrder.normalizeWith
@@ -196,3 +198,24 @@ def test_reference_order_accumulates_across_arrivals(corpus, profile):
         if lp.coeff_authority > 12:  # the host counts exist (and enter cardinal) only then
             assert ev.authority(hosts) == [order.authority(h) for h in hosts]
             assert info.maxdomcount == order.maxdomcount
+
+
+def test_reference_order_events_reuse_memory_and_bound_hosts(corpus):
+    """Order-only events (GpuReferenceOrder, one per SearchEvent) reuse closed
+    events' device blocks: a second order after a first was closed starts from a
+    clean state (the same scores as the first); an authority profile whose
+    containers bring more hosts than max_hosts fails with YRWI_E_CAPACITY."""
+    cfg, idx, ix = corpus
+    c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+    rows = np.asarray(idx.rows, dtype=np.uint8)[:3000]
+    firsts = []
+    for _ in range(3):
+        with ix.reference_order(c5, "en", NOW, max_hosts=4096) as ev:
+            firsts.append(ev.order(rows[:1500], True).tolist())
+            ev.order(rows[1500:], False)
+    assert firsts[0] == firsts[1] == firsts[2]
+    nhosts = len({bytes(r[6:12]) for r in rows})
+    assert nhosts > 64
+    with ix.reference_order(c5, "en", NOW, max_hosts=8) as ev:
+        with pytest.raises(Exception):
+            ev.order(rows, True)

@@ -246,12 +246,12 @@ void hostx_close(HostX* x, bool unlink_name) {
 // YRWI_HOSTX_TIMEOUT_S (default 300 s: a peer that never arrives fails the batch
 // instead of hanging it; a peer busy rebuilding its url dictionary arrives late)
 template <class F>
-static bool hx_wait(const HostX* x, int64_t seq, F ready) {
+static bool hx_wait(const HostX* x, int64_t seq, F ready) {  // (x may be null: no abort table)
   static const double limit_s = getenv("YRWI_HOSTX_TIMEOUT_S") ? atof(getenv("YRWI_HOSTX_TIMEOUT_S")) : 300.0;
   const auto t0 = std::chrono::steady_clock::now();
   for (int64_t i = 0;; i++) {
     if (ready()) return true;
-    if (x->aborted(seq)) return false;
+    if (x && x->aborted(seq)) return false;
     if (i < 2000) {
       __builtin_ia32_pause();
       continue;
@@ -373,6 +373,176 @@ extern "C" int yrwi_hostx_selftest(const uint8_t id[128], int world, int rank, i
 
 namespace yrwi {
 
+// ------------------------------------------------- host-staged device collectives
+// When RCCL cannot form the group -- several ranks on ONE device (RCCL refuses a
+// duplicate GPU), as on a one-GPU test box -- the shards of one node exchange the
+// rank phase's device buffers (ShardSum all-gather, host-count exchange, flag
+// counts, top-k all-gather) through a shared-memory segment instead: each rank
+// copies its payload into its region, and reads its peers' regions once all have
+// posted the round.  The collective turn (CollTurn) already orders every device
+// collective of a rank in one total order, the same on every rank, so one round
+// is in progress at a time; a round is keyed by (batch part, call), and peers'
+// `posted` / `done` words are compared for equality with that key (a peer can be
+// at most one round behind).  Synchronous with the lane's stream; latency, not
+// bandwidth, is what it costs -- it is the transport of the multi-process tests
+// on one GPU, not of the 8-GPU node (RCCL over xGMI).
+namespace {
+constexpr int DX_MAXW = 16, DX_MAXE = 64;
+struct DxEnt {
+  int32_t peer;  // destination rank, -1: every rank (all-gather)
+  int32_t pad;
+  uint64_t off, bytes;
+};
+struct DxRank {
+  std::atomic<int64_t> posted;  // key of the round whose payload is in place
+  std::atomic<int64_t> done;    // key of the round this rank has finished reading
+  int32_t nent, pad;
+  DxEnt ent[DX_MAXE];
+  char pad2[48];
+};
+struct DxHead {
+  std::atomic<int32_t> attached;
+  int32_t pad;
+  char pad2[56];
+  DxRank r[DX_MAXW];
+};
+}  // namespace
+
+struct DevX {
+  void* base = nullptr;
+  size_t bytes = 0, cap = 0;  // segment size; payload bytes per rank
+  int world = 0, rank = 0;
+  std::string name;
+  HostX* hx = nullptr;  // abort table of the batch parts (hostx_abort)
+  int64_t unordered = 0;
+  DxHead* head() const { return static_cast<DxHead*>(base); }
+  uint8_t* region(int r) const {
+    return static_cast<uint8_t*>(base) + ((sizeof(DxHead) + 4095) & ~(size_t)4095) + (size_t)r * cap;
+  }
+};
+
+DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx) {
+  if (world < 2 || world > DX_MAXW || !hx) return nullptr;
+  uint64_t h = 1469598103934665603ull;
+  for (int i = 0; i < 128; i++) h = (h ^ id[i]) * 1099511628211ull;
+  char nm[64];
+  snprintf(nm, sizeof(nm), "/yrwi-dx-%016llx-%d", (unsigned long long)h, world);
+  // payload bytes per rank (YRWI_DEVX_MB, default 256): the largest round is the
+  // host-count exchange (12 B per distinct (query, host) of the part); untouched
+  // pages of the segment cost nothing
+  const char* e = getenv("YRWI_DEVX_MB");
+  const size_t cap = (size_t)((e ? atof(e) : 256.0) * (double)(1 << 20) + 4095) & ~(size_t)4095;
+  const size_t bytes = ((sizeof(DxHead) + 4095) & ~(size_t)4095) + (size_t)world * cap;
+  const int fd = shm_open(nm, O_CREAT | O_RDWR, 0600);
+  if (fd < 0) return nullptr;
+  if (ftruncate(fd, (off_t)bytes) != 0) {
+    close(fd);
+    return nullptr;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return nullptr;
+  DevX* x = new DevX();
+  x->base = p;
+  x->bytes = bytes;
+  x->cap = cap;
+  x->world = world;
+  x->rank = rank;
+  x->name = nm;
+  x->hx = hx;
+  // posted / done start at the "no round" key (a new segment is zero-filled, and
+  // keys are never 0: see dx_key)
+  if (x->head()->attached.fetch_add(1, std::memory_order_acq_rel) + 1 == world) shm_unlink(nm);
+  return x;
+}
+
+void devx_close(DevX* x, bool unlink_name) {
+  if (!x) return;
+  munmap(x->base, x->bytes);
+  if (unlink_name) shm_unlink(x->name.c_str());
+  delete x;
+}
+
+// the round's key: (batch part, call) -- never 0, so a fresh segment's zeros
+// match no round; unordered callers (no part sequence) count apart
+static int64_t dx_key(Lane* L) {
+  if (L->seq >= 0) return ((L->seq + 1) << 8) | (int64_t)(L->dcall++ & 0xFF);
+  return -(++L->devx->unordered);
+}
+
+// One round: my payload (entries to peers) into my region, wait until every rank
+// posted this key, `take` copies what is mine out of the peers' regions, then
+// signal done and wait until every rank has read (my region is reused next round).
+template <class F>
+static int dx_round(Lane* L, const std::vector<Xfer>& sends, bool all, F take) {
+  DevX* x = L->devx;
+  const int64_t key = dx_key(L), seq = L->seq;
+  DxRank& me = x->head()->r[x->rank];
+  auto gave_up = [&](const char* why) {
+    return L->fail(YRWI_E_RCCL, x->hx && x->hx->aborted(seq) ? "host-staged collective: a peer's batch part failed"
+                                                              : why);
+  };
+  HIPCHK(L, lane_sync(L));  // the payloads are complete
+  uint64_t off = 0;
+  int32_t ne = 0;
+  for (const Xfer& s : sends) {
+    if (ne == DX_MAXE) return L->fail(YRWI_E_RCCL, "host-staged collective: too many peers");
+    if (off + s.bytes > x->cap)
+      return L->fail(YRWI_E_RCCL, "host-staged collective: payload above YRWI_DEVX_MB per rank");
+    if (s.bytes) HIPCHK(L, hipMemcpy(x->region(x->rank) + off, s.ptr, s.bytes, hipMemcpyDeviceToHost));
+    me.ent[ne++] = DxEnt{all ? -1 : s.peer, 0, off, s.bytes};
+    off += (s.bytes + 255) & ~(uint64_t)255;
+  }
+  me.nent = ne;
+  me.posted.store(key, std::memory_order_release);
+  if (!hx_wait(x->hx, seq, [&] {
+        for (int r = 0; r < x->world; r++)
+          if (x->head()->r[r].posted.load(std::memory_order_acquire) != key) return false;
+        return true;
+      }))
+    return gave_up("host-staged collective: a rank never arrived");
+  int rc = take(x);
+  if (!rc && lane_sync(L) != hipSuccess) rc = L->fail(YRWI_E_HIP, "host-staged collective: copy");
+  me.done.store(key, std::memory_order_release);
+  if (!hx_wait(x->hx, seq, [&] {
+        for (int r = 0; r < x->world; r++)
+          if (x->head()->r[r].done.load(std::memory_order_acquire) != key) return false;
+        return true;
+      }))
+    return rc ? rc : gave_up("host-staged collective: a rank never finished reading");
+  return rc;
+}
+
+static int dx_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
+  return dx_round(L, {Xfer{-1, const_cast<void*>(send), bytes}}, true, [&](DevX* x) {
+    for (int p = 0; p < x->world; p++) {
+      const DxRank& q = x->head()->r[p];
+      if (q.nent != 1 || q.ent[0].bytes != bytes) return L->fail(YRWI_E_RCCL, "host-staged all-gather: size mismatch");
+      if (bytes && hipMemcpyAsync(static_cast<uint8_t*>(recv) + (size_t)p * bytes, x->region(p) + q.ent[0].off, bytes,
+                                  hipMemcpyHostToDevice, L->stream) != hipSuccess)
+        return L->fail(YRWI_E_HIP, "host-staged all-gather: copy");
+    }
+    return 0;
+  });
+}
+
+static int dx_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) {
+  return dx_round(L, sends, false, [&](DevX* x) {
+    for (const Xfer& rv : recvs) {
+      if (!rv.bytes) continue;
+      const DxRank& q = x->head()->r[rv.peer];
+      const DxEnt* src = nullptr;
+      for (int i = 0; i < q.nent; i++)
+        if (q.ent[i].peer == L->rank && q.ent[i].bytes) src = &q.ent[i];
+      if (!src || src->bytes != rv.bytes) return L->fail(YRWI_E_RCCL, "host-staged exchange: unmatched receive");
+      if (hipMemcpyAsync(rv.ptr, x->region(rv.peer) + src->off, rv.bytes, hipMemcpyHostToDevice, L->stream) !=
+          hipSuccess)
+        return L->fail(YRWI_E_HIP, "host-staged exchange: copy");
+    }
+    return 0;
+  });
+}
+
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
   if (L->sharded) turn_acquire(L);
   if (!L->sharded) {
@@ -380,6 +550,7 @@ int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
       return L->fail(YRWI_E_HIP, "copy");
     return 0;
   }
+  if (L->devx) return dx_allgather(L, send, recv, bytes);
   if (!L->loop) {
     if (ncclAllGather(send, recv, bytes, ncclChar, L->comm, L->stream) != ncclSuccess)
       return L->fail(YRWI_E_RCCL, "allgather");
@@ -400,7 +571,7 @@ int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes) {
 int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op) {
   if (!L->sharded || n == 0) return 0;
   turn_acquire(L);
-  if (!L->loop) {
+  if (!L->loop && !L->devx) {
     if (ncclAllReduce(buf, buf, n, ncclInt32, max_op ? ncclMax : ncclSum, L->comm, L->stream) != ncclSuccess)
       return L->fail(YRWI_E_RCCL, "allreduce");
     return 0;
@@ -414,6 +585,7 @@ int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op) {
 
 int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) {
   turn_acquire(L);
+  if (L->devx) return dx_exchange(L, sends, recvs);
   if (!L->loop) {
     if (ncclGroupStart() != ncclSuccess) return L->fail(YRWI_E_RCCL, "group");
     for (const Xfer& x : sends)

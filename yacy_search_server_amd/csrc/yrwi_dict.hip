@@ -803,6 +803,7 @@ int ensure_url_ids(CtxBase* ctx) {
   }
   ctx->dict_pending.clear();
   ctx->uid_dirty = false;
+  measure_scratch(ctx);  // what the index leaves for the lanes' scratch
   return 0;
 }
 

@@ -21,6 +21,8 @@ struct DDEntry {
 struct yrwi_event {
   EvDev h{};         // host copy of the device descriptor
   void* mem = nullptr;
+  size_t bytes = 0;  // of mem
+  bool pooled = false;  // order-only event: mem goes back to the context's pool at close
   int32_t k = 0;
   // SearchEvent.doubleDomCache: host hash (url-hash chars 6..11) -> that host's
   // queued entries in ReverseElement order; a host with an empty queue has had
@@ -41,10 +43,83 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// the event entry points may be called from several host threads (YaCy scores
+// remote peers' containers on their own threads): one at a time per context
+#define EVENT_LOCK(ctx) std::lock_guard<std::recursive_mutex> _evlk((ctx)->api_mu)
+
+static void fill_rankq(RankQ& q, const yrwi_profile* prof, const char* language, int64_t now_ms) {
+  if (prof) q.prof = *prof; else yrwi_profile_default(&q.prof);
+  const char* lang = language ? language : "";
+  const size_t ll = std::strlen(lang);
+  q.lang_ok = ll == 2;
+  q.lang[0] = ll > 0 ? (uint8_t)lang[0] : 0;
+  q.lang[1] = ll > 1 ? (uint8_t)lang[1] : 0;
+  q.now_ms = now_ms != 0 ? now_ms
+                         : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::system_clock::now().time_since_epoch()).count();
+  q.want_authority = q.prof.coeff_authority > 12;
+}
+
+extern "C" int yrwi_event_open_order(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms,
+                                     int64_t max_hosts, yrwi_event** out) {
+  if (!ctx || !out || max_hosts < 0) return YRWI_E_ARG;
+  *out = nullptr;
+  EVENT_LOCK(ctx);
+  hipSetDevice(ctx->device);
+  EvDev h{};
+  RankQ& q = h.q;
+  fill_rankq(q, prof, language, now_ms);
+  q.k = 1;
+  // no url set, no stack (yrwi_event_order touches neither): the state and, for an
+  // authority profile, the host table (2 slots per expected host)
+  const int64_t hslots = q.want_authority ? (int64_t)1 << ceil_log2(std::max<int64_t>(2 * max_hosts, 64)) : 1;
+  q.hmask = (uint64_t)(hslots - 1);
+  const size_t o_st = 0, o_hk = align256(sizeof(EvState)), o_hc = o_hk + align256((size_t)hslots * 8);
+  const size_t need = o_hc + align256((size_t)hslots * 4);
+  // device memory from the context's pool of closed order-only events (a hipMalloc
+  // would synchronise the whole device once per SearchEvent)
+  void* mem = nullptr;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->ev_pool_mu);
+    for (size_t i = 0; i < ctx->ev_pool.size(); i++)
+      if (ctx->ev_pool[i].first >= need && ctx->ev_pool[i].first <= 4 * need + (1 << 20)) {
+        bytes = ctx->ev_pool[i].first;
+        mem = ctx->ev_pool[i].second;
+        ctx->ev_pool.erase(ctx->ev_pool.begin() + (std::ptrdiff_t)i);
+        break;
+      }
+  }
+  if (!mem) {
+    if (hipMalloc(&mem, need) != hipSuccess) return ctx->fail(YRWI_E_NOMEM, "event allocation failed");
+    bytes = need;
+  }
+  uint8_t* base = static_cast<uint8_t*>(mem);
+  h.st = reinterpret_cast<EvState*>(base + o_st);
+  q.hkeys = reinterpret_cast<uint64_t*>(base + o_hk);
+  q.hcnt = reinterpret_cast<uint32_t*>(base + o_hc);
+  // zeroed on the order lane's stream, which runs every later call of the event
+  Lane* L = ctx->lanes[0];
+  if (hipMemsetAsync(base, 0, need, L->stream) != hipSuccess) {
+    std::lock_guard<std::mutex> lk(ctx->ev_pool_mu);
+    ctx->ev_pool.emplace_back(bytes, mem);
+    return ctx->fail(YRWI_E_HIP, "event init");
+  }
+  yrwi_event* e = new yrwi_event;
+  e->h = h;
+  e->mem = mem;
+  e->bytes = bytes;
+  e->pooled = true;
+  e->k = 1;
+  *out = e;
+  return 0;
+}
+
 extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms,
                                int32_t k, const yrwi_filter* filter, int64_t max_postings, yrwi_event** out) {
   if (!ctx || !out || k <= 0 || k > YRWI_MAX_K || max_postings < 0) return YRWI_E_ARG;
   *out = nullptr;
+  EVENT_LOCK(ctx);
   if (filter && (filter->nsiteexcludes < 0 || filter->nurlhashes < 0 ||
                  (filter->nsiteexcludes > 0 && !filter->siteexcludes) || (filter->nurlhashes > 0 && !filter->urlhashes)))
     return ctx->fail(YRWI_E_ARG, "filter: bad siteexcludes / urlhashes");
@@ -55,17 +130,8 @@ extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const ch
 
   EvDev h{};
   RankQ& q = h.q;
-  if (prof) q.prof = *prof; else yrwi_profile_default(&q.prof);
-  const char* lang = language ? language : "";
-  const size_t ll = std::strlen(lang);
-  q.lang_ok = ll == 2;
-  q.lang[0] = ll > 0 ? (uint8_t)lang[0] : 0;
-  q.lang[1] = ll > 1 ? (uint8_t)lang[1] : 0;
-  q.now_ms = now_ms != 0 ? now_ms
-                         : (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
-                               std::chrono::system_clock::now().time_since_epoch()).count();
+  fill_rankq(q, prof, language, now_ms);
   q.k = k;
-  q.want_authority = q.prof.coeff_authority > 12;
   std::vector<uint64_t> siteex;
   std::vector<KeyT> seeds;
   if (filter) {
@@ -132,6 +198,7 @@ extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const ch
   yrwi_event* e = new yrwi_event;
   e->h = h;
   e->mem = mem;
+  e->bytes = off;
   e->k = k;
   *out = e;
   return 0;
@@ -139,6 +206,7 @@ extern "C" int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const ch
 
 extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
   if (!ctx || narr < 0 || (narr > 0 && !arr)) return YRWI_E_ARG;
+  EVENT_LOCK(ctx);
   if (narr == 0) return 0;
   for (int32_t i = 0; i < narr; i++) {
     arr[i].rc = 0;
@@ -208,6 +276,7 @@ extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
 extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* rows40, int64_t n, int32_t local,
                                 int64_t* scores) {
   if (!ctx || !ev || n < 0 || n >= ((int64_t)1 << 31) || (n > 0 && (!rows40 || !scores))) return YRWI_E_ARG;
+  EVENT_LOCK(ctx);
   if (n == 0) return 0;
   hipSetDevice(ctx->device);
   drain(ctx);
@@ -248,6 +317,7 @@ extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* ro
 
 extern "C" int yrwi_event_authority(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* hosts6, int32_t n, int32_t* out) {
   if (!ctx || !ev || n < 0 || (n > 0 && (!hosts6 || !out))) return YRWI_E_ARG;
+  EVENT_LOCK(ctx);
   if (n == 0) return 0;
   std::vector<uint64_t> keys((size_t)n);
   for (int32_t i = 0; i < n; i++) {
@@ -278,6 +348,7 @@ extern "C" int yrwi_event_authority(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t
 extern "C" int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
                                  yrwi_event_info* info) {
   if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out)) return YRWI_E_ARG;
+  EVENT_LOCK(ctx);
   hipSetDevice(ctx->device);
   drain(ctx);
   Lane* L = ctx->lanes[0];
@@ -335,6 +406,7 @@ void dd_put(std::vector<DDEntry>& q, const DDEntry& e) {
 extern "C" int yrwi_event_pull(yrwi_ctx* ctx, yrwi_event* ev, int32_t skip_double_dom, yrwi_hit* out, int32_t maxn,
                                int32_t* nout) {
   if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out) || !nout) return YRWI_E_ARG;
+  EVENT_LOCK(ctx);
   *nout = 0;
   hipSetDevice(ctx->device);
   drain(ctx);
@@ -407,7 +479,18 @@ extern "C" int yrwi_event_pull(yrwi_ctx* ctx, yrwi_event* ev, int32_t skip_doubl
 extern "C" void yrwi_event_close(yrwi_ctx* ctx, yrwi_event* ev) {
   if (!ev) return;
   if (ctx) {
+    EVENT_LOCK(ctx);
     hipSetDevice(ctx->device);
+    if (ev->pooled) {
+      // the event's last call synchronised its lane (lanes[0]); its block is reused
+      // by the next order-only event, zeroed on that lane's stream first
+      std::lock_guard<std::mutex> lk(ctx->ev_pool_mu);
+      if (ctx->ev_pool.size() < 64) {
+        ctx->ev_pool.emplace_back(ev->bytes, ev->mem);
+        delete ev;
+        return;
+      }
+    }
     drain(ctx);
     lane_sync(ctx->lanes[0]);
   }

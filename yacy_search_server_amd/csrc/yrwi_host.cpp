@@ -207,6 +207,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
     L->hostreg = &ctx->hostreg;
     L->turn = &ctx->turn;
     L->scratch_hint = &ctx->scratch_hint;
+    L->scratch_total = &ctx->scratch_total;
     L->nlanes = nl;
     L->start_worker();
   }
@@ -262,7 +263,21 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
     ncclUniqueId u;
     std::memcpy(&u, nccl_id, 128);
     ncclComm_t c0 = nullptr;
-    bool ok = ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
+    // YRWI-HOSTSTAGE group ids (tests) skip RCCL for the host-staged transport
+    const bool staged = world > 1 && std::memcmp(nccl_id, STAGE_TAG, sizeof(STAGE_TAG)) == 0;
+    bool ok = !staged && ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
+    if (!ok && world > 1 && ctx->hostx && hostx_attached(ctx->hostx) == world) {
+      // RCCL could not form the group (several ranks on one device: it refuses a
+      // duplicate GPU; the init fails on every rank alike) but every rank mapped
+      // the node's mailbox: the rank phase's device collectives go through host
+      // shared memory (yrwi_coll.cpp, host-staged collectives)
+      if (c0) ncclCommDestroy(c0);
+      ctx->devx = devx_open(nccl_id, world, rank, ctx->hostx);
+      if (ctx->devx) {
+        for (Lane* L : ctx->lanes) L->devx = ctx->devx;
+        return 0;
+      }
+    }
     if (ok) ctx->lanes[0]->comm = c0;
     // the mailbox only works if every rank mapped the same segment (one node, one
     // /dev/shm): every rank opened it before the init above, so after it each
@@ -312,6 +327,10 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   // case some rank never did (ENOENT is harmless)
   hostx_close(ctx->hostx, ctx->rank == 0);
   ctx->hostx = nullptr;
+  devx_close(ctx->devx, ctx->rank == 0);
+  ctx->devx = nullptr;
+  for (auto& b : ctx->ev_pool) hipFree(b.second);
+  ctx->ev_pool.clear();
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
   if (ctx->head_all) hipFree(ctx->head_all);
@@ -2042,13 +2061,30 @@ static int64_t scratch_estimate(const Plan& P) {
 // the estimate depends on the local shard), so they keep one pass per batch.
 static int64_t scratch_budget(const Lane* L) {
   if (L->sharded) return INT64_MAX;
-  // per lane; default 192 GiB shared by the lanes (C4: 16 GiB per lane ran 7 passes
-  // a batch at 10.3 ms/step, 24 GiB 9.86, 32 GiB 9.73 -- the passes' fixed
-  // kernels and syncs; the arenas stayed inside the 288 GB beside the 1 B-posting
-  // index: profiles/r04_scratch_c4.txt)
+  // per lane: YRWI_SCRATCH_GB, else the device memory left beside the resident
+  // index (measured after it was built, ensure_url_ids: free memory + the lanes'
+  // arenas then - 8 GiB headroom) shared by the lanes, at most 192 GiB in all (C4:
+  // 16 GiB per lane ran 7 passes a batch at 10.3 ms/step, 24 GiB 9.86, 32 GiB 9.73
+  // -- the passes' fixed kernels and syncs; profiles/r04_scratch_c4.txt)
   const char* e = getenv("YRWI_SCRATCH_GB");
-  const double gb = e ? atof(e) : 192.0 / (double)std::max(1, L->nlanes);
-  return (int64_t)(std::max(gb, 0.001) * (double)(1ll << 30));
+  if (e) return (int64_t)(std::max(atof(e), 0.001) * (double)(1ll << 30));
+  const int64_t cap = (int64_t)192 << 30;
+  const int64_t tot = L->scratch_total ? L->scratch_total->load() : 0;
+  const int64_t all = tot > 0 ? std::min(tot, cap) : cap;
+  return std::max<int64_t>(all / std::max(1, L->nlanes), (int64_t)256 << 20);
+}
+
+// the scratch budget's base (scratch_budget): device memory free beside the index,
+// dictionary and bitmaps, plus what the lanes' arenas hold now, minus headroom
+void yrwi::measure_scratch(CtxBase* ctx) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  int64_t arenas = 0;
+  for (Lane* L : ctx->lanes) arenas += (int64_t)L->arena.capacity();
+  ctx->scratch_total = std::max<int64_t>((int64_t)fr + arenas - ((int64_t)8 << 30), (int64_t)1 << 30);
 }
 
 static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q, int32_t nq, int32_t kmax,
@@ -2210,6 +2246,7 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   for (int l = 0; l < nl; l++) {
     ctx->lanes[(size_t)l]->seq = seq0 + l;
     ctx->lanes[(size_t)l]->xcall = 0;
+    ctx->lanes[(size_t)l]->dcall = 0;
   }
   auto part = [=, &pst](int l) {
     Lane* L = ctx->lanes[(size_t)l];
@@ -2280,6 +2317,7 @@ extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, 
   ctx->next_ticket++;
   L->seq = ctx->coll_seq++;  // collective order (CollTurn): submission order, the same on every rank
   L->xcall = 0;
+  L->dcall = 0;
   L->submit([=] {
     if (st) std::memset(st, 0, sizeof(*st));
     const int rc = nq == 0 ? 0 : run_batch_part(ctx, L, q, nq, kmax, out, nout, st);

@@ -231,6 +231,7 @@ struct HostRegistry {
 
 struct LoopGroup;  // in-process shard group (yrwi_coll.cpp)
 struct HostX;      // shared-memory mailbox of the node's ranks (yrwi_coll.cpp)
+struct DevX;       // host-staged device collectives of the node's ranks (yrwi_coll.cpp)
 
 // Order of the collectives of concurrently running batch parts (sharded
 // contexts).  Every batch part gets a sequence number in
@@ -263,6 +264,8 @@ struct Lane {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   LoopGroup* loop = nullptr;  // test transport instead of comm (yrwi_coll.cpp)
+  DevX* devx = nullptr;       // host-staged collectives instead of comm (RCCL could not form the group)
+  int32_t dcall = 0;          // host-staged collective rounds of the running part
   hipEvent_t coll_ev[2] = {nullptr, nullptr};
   Stage stage;
   Stage out_stage;           // pinned landing buffer for results
@@ -295,6 +298,9 @@ struct Lane {
   // smaller takes that size at the start of its next pass instead of growing
   // inside it (one allocation, before any of the pass's kernels)
   std::atomic<size_t>* scratch_hint = nullptr;
+  // the scratch the lanes may use together (bytes; 0: not measured yet): device
+  // memory left after the index, dictionary and bitmaps (ensure_url_ids)
+  std::atomic<int64_t>* scratch_total = nullptr;
   // collective order (CollTurn): the running part's sequence number (-1: none,
   // unordered), whether it holds the turn, and whether its last pass passes the
   // turn on right after its final collective
@@ -387,7 +393,9 @@ struct CtxBase {
   CollTurn turn;
   int64_t coll_seq = 0;
   HostX* hostx = nullptr;
+  DevX* devx = nullptr;
   std::atomic<size_t> scratch_hint{0};  // Lane::scratch_hint
+  std::atomic<int64_t> scratch_total{0};  // Lane::scratch_total
   std::mutex st_mu;
   std::unordered_map<int64_t, std::pair<int, std::string>> status;
   std::unordered_map<KeyT, ListRec, KeyHash> lists;
@@ -416,6 +424,11 @@ struct CtxBase {
   int64_t dict_full_builds = 0, dict_incremental = 0;
   std::string err;
   int64_t npostings = 0;
+  // search events (yrwi_event.cpp): their entry points serialise on api_mu; device
+  // blocks of closed order-only events are reused (bytes, pointer)
+  std::recursive_mutex api_mu;
+  std::mutex ev_pool_mu;
+  std::vector<std::pair<size_t, void*>> ev_pool;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -589,6 +602,8 @@ struct Xfer {
 };
 // (re)build the url dictionary and every list's url ids if the index changed
 int ensure_url_ids(CtxBase* ctx);
+// device memory left for the lanes' scratch after the index is resident (CtxBase::scratch_total)
+void measure_scratch(CtxBase* ctx);
 // the list of `term` was added / replaced (added = true) or removed: url ids are due
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added);
 // brings the url ids up to date, then counts inconsistencies (0: every id names its key)
@@ -599,6 +614,9 @@ void hostx_close(HostX* x, bool unlink_name);
 void hostx_abort(HostX* x, int64_t seq);  // batch part `seq` failed: every rank's exchanges of that part fail at once
 int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
+// host-staged device collectives (ranks that share a device: RCCL refuses them)
+DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx);
+void devx_close(DevX* x, bool unlink_name);
 void turn_acquire(Lane* L);  // wait until L's batch part may enqueue collectives (no-op: seq < 0)
 void turn_release(Lane* L);  // pass the turn to the next part (waits for L's turn first); idempotent
 int coll_allgather(Lane* L, const void* send, void* recv, size_t bytes);  // recv: world * bytes, rank order
@@ -606,6 +624,9 @@ int coll_allreduce_i32(Lane* L, int32_t* buf, size_t n, bool max_op);    // in p
 int coll_exchange(Lane* L, const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs);  // grouped send/recv
 // loopback groups: a 128-byte id starting with this tag names an in-process group
 constexpr char LOOP_TAG[] = "YRWI-LOOPBACK";
+// a 128-byte id starting with this tag names a group of processes that share one
+// device: host-staged collectives without trying RCCL first
+constexpr char STAGE_TAG[] = "YRWI-HOSTSTAGE";
 LoopGroup* loop_join(const uint8_t id[128], int world, int rank);
 void loop_leave(LoopGroup* g);
 

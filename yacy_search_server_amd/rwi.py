@@ -150,14 +150,18 @@ class SearchEvent:
     rwiStack persist on the GPU between arrivals (yrwi_event_* in include/yrwi.h)."""
 
     def __init__(self, index: "RWIIndex", profile: Optional[RankingProfile], language: str, now_ms: int, k: int,
-                 filter: Optional[QueryFilter], max_postings: int):
+                 filter: Optional[QueryFilter], max_postings: int, order_only_hosts: Optional[int] = None):
         self._ix = index
         self.k = k
         prof = profile or RankingProfile()
         e = ctypes.c_void_p()
-        fp = ctypes.byref(filter.c) if filter is not None else None
-        _check(index._h, _lib.lib().yrwi_event_open(index._h, ctypes.byref(prof._c), language.encode(), now_ms, k, fp,
-                                                    max_postings, ctypes.byref(e)))
+        if order_only_hosts is not None:  # yrwi_event_open_order: order() / authority() only
+            _check(index._h, _lib.lib().yrwi_event_open_order(index._h, ctypes.byref(prof._c), language.encode(),
+                                                              now_ms, order_only_hosts, ctypes.byref(e)))
+        else:
+            fp = ctypes.byref(filter.c) if filter is not None else None
+            _check(index._h, _lib.lib().yrwi_event_open(index._h, ctypes.byref(prof._c), language.encode(), now_ms, k,
+                                                        fp, max_postings, ctypes.byref(e)))
         self._e = e
 
     def add_rwis(self, rows: np.ndarray, local: bool = False) -> int:
@@ -356,6 +360,12 @@ class RWIIndex:
     def event(self, profile: Optional[RankingProfile] = None, language: str = "en", now_ms: int = 0, k: int = 100,
               filter: Optional[QueryFilter] = None, max_postings: int = 1 << 16) -> "SearchEvent":
         return SearchEvent(self, profile, language, now_ms, k, filter, max_postings)
+
+    def reference_order(self, profile: Optional[RankingProfile] = None, language: str = "en", now_ms: int = 0,
+                        max_hosts: int = 1 << 16) -> "SearchEvent":
+        """A SearchEvent's ReferenceOrder alone (yrwi_event_open_order, what
+        GpuReferenceOrder holds): order() and authority(); no url set, no stack."""
+        return SearchEvent(self, profile, language, now_ms, 1, None, 0, order_only_hosts=max_hosts)
 
     def add_rwis(self, arrivals: Sequence[Tuple["SearchEvent", np.ndarray, bool]]) -> List[int]:
         """Applies (event, rows (n, 40) uint8, local) arrivals in order, events in
