@@ -151,8 +151,8 @@ typedef struct yrwi_stats {
      their number and device time (HIP events around each) */
   int64_t n_probe_dispatches;
   int64_t t_probe_all_ns;
-  /* rank phase, per pass: k_reduce + k_shard_fin (one launch each) and the k_score launches, HIP events
-     around each group; the bytes their kernels must read: k_reduce the 32-B ranking record of every
+  /* rank phase, per pass: the k_reduce launch and the k_score launches (k_shard_fin / k_score_full
+     excluded: the populations rocprofv3 averages), HIP events around each; the bytes their kernels must read: k_reduce the 32-B ranking record of every
      joined row (+ its 1-B exclusion mark), k_score the same records (an upper bound: chunks pruned by
      the per-query threshold read only words 2-3) */
   int64_t n_rank_passes;

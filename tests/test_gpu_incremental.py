@@ -10,21 +10,32 @@ import numpy as np
 import pytest
 
 import oracle as orc
-from yacy_search_server_amd import Query, RWIIndex, synth
+from yacy_search_server_amd import Query, RankingProfile, RWIIndex, synth
 
 pytestmark = pytest.mark.gpu
 
 NOW = 20741 * 86400000 + 777
 
 
+# every other query under an authority profile: its host counts key on the dense
+# host ids the index records carry (ensure_host_ids), rebuilt after every change
+C5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+
+
+def _batch(qs, hashes):
+    return [Query([hashes[t] for t in inc], [hashes[t] for t in exc], now_ms=NOW, k=50,
+                  profile=(C5 if i % 2 else None)) for i, (inc, exc) in enumerate(qs)]
+
+
 def _results(ix, lists, qs, hashes, fresh=None):
-    batch = [Query([hashes[t] for t in inc], [hashes[t] for t in exc], now_ms=NOW, k=50) for inc, exc in qs]
+    batch = _batch(qs, hashes)
     got = [[(h.urlhash, h.score, h.tiebreak) for h in r] for r in ix.search_batch(batch)]
     if fresh is not None:
         assert got == fresh
     for qi, (inc, exc) in enumerate(qs):
         d = {hashes[t]: lists[hashes[t]] for t in inc + exc if hashes[t] in lists}
-        assert got[qi] == orc.search(d, batch[qi].include, batch[qi].exclude, now_ms=NOW, k=50), qi
+        prof = orc.profile_from(C5) if qi % 2 else None
+        assert got[qi] == orc.search(d, batch[qi].include, batch[qi].exclude, profile=prof, now_ms=NOW, k=50), qi
     return got
 
 
@@ -36,8 +47,7 @@ def _fresh(lists, qs, hashes, monkeypatch):
             ix.add(h, r)
         bad, nurls = ix.check_url_ids()
         assert bad == 0
-        batch = [Query([hashes[t] for t in inc], [hashes[t] for t in exc], now_ms=NOW, k=50) for inc, exc in qs]
-        return [[(h.urlhash, h.score, h.tiebreak) for h in r] for r in ix.search_batch(batch)], nurls
+        return [[(h.urlhash, h.score, h.tiebreak) for h in r] for r in ix.search_batch(_batch(qs, hashes))], nurls
     finally:
         ix.close()
         monkeypatch.delenv("YRWI_DICT_FULL")

@@ -745,10 +745,120 @@ int repack_index(CtxBase* ctx, bool force) {
   return 0;
 }
 
+// ------------------------------------------------------------ dense host ids
+// Authority (ReferenceOrder.java:176-216) counts the joined postings per host.
+// Every url id's host hash (its key's low 36 bits) gets a dense id (the rank of
+// the host among the context's distinct hosts), and every index record carries
+// its url's id in word 3 (bits 34..63): the host counts then key on a field of
+// the record the ranking kernels already read, instead of gathering each
+// posting's url key from the dictionary (two random lines per posting).
+__global__ void k_host_keys(const uint64_t* __restrict__ dh, const uint8_t* __restrict__ dl, int64_t n,
+                            uint64_t* __restrict__ hk, uint32_t* __restrict__ idx) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n) return;
+  hk[u] = ((dh[u] & 0xFFFFFFFull) << 8) | (uint64_t)dl[u];
+  idx[u] = (uint32_t)u;
+}
+__global__ void k_host_flags(const uint64_t* __restrict__ hk, int64_t n, uint32_t* __restrict__ flag) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) flag[j] = (j == 0 || hk[j] != hk[j - 1]) ? 1u : 0u;
+}
+__global__ void k_host_scatter(const uint64_t* __restrict__ hk, const uint32_t* __restrict__ idx,
+                               const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rank1, int64_t n,
+                               uint32_t* __restrict__ hid, uint64_t* __restrict__ host_key) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t h = rank1[j] - 1u;
+  hid[idx[j]] = h;
+  if (flag[j]) host_key[h] = hk[j];
+}
+struct StampSeg {
+  const uint32_t* uid;
+  uint64_t* feat;
+};
+__global__ void k_host_stamp(const StampSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
+                             const uint32_t* __restrict__ hid) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = seg_of(off, nseg, i);
+  const int64_t j = i - off[s];
+  uint64_t* w3 = segs[s].feat + j * FEAT_WORDS + 3;
+  *w3 = (*w3 & 0x3FFFFFFFFull) | (uint64_t)hid[segs[s].uid[j]] << 34;
+}
+
 }  // namespace
+
+int ensure_host_ids(CtxBase* ctx) {
+  if (ctx->host_ids || ctx->uid_dirty || ctx->nurls <= 0) return 0;
+  hipStream_t st = ctx->stream;
+  const int64_t n = ctx->nurls;
+  if (n > (int64_t)INT32_MAX) return 0;  // (the key path serves)
+  DevBuf bhk, bhk2, bidx, bidx2, bflag, brank, bhid, btmp;
+  uint64_t* hk = bhk.get<uint64_t>((size_t)n);
+  uint64_t* hk2 = bhk2.get<uint64_t>((size_t)n);
+  uint32_t* idx = bidx.get<uint32_t>((size_t)n);
+  uint32_t* idx2 = bidx2.get<uint32_t>((size_t)n);
+  uint32_t* flag = bflag.get<uint32_t>((size_t)n);
+  uint32_t* rank1 = brank.get<uint32_t>((size_t)n);
+  uint32_t* hid = bhid.get<uint32_t>((size_t)n);
+  if (!hk || !hk2 || !idx || !idx2 || !flag || !rank1 || !hid) return ctx->fail(YRWI_E_NOMEM, "host id scratch");
+  hipLaunchKernelGGL(k_host_keys, dim3(nb(n)), dim3(256), 0, st, ctx->dkhi, ctx->dklo, n, hk, idx);
+  size_t t1 = 0, t2 = 0;
+  const int ni = (int)n;
+  HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, hk, hk2, idx, idx2, ni, 0, 36, st));
+  HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, t2, flag, rank1, ni, st));
+  void* tmp = btmp.get<uint8_t>(std::max(t1, t2));
+  if (!tmp) return ctx->fail(YRWI_E_NOMEM, "host id scratch");
+  HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t1, hk, hk2, idx, idx2, ni, 0, 36, st));
+  hipLaunchKernelGGL(k_host_flags, dim3(nb(n)), dim3(256), 0, st, hk2, n, flag);
+  HIPCHK(ctx, hipcub::DeviceScan::InclusiveSum(tmp, t2, flag, rank1, ni, st));
+  uint32_t nh = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&nh, rank1 + (n - 1), 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (nh >= (1u << 30)) return 0;  // ids must fit the record's 30 bits (the key path serves)
+  if ((size_t)nh > ctx->host_key_cap) {
+    if (ctx->host_key) hipFree(ctx->host_key);
+    ctx->host_key = nullptr;
+    ctx->host_key_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->host_key), (size_t)nh * 8) != hipSuccess)
+      return ctx->fail(YRWI_E_NOMEM, "host key table");
+    ctx->host_key_cap = nh;
+  }
+  hipLaunchKernelGGL(k_host_scatter, dim3(nb(n)), dim3(256), 0, st, hk2, idx2, flag, rank1, n, hid, ctx->host_key);
+  std::vector<StampSeg> segs;
+  std::vector<int64_t> off;
+  int64_t np = 0;
+  for (auto& kv : ctx->lists) {
+    const ListRec& L = kv.second;
+    if (L.n == 0 || !L.feat || !L.uid) continue;
+    segs.push_back({L.uid, L.feat});
+    off.push_back(np);
+    np += L.n;
+  }
+  DevBuf bsegs, boff;
+  if (np > 0) {
+    StampSeg* d_segs = bsegs.get<StampSeg>(segs.size());
+    int64_t* d_off = boff.get<int64_t>(off.size());
+    if (!d_segs || !d_off) return ctx->fail(YRWI_E_NOMEM, "host id scratch");
+    HIPCHK(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(StampSeg), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_host_stamp, dim3(nb(np)), dim3(256), 0, st, d_segs, d_off, (int)segs.size(), np, hid);
+  }
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));  // scratch is freed on return
+  ctx->nhosts = nh;
+  ctx->host_ids = true;
+  for (Lane* L : ctx->lanes) {
+    L->host_ids = true;
+    L->host_key = ctx->host_key;
+  }
+  return 0;
+}
 
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
   ctx->uid_dirty = true;
+  ctx->host_ids = false;  // a new list's records carry no host ids; new urls may bring new hosts
+  for (Lane* L : ctx->lanes) L->host_ids = false;
   ctx->dict_churn += old_n;
   if (added) ctx->dict_pending.insert(term);
   else ctx->dict_pending.erase(term);

@@ -331,6 +331,7 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   ctx->devx = nullptr;
   for (auto& b : ctx->ev_pool) hipFree(b.second);
   ctx->ev_pool.clear();
+  if (ctx->host_key) hipFree(ctx->host_key);
   ctx->index_mem.release();
   if (ctx->uid_all) hipFree(ctx->uid_all);
   if (ctx->head_all) hipFree(ctx->head_all);
@@ -1580,7 +1581,8 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   HIPCHK(ctx, hipMemsetAsync(d_ocnt, 0, W * 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(d_gmax, 0, nq * 4, ctx->stream));
   if (upload(ctx, d_sb, slot_base)) return YRWI_E_HIP;
-  if (launch_host_count(d_hkeys, nslots, W, d_ocnt, ctx->stream)) return ctx->fail(YRWI_E_HIP, "host count");
+  const uint64_t* hkey = ctx->host_ids ? ctx->host_key : nullptr;  // tables of dense host ids (run_rank_phase)
+  if (launch_host_count(d_hkeys, nslots, W, d_ocnt, ctx->stream, hkey)) return ctx->fail(YRWI_E_HIP, "host count");
   if (int rc = coll_allgather(ctx, d_ocnt, d_M, (size_t)W * 4)) return rc;
   const uint8_t* hm = readback(ctx, &ctx->down_stage, d_M, (int64_t)W * W, 4, 4);
   if (!hm) return YRWI_E_HIP;
@@ -1611,7 +1613,7 @@ static int exchange_host_counts(Lane* ctx, int nq, int64_t nslots, const std::ve
   if (upload(ctx, d_cur, cur)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_okeys, 0, ocap * 8, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(d_ovals, 0, ocap * 4, ctx->stream));
-  if (launch_host_pack(d_hkeys, d_hcnt, d_sb, nq, nslots, W, d_cur, d_send, d_sslot, ctx->stream))
+  if (launch_host_pack(d_hkeys, d_hcnt, d_sb, nq, nslots, W, d_cur, d_send, d_sslot, ctx->stream, hkey))
     return ctx->fail(YRWI_E_HIP, "host pack");
   {
     std::vector<Xfer> snd, rcv;
@@ -1676,6 +1678,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.want_authority = P.prof.coeff_authority > 12 && R.n > 0;
     R.idx_tag = shx ? (uint32_t)ctx->rank << 28 : 0u;
     R.doubledom = P.filter && P.filter->skip_double_dom ? 1 : 0;
+    R.host_rec = ctx->host_ids && P.cont.uid != nullptr ? 1 : 0;  // index records: dense host ids
     R.kout = P.k;
     if (R.doubledom) R.k = YRWI_MAX_K;  // pullOneRWI draws from the whole rwiStack (max_results_rwi)
     // identical on every rank (same queries): decides the collective host-count exchange
@@ -1792,9 +1795,11 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream)) return ctx->fail(YRWI_E_HIP, "reduce launch");
+  hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid))
+    return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
-  if (tm) tm->kreduce.push_back(tm->spans.back());
+  if (tm) tm->kreduce.push_back({sp, rmid});  // k_reduce alone: the population rocprofv3 averages
   if (st) {
     st->n_rank_passes++;
     for (int qi = 0; qi < nq; qi++) {
@@ -1868,11 +1873,12 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   // start with a threshold, measured 39 + 86 us against 99 us for one launch:
   // the seed launch is one round of full-length blocks)
   const int64_t seed = 0;
+  hipEvent_t smid = tm ? ctx->event() : nullptr;  // after the k_score launches, before k_score_full
   if (launch_score(d_q, d_cq, d_order, nq, chunks, seed, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq,
-                   ctx->stream))
+                   ctx->stream, smid))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
-  if (tm) tm->kscore.push_back(tm->spans.back());
+  if (tm) tm->kscore.push_back({sp, smid});  // the k_score launches alone
   mark(4);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
@@ -2224,6 +2230,13 @@ void yrwi::drain(CtxBase* ctx) {
   for (Lane* L : ctx->lanes) L->wait();
 }
 
+// an authority profile in the batch (ReferenceOrder.cardinal, coeff_authority > 12)
+static bool wants_authority(const yrwi_query_desc* q, int32_t nq) {
+  for (int32_t i = 0; i < nq; i++)
+    if (q[i].profile && q[i].profile->coeff_authority > 12) return true;
+  return false;
+}
+
 extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq, int32_t kmax, yrwi_hit* out,
                                 int32_t* nout, yrwi_stats* st) {
   if (int rc = check_batch_args(ctx, q, nq, kmax, out, nout)) return rc;
@@ -2234,6 +2247,8 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
   hipSetDevice(ctx->device);
   drain(ctx);
   if (int rc = ensure_url_ids(ctx)) return rc;
+  if (wants_authority(q, nq))
+    if (int rc = ensure_host_ids(ctx)) return rc;
   const int64_t t0 = now_ns();
   // contiguous parts of equal query count, one per lane, each planned and run
   // by its lane's thread (every rank splits a sharded batch identically)
@@ -2310,6 +2325,10 @@ extern "C" int yrwi_query_batch_submit(yrwi_ctx* ctx, const yrwi_query_desc* q, 
   if (ctx->uid_dirty) {  // the index changed: nothing can be in flight (put_list drained)
     drain(ctx);
     if (int rc = ensure_url_ids(ctx)) return rc;
+  }
+  if (!ctx->host_ids && wants_authority(q, nq)) {  // the first authority batch since the index changed
+    drain(ctx);
+    if (int rc = ensure_host_ids(ctx)) return rc;
   }
   const int64_t t = ctx->next_ticket;
   Lane* L = ctx->lanes[(size_t)(t % (int64_t)ctx->lanes.size())];

@@ -275,6 +275,9 @@ struct Lane {
   int64_t nurls = 0;         // url ids of the context's dictionary (set with dkhi)
   const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
   const uint8_t* dklo = nullptr;
+  // the index records carry dense host ids (ensure_host_ids); host_key[id] = the host hash
+  bool host_ids = false;
+  const uint64_t* host_key = nullptr;
   Arena arena{(size_t)256 << 20};
   std::string err;
   std::vector<hipEvent_t> evpool;
@@ -413,6 +416,14 @@ struct CtxBase {
   uint8_t* dklo = nullptr;
   size_t dict_cap = 0;
   int64_t nurls = 0;
+  // dense host ids (authority host counts, yrwi_dict.hip ensure_host_ids): every
+  // index record carries its url's host id; host_key[id] = the host hash (url-hash
+  // chars 6..11, 36 bits).  Built on the first authority batch after an index
+  // change, dropped by any change.
+  bool host_ids = false;
+  uint64_t* host_key = nullptr;
+  size_t host_key_cap = 0;
+  int64_t nhosts = 0;
   // incremental maintenance (yrwi_dict.hip): lists added or replaced since the
   // dictionary was last brought up to date; keys of removed postings stay in it
   // (an id without postings changes no join) until the next full rebuild
@@ -604,6 +615,8 @@ struct Xfer {
 int ensure_url_ids(CtxBase* ctx);
 // device memory left for the lanes' scratch after the index is resident (CtxBase::scratch_total)
 void measure_scratch(CtxBase* ctx);
+// dense host ids in every index record (after ensure_url_ids; no batch in flight)
+int ensure_host_ids(CtxBase* ctx);
 // the list of `term` was added / replaced (added = true) or removed: url ids are due
 void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added);
 // brings the url ids up to date, then counts inconsistencies (0: every id names its key)

@@ -73,7 +73,8 @@ __host__ __device__ constexpr int64_t heads_cap(int64_t n) { return head1_cap(n)
 //   w1 = r | o << 8 | i << 16 | x << 24 | y << 32 | m << 40 | n << 48 | d << 56
 //        posinphrase, posofphrase, worddistance, llocal, lother, urllength, urlcomps, doctype
 //   w2 = a | l << 16 | z << 32          lastModified days, language (byte 22 low), flags (byte 29 low)
-//   w3 = h | dl << 32                   ByteArray.hashCode(urlhash), domLengthEstimation key (ahpla[urlhash[11]] & 3)
+//   w3 = h | dl << 32 | host << 34      ByteArray.hashCode(urlhash), domLengthEstimation key (ahpla[urlhash[11]] & 3),
+//                                       the url's dense host id in the context (ensure_host_ids; 0 until built)
 // The J5 inputs of the joined side (t w p u c r o) are words 0 and 1.
 constexpr int FEAT_WORDS = 4;
 constexpr int FEAT_BYTES = 8 * FEAT_WORDS;
@@ -288,7 +289,7 @@ struct RankQ {
   int32_t kout;            // results wanted (k is the stack bound: 3000 with doubledom)
   const FilterQ* filt;     // addRWIs constraints or nullptr
   int32_t doubledom;       // results in pullOneRWI(skipDoubleDom) order
-  int32_t pad2;
+  int32_t host_rec;        // the records carry their url's dense host id (w3 >> 34): the host tables key on it
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -317,9 +318,12 @@ int launch_copy_in(const CopyIn& c, void* stream);
 // device -> pinned host readback (dst: device address of pinned host memory): n
 // elements of `elem` bytes, the source's `stride` bytes apart (4-B words when aligned)
 int launch_gather_out(uint8_t* dst, const uint8_t* src, int64_t n, int32_t elem, int64_t stride, void* stream);
-int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* stream);
+// host_key (nullptr: the tables hold host hashes): the tables hold dense host ids + 1, host_key[id] = host hash
+int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* stream,
+                      const uint64_t* host_key = nullptr);
 int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
-                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* stream);
+                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* stream,
+                     const uint64_t* host_key = nullptr);
 int launch_host_owner(const HostMsg* recv, int64_t nrecv, uint64_t* okeys, uint32_t* ocnt, uint64_t omask,
                       int32_t* gmax, uint32_t* reply, void* stream);
 int launch_host_apply(const uint32_t* back, const uint64_t* send_slot, int64_t n, uint32_t* hcnt_all,
@@ -382,13 +386,14 @@ int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
-                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* stream);
+                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* stream,
+                 void* ev_mid = nullptr);
 // candidates one k_topq group may hold (lists per group = min(64, capacity / list stride))
 int topq_capacity(int32_t keff);
 // top-k of candidate-list groups: group g = lists [gbase[g], gbase[g]+gn[g]) of d_in (stride

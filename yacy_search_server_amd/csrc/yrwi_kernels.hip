@@ -436,6 +436,16 @@ __device__ __forceinline__ void key_at(const RankQ& Q, int64_t e, uint64_t& hi, 
 __device__ __forceinline__ uint64_t key_host36(uint64_t hi, uint32_t lo) {
   return ((hi & 0xFFFFFFFull) << 8) | (lo & 0xFFu);
 }
+// the host of container element e (record q) as the authority host tables key it
+// (host_count adds 1): the dense host id its record carries (Q.host_rec, no url
+// key gathered), or the host hash of its url key
+__device__ __forceinline__ uint64_t elem_host(const RankQ& Q, uint64_t w3, int64_t e) {
+  if (Q.host_rec) return w3 >> 34;
+  uint64_t hi;
+  uint32_t lo;
+  key_at(Q, e, hi, lo);
+  return key_host36(hi, lo);
+}
 
 // =========================================================== join: partition
 // One thread per merge tile: the merge-path split of the tile's first and last
@@ -2258,10 +2268,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
       if (Q.want_authority) {
-        uint64_t khi;
-        uint32_t klo;
-        key_at(Q, e, khi, klo);
-        const uint64_t key = key_host36(khi, klo) + 1;
+        const uint64_t key = elem_host(Q, rg[s % RED_GROUP].w[3], e) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
           // (a plain read before the compare-and-swap, to skip it for hosts already
@@ -3290,9 +3297,10 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
       const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
       if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
     }
-    if (!F && Q.want_authority) key_at(Q, e, khi, klo);
+    if (!F && Q.want_authority && !Q.host_rec) key_at(Q, e, khi, klo);
     const Feat t = decode_rec(q);
-    const int32_t hc = Q.want_authority ? host_count(Q, key_host36(khi, klo)) : 0;
+    const int32_t hc =
+        Q.want_authority ? host_count(Q, Q.host_rec ? q.w[3] >> 34 : key_host36(khi, klo)) : 0;
     a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
     if (a[s] < T) {
       a[s] = 0;
@@ -3946,14 +3954,9 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
   for (int s = threadIdx.x; s < CHUNK; s += blockDim.x) {
     const int64_t e = c * CHUNK + s;
     if (e >= Q.n) break;
-    const Feat t = decode_rec(load_rec(Q.feat, e));
-    int32_t hc = 0;
-    if (Q.want_authority) {
-      uint64_t khi;
-      uint32_t klo;
-      key_at(Q, e, khi, klo);
-      hc = host_count(Q, key_host36(khi, klo));
-    }
+    const Rec q = load_rec(Q.feat, e);
+    const Feat t = decode_rec(q);
+    const int32_t hc = Q.want_authority ? host_count(Q, elem_host(Q, q.w[3], e)) : 0;
     out[e] = cardinal(t, N, Q, hc);
   }
 }
@@ -3966,21 +3969,27 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t key, int world) {
   return (uint32_t)((mix64(key ^ 0x5BD1E995ull) >> 32) % (uint64_t)world);
 }
 
+// a host table's slot key as the exchange names hosts (host hash + 1): tables of
+// dense host ids (host_key != nullptr) translate theirs
+__device__ __forceinline__ uint64_t slot_host(uint64_t k, const uint64_t* __restrict__ host_key) {
+  return (k && host_key) ? host_key[k - 1] + 1 : k;
+}
+
 __global__ void k_host_count(const uint64_t* __restrict__ hkeys, int64_t nslots, int world,
-                             uint32_t* __restrict__ owner_cnt) {
+                             uint32_t* __restrict__ owner_cnt, const uint64_t* __restrict__ host_key) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nslots) return;
-  const uint64_t k = hkeys[i];
+  const uint64_t k = slot_host(hkeys[i], host_key);
   if (k) atomicAdd(&owner_cnt[owner_of(k, world)], 1u);
 }
 
 __global__ void k_host_pack(const uint64_t* __restrict__ hkeys, const uint32_t* __restrict__ hcnt,
                             const int64_t* __restrict__ slot_base, int nq, int64_t nslots, int world,
                             uint32_t* __restrict__ cursor, HostMsg* __restrict__ send,
-                            uint64_t* __restrict__ send_slot) {
+                            uint64_t* __restrict__ send_slot, const uint64_t* __restrict__ host_key) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nslots) return;
-  const uint64_t k = hkeys[i];
+  const uint64_t k = slot_host(hkeys[i], host_key);
   if (!k) return;
   const int q = find_job(slot_base, nq, i);
   const uint32_t pos = atomicAdd(&cursor[owner_of(k, world)], 1u);
@@ -4196,16 +4205,19 @@ int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njob
 
 static inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
-int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* st) {
-  if (nslots > 0) hipLaunchKernelGGL(k_host_count, dim3(nblk(nslots)), dim3(256), 0, S(st), hkeys, nslots, world, owner_cnt);
+int launch_host_count(const uint64_t* hkeys, int64_t nslots, int world, uint32_t* owner_cnt, void* st,
+                      const uint64_t* host_key) {
+  if (nslots > 0)
+    hipLaunchKernelGGL(k_host_count, dim3(nblk(nslots)), dim3(256), 0, S(st), hkeys, nslots, world, owner_cnt, host_key);
   return rc(hipGetLastError());
 }
 
 int launch_host_pack(const uint64_t* hkeys, const uint32_t* hcnt, const int64_t* slot_base, int nq, int64_t nslots,
-                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* st) {
+                     int world, uint32_t* cursor, HostMsg* send, uint64_t* send_slot, void* st,
+                     const uint64_t* host_key) {
   if (nslots > 0)
     hipLaunchKernelGGL(k_host_pack, dim3(nblk(nslots)), dim3(256), 0, S(st), hkeys, hcnt, slot_base, nq, nslots, world,
-                       cursor, send, send_slot);
+                       cursor, send, send_slot, host_key);
   return rc(hipGetLastError());
 }
 
@@ -4238,10 +4250,11 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid) {
   if (total_chunks > 0)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
+  if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // k_reduce alone (statistics)
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
 }
@@ -4254,7 +4267,7 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
-                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* st) {
+                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* st, void* ev_mid) {
   if (total_chunks <= 0) return 0;
   // seed_chunks (0 < seed < total): the first chunks of `order` run as a launch of
   // their own, so every later chunk starts with its query's threshold set
@@ -4264,6 +4277,7 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_or
   if (s0 < total_chunks)
     hipLaunchKernelGGL(k_score, dim3((unsigned)(total_chunks - s0)), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_order + 2 * s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+  if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // the k_score launches alone (statistics)
   const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
   hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
                      d_cand_cnt, kc, d_redo, d_nredo);
