@@ -56,9 +56,13 @@ def _rank_main(rank, world, uid, out_q):
 
 
 @pytest.mark.parametrize("world,transport", [(2, "auto"), (2, "staged"), (4, "staged")])
-def test_sharded_query_on_one_gpu(world, transport):
+def test_sharded_query_on_one_gpu(world, transport, monkeypatch):
+    import queue
+    import time
     import torch.multiprocessing as mp
     from yacy_search_server_amd import unique_id
+    # a rank that fails must not leave its peers waiting out the default 300 s
+    monkeypatch.setenv("YRWI_HOSTX_TIMEOUT_S", "30")
     uid = unique_id() if transport == "auto" else b"YRWI-HOSTSTAGE\0" + os.urandom(113)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -66,12 +70,17 @@ def test_sharded_query_on_one_gpu(world, transport):
     for p in procs:
         p.start()
     res = []
-    for _ in procs:
-        res.append(q.get(timeout=300))
+    deadline = time.time() + 90
+    try:
+        for _ in procs:
+            res.append(q.get(timeout=max(1.0, deadline - time.time())))
+    except queue.Empty:
+        pass
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=max(1.0, deadline + 10 - time.time()))
         if p.is_alive():
             p.kill()
+    assert len(res) == world, ("ranks that never reported", res)
     for rank, status, info in res:
         assert status == "ok", (rank, info)
         assert info == [], (rank, info)

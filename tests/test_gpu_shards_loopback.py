@@ -287,3 +287,40 @@ def test_loopback_many_batches_in_flight(world, hostx, monkeypatch):
                for inc, exc in qs]
         for r in range(world):
             assert [[(h.urlhash, h.score, h.tiebreak) for h in g] for g in res[r][i]] == exp, (r, i)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_count_first_four_terms(world, monkeypatch):
+    """4-term chained folds counted first (YRWI_CHAIN_CF=2 forces it; J2 puts the
+    int-wrapped big lists first in C4's real queries): lists 0..2 with url-id
+    bitmaps count |list 0 x list 1| and |list 0 x list 1 x list 2| by popcounts and
+    the chain starts from list 3.  Whether every shard has those bitmaps is decided
+    in the planning exchange (Plan::inc_allbm), so all ranks take the same fold;
+    the counts are summed over the shards.  Bit-exact against the oracle, with the
+    authority profile and an exclude term in some queries."""
+    monkeypatch.setenv("YRWI_CHAIN_CF", "2")
+    full = synth.preset("small" if world == 2 else "C1")  # big lists hold >= 4096 postings on every shard
+    whole_ix = synth.build_index(full)
+    whole, H = whole_ix.as_dict(), whole_ix.hashes
+    parts = [synth.build_index(full.shard(r, world)).as_dict() for r in range(world)]
+    big = [int(t) for t in np.argsort(-whole_ix.sizes)[:7]]
+    # the bitmap lists (>= 4096 postings on every shard: build_bitmaps' floor)
+    assert all(len(parts[r][H[t]]) >= 4096 for r in range(world) for t in big[:5])
+    rng = np.random.default_rng(11)
+    cases = []
+    for i in range(16):
+        inc = [int(x) for x in rng.choice(big[:5], 3, replace=False)] + [int(rng.choice(big[5:]))]
+        exc = [int(rng.choice([t for t in big if t not in inc]))] if i % 4 == 3 else []
+        cases.append((inc, exc))
+    c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
+
+    def fn(r, ix):
+        return ix.search_batch([Query([H[t] for t in inc], [H[t] for t in exc], now_ms=NOW, k=100,
+                                      profile=(c5 if i % 2 else None)) for i, (inc, exc) in enumerate(cases)])
+
+    res = _run_parts(parts, world, fn)
+    for i, (inc, exc) in enumerate(cases):
+        exp = orc.search(whole, [H[t] for t in inc], [H[t] for t in exc],
+                         profile=(orc.profile_from(c5) if i % 2 else None), now_ms=NOW, k=100)
+        for r in range(world):
+            assert [(h.urlhash, h.score, h.tiebreak) for h in res[r][i]] == exp, (r, i)

@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "yrwi_host.h"
@@ -230,6 +231,17 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank) {
 }
 
 int hostx_attached(const HostX* x) { return x ? x->head()->attached.load(std::memory_order_acquire) : 0; }
+
+// wait (up to limit_s) until every rank of the group mapped the mailbox; false on timeout
+bool hostx_wait_attached(const HostX* x, double limit_s) {
+  if (!x) return false;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hostx_attached(x) < x->world) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) return false;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  return true;
+}
 
 void hostx_abort(HostX* x, int64_t seq) {
   if (x && seq >= 0) x->head()->aborted[seq % HX_ABORTS].store(seq + 1, std::memory_order_release);

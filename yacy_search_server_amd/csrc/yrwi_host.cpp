@@ -266,7 +266,9 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
     // YRWI-HOSTSTAGE group ids (tests) skip RCCL for the host-staged transport
     const bool staged = world > 1 && std::memcmp(nccl_id, STAGE_TAG, sizeof(STAGE_TAG)) == 0;
     bool ok = !staged && ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
-    if (!ok && world > 1 && ctx->hostx && hostx_attached(ctx->hostx) == world) {
+    // (a staged group has had no rendezvous yet: wait for the peers to map the
+    // mailbox; after a failed RCCL init they have, the init met them)
+    if (!ok && world > 1 && ctx->hostx && hostx_wait_attached(ctx->hostx, staged ? 120.0 : 10.0)) {
       // RCCL could not form the group (several ranks on one device: it refuses a
       // duplicate GPU; the init fails on every rank alike) but every rank mapped
       // the node's mailbox: the rank phase's device collectives go through host
@@ -741,23 +743,26 @@ static int plan_batch(Lane* L, std::vector<Plan>& plans) {
   if (!L->sharded) {  // one context: its own sizes are the global ones
     for (Plan& P : plans) {
       int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
+      for (int i = 0; i < P.ninc; i++) P.inc_allbm[i] = !P.has_sel && P.linc[i] && P.linc[i]->bm;
       for (int i = 0; i < P.ninc; i++) gi[i] = inc_n(P, i);
       for (int i = 0; i < P.nexc; i++) ge[i] = exc_n(P, i);
       plan_finish(&P, gi, ge);
     }
     return 0;
   }
+  // every slot carries size * 128 + (this shard's list has a url-id bitmap): the
+  // sum over the shards is the global size * 128 + the shards with a bitmap (< 128)
   std::unordered_map<KeyT, size_t, KeyHash> slot;
   std::vector<int64_t> sz;
   auto slot_of = [&](const KeyT& k, const ListRec* l) {
     auto it = slot.find(k);
     if (it != slot.end()) return it->second;
     slot.emplace(k, sz.size());
-    sz.push_back(l ? l->n : 0);
+    sz.push_back(l ? l->n * 128 + (l->bm ? 1 : 0) : 0);
     return sz.size() - 1;
   };
   auto own_slot = [&](int64_t n) {  // a selection query's restricted size: a slot of its own
-    sz.push_back(n);
+    sz.push_back(n * 128);
     return sz.size() - 1;
   };
   // first-appearance order over the batch's queries: identical on every rank
@@ -773,8 +778,12 @@ static int plan_batch(Lane* L, std::vector<Plan>& plans) {
   for (size_t q = 0; q < plans.size(); q++) {
     Plan& P = plans[q];
     int64_t gi[YRWI_MAX_TERMS], ge[YRWI_MAX_TERMS];
-    for (int i = 0; i < P.ninc; i++) gi[i] = sz[idx[q][(size_t)i]];
-    for (int i = 0; i < P.nexc; i++) ge[i] = sz[idx[q][(size_t)(YRWI_MAX_TERMS + i)]];
+    for (int i = 0; i < P.ninc; i++) {
+      const int64_t v = sz[idx[q][(size_t)i]];
+      gi[i] = v >> 7;
+      P.inc_allbm[i] = !P.has_sel && (v & 127) == L->world;
+    }
+    for (int i = 0; i < P.nexc; i++) ge[i] = sz[idx[q][(size_t)(YRWI_MAX_TERMS + i)]] >> 7;
     plan_finish(&P, gi, ge);
   }
   return 0;
@@ -1321,7 +1330,10 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     // the survivors are chained from list 2 (probing list 0, then testing list 1)
     // (t = 4 too: the chain's first test, list 1, leaves |list 0..2| -- step 2's
     // dispatch -- and list 3 follows)
-    P.cf3 = cf_mode != 0 && t == 4 && !ns && !ctx->sharded && P.seq[0]->bm && P.seq[1]->bm && P.seq[2]->bm &&
+    // (lists 0..2 with bitmaps on every shard -- the planning exchange decides it
+    // alike on every rank -- so every shard counts by popcounts)
+    P.cf3 = cf_mode != 0 && t == 4 && !ns && P.inc_allbm[P.seq_term[0]] && P.inc_allbm[P.seq_term[1]] &&
+            P.inc_allbm[P.seq_term[2]] &&
             (cf_mode == 2 || (P.seq_ng[3] < P.seq_ng[0] && P.seq_ng[3] < P.seq_ng[1] && P.seq_ng[3] < P.seq_ng[2]));
     P.cf = !P.cf3 && cf_mode != 0 && (t == 3 || t == 4) && !ns &&
            (cf_mode == 2 || (P.seq_ng[2] < P.seq_ng[0] && P.seq_ng[2] < P.seq_ng[1]));

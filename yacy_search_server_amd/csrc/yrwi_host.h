@@ -166,6 +166,9 @@ struct Plan {
   bool empty = true;                 // no result anywhere (J1 on global sizes)
   std::vector<const ListRec*> seq;   // fold order; a list absent from this shard is an empty ListRec
   std::vector<int64_t> seq_ng;       // global size of each seq list (sum over shards)
+  // include term i has a url-id bitmap on every shard (the planning exchange; one
+  // context: its own list's): the count-first popcounts (cf3) are then shard-safe
+  bool inc_allbm[YRWI_MAX_TERMS] = {};
   std::vector<const ListRec*> excl;  // this shard's exclusion lists (empty: no exclusion)
   // term keys (HandleSet order) and their lists on this shard (nullptr: absent)
   int ninc = 0, nexc = 0;
@@ -626,6 +629,7 @@ HostX* hostx_open(const uint8_t id[128], int world, int rank);  // nullptr: not 
 void hostx_close(HostX* x, bool unlink_name);
 void hostx_abort(HostX* x, int64_t seq);  // batch part `seq` failed: every rank's exchanges of that part fail at once
 int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
+bool hostx_wait_attached(const HostX* x, double limit_s);  // every rank mapped it (false: timeout)
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 // host-staged device collectives (ranks that share a device: RCCL refuses them)
 DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx);
