@@ -397,8 +397,13 @@ class Runner:
             self.dist.all_reduce(tt)
             return float(tmax.item()), float(tt[1].item())
 
-        # every distinct batch once with statistics (in flight like the timed steps), then the warm-up
+        # every distinct batch once with statistics (in flight like the timed steps), then
+        # every lane's scratch and staging sized to the largest of them (yrwi_settle_scratch:
+        # no lane grows on its first large batch inside the timed region), then the warm-up
         run_steps(D)
+        rc = _lib.lib().yrwi_settle_scratch(ix._h)
+        if rc:
+            raise RuntimeError(f"yrwi_settle_scratch: {rc}")
         run_steps(warmup)
         # timed region without per-batch statistics (no HIP events, as a production
         # caller runs); YRWI_BENCH_STATS=1 collects them in the timed region

@@ -232,6 +232,11 @@ int yrwi_index_info_get(yrwi_ctx* ctx, yrwi_index_info* info);
  * runs).  A caller counts them around a timed region without per-batch
  * statistics; steady-state batches make none. */
 int64_t yrwi_realloc_events(void);
+/* Sizes every lane's scratch arena and pinned staging to the largest any lane has
+ * needed so far (one allocation each): call after a few representative batches,
+ * and later batches of that workload make no device-wide allocation on any lane
+ * (a lane otherwise grows on its own first large batch). */
+int yrwi_settle_scratch(yrwi_ctx* ctx);
 /* Diagnostic of the node's shared-memory size exchange (no GPU needed): rank
  * `rank` of `world` processes / threads sharing group id `id` runs `nparts`
  * batch parts of `ncalls` exchanges each, vectors of n values (rank + part +

@@ -2237,6 +2237,28 @@ static int check_batch_args(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t nq,
   return 0;
 }
 
+extern "C" int yrwi_settle_scratch(yrwi_ctx* ctx) {
+  if (!ctx) return YRWI_E_ARG;
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  size_t a = ctx->scratch_hint.load(), s0 = 0, s1 = 0, s2 = 0;
+  for (Lane* L : ctx->lanes) {
+    a = std::max(a, L->arena.capacity());
+    s0 = std::max(s0, L->stage.cap);
+    s1 = std::max(s1, L->out_stage.cap);
+    s2 = std::max(s2, L->down_stage.cap);
+  }
+  for (Lane* L : ctx->lanes) {
+    L->arena.reserve(a);  // one chunk of the largest scratch any lane has needed
+    if ((s0 && !stage_reserve(L, &L->stage, s0, true)) || (s1 && !stage_reserve(L, &L->out_stage, s1, true)) ||
+        (s2 && !stage_reserve(L, &L->down_stage, s2, true)))
+      return ctx->take(L, YRWI_E_HIP);
+    if (a && L->arena.capacity() < a) return ctx->fail(YRWI_E_NOMEM, "scratch reservation");
+  }
+  ctx->scratch_hint = a;
+  return 0;
+}
+
 // wait until no asynchronous batch is in flight (their statuses stay recorded)
 void yrwi::drain(CtxBase* ctx) {
   for (Lane* L : ctx->lanes) L->wait();
