@@ -1855,6 +1855,12 @@ __device__ __forceinline__ Rec joined_rec(Rec o, uint64_t b0, uint64_t b1, int m
 #endif
 constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
 constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
+// Cost-attribution builds only (their records are wrong; never the product):
+// bit 0 skips the accumulated side's record gather, bit 1 the joined side's J5
+// gather, bit 2 the url-id write -- what each part of k_compact's time costs.
+#ifndef YRWI_COMPACT_WHATIF
+#define YRWI_COMPACT_WHATIF 0
+#endif
 
 struct CompactJob {
   const uint64_t* af;
@@ -2045,10 +2051,12 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                     X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
         continue;
       }
-      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+      if (YRWI_COMPACT_WHATIF & 1) {
+        A[u].w[0] = pr[u].x; A[u].w[1] = pr[u].y; A[u].w[2] = A[u].w[3] = 0;
+      } else if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
       else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
       else A[u] = load_rec(X.af, pr[u].x);
-      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
+      if (X.mode == JM_ENUM && !(YRWI_COMPACT_WHATIF & 2)) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
@@ -2056,7 +2064,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       const CompactJob& X = sJ[tl[u]];
       const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
       store_rec(X.ofeat, o, (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
-      stg(X.ouid + o, uid[u]);
+      if (!(YRWI_COMPACT_WHATIF & 4)) stg(X.ouid + o, uid[u]);
     }
   }
 }
