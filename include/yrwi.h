@@ -378,6 +378,14 @@ typedef struct yrwi_event_info {
   int32_t err;                  /* YRWI_E_CAPACITY once the event's tables overflowed */
   int32_t stack_size;
 } yrwi_event_info;
+/* Where each url entered the event's doublecheck set (SearchEvent.urlhashes,
+ * :736-805: the first posting of the url that passed the constraints):
+ * arrival[i] = its yrwi_event_add arrival (1 = the event's first), row[i] = its row
+ * in that arrival's rows; arrival 0 = seeded by the filter's urlhashes; -1 = not in
+ * the set.  A caller that keeps the arrivals' rows (GpuRWIStack) turns a pulled hit
+ * back into its posting. */
+int yrwi_event_source(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* urls12, int32_t n, int32_t* arrival,
+                      int32_t* row);
 /* The stack in rwiStack order (best first), up to maxn entries. */
 int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
                       yrwi_event_info* info);

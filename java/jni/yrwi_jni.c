@@ -289,6 +289,76 @@ JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpen(JNIEnv* env,
   return rc == 0 ? (jlong)(intptr_t)ev : 0;
 }
 
+/* GpuRWIStack's event: url set, rwiStack and doubleDomCache under the addRWIs constraints
+ * (the same filter fields as queryFiltered; urlHashes seed the doublecheck set) */
+JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpenFiltered(
+    JNIEnv* env, jclass c, jlong ctx, jintArray prof, jstring lang, jlong now, jint k, jlong maxPostings,
+    jbyteArray constraint, jboolean allOf, jint contentdom, jboolean strictDom, jstring modLang, jbyteArray site,
+    jbyteArray altSite, jbyteArray siteExcludes, jbyteArray urlHashes) {
+  yrwi_profile p;
+  to_profile(env, prof, &p);
+  yrwi_filter f;
+  memset(&f, 0, sizeof(f));
+  if (constraint) { (*env)->GetByteArrayRegion(env, constraint, 0, 4, (jbyte*)f.constraint); f.has_constraint = 1; }
+  f.all_of_constraint = allOf;
+  f.contentdom = contentdom;
+  f.strict_contentdom = strictDom;
+  if (modLang) {
+    const char* ml = (*env)->GetStringUTFChars(env, modLang, NULL);
+    strncpy(f.language, ml, sizeof(f.language) - 1);
+    (*env)->ReleaseStringUTFChars(env, modLang, ml);
+  }
+  if (site) { (*env)->GetByteArrayRegion(env, site, 0, 6, (jbyte*)f.sitehash); f.has_sitehash = 1; }
+  if (altSite) { (*env)->GetByteArrayRegion(env, altSite, 0, 6, (jbyte*)f.alt_sitehash); f.has_alt_sitehash = 1; }
+  const jsize nsx = siteExcludes ? (*env)->GetArrayLength(env, siteExcludes) / 6 : 0;
+  const jsize nuh = urlHashes ? (*env)->GetArrayLength(env, urlHashes) / 12 : 0;
+  uint8_t* sx = nsx ? copy_in(env, siteExcludes, (int64_t)nsx * 6) : NULL;
+  uint8_t* uh = nuh ? copy_in(env, urlHashes, (int64_t)nuh * 12) : NULL;
+  f.siteexcludes = sx;
+  f.nsiteexcludes = sx ? nsx : 0;
+  f.urlhashes = uh;
+  f.nurlhashes = uh ? nuh : 0;
+  const char* l = (*env)->GetStringUTFChars(env, lang, NULL);
+  yrwi_event* ev = NULL;
+  int rc = yrwi_event_open((yrwi_ctx*)(intptr_t)ctx, &p, l, now, k, &f, maxPostings, &ev);
+  (*env)->ReleaseStringUTFChars(env, lang, l);
+  free(sx);
+  free(uh);
+  return rc == 0 ? (jlong)(intptr_t)ev : 0;
+}
+
+/* (arrival, row) of the admitted posting of each of n url hashes (yrwi_event_source): int[2n] */
+JNIEXPORT jintArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventSource(JNIEnv* env, jclass c, jlong ctx, jlong ev,
+                                                                         jbyteArray urls, jint n) {
+  uint8_t* u = copy_in(env, urls, (int64_t)n * 12);
+  if (!u) return NULL;
+  int32_t* a = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)(n > 0 ? n : 1));
+  int rc = a ? yrwi_event_source((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, u, n, a, a + (n > 0 ? n : 1))
+             : YRWI_E_NOMEM;
+  free(u);
+  jintArray res = NULL;
+  if (rc == 0) {
+    jint* v = (jint*)malloc(sizeof(jint) * 2 * (size_t)(n > 0 ? n : 1));
+    for (jint i = 0; v && i < n; i++) { v[2 * i] = a[i]; v[2 * i + 1] = a[(n > 0 ? n : 1) + i]; }
+    res = (*env)->NewIntArray(env, 2 * n);
+    if (v) (*env)->SetIntArrayRegion(env, res, 0, 2 * n, v);
+    free(v);
+  }
+  free(a);
+  return res;
+}
+
+/* SearchEvent.flagcount of an event (yrwi_event_result's info, no hits copied) */
+JNIEXPORT jintArray JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventFlagCount(JNIEnv* env, jclass c, jlong ctx,
+                                                                            jlong ev) {
+  yrwi_event_info info;
+  int32_t n = 0;
+  if (yrwi_event_result((yrwi_ctx*)(intptr_t)ctx, (yrwi_event*)(intptr_t)ev, NULL, 0, &n, &info) != 0) return NULL;
+  jintArray res = (*env)->NewIntArray(env, 32);
+  (*env)->SetIntArrayRegion(env, res, 0, 32, (const jint*)info.flagcount);
+  return res;
+}
+
 /* GpuReferenceOrder's event: the ReferenceOrder state and host table only (yrwi_event_open_order) */
 JNIEXPORT jlong JNICALL Java_net_yacy_kelondro_rwi_GpuRWI_eventOpenOrder(JNIEnv* env, jclass c, jlong ctx,
                                                                         jintArray prof, jstring lang, jlong now,

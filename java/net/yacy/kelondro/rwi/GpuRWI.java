@@ -128,6 +128,43 @@ public final class GpuRWI implements AutoCloseable {
         return eventOpen(this.ctx, profile32, language, nowMillis, k, maxPostings);
     }
 
+    /** SearchEvent.addRWIs constraints of one event (SearchEvent.java:736-806), the
+     *  fields of QueryParams queryFiltered takes; null arrays: no such constraint. */
+    public static final class EventFilter {
+        public byte[] constraint;          // Bitfield bytes (4) or null
+        public boolean allOfConstraint;
+        public int contentdom = -1;        // ContentDomain code, -1: ALL
+        public boolean strictContentDom;
+        public String modifierLanguage;    // QueryModifier.language or null
+        public byte[] sitehash, altSitehash;  // 6-byte host hashes or null
+        public byte[][] siteexcludes;      // 6-byte host hashes or null
+        public byte[][] urlhashes;         // url hashes already in SearchEvent.urlhashes (doublecheck) or null
+    }
+
+    /** A full search event (url set, rwiStack, doubleDomCache) under constraints: GpuRWIStack. */
+    public synchronized long eventOpenFiltered(final int[] profile32, final String language, final long nowMillis,
+                                               final int k, final long maxPostings, final EventFilter f) {
+        if (f == null) return eventOpen(this.ctx, profile32, language, nowMillis, k, maxPostings);
+        return eventOpenFiltered(this.ctx, profile32, language, nowMillis, k, maxPostings, f.constraint,
+                                 f.allOfConstraint, f.contentdom, f.strictContentDom, f.modifierLanguage, f.sitehash,
+                                 f.altSitehash, flattenN(f.siteexcludes, 6), flattenN(f.urlhashes, 12));
+    }
+
+    /** (arrival, row) pairs of the postings the event's doublecheck admitted for n url
+     *  hashes (12 bytes each): arrival 1 = the first addRWIs, 0 = seeded, -1 = absent. */
+    public synchronized int[] eventSource(final long event, final byte[] urls, final int n) {
+        final int[] s = eventSource(this.ctx, event, urls, n);
+        if (s == null) throw new IllegalStateException("yrwi_event_source failed");
+        return s;
+    }
+
+    /** SearchEvent.flagcount of an event (yrwi_event_result's info). */
+    public synchronized int[] eventFlagCount(final long event) {
+        final int[] fc = eventFlagCount(this.ctx, event);
+        if (fc == null) throw new IllegalStateException("yrwi_event_result failed");
+        return fc;
+    }
+
     /** An event holding only a SearchEvent's ReferenceOrder (yrwi_event_open_order):
      *  eventOrder / eventAuthority only, the host table sized for maxHosts hosts; device
      *  memory comes from closed order-only events (no device-wide allocation per event). */
@@ -247,6 +284,12 @@ public final class GpuRWI implements AutoCloseable {
                                                boolean skipDoubleDom, int[] flagCount);
     private static native long eventOpen(long ctx, int[] profile32, String language, long nowMillis, int k,
                                          long maxPostings);
+    private static native long eventOpenFiltered(long ctx, int[] profile32, String language, long nowMillis, int k,
+                                                 long maxPostings, byte[] constraint, boolean allOf, int contentdom,
+                                                 boolean strictDom, String modifierLanguage, byte[] site,
+                                                 byte[] altSite, byte[] siteExcludes, byte[] urlHashes);
+    private static native int[] eventFlagCount(long ctx, long event);
+    private static native int[] eventSource(long ctx, long event, byte[] urls, int n);
     private static native long eventOpenOrder(long ctx, int[] profile32, String language, long nowMillis,
                                               long maxHosts);
     private static native int eventAdd(long ctx, long event, byte[] rows, int n, boolean local);

@@ -150,6 +150,7 @@ SIGNATURES = {
     "yrwi_event_open": (ctypes.c_int, [_VP, ctypes.POINTER(CProfile), ctypes.c_char_p, ctypes.c_int64,
                                        ctypes.c_int32, ctypes.POINTER(CFilter), ctypes.c_int64, _VP]),
     "yrwi_settle_scratch": (ctypes.c_int, [_VP]),
+    "yrwi_event_source": (ctypes.c_int, [_VP, _VP, ctypes.c_char_p, ctypes.c_int32, _VP, _VP]),
     "yrwi_event_open_order": (ctypes.c_int, [_VP, ctypes.POINTER(CProfile), ctypes.c_char_p, ctypes.c_int64,
                                              ctypes.c_int64, _VP]),
     "yrwi_event_add": (ctypes.c_int, [_VP, ctypes.POINTER(CArrival), ctypes.c_int32]),

@@ -345,6 +345,43 @@ extern "C" int yrwi_event_authority(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t
   return 0;
 }
 
+extern "C" int yrwi_event_source(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* urls12, int32_t n, int32_t* arrival,
+                                 int32_t* row) {
+  if (!ctx || !ev || n < 0 || (n > 0 && (!urls12 || !arrival || !row))) return YRWI_E_ARG;
+  if (n == 0) return 0;
+  if (!ev->h.ukey) return ctx->fail(YRWI_E_ARG, "an order-only event has no url set");
+  EVENT_LOCK(ctx);
+  std::vector<uint64_t> hi((size_t)n);
+  std::vector<uint8_t> lo((size_t)n);
+  for (int32_t i = 0; i < n; i++) {
+    KeyT k;
+    if (!key_of(urls12 + 12 * (size_t)i, &k)) return ctx->fail(YRWI_E_HASH, "url hash is not well-formed Base64");
+    hi[(size_t)i] = k.hi;
+    lo[(size_t)i] = (uint8_t)k.lo;
+  }
+  hipSetDevice(ctx->device);
+  drain(ctx);
+  Lane* L = ctx->lanes[0];
+  if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  uint64_t* d_hi = arena_alloc<uint64_t>(L, n);
+  uint8_t* d_lo = arena_alloc<uint8_t>(L, n);
+  uint64_t* d_out = arena_alloc<uint64_t>(L, n);
+  EvDev* d_ev = arena_alloc<EvDev>(L, 1);
+  if (!d_hi || !d_lo || !d_out || !d_ev) return ctx->fail(YRWI_E_NOMEM, "arena");
+  std::vector<EvDev> hev{ev->h};
+  if (upload(L, d_ev, hev, d_hi, hi, d_lo, lo)) return ctx->take(L, YRWI_E_HIP);
+  if (launch_event_where(d_ev, d_hi, d_lo, n, d_out, L->stream)) return ctx->fail(YRWI_E_HIP, "event_source launch");
+  std::vector<uint64_t> v((size_t)n);
+  HIPCHK(ctx, hipMemcpyAsync(v.data(), d_out, (size_t)n * 8, hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  for (int32_t i = 0; i < n; i++) {
+    const uint64_t x = v[(size_t)i];
+    arrival[i] = x == ~0ull ? -1 : (int32_t)(x >> 32);
+    row[i] = x == ~0ull ? -1 : (int32_t)(uint32_t)x;
+  }
+  return 0;
+}
+
 extern "C" int yrwi_event_result(yrwi_ctx* ctx, yrwi_event* ev, yrwi_hit* out, int32_t maxn, int32_t* nout,
                                  yrwi_event_info* info) {
   if (!ctx || !ev || maxn < 0 || (maxn > 0 && !out)) return YRWI_E_ARG;

@@ -2199,6 +2199,9 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
         if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) st->t_chain_ns += (int64_t)(ms * 1e6);
       if (tm.tn && hipEventElapsedTime(&ms, tm.tj, tm.tn) == hipSuccess) st->t_norm_ns += (int64_t)(ms * 1e6);
       if (tm.ts && tm.tn && hipEventElapsedTime(&ms, tm.tn, tm.ts) == hipSuccess) st->t_score_ns += (int64_t)(ms * 1e6);
+      // a statistics event that could not be read is not the batch's error: it must
+      // not linger as this thread's last HIP error (a later launch check reads it)
+      (void)hipGetLastError();
     }
     g0 = g1;
   }

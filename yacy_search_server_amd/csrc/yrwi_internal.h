@@ -497,6 +497,9 @@ int launch_sel_pick(const SelPick* d_jobs, int32_t njobs, void* stream);
 // ReferenceOrder.authority (ReferenceOrder.java:213-216) of n host keys (host36 + 1)
 // against an event's accumulated host counts
 int launch_event_authority(const EvDev* d_ev, const uint64_t* d_keys, int32_t n, int32_t* d_out, void* stream);
+// (arrival epoch << 32 | row) of each url's admitted posting in the event's url set, ~0: absent
+int launch_event_where(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int32_t n, uint64_t* d_out,
+                       void* stream);
 // seeds the url set with the doublecheck urls of the filter (epoch 0)
 int launch_event_seed(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int64_t n, void* stream);
 

@@ -1857,7 +1857,8 @@ constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
 constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
 // Cost-attribution builds only (their records are wrong; never the product):
 // bit 0 skips the accumulated side's record gather, bit 1 the joined side's J5
-// gather, bit 2 the url-id write -- what each part of k_compact's time costs.
+// gather -- what each part of k_compact's time costs.  (The url ids are always
+// written: the rank phase gathers dictionary keys by them.)
 #ifndef YRWI_COMPACT_WHATIF
 #define YRWI_COMPACT_WHATIF 0
 #endif
@@ -2064,7 +2065,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       const CompactJob& X = sJ[tl[u]];
       const int64_t o = X.off + (m0 + u * 256 - sPre[tl[u]]);
       store_rec(X.ofeat, o, (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));
-      if (!(YRWI_COMPACT_WHATIF & 4)) stg(X.ouid + o, uid[u]);
+      stg(X.ouid + o, uid[u]);
     }
   }
 }
@@ -4276,7 +4277,10 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
                  int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* st, void* ev_mid) {
-  if (total_chunks <= 0) return 0;
+  if (total_chunks <= 0) {  // (the statistics' event is recorded all the same: its elapsed time is read)
+    if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));
+    return 0;
+  }
   // seed_chunks (0 < seed < total): the first chunks of `order` run as a launch of
   // their own, so every later chunk starts with its query's threshold set
   const int64_t s0 = (seed_chunks > 0 && seed_chunks < total_chunks) ? seed_chunks : total_chunks;
@@ -4911,6 +4915,23 @@ int launch_sel_count(const SelCount* d_jobs, int32_t njobs, void* st) {
 }
 int launch_sel_pick(const SelPick* d_jobs, int32_t njobs, void* st) {
   if (njobs > 0) hipLaunchKernelGGL(k_sel_pick, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs);
+  return rc(hipGetLastError());
+}
+
+// where each url entered the event's doublecheck set (SearchEvent.urlhashes): the
+// (arrival epoch << 32 | row) of its admitted posting, ~0 if the url is not in it
+__global__ void k_event_where(const EvDev* __restrict__ ev, const uint64_t* __restrict__ hi,
+                              const uint8_t* __restrict__ lo, int32_t n, uint64_t* __restrict__ out) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const int64_t s = uset_find(ev->ukey, ev->ulog, hi[i], lo[i]);
+  out[i] = s >= 0 ? ld_dev(ev->uval + s) : ~0ull;
+}
+
+int launch_event_where(const EvDev* d_ev, const uint64_t* d_hi, const uint8_t* d_lo, int32_t n, uint64_t* d_out,
+                       void* st) {
+  if (n > 0) hipLaunchKernelGGL(k_event_where, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(st), d_ev, d_hi, d_lo,
+                                n, d_out);
   return rc(hipGetLastError());
 }
 

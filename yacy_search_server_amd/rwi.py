@@ -188,6 +188,17 @@ class SearchEvent:
             _check(self._ix._h, _lib.lib().yrwi_event_authority(self._ix._h, self._e, buf, len(hosthashes), out))
         return [int(out[i]) for i in range(len(hosthashes))]
 
+    def source(self, urlhashes: Sequence[bytes]) -> List[Tuple[int, int]]:
+        """(arrival, row) of each url's admitted posting (yrwi_event_source): arrival 1 is
+        the event's first add_rwis arrival, 0 a seeded doublecheck url, -1 not admitted."""
+        n = len(urlhashes)
+        a = np.zeros(max(1, n), dtype=np.int32)
+        r = np.zeros(max(1, n), dtype=np.int32)
+        if n:
+            _check(self._ix._h, _lib.lib().yrwi_event_source(self._ix._h, self._e, b"".join(bytes(u) for u in urlhashes),
+                                                             n, a.ctypes.data, r.ctypes.data))
+        return [(int(a[i]), int(r[i])) for i in range(n)]
+
     def results(self) -> Tuple[List["Hit"], "CEventInfo"]:
         out = (_lib.CHit * max(1, self.k))()
         n = ctypes.c_int32()
