@@ -28,6 +28,8 @@ import java.nio.ByteOrder;
 import java.util.ArrayList;
 import java.util.List;
 
+import net.yacy.cora.document.encoding.ASCII;
+import net.yacy.cora.document.id.DigestURL;
 import net.yacy.cora.sorting.WeakPriorityBlockingQueue;
 import net.yacy.kelondro.data.word.WordReference;
 import net.yacy.kelondro.data.word.WordReferenceRow;
@@ -77,6 +79,34 @@ public final class GpuRWIStack implements AutoCloseable {
         if (this.event == 0) throw new IllegalStateException("yrwi_event_open failed");
         this.release = new Release(gpu, this.event);
         this.cleanable = CLEANER.register(this, this.release);
+    }
+
+    /** The addRWIs constraints of a query (SearchEvent.java:736-806) as the event takes
+     *  them; the alternative site hash is SearchEvent's acceptableAlternativeSitehash
+     *  (:716-718).  Urls SearchEvent already holds go in via filter.urlhashes. */
+    public static GpuRWI.EventFilter filterOf(final QueryParams q) {
+        final GpuRWI.EventFilter f = new GpuRWI.EventFilter();
+        if (q.constraint != null) f.constraint = q.constraint.bytes();
+        f.allOfConstraint = q.allofconstraint;
+        f.contentdom = q.contentdom.getCode();
+        f.strictContentDom = q.isStrictContentDom();
+        f.modifierLanguage = q.modifier.language;
+        if (q.modifier.sitehash != null) {
+            f.sitehash = ASCII.getBytes(q.modifier.sitehash);
+            if (q.modifier.sitehost != null && q.modifier.sitehost.length() > 0) {
+                try {
+                    f.altSitehash = ASCII.getBytes(DigestURL.hosthash(q.modifier.sitehost.startsWith("www.")
+                        ? q.modifier.sitehost.substring(4) : "www." + q.modifier.sitehost, 80));
+                } catch (final java.net.MalformedURLException e) {
+                    f.altSitehash = null;  // as SearchEvent: no alternative then
+                }
+            }
+        } else if (q.siteexcludes != null) {
+            f.siteexcludes = new byte[q.siteexcludes.size()][];
+            int i = 0;
+            for (final String h : q.siteexcludes) f.siteexcludes[i++] = ASCII.getBytes(h);
+        }
+        return f;
     }
 
     /** SearchEvent.addRWIs(index, local, ...) for the posting loop (:673-836); the

@@ -1885,12 +1885,15 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   // start with a threshold, measured 39 + 86 us against 99 us for one launch:
   // the seed launch is one round of full-length blocks)
   const int64_t seed = 0;
-  hipEvent_t smid = tm ? ctx->event() : nullptr;  // after the k_score launches, before k_score_full
+  // the k_score launches alone (the population rocprofv3 averages): from right
+  // before them to before k_score_full
+  hipEvent_t s0 = span_open(ctx, tm);
+  hipEvent_t smid = tm ? ctx->event() : nullptr;
   if (launch_score(d_q, d_cq, d_order, nq, chunks, seed, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq,
                    ctx->stream, smid))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
-  if (tm) tm->kscore.push_back({sp, smid});  // the k_score launches alone
+  if (tm) tm->kscore.push_back({s0, smid});
   mark(4);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
