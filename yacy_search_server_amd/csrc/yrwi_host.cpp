@@ -1691,6 +1691,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.idx_tag = shx ? (uint32_t)ctx->rank << 28 : 0u;
     R.doubledom = P.filter && P.filter->skip_double_dom ? 1 : 0;
     R.host_rec = ctx->host_ids && P.cont.uid != nullptr ? 1 : 0;  // index records: dense host ids
+    R.host_bits = ctx->host_bits;
     R.kout = P.k;
     if (R.doubledom) R.k = YRWI_MAX_K;  // pullOneRWI draws from the whole rwiStack (max_results_rwi)
     // identical on every rank (same queries): decides the collective host-count exchange
@@ -1807,8 +1808,10 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
-  hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid))
+  hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_host_sort / k_shard_fin
+  bool host_sort = false;  // authority counts by k_host_sort (records with host ids)
+  for (const RankQ& R : rq) host_sort |= R.want_authority && R.host_rec;
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid, host_sort))
     return ctx->fail(YRWI_E_HIP, "reduce launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kreduce.push_back({sp, rmid});  // k_reduce alone: the population rocprofv3 averages

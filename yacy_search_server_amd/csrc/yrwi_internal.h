@@ -290,6 +290,8 @@ struct RankQ {
   const FilterQ* filt;     // addRWIs constraints or nullptr
   int32_t doubledom;       // results in pullOneRWI(skipDoubleDom) order
   int32_t host_rec;        // the records carry their url's dense host id (w3 >> 34): the host tables key on it
+  int32_t host_bits;       // host ids (and an invalid marker above them) fit this many bits (k_host_sort)
+  int32_t pad3;
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -386,7 +388,8 @@ int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr,
+                  bool host_sort = false);
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip

@@ -22,6 +22,7 @@
 // -ffp-contract=off so the one fp64 term (tf) rounds exactly like Java.
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "yrwi_internal.h"
 
@@ -2276,7 +2277,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       myfirst = min(myfirst, eo);
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
-      if (Q.want_authority) {
+      if (Q.want_authority && !Q.host_rec) {  // (host ids in the records: k_host_sort counts)
         const uint64_t key = elem_host(Q, rg[s % RED_GROUP].w[3], e) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
@@ -2295,7 +2296,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     }
     sPO[eo + (eo >> 5)] = po;
   }
-  if (Q.want_authority) {  // block-uniform: one atomicMax per wave instead of one per posting
+  if (Q.want_authority && !Q.host_rec) {  // block-uniform: one atomicMax per wave instead of one per posting
     const int32_t wm = wave_max_i(hmax);
     if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
   }
@@ -2606,6 +2607,77 @@ __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t 
     f.first = X.first;
   }
   return f;
+}
+
+// Authority host counts of the chunks whose records carry dense host ids
+// (ReferenceOrder doms / maxdomcount, :176-216; RankQ::host_rec): one workgroup
+// per CHUNK elements of one query sorts the chunk's host ids in LDS (block radix
+// sort over Q.host_bits bits) and adds each run -- one host, its count in the
+// chunk -- to the query's host table with one compare-and-swap probe and one
+// atomic add.  A host popular in the chunk costs one global atomic instead of one
+// per posting, and no url key is gathered.  The last add of every host returns
+// its final count, so the maximum of the returned counts is maxdomcount.
+__global__ __launch_bounds__(CHUNK_THREADS) void k_host_sort(const RankQ* __restrict__ qs,
+                                                             const int32_t* __restrict__ chunk_q,
+                                                             ShardSum* __restrict__ shard) {
+  using BRS = hipcub::BlockRadixSort<uint32_t, CHUNK_THREADS, CHUNK_IPT>;
+  __shared__ typename BRS::TempStorage sSort;
+  __shared__ uint32_t sKey[CHUNK];
+  __shared__ int32_t sStart[CHUNK + 1];
+  __shared__ int32_t sScan[4];
+  const int64_t b = blockIdx.x;
+  const int qi = chunk_q[b];
+  const RankQ& Q = qs[qi];
+  if (!Q.want_authority || !Q.host_rec) return;  // block-uniform
+  const int64_t c = b - Q.chunk_base;
+  const int t = (int)threadIdx.x;
+  const uint32_t sent = (1u << Q.host_bits) - 1u;  // above every host id: invalid elements sort last
+  uint32_t k[CHUNK_IPT];
+  int32_t nv = 0;
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {  // coalesced: the order of the keys does not matter
+    const int64_t e = c * CHUNK + s * CHUNK_THREADS + t;
+    const bool v = e < Q.n && !(Q.removed && ldg(Q.removed + e));
+    k[s] = v ? (uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34) : sent;
+    nv += v ? 1 : 0;
+  }
+  BRS(sSort).Sort(k, 0, Q.host_bits);  // blocked: thread t holds sorted positions t * CHUNK_IPT ..
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) sKey[t * CHUNK_IPT + s] = k[s];
+  int32_t nvalid;
+  (void)block_excl_sum256(nv, sScan, &nvalid);  // (its barriers also publish sKey)
+  int32_t nst = 0;
+  bool st[CHUNK_IPT];
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int p = t * CHUNK_IPT + s;
+    st[s] = p < nvalid && (p == 0 || sKey[p - 1] != k[s]);
+    nst += st[s] ? 1 : 0;
+  }
+  int32_t R;
+  int32_t o = block_excl_sum256(nst, sScan, &R);
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++)
+    if (st[s]) sStart[o++] = t * CHUNK_IPT + s;
+  if (t == 0) sStart[R] = nvalid;
+  __syncthreads();
+  int32_t hmax = 0;
+  for (int r = t; r < R; r += CHUNK_THREADS) {
+    const int32_t p = sStart[r];
+    const uint64_t key = (uint64_t)sKey[p] + 1;
+    const uint32_t cnt = (uint32_t)(sStart[r + 1] - p);
+    uint64_t slot = mix64(key) & Q.hmask;
+    while (true) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
+      if (prev == 0ull || prev == key) {
+        hmax = max(hmax, (int32_t)(atomicAdd(&Q.hcnt[slot], cnt) + cnt));
+        break;
+      }
+      slot = (slot + 1) & Q.hmask;
+    }
+  }
+  const int32_t wm = wave_max_i(hmax);
+  if ((t & 63) == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
 }
 
 // one wave per query: ordered combination of the chunk summaries of this shard
@@ -4259,11 +4331,13 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid, bool host_sort) {
   if (total_chunks > 0)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
   if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // k_reduce alone (statistics)
+  if (host_sort && total_chunks > 0)  // authority host counts of records with host ids
+    hipLaunchKernelGGL(k_host_sort, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_shard);
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
 }
