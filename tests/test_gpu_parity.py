@@ -662,3 +662,31 @@ def test_urlselection_restricts_every_list(corpus):
     if two is not None:
         with pytest.raises(YrwiError):
             ix.search_batch([Query([idx.hashes[t] for t in two], [], max_distance=1, now_ms=NOW, urlselection=sel)])
+
+
+@pytest.mark.parametrize("maxb", [None, "4", "1"])
+def test_authority_host_partition(corpus, maxb, monkeypatch):
+    """Authority (coeff_authority > 12) host counts by partition: every query's
+    hosts hashed into buckets (k_hpart_hist / k_hpart_scatter), each bucket
+    counted in LDS (k_hbucket), every element's count written for cardinal and the
+    largest folded into maxdomcount.  YRWI_HPART_MAXB caps the buckets per query:
+    at 1 a query over the biggest lists has thousands of hosts in its one bucket,
+    which overflow the LDS table into the query's global host table.  Bit-exact
+    against the oracle (ReferenceOrder.java:176-216, 223-265)."""
+    if maxb:
+        monkeypatch.setenv("YRWI_HPART_MAXB", maxb)
+    cfg, idx, ix = corpus
+    d = idx.as_dict()
+    big = [int(t) for t in np.argsort(-idx.sizes)[:4]]
+    qs = [([big[0]], []), ([big[1]], []), ([big[0], big[1]], []), ([big[0]], [big[2]])]
+    qs += synth.queries(cfg, 12, 1, 3, 1, qseed=44)
+    c5 = jl.RankingProfile.parse("", "date=15,domlength=15,authority=13,tf=10")
+    a14 = jl.RankingProfile()
+    a14.coeff_authority = 14
+    for prof in (c5, a14):
+        batch = [Query([idx.hashes[t] for t in inc], [idx.hashes[t] for t in exc], k=100, profile=_rp(prof),
+                       now_ms=NOW) for inc, exc in qs]
+        got = ix.search_batch(batch)
+        for qi, (q, g) in enumerate(zip(batch, got)):
+            exp = orc.search(d, q.include, q.exclude, orc.profile_from(prof), "en", now_ms=NOW, k=100)
+            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, (maxb, qi)

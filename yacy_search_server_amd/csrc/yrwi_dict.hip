@@ -847,14 +847,10 @@ int ensure_host_ids(CtxBase* ctx) {
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipStreamSynchronize(st));  // scratch is freed on return
   ctx->nhosts = nh;
-  int hb = 1;
-  while (hb < 31 && ((uint64_t)1 << hb) <= (uint64_t)nh + 1) hb++;  // (1 << hb) - 1 > every id
-  ctx->host_bits = hb;
   ctx->host_ids = true;
   for (Lane* L : ctx->lanes) {
     L->host_ids = true;
     L->host_key = ctx->host_key;
-    L->host_bits = hb;
   }
   return 0;
 }

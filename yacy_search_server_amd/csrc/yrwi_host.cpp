@@ -1691,7 +1691,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.idx_tag = shx ? (uint32_t)ctx->rank << 28 : 0u;
     R.doubledom = P.filter && P.filter->skip_double_dom ? 1 : 0;
     R.host_rec = ctx->host_ids && P.cont.uid != nullptr ? 1 : 0;  // index records: dense host ids
-    R.host_bits = ctx->host_bits;
     R.kout = P.k;
     if (R.doubledom) R.k = YRWI_MAX_K;  // pullOneRWI draws from the whole rwiStack (max_results_rwi)
     // identical on every rank (same queries): decides the collective host-count exchange
@@ -1728,6 +1727,46 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       R.hkeys = d_hkeys + slot_base[(size_t)qi];
       R.hcnt = d_hcnt + slot_base[(size_t)qi];
     }
+  }
+  // authority by partition (RankQ::ecnt; one context, records with host ids): each
+  // query's hosts hashed into ~HPART_TARGET-element buckets, per-element counts
+  int64_t hp_hist = 0, hp_elems = 0, hp_buckets = 0;
+  std::vector<int2> bq;
+  const char* hpm = getenv("YRWI_HPART_MAXB");  // (tests: fewer buckets, so large queries overflow the LDS tables)
+  const int64_t maxb = hpm ? std::max(1, std::min(HPART_MAXS, atoi(hpm))) : HPART_MAXS;
+  for (int qi = 0; qi < nq; qi++) {
+    RankQ& R = rq[(size_t)qi];
+    if (!R.want_authority || !R.host_rec || shx) continue;
+    R.hp_nb = (int32_t)std::min<int64_t>(maxb, std::max<int64_t>(1, ceil_div(R.n, HPART_TARGET)));
+    R.hp_hoff = hp_hist;
+    hp_hist += R.nchunks * R.hp_nb;
+    for (int32_t s = 0; s < R.hp_nb; s++) bq.push_back(make_int2(qi, s));
+    hp_buckets += R.hp_nb;
+  }
+  int32_t *d_hist = nullptr, *d_hoffs = nullptr, *d_ecnt = nullptr;
+  uint2* d_part = nullptr;
+  int2* d_bq = nullptr;
+  void* d_hptmp = nullptr;
+  size_t hp_tmp = 0;
+  if (hp_buckets > 0) {
+    for (int qi = 0; qi < nq; qi++) if (rq[(size_t)qi].hp_nb) hp_elems += rq[(size_t)qi].n;
+    hp_tmp = host_part_tmp_bytes(hp_hist);
+    d_hist = arena_alloc<int32_t>(ctx, hp_hist + 1);
+    d_hoffs = arena_alloc<int32_t>(ctx, hp_hist + 1);
+    d_ecnt = arena_alloc<int32_t>(ctx, hp_elems);
+    d_part = arena_alloc<uint2>(ctx, hp_elems);
+    d_bq = arena_alloc<int2>(ctx, hp_buckets);
+    d_hptmp = arena_alloc<uint8_t>(ctx, (int64_t)std::max<size_t>(hp_tmp, 1));
+    if (!d_hist || !d_hoffs || !d_ecnt || !d_part || !d_bq || !d_hptmp) return ctx->fail(YRWI_E_NOMEM, "arena");
+    HIPCHK(ctx, hipMemsetAsync(d_hist + hp_hist, 0, 4, ctx->stream));  // the scan's extra entry: the total
+    int64_t eb = 0;
+    for (int qi = 0; qi < nq; qi++) {
+      RankQ& R = rq[(size_t)qi];
+      if (!R.hp_nb) continue;
+      R.ecnt = d_ecnt + eb;
+      eb += R.n;
+    }
+    if (upload(ctx, d_bq, bq)) return YRWI_E_HIP;
   }
   // addRWIs constraints: one FilterQ per filtered query, key arrays and flag counters
   std::vector<int> fidx((size_t)nq, -1);
@@ -1808,11 +1847,13 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
-  hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_host_sort / k_shard_fin
-  bool host_sort = false;  // authority counts by k_host_sort (records with host ids)
-  for (const RankQ& R : rq) host_sort |= R.want_authority && R.host_rec;
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid, host_sort))
+  hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid))
     return ctx->fail(YRWI_E_HIP, "reduce launch");
+  if (hp_buckets > 0 &&
+      launch_host_part(d_q, d_cq, chunks, d_hist, d_hoffs, hp_hist, d_hptmp, hp_tmp, d_part, d_bq,
+                       (int32_t)hp_buckets, d_ss, ctx->stream))
+    return ctx->fail(YRWI_E_HIP, "host count launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kreduce.push_back({sp, rmid});  // k_reduce alone: the population rocprofv3 averages
   if (st) {

@@ -281,7 +281,6 @@ struct Lane {
   // the index records carry dense host ids (ensure_host_ids); host_key[id] = the host hash
   bool host_ids = false;
   const uint64_t* host_key = nullptr;
-  int32_t host_bits = 0;
   Arena arena{(size_t)256 << 20};
   std::string err;
   std::vector<hipEvent_t> evpool;
@@ -428,7 +427,6 @@ struct CtxBase {
   uint64_t* host_key = nullptr;
   size_t host_key_cap = 0;
   int64_t nhosts = 0;
-  int32_t host_bits = 0;  // bits of nhosts + 1: every host id and an invalid marker above them
   // incremental maintenance (yrwi_dict.hip): lists added or replaced since the
   // dictionary was last brought up to date; keys of removed postings stay in it
   // (an id without postings changes no join) until the next full rebuild

@@ -290,8 +290,9 @@ struct RankQ {
   const FilterQ* filt;     // addRWIs constraints or nullptr
   int32_t doubledom;       // results in pullOneRWI(skipDoubleDom) order
   int32_t host_rec;        // the records carry their url's dense host id (w3 >> 34): the host tables key on it
-  int32_t host_bits;       // host ids (and an invalid marker above them) fit this many bits (k_host_sort)
-  int32_t pad3;
+  int32_t hp_nb;           // authority by partition (ecnt): the query's host buckets
+  int32_t* ecnt;           // ... and every element's host count (nullptr: the host tables serve)
+  int64_t hp_hoff;         // ... its first histogram entry (bucket-major: hp_hoff + bucket * nchunks + chunk)
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -388,8 +389,14 @@ int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr,
-                  bool host_sort = false);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr);
+// authority host counts by partition (RankQ::ecnt): histogram per (query bucket, chunk) -> scan ->
+// scatter (host id, element) -> per-bucket LDS counts, every element's count, maxdomcount
+int launch_host_part(const RankQ* d_q, const int32_t* d_chunk_q, int64_t total_chunks, int32_t* d_hist,
+                     int32_t* d_hoffs, int64_t nhist, void* d_tmp, size_t tmp_bytes, uint2* d_part, const int2* d_bq,
+                     int32_t nbuckets, ShardSum* d_shard, void* stream);
+size_t host_part_tmp_bytes(int64_t nhist);  // scan scratch for nhist + 1 histogram entries
+constexpr int HPART_MAXS = 1024, HPART_TARGET = 512;  // buckets per query at most; elements per bucket aimed at
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world,
                    NormState* d_norm, void* stream);
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip

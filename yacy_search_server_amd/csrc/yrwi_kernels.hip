@@ -2277,7 +2277,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       myfirst = min(myfirst, eo);
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
-      if (Q.want_authority && !Q.host_rec) {  // (host ids in the records: k_host_sort counts)
+      if (Q.want_authority && !Q.ecnt) {  // (a partitioned query: k_hbucket counts)
         const uint64_t key = elem_host(Q, rg[s % RED_GROUP].w[3], e) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
         while (true) {
@@ -2296,7 +2296,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
     }
     sPO[eo + (eo >> 5)] = po;
   }
-  if (Q.want_authority && !Q.host_rec) {  // block-uniform: one atomicMax per wave instead of one per posting
+  if (Q.want_authority && !Q.ecnt) {  // block-uniform: one atomicMax per wave instead of one per posting
     const int32_t wm = wave_max_i(hmax);
     if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
   }
@@ -2609,75 +2609,131 @@ __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t 
   return f;
 }
 
-// Authority host counts of the chunks whose records carry dense host ids
-// (ReferenceOrder doms / maxdomcount, :176-216; RankQ::host_rec): one workgroup
-// per CHUNK elements of one query sorts the chunk's host ids in LDS (block radix
-// sort over Q.host_bits bits) and adds each run -- one host, its count in the
-// chunk -- to the query's host table with one compare-and-swap probe and one
-// atomic add.  A host popular in the chunk costs one global atomic instead of one
-// per posting, and no url key is gathered.  The last add of every host returns
-// its final count, so the maximum of the returned counts is maxdomcount.
-__global__ __launch_bounds__(CHUNK_THREADS) void k_host_sort(const RankQ* __restrict__ qs,
-                                                             const int32_t* __restrict__ chunk_q,
-                                                             ShardSum* __restrict__ shard) {
-  using BRS = hipcub::BlockRadixSort<uint32_t, CHUNK_THREADS, CHUNK_IPT>;
-  __shared__ typename BRS::TempStorage sSort;
-  __shared__ uint32_t sKey[CHUNK];
-  __shared__ int32_t sStart[CHUNK + 1];
-  __shared__ int32_t sScan[4];
+// Authority host counts by partition (ReferenceOrder doms / maxdomcount,
+// :176-216) for queries whose records carry dense host ids, on one context
+// (RankQ::ecnt; sharded contexts keep the host tables the owner exchange reads).
+// A query's valid elements are spread over hp_nb buckets by a hash of their host
+// id (k_hpart_hist counts per chunk and bucket, a scan gives every (bucket, chunk)
+// its place, k_hpart_scatter writes (host id, element) there); every host lands in
+// exactly one bucket, so one workgroup per bucket (k_hbucket) counts its hosts in
+// LDS, writes every element's host count (ecnt, what cardinal reads) and folds
+// the bucket's largest count into maxdomcount -- no global atomic per posting, no
+// table probe per scored posting.  A bucket whose hosts overflow its LDS table
+// counts the rest in the query's global host table (only its workgroup touches
+// those hosts, so their counts are final when it reads them back).
+constexpr int HB_SLOTS = 4096;   // LDS table slots of a bucket
+__device__ __forceinline__ uint32_t hp_bucket(uint32_t hid, int32_t nb) {
+  uint32_t x = hid * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  return (uint32_t)(((uint64_t)x * (uint64_t)nb) >> 32);
+}
+
+__global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_hist(const RankQ* __restrict__ qs,
+                                                              const int32_t* __restrict__ chunk_q,
+                                                              int32_t* __restrict__ hist) {
+  __shared__ int32_t sH[HPART_MAXS];
   const int64_t b = blockIdx.x;
-  const int qi = chunk_q[b];
-  const RankQ& Q = qs[qi];
-  if (!Q.want_authority || !Q.host_rec) return;  // block-uniform
+  const RankQ& Q = qs[chunk_q[b]];
+  if (!Q.ecnt) return;  // block-uniform
   const int64_t c = b - Q.chunk_base;
-  const int t = (int)threadIdx.x;
-  const uint32_t sent = (1u << Q.host_bits) - 1u;  // above every host id: invalid elements sort last
-  uint32_t k[CHUNK_IPT];
-  int32_t nv = 0;
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {  // coalesced: the order of the keys does not matter
-    const int64_t e = c * CHUNK + s * CHUNK_THREADS + t;
-    const bool v = e < Q.n && !(Q.removed && ldg(Q.removed + e));
-    k[s] = v ? (uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34) : sent;
-    nv += v ? 1 : 0;
-  }
-  BRS(sSort).Sort(k, 0, Q.host_bits);  // blocked: thread t holds sorted positions t * CHUNK_IPT ..
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) sKey[t * CHUNK_IPT + s] = k[s];
-  int32_t nvalid;
-  (void)block_excl_sum256(nv, sScan, &nvalid);  // (its barriers also publish sKey)
-  int32_t nst = 0;
-  bool st[CHUNK_IPT];
+  const int nb = Q.hp_nb;
+  for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) sH[i] = 0;
+  __syncthreads();
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
-    const int p = t * CHUNK_IPT + s;
-    st[s] = p < nvalid && (p == 0 || sKey[p - 1] != k[s]);
-    nst += st[s] ? 1 : 0;
+    const int64_t e = c * CHUNK + s * CHUNK_THREADS + threadIdx.x;
+    if (e < Q.n && !(Q.removed && ldg(Q.removed + e)))
+      atomicAdd(&sH[hp_bucket((uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34), nb)], 1);
   }
-  int32_t R;
-  int32_t o = block_excl_sum256(nst, sScan, &R);
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++)
-    if (st[s]) sStart[o++] = t * CHUNK_IPT + s;
-  if (t == 0) sStart[R] = nvalid;
   __syncthreads();
-  int32_t hmax = 0;
-  for (int r = t; r < R; r += CHUNK_THREADS) {
-    const int32_t p = sStart[r];
-    const uint64_t key = (uint64_t)sKey[p] + 1;
-    const uint32_t cnt = (uint32_t)(sStart[r + 1] - p);
-    uint64_t slot = mix64(key) & Q.hmask;
-    while (true) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[slot], 0ull, (unsigned long long)key);
-      if (prev == 0ull || prev == key) {
-        hmax = max(hmax, (int32_t)(atomicAdd(&Q.hcnt[slot], cnt) + cnt));
-        break;
-      }
-      slot = (slot + 1) & Q.hmask;
+  for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) hist[Q.hp_hoff + (int64_t)i * Q.nchunks + c] = sH[i];
+}
+
+__global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_scatter(const RankQ* __restrict__ qs,
+                                                                 const int32_t* __restrict__ chunk_q,
+                                                                 const int32_t* __restrict__ hoffs,
+                                                                 uint2* __restrict__ part) {
+  __shared__ int32_t sC[HPART_MAXS];
+  const int64_t b = blockIdx.x;
+  const RankQ& Q = qs[chunk_q[b]];
+  if (!Q.ecnt) return;
+  const int64_t c = b - Q.chunk_base;
+  const int nb = Q.hp_nb;
+  for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) sC[i] = hoffs[Q.hp_hoff + (int64_t)i * Q.nchunks + c];
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < CHUNK_IPT; s++) {
+    const int64_t e = c * CHUNK + s * CHUNK_THREADS + threadIdx.x;
+    if (e < Q.n && !(Q.removed && ldg(Q.removed + e))) {
+      const uint32_t h = (uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34);
+      const int32_t pos = atomicAdd(&sC[hp_bucket(h, nb)], 1);
+      part[pos] = make_uint2(h, (uint32_t)e);
     }
   }
+}
+
+__global__ __launch_bounds__(CHUNK_THREADS) void k_hbucket(const RankQ* __restrict__ qs, const int2* __restrict__ bq,
+                                                           const int32_t* __restrict__ hoffs,
+                                                           const uint2* __restrict__ part,
+                                                           ShardSum* __restrict__ shard) {
+  __shared__ uint32_t sK[HB_SLOTS];
+  __shared__ uint32_t sN[HB_SLOTS];
+  const int2 qb = bq[blockIdx.x];
+  const RankQ& Q = qs[qb.x];
+  const int64_t i0 = hoffs[Q.hp_hoff + (int64_t)qb.y * Q.nchunks];
+  const int64_t i1 = hoffs[Q.hp_hoff + (int64_t)(qb.y + 1) * Q.nchunks];
+  for (int i = threadIdx.x; i < HB_SLOTS; i += CHUNK_THREADS) sK[i] = sN[i] = 0;
+  __syncthreads();
+  // count: LDS table (key = host id + 1), the query's global table past 32 probes
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += CHUNK_THREADS) {
+    const uint32_t key = ldg(&part[i].x) + 1u;
+    uint32_t slot = (key * 0x9E3779B1u) >> 20;  // (HB_SLOTS = 2^12)
+    bool done = false;
+    for (int p = 0; p < 32 && !done; p++, slot = (slot + 1) & (HB_SLOTS - 1)) {
+      const uint32_t prev = atomicCAS(&sK[slot], 0u, key);
+      if (prev == 0u || prev == key) {
+        atomicAdd(&sN[slot], 1u);
+        done = true;
+      }
+    }
+    if (!done) {
+      uint64_t gs = mix64((uint64_t)key) & Q.hmask;
+      while (true) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&Q.hkeys[gs], 0ull, (unsigned long long)key);
+        if (prev == 0ull || prev == (unsigned long long)key) {
+          atomicAdd(&Q.hcnt[gs], 1u);
+          break;
+        }
+        gs = (gs + 1) & Q.hmask;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_block();
+  // every element's host count (what cardinal reads), the bucket's largest count
+  int32_t hmax = 0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += CHUNK_THREADS) {
+    const uint2 it = part[i];
+    const uint32_t key = it.x + 1u;
+    uint32_t slot = (key * 0x9E3779B1u) >> 20;
+    int32_t cnt = -1;
+    for (int p = 0; p < 32; p++, slot = (slot + 1) & (HB_SLOTS - 1)) {
+      const uint32_t k = sK[slot];
+      if (k == key) { cnt = (int32_t)sN[slot]; break; }
+      if (k == 0u) break;
+    }
+    if (cnt < 0) {  // counted in the global table: read it with atomics (this kernel wrote it)
+      uint64_t gs = mix64((uint64_t)key) & Q.hmask;
+      while (atomicAdd((unsigned long long*)&Q.hkeys[gs], 0ull) != (unsigned long long)key) gs = (gs + 1) & Q.hmask;
+      cnt = (int32_t)atomicAdd(&Q.hcnt[gs], 0u);
+    }
+    stg(Q.ecnt + it.y, cnt);
+    hmax = max(hmax, cnt);
+  }
   const int32_t wm = wave_max_i(hmax);
-  if ((t & 63) == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
+  if ((threadIdx.x & 63) == 0 && wm > 0) atomicMax(&shard[qb.x].maxdom, wm);
 }
 
 // one wave per query: ordered combination of the chunk summaries of this shard
@@ -3378,10 +3434,11 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
       const int64_t ub = score_bound(q, N, Q, *P, &valid, tab);
       if (valid && ((uint64_t)ub ^ 0x8000000000000000ull) < T) continue;
     }
-    if (!F && Q.want_authority && !Q.host_rec) key_at(Q, e, khi, klo);
+    if (!F && Q.want_authority && !Q.host_rec && !Q.ecnt) key_at(Q, e, khi, klo);
     const Feat t = decode_rec(q);
-    const int32_t hc =
-        Q.want_authority ? host_count(Q, Q.host_rec ? q.w[3] >> 34 : key_host36(khi, klo)) : 0;
+    const int32_t hc = !Q.want_authority ? 0
+                       : Q.ecnt ? ldg(Q.ecnt + e)
+                                : host_count(Q, Q.host_rec ? q.w[3] >> 34 : key_host36(khi, klo));
     a[s] = (uint64_t)cardinal(t, N, Q, hc, tab) ^ 0x8000000000000000ull;
     if (a[s] < T) {
       a[s] = 0;
@@ -4037,7 +4094,7 @@ __global__ __launch_bounds__(256) void k_score_all(const RankQ* __restrict__ qs,
     if (e >= Q.n) break;
     const Rec q = load_rec(Q.feat, e);
     const Feat t = decode_rec(q);
-    const int32_t hc = Q.want_authority ? host_count(Q, elem_host(Q, q.w[3], e)) : 0;
+    const int32_t hc = !Q.want_authority ? 0 : Q.ecnt ? ldg(Q.ecnt + e) : host_count(Q, elem_host(Q, q.w[3], e));
     out[e] = cardinal(t, N, Q, hc);
   }
 }
@@ -4331,15 +4388,33 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid, bool host_sort) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid) {
   if (total_chunks > 0)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
                        d_chunks, d_shard);
   if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // k_reduce alone (statistics)
-  if (host_sort && total_chunks > 0)  // authority host counts of records with host ids
-    hipLaunchKernelGGL(k_host_sort, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_shard);
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
+}
+
+int launch_host_part(const RankQ* d_q, const int32_t* d_chunk_q, int64_t total_chunks, int32_t* d_hist,
+                     int32_t* d_hoffs, int64_t nhist, void* d_tmp, size_t tmp_bytes, uint2* d_part, const int2* d_bq,
+                     int32_t nbuckets, ShardSum* d_shard, void* st) {
+  if (total_chunks <= 0 || nbuckets <= 0) return 0;
+  hipLaunchKernelGGL(k_hpart_hist, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_hist);
+  size_t t = tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(d_tmp, t, d_hist, d_hoffs, (int)(nhist + 1), S(st)) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_hpart_scatter, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
+                     (const int32_t*)d_hoffs, d_part);
+  hipLaunchKernelGGL(k_hbucket, dim3((unsigned)nbuckets), dim3(CHUNK_THREADS), 0, S(st), d_q, d_bq,
+                     (const int32_t*)d_hoffs, (const uint2*)d_part, d_shard);
+  return rc(hipGetLastError());
+}
+
+size_t host_part_tmp_bytes(int64_t nhist) {
+  size_t t = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, t, (int32_t*)nullptr, (int32_t*)nullptr, (int)(nhist + 1), (hipStream_t)0);
+  return t;
 }
 
 int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32_t world, NormState* d_norm,
