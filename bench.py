@@ -412,6 +412,8 @@ class Runner:
         if gap > 0:
             time.sleep(gap / 1e3)
         dt, timed, throttle = timed_region(steps, timed_stats, lambda i: i % D)
+        if gap > 0:  # (diagnosis: the same idle time after it, so a kernel trace shows where it ends)
+            time.sleep(gap / 1e3)
         dt, total_post = over_ranks(dt, float(timed["postings_in"]))
         # the timed region's own results: slot s last ran step i_s (batch i_s % D)
         out = {}
