@@ -315,6 +315,33 @@ def test_j5_side_arrays(long_lists, j5, monkeypatch):
         ix.close()
 
 
+@pytest.mark.parametrize("bmenum,chain", [("2", "1"), ("2", "0"), ("0", "0")],
+                         ids=["enum_chained", "enum_stepwise", "probe_stepwise"])
+def test_bitmap_enumeration(long_lists, bmenum, chain, monkeypatch):
+    """JA_BMENUM (YRWI_BMENUM=2: every unchained, undistanced join of two dense
+    bitmap lists enumerates the AND of both bitmaps; 0: never): the pairs and their
+    order equal the probe's -- term_search rows, top-k with tie-breaks, with and
+    without excluded terms, stepwise (YRWI_NO_CHAIN=1: every fold step a join job)
+    and chained (only the unchained steps enumerate)."""
+    monkeypatch.setenv("YRWI_BMENUM", bmenum)
+    monkeypatch.setenv("YRWI_NO_CHAIN", "1" if chain == "0" else "0")
+    cfg, df, big, idx, ix = long_lists
+    d = idx.as_dict()
+    rng = np.random.default_rng(13)
+    for n in (2, 2, 3):
+        pick = [int(x) for x in rng.permutation(big)[:n + 1]]
+        ih = [idx.hashes[t] for t in pick[:n]]
+        for eh, md in (([], 2147483647), ([idx.hashes[pick[n]]], 2147483647), ([], 60)):
+            assert np.array_equal(ix.term_search(ih, eh, md, NOW), orc.term_search(d, ih, eh, md, NOW)), (pick, md)
+    batch = []
+    for i in range(12):
+        pick = [int(x) for x in rng.permutation(big)]
+        ni, ne = 2 + i % 3, (i // 3) % 2
+        batch.append(Query([idx.hashes[t] for t in pick[:ni]], [idx.hashes[t] for t in pick[ni:ni + ne]], now_ms=NOW))
+    for q, g in zip(batch, ix.search_batch(batch)):
+        assert [(h.urlhash, h.score, h.tiebreak) for h in g] == orc.search(d, q.include, q.exclude, now_ms=NOW, k=100)
+
+
 @pytest.mark.parametrize("ratio", ["1", "1000000000"])
 def test_forced_join_algorithm(corpus, ratio, monkeypatch):
     """Every join/exclusion step through the probe kernel (ratio 1) or through

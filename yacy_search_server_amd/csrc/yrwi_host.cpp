@@ -819,6 +819,7 @@ static int64_t loaded_bytes(const JoinQ& J) {
   const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
   if (J.algo == JA_MERGE) return 4 * (ns + nl);
   if (J.algo == JA_BMAND) return 16 * J.bm_words;  // the bits of both bitmaps (8 B of every 16-B word)
+  if (J.algo == JA_BMENUM) return 32 * J.bm_words;  // both bitmaps' 16-B words
   const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
   return bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
 }
@@ -864,7 +865,7 @@ static bool chain_fused() {
 
 static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& jobs, std::vector<int>& owner,
                         std::vector<int64_t>& tile_base, int* nmerge, int64_t* merge_tiles, int64_t* tiles,
-                        bool* long_tiles) {
+                        bool* long_tiles, int bm_enum) {
   *long_tiles = false;
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
@@ -887,6 +888,22 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     if (J.B.bm && J.B.n * 64 < nurls) J.B.bm = nullptr;
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
     J.small_is_A = J.A.n <= J.B.n;
+    // both lists with dense bitmaps, the smaller one above 1/8 of the url ids:
+    // their AND streams 32 B per 64 url ids, less than its 4-B ids (JA_BMENUM; a
+    // job whose pairs go to the chain tests, an exclusion or a distance filter
+    // keeps the probe)
+    if (bm_enum && J.A.bm && J.B.bm && !J.chained && J.mode != JM_MARK && J.maxd >= 65535 && nurls > 0) {
+      const int64_t words = (nurls + 63) / 64;
+      if (bm_enum == 2 || 8 * words < ns) {
+        J.algo = JA_BMENUM;
+        J.ptile = BMENUM_WORDS;
+        J.bm_words = words;
+        J.ntiles = ceil_div(words, BMENUM_WORDS);
+        J.chain_bm = nullptr;
+        order[i] = i;
+        continue;
+      }
+    }
     // skewed sizes: probe the large list; a large list with a url-id bitmap is
     // probed at any ratio (the small side's ids stream, the bitmap stays in L2)
     const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
@@ -1004,7 +1021,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       const ChainQ& Cq = (*chq)[(size_t)owner[j]];
       jobs[j].chain_bm = jobs[j].chained && Cq.pos0 == 0 && Cq.ninc >= 1 ? Cq.l[0].bm : nullptr;
     }
-  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles,
+              ctx->bm_enum);
   const int nj = (int)jobs.size();
   const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
@@ -1037,6 +1055,14 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   }
   JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
   int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
+  unsigned long long* d_cursor = nullptr;  // JA_BMENUM jobs' pair-slot cursors
+  for (int j = 0; j < nj && !d_cursor; j++)
+    if (jobs[(size_t)j].algo == JA_BMENUM) {
+      if (!(d_cursor = arena_alloc<unsigned long long>(ctx, nj))) return ctx->fail(YRWI_E_NOMEM, "arena");
+      HIPCHK(ctx, hipMemsetAsync(d_cursor, 0, (size_t)nj * 8, ctx->stream));
+    }
+  if (d_cursor)
+    for (int j = 0; j < nj; j++) jobs[(size_t)j].cursor = d_cursor + j;
   TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
   uint2* d_pairs = arena_alloc<uint2>(ctx, npairs);
@@ -1226,7 +1252,8 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   int nmerge;
   int64_t merge_tiles, tiles;
   bool long_tiles;
-  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles,
+              ctx->bm_enum);
   const int nj = (int)jobs.size();
   if (st)
     for (const JoinQ& J : jobs) st->bytes_alg_capped += std::min<int64_t>(12 * J.B.n, loaded_bytes(J));

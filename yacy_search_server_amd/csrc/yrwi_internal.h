@@ -93,8 +93,20 @@ enum JoinMode : int32_t {
 // JA_BMAND: a counted-only join of two lists that both have url-id bitmaps:
 // popcount(bits A & bits B) over ranges of bitmap words (tiles of BMAND_WORDS),
 // in place of probing one list's ids into the other (k_probe)
-enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2 };
+// JA_BMENUM: the matched pairs of two lists that both have dense url-id bitmaps,
+// from the AND of the bitmaps (tiles of BMENUM_WORDS words): each set bit is a
+// match, its rows are each word's rank + the bits below it -- no id of either
+// list is read.  Taken where streaming both bitmaps (32 B per 64 url ids) costs
+// less than the smaller list's ids alone (4 B per id: the probe's bitmap words
+// mostly hit L2, since a batch's jobs over one large list run back to back --
+// at 20 B per probed id C2 took it for lists above 1/40 density and k_probe went
+// 119 -> 165 us, k_compact 225 -> 337 us with four-word-per-thread tiles, whose
+// match runs left few compaction workgroups).  A
+// tile claims its run of the job's pair slots with one atomic add on the job's
+// cursor (the compaction reads every tile at tile_src, in tile order).
+enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2, JA_BMENUM = 3 };
 constexpr int BMAND_WORDS = 4096;
+constexpr int BMENUM_WORDS = 256;  // bitmap words per JA_BMENUM tile: one per thread (16384 url ids)
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
 #ifndef YRWI_BM_TILE
 #define YRWI_BM_TILE 1024
@@ -179,8 +191,9 @@ struct JoinQ {
   int32_t* chain_tup0;
   int32_t chain_fill;
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
-  int64_t bm_words;    // JA_BMAND: bitmap words of the url-id space
+  int64_t bm_words;    // JA_BMAND / JA_BMENUM: bitmap words of the url-id space
   const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
+  unsigned long long* cursor;  // JA_BMENUM: pair slots claimed so far (zeroed per step)
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A

@@ -848,7 +848,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
   const JoinQ& J = jobs[j];
-  if (J.algo == JA_BMAND) {  // a range of bitmap words: no ids to read, no range
+  if (J.algo == JA_BMAND || J.algo == JA_BMENUM) {  // a range of bitmap words: no ids to read, no range
     const uint32_t id0 = (uint32_t)min((tile0 + t - tile_base[j]) * (int64_t)J.ptile * 64, (int64_t)0xFFFFFFFF);
     if (tile_key) tile_key[tile0 + t] = id0;
     if (tile_job) tile_job[tile0 + t] = j;
@@ -1038,6 +1038,62 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
 }
 
 
+// One JA_BMENUM tile: BMENUM_WORDS bitmap words, WPT consecutive words per
+// thread (the 16-B entries of both lists stream coalesced: the 64 id bits and
+// the list position of the word's first id).  A match is a bit set in both;
+// its rows are each list's word position + the bits below it.  Matches leave in
+// url-id order (thread-consecutive words, block scan of the counts) into the run
+// the tile claims from the job's cursor.
+__device__ __forceinline__ void probe_bmenum(const JoinQ& J, int64_t tj, int64_t b, uint2* __restrict__ pairs,
+                                             uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
+                                             int32_t* __restrict__ tile_cnt, int32_t* sScan) {
+  constexpr int WPT = BMENUM_WORDS / PROBE_TILE;
+  static_assert(WPT * PROBE_TILE == BMENUM_WORDS, "whole words per thread");
+  __shared__ int64_t sBase;
+  const int64_t w0 = tj * BMENUM_WORDS + (int64_t)threadIdx.x * WPT;
+  uint64_t xa[WPT], xb[WPT];
+  uint32_t ra[WPT], rb[WPT];
+  int32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < WPT; k++) {
+    const int64_t w = w0 + k;
+    xa[k] = xb[k] = 0;
+    ra[k] = rb[k] = 0;
+    if (w < J.bm_words) {
+      const ulonglong2 a = ldg(reinterpret_cast<const ulonglong2*>(J.A.bm) + w);
+      const ulonglong2 c = ldg(reinterpret_cast<const ulonglong2*>(J.B.bm) + w);
+      xa[k] = a.x;
+      ra[k] = (uint32_t)a.y;  // list positions < 2^31
+      xb[k] = c.x;
+      rb[k] = (uint32_t)c.y;
+      cnt += __popcll(a.x & c.x);
+    }
+  }
+  int32_t tot;
+  int32_t off = block_excl_sum256(cnt, sScan, &tot);
+  if (threadIdx.x == 0) {
+    const int64_t base = tot ? (int64_t)atomicAdd(J.cursor, (unsigned long long)tot) : 0;
+    sBase = base;
+    tile_src[b] = J.pair_base + base;
+    tile_cnt[b] = tot;
+  }
+  __syncthreads();
+  const int64_t src = J.pair_base + sBase + off;
+  int32_t o = 0;
+#pragma unroll
+  for (int k = 0; k < WPT; k++) {
+    const uint64_t m = xa[k] & xb[k];
+    for (uint64_t r = m; r; r &= r - 1) {
+      const uint64_t below = (r & (~r + 1)) - 1;  // the bits below the lowest set bit
+      const uint32_t ia = ra[k] + (uint32_t)__popcll(xa[k] & below);
+      const uint32_t ib = rb[k] + (uint32_t)__popcll(xb[k] & below);
+      pairs[src + o] = make_uint2(ia, ib);
+      pair_uid[src + o] = (uint32_t)((w0 + k) * 64 + __popcll(below));
+      o++;
+    }
+  }
+}
+
 __device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t src, int32_t cnt,
                                const uint16_t* sLoc, const uint32_t* sPos, const uint32_t* __restrict__ small_uid,
                                int64_t s0, bool small_is_A, uint2* __restrict__ pairs,
@@ -1088,6 +1144,10 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
       tile_src[b] = J.pair_base;
       tile_cnt[b] = tot;
     }
+    return;
+  }
+  if (!MARK && J.algo == JA_BMENUM) {  // workgroup-uniform: the matches from the AND of both bitmaps
+    probe_bmenum(J, b - tile_base[D.job], b, pairs, pair_uid, tile_src, tile_cnt, sScan);
     return;
   }
   const DList& Sm = J.small_is_A ? J.A : J.B;
