@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "yrwi_host.h"
+#include "yrwi_bitmap.h"
 
 namespace yrwi {
 namespace {
@@ -241,8 +242,8 @@ struct DevBuf {
   }
 };
 
-// url-id bitmaps of the large lists (DList::bm): per posting, its id's bit, and
-// the list position of the first posting of every 64-id word (the word's rank)
+// url-id bitmaps of the large lists (DList::bm, yrwi_bitmap.h): per posting, its
+// id's bit, and the list position of the first posting of every 96-id unit (its rank)
 struct BmSeg {
   const uint32_t* uid;
   uint64_t* bm;
@@ -261,13 +262,14 @@ __global__ void k_bitmap_set(const BmSeg* __restrict__ segs, const int64_t* __re
   const BmSeg S = segs[lo];
   const int64_t j = i - off[lo];
   const uint32_t u = S.uid[j];
-  const uint64_t w = u >> 6;
-  atomicOr(reinterpret_cast<unsigned long long*>(S.bm + 2 * w), 1ull << (u & 63u));
-  if (j == 0 || (S.uid[j - 1] >> 6) != w) S.bm[2 * w + 1] = (uint64_t)j;
+  const BmAt a = bm_at(u);
+  uint32_t* b32 = reinterpret_cast<uint32_t*>(S.bm) + (size_t)a.unit * 4;
+  atomicOr(b32 + (a.bit >> 5), 1u << (a.bit & 31u));
+  if (j == 0 || bm_at(S.uid[j - 1]).unit != a.unit) b32[3] = (uint32_t)j;  // the unit's first posting
   if (S.j5) reinterpret_cast<ulonglong2*>(S.j5)[j] = reinterpret_cast<const ulonglong2*>(S.feat + j * FEAT_WORDS)[0];
 }
 
-// bitmap lists: every posting's bit is set and its word's rank + the bits below give its position
+// bitmap lists: every posting's bit is set and its unit's rank + the bits below give its position
 __global__ void k_bitmap_check(const BmSeg* __restrict__ segs, const int64_t* __restrict__ off, int nseg, int64_t n,
                                unsigned long long* __restrict__ bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -280,8 +282,9 @@ __global__ void k_bitmap_check(const BmSeg* __restrict__ segs, const int64_t* __
   const BmSeg S = segs[lo];
   const int64_t j = i - off[lo];
   const uint32_t u = S.uid[j];
-  const uint64_t bits = S.bm[2 * (u >> 6)], bit = 1ull << (u & 63u);
-  if (!(bits & bit) || (int64_t)S.bm[2 * (u >> 6) + 1] + __popcll(bits & (bit - 1ull)) != j) atomicAdd(bad, 1ull);
+  const BmAt a = bm_at(u);
+  const uint4 U = reinterpret_cast<const uint4*>(S.bm)[a.unit];
+  if (!bm_test(a, U) || bm_pos(a, U) != j) atomicAdd(bad, 1ull);
   if (S.j5 && (S.j5[2 * j] != S.feat[j * FEAT_WORDS] || S.j5[2 * j + 1] != S.feat[j * FEAT_WORDS + 1]))
     atomicAdd(bad, 1ull);
 }
@@ -587,7 +590,7 @@ int build_heads(CtxBase* ctx, const std::vector<ListRec*>& lists) {
 }
 
 // Bitmaps for the lists holding at least 1/YRWI_BM_DIV (default 256) of the url
-// ids (and 4096 postings): nurls/4 bytes each, so at most 64x the list's own ids
+// ids (and 4096 postings): nurls/6 bytes each, so at most 43x the list's own ids
 // (at 1/256 density); total capped by YRWI_BM_GB (default 8), largest lists first.
 // YRWI_BM_DIV=0: none.  The joins probe only the dense ones (>= 1/64, layout_jobs);
 // the sparser ones answer k_chain's tests of a chained fold's later lists and the
@@ -606,8 +609,7 @@ int build_bitmaps(CtxBase* ctx, const std::vector<ListRec*>& lists) {
   const char* g = getenv("YRWI_BM_GB");
   const int64_t cap_bytes = (int64_t)((g ? atof(g) : 8.0) * (double)(1ll << 30));
   if (div <= 0 || ctx->nurls <= 0) return 0;
-  const int64_t words = (ctx->nurls + 63) / 64;
-  const int64_t per = 2 * words;  // uint64 per bitmap
+  const int64_t per = 2 * bm_units(ctx->nurls);  // uint64 per bitmap
   const int64_t thr = std::max<int64_t>(4096, ctx->nurls / div);
   std::vector<ListRec*> big;
   for (ListRec* L : lists)

@@ -818,8 +818,8 @@ static int64_t step_bytes(int32_t mode, int64_t na, int64_t nb) {
 static int64_t loaded_bytes(const JoinQ& J) {
   const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
   if (J.algo == JA_MERGE) return 4 * (ns + nl);
-  if (J.algo == JA_BMAND) return 16 * J.bm_words;  // the bits of both bitmaps (8 B of every 16-B word)
-  if (J.algo == JA_BMENUM) return 32 * J.bm_words;  // both bitmaps' 16-B words
+  if (J.algo == JA_BMAND) return (J.bm3 ? 48 : 32) * J.bm_words;  // every bitmap's 16-B units
+  if (J.algo == JA_BMENUM) return 32 * J.bm_words;  // both bitmaps' 16-B units
   const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
   return bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
 }
@@ -875,7 +875,7 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
       J.algo = JA_BMAND;
       J.small_is_A = 1;
       J.ptile = BMAND_WORDS;
-      J.bm_words = (nurls + 63) / 64;
+      J.bm_words = bm_units(nurls);
       J.ntiles = ceil_div(J.bm_words, BMAND_WORDS);
       J.chain_bm = nullptr;
       order[i] = i;
@@ -888,12 +888,14 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     if (J.B.bm && J.B.n * 64 < nurls) J.B.bm = nullptr;
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
     J.small_is_A = J.A.n <= J.B.n;
-    // both lists with dense bitmaps, the smaller one above 1/8 of the url ids:
-    // their AND streams 32 B per 64 url ids, less than its 4-B ids (JA_BMENUM; a
-    // job whose pairs go to the chain tests, an exclusion or a distance filter
-    // keeps the probe)
+    // both lists with dense bitmaps, the smaller one above 1/12 of the url ids:
+    // their AND streams 2 x 16 B per 96 url ids, less than its 4-B ids
+    // (JA_BMENUM, YRWI_BMENUM=1; a job whose pairs go to the chain tests, an
+    // exclusion or a distance filter keeps the probe).  Off by default: on C2 it
+    // took k_probe 116 -> 124 us and k_compact 228 -> 276 us (a tile's matches
+    // are one compaction workgroup's: far more than a probe tile's)
     if (bm_enum && J.A.bm && J.B.bm && !J.chained && J.mode != JM_MARK && J.maxd >= 65535 && nurls > 0) {
-      const int64_t words = (nurls + 63) / 64;
+      const int64_t words = bm_units(nurls);
       if (bm_enum == 2 || 8 * words < ns) {
         J.algo = JA_BMENUM;
         J.ptile = BMENUM_WORDS;

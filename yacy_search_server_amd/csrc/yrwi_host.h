@@ -274,7 +274,7 @@ struct Lane {
   Stage out_stage;           // pinned landing buffer for results
   Stage down_stage;          // pinned landing buffer for small per-step readbacks (joined sizes)
   int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
-  int bm_enum = 1;           // JA_BMENUM: 0 never, 1 where it reads fewer bytes, 2 whenever both bitmaps are dense (YRWI_BMENUM)
+  int bm_enum = 0;           // JA_BMENUM: 0 never (default), 1 where it reads fewer bytes, 2 whenever both bitmaps are dense (YRWI_BMENUM)
   bool band_order = true;    // band-major compaction schedule (BandOrder); YRWI_BAND_ORDER
   int64_t nurls = 0;         // url ids of the context's dictionary (set with dkhi)
   const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
@@ -604,7 +604,7 @@ inline int begin_pass(Lane* ctx) {
   const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
   ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)8;
   const char* be = getenv("YRWI_BMENUM");  // tests force or forbid the bitmap-AND enumeration
-  ctx->bm_enum = be ? atoi(be) : 1;
+  ctx->bm_enum = be ? atoi(be) : 0;
   const char* b = getenv("YRWI_BAND_ORDER");  // 0: job-order tile schedule (A/B measurements; same results)
   ctx->band_order = !(b && b[0] == '0');
   return 0;

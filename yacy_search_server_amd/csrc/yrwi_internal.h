@@ -49,9 +49,9 @@ struct DList {
   // rows of the fold's lists 0..tw-1 it joins, tw per row (tup[row * tw + list])
   const int32_t* tup;
   int32_t tw;
-  // url-id bitmap of a large index list (nullptr: none), 16 B per 64 ids: word
-  // 2w = bits of ids 64w..64w+63, word 2w+1 = the list position of the first id
-  // of word 2w (rank): membership and position of an id in one 16-B load.
+  // url-id bitmap of a large index list (nullptr: none), 16-B units of
+  // BM_UNIT_IDS = 96 ids: 96 bits and the list position of the unit's first id
+  // (yrwi_bitmap.h): membership and position of an id in one 16-B load.
   // k_probe looks the smaller side's ids up in it instead of searching the list.
   const uint64_t* bm;
   // words 0-1 of every posting's record (2 per posting; bitmap lists only, else
@@ -91,12 +91,12 @@ enum JoinMode : int32_t {
 // merge-path tiles for comparable sizes, per-element probing of the large list
 // for skewed ones (the galloping bound of BASELINE.md §4).
 // JA_BMAND: a counted-only join of two lists that both have url-id bitmaps:
-// popcount(bits A & bits B) over ranges of bitmap words (tiles of BMAND_WORDS),
-// in place of probing one list's ids into the other (k_probe)
+// popcount(bits A & bits B) over ranges of bitmap units (tiles of BMAND_WORDS
+// 16-B units), in place of probing one list's ids into the other (k_probe)
 // JA_BMENUM: the matched pairs of two lists that both have dense url-id bitmaps,
-// from the AND of the bitmaps (tiles of BMENUM_WORDS words): each set bit is a
-// match, its rows are each word's rank + the bits below it -- no id of either
-// list is read.  Taken where streaming both bitmaps (32 B per 64 url ids) costs
+// from the AND of the bitmaps (tiles of BMENUM_WORDS units): each set bit is a
+// match, its rows are each unit's rank + the bits below it -- no id of either
+// list is read.  Taken where streaming both bitmaps (32 B per 96 url ids) costs
 // less than the smaller list's ids alone (4 B per id: the probe's bitmap words
 // mostly hit L2, since a batch's jobs over one large list run back to back --
 // at 20 B per probed id C2 took it for lists above 1/40 density and k_probe went
@@ -105,8 +105,11 @@ enum JoinMode : int32_t {
 // tile claims its run of the job's pair slots with one atomic add on the job's
 // cursor (the compaction reads every tile at tile_src, in tile order).
 enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2, JA_BMENUM = 3 };
-constexpr int BMAND_WORDS = 4096;
-constexpr int BMENUM_WORDS = 256;  // bitmap words per JA_BMENUM tile: one per thread (16384 url ids)
+constexpr int BMAND_WORDS = 4096;  // 16-B bitmap units per JA_BMAND tile
+constexpr int BMENUM_WORDS = 256;  // 16-B bitmap units per JA_BMENUM tile: one per thread (24576 url ids)
+// url-id bitmap units (DList::bm, yrwi_bitmap.h): 96 ids per 16 B
+constexpr int64_t BM_UNIT_IDS = 96;
+inline int64_t bm_units(int64_t nurls) { return (nurls + BM_UNIT_IDS - 1) / BM_UNIT_IDS; }
 constexpr int PROBE_TILE = 256;  // small-list elements per probe workgroup
 #ifndef YRWI_BM_TILE
 #define YRWI_BM_TILE 1024
@@ -191,7 +194,7 @@ struct JoinQ {
   int32_t* chain_tup0;
   int32_t chain_fill;
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
-  int64_t bm_words;    // JA_BMAND / JA_BMENUM: bitmap words of the url-id space
+  int64_t bm_words;    // JA_BMAND / JA_BMENUM: 16-B bitmap units of the url-id space (bm_units)
   const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
   unsigned long long* cursor;  // JA_BMENUM: pair slots claimed so far (zeroed per step)
 };

@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "yrwi_internal.h"
+#include "yrwi_bitmap.h"
 
 namespace yrwi {
 
@@ -848,8 +849,9 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
   const JoinQ& J = jobs[j];
-  if (J.algo == JA_BMAND || J.algo == JA_BMENUM) {  // a range of bitmap words: no ids to read, no range
-    const uint32_t id0 = (uint32_t)min((tile0 + t - tile_base[j]) * (int64_t)J.ptile * 64, (int64_t)0xFFFFFFFF);
+  if (J.algo == JA_BMAND || J.algo == JA_BMENUM) {  // a range of bitmap units: no ids to read, no range
+    const uint32_t id0 =
+        (uint32_t)min((tile0 + t - tile_base[j]) * (int64_t)J.ptile * BM_UNIT_IDS, (int64_t)0xFFFFFFFF);
     if (tile_key) tile_key[tile0 + t] = id0;
     if (tile_job) tile_job[tile0 + t] = j;
     if (probe_key) probe_key[t] = id0 >> probe_shift;
@@ -913,44 +915,41 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
                                                 int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64,
                                                 uint16_t* sLoc = nullptr, uint32_t* sPos = nullptr,
                                                 int64_t* src_out = nullptr, int32_t* tile_lvl = nullptr) {
-  // url-id bitmap of the large list: one 16-B load per key gives membership and,
-  // for a hit, its list position (rank of the word + bits below the id).  BM_TILE
+  // url-id bitmap of the large list: one 16-B load per key (yrwi_bitmap.h) gives
+  // membership and, for a hit, its list position (rank + bits below).  BM_TILE
   // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
   // one load instruction's 64 lanes read 64 consecutive small-list ids and their
   // bitmap words fall into a few 128-B lines (thread-consecutive keys spread an
   // instruction over up to 64 lines: C2 k_probe 123 -> 114 us)
   static_assert(KPT <= 8, "bitmap tile: one 16-bit prefix field per key slot, four per 64-bit scan");
   const int64_t s0 = (b - tile_base0) * (KPT * PROBE_TILE);
-  const __amdgpu_buffer_rsrc_t rbm =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(Lg.bm), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbm = bm_rsrc(Lg.bm);
   uint32_t keys[KPT];
 #pragma unroll
   for (int k = 0; k < KPT; k++) keys[k] = ldg(Sm.uid + min(s0 + k * PROBE_TILE + (int64_t)threadIdx.x, Sm.n - 1));
-  // every bitmap word of the thread in flight at once: whole 16-B buffer loads
-  // (a plain load was split, its second half loaded only on a hit, and each key
-  // waited for the previous one)
+  // every bitmap load of the thread in flight at once: whole 16-B units through
+  // buffer loads (a plain load was split, its second half loaded only on a hit,
+  // and each key waited for the previous one)
   uint4 E[KPT];
 #pragma unroll
-  for (int k = 0; k < KPT; k++)
-    E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(keys[k] >> 6) * 16, 0, 0));
+  for (int k = 0; k < KPT; k++) E[k] = bm_unit(rbm, bm_at(keys[k]));
   uint32_t hm = 0;
-  int64_t jls[KPT];
+  int32_t jls[KPT];  // large-list positions < 2^31
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     jls[k] = 0;
     if (s0 + k * PROBE_TILE + (int64_t)threadIdx.x >= Sm.n) continue;
-    const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x, ey = (uint64_t)E[k].w << 32 | E[k].z;
-    const uint64_t bit = 1ull << (keys[k] & 63u);
-    if (ex & bit) {
+    const BmAt a = bm_at(keys[k]);
+    if (bm_test(a, E[k])) {
       hm |= 1u << k;
-      jls[k] = (int64_t)ey + __popcll(ex & (bit - 1ull));
+      jls[k] = bm_pos(a, E[k]);
     }
   }
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     if (!((hm >> k) & 1u)) continue;
     const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
-    const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
+    const int64_t ia = J.small_is_A ? ik : (int64_t)jls[k], ib = J.small_is_A ? (int64_t)jls[k] : ik;
     if (mark) {
       stg(J.removed + ia, (uint8_t)1);
     } else if (J.maxd < 65535 &&
@@ -967,21 +966,18 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
   int32_t tp[KPT];
   uint32_t hm0 = hm;
   if (pre) {
-    const __amdgpu_buffer_rsrc_t r2 =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(J.chain_bm), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2 = bm_rsrc(J.chain_bm);
     uint4 E2[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
       E2[k] = make_uint4(0, 0, 0, 0);
-      if ((hm >> k) & 1u)
-        E2[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r2, (int)(keys[k] >> 6) * 16, 0, 0));
+      if ((hm >> k) & 1u) E2[k] = bm_unit(r2, bm_at(keys[k]));
     }
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
-      const uint64_t ex2 = (uint64_t)E2[k].y << 32 | E2[k].x;
-      const uint64_t bit = 1ull << (keys[k] & 63u);
-      tp[k] = (int32_t)(E2[k].z + __popcll(ex2 & (bit - 1ull)));  // list positions < 2^31
-      if (!(ex2 & bit)) hm &= ~(1u << k);
+      const BmAt a = bm_at(keys[k]);
+      tp[k] = bm_pos(a, E2[k]);  // list positions < 2^31
+      if (!bm_test(a, E2[k])) hm &= ~(1u << k);
     }
   }
   // hits leave in key order (slot k's 256 keys, then slot k+1's): one 64-bit scan
@@ -1022,7 +1018,7 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
   for (int k = 0; k < KPT; k++) {
     if (!((hm >> k) & 1u)) continue;
     const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
-    const int64_t ia = J.small_is_A ? ik : jls[k], ib = J.small_is_A ? jls[k] : ik;
+    const int64_t ia = J.small_is_A ? ik : (int64_t)jls[k], ib = J.small_is_A ? (int64_t)jls[k] : ik;
     const int32_t lo = base[k] + (int32_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
     if (J.count_only) {  // counted only
     } else if (sLoc) {  // a chained job's tile: its matches stay in LDS for the chain tests
@@ -1038,35 +1034,28 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
 }
 
 
-// One JA_BMENUM tile: BMENUM_WORDS bitmap words, WPT consecutive words per
-// thread (the 16-B entries of both lists stream coalesced: the 64 id bits and
-// the list position of the word's first id).  A match is a bit set in both;
-// its rows are each list's word position + the bits below it.  Matches leave in
-// url-id order (thread-consecutive words, block scan of the counts) into the run
-// the tile claims from the job's cursor.
+// One JA_BMENUM tile: BMENUM_WORDS 16-B bitmap units, WPT consecutive units per
+// thread (both lists' units stream coalesced).  A match is a bit set in both;
+// its rows are each unit's rank + the bits below it.  Matches leave in url-id
+// order (thread-consecutive units, block scan of the counts) into the run the
+// tile claims from the job's cursor.
 __device__ __forceinline__ void probe_bmenum(const JoinQ& J, int64_t tj, int64_t b, uint2* __restrict__ pairs,
                                              uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
                                              int32_t* __restrict__ tile_cnt, int32_t* sScan) {
   constexpr int WPT = BMENUM_WORDS / PROBE_TILE;
-  static_assert(WPT * PROBE_TILE == BMENUM_WORDS, "whole words per thread");
+  static_assert(WPT * PROBE_TILE == BMENUM_WORDS, "whole units per thread");
   __shared__ int64_t sBase;
   const int64_t w0 = tj * BMENUM_WORDS + (int64_t)threadIdx.x * WPT;
-  uint64_t xa[WPT], xb[WPT];
-  uint32_t ra[WPT], rb[WPT];
+  uint4 xa[WPT], xb[WPT];
   int32_t cnt = 0;
 #pragma unroll
   for (int k = 0; k < WPT; k++) {
     const int64_t w = w0 + k;
-    xa[k] = xb[k] = 0;
-    ra[k] = rb[k] = 0;
+    xa[k] = xb[k] = make_uint4(0, 0, 0, 0);
     if (w < J.bm_words) {
-      const ulonglong2 a = ldg(reinterpret_cast<const ulonglong2*>(J.A.bm) + w);
-      const ulonglong2 c = ldg(reinterpret_cast<const ulonglong2*>(J.B.bm) + w);
-      xa[k] = a.x;
-      ra[k] = (uint32_t)a.y;  // list positions < 2^31
-      xb[k] = c.x;
-      rb[k] = (uint32_t)c.y;
-      cnt += __popcll(a.x & c.x);
+      xa[k] = ldg(reinterpret_cast<const uint4*>(J.A.bm) + w);
+      xb[k] = ldg(reinterpret_cast<const uint4*>(J.B.bm) + w);
+      cnt += __popc(xa[k].x & xb[k].x) + __popc(xa[k].y & xb[k].y) + __popc(xa[k].z & xb[k].z);
     }
   }
   int32_t tot;
@@ -1082,14 +1071,20 @@ __device__ __forceinline__ void probe_bmenum(const JoinQ& J, int64_t tj, int64_t
   int32_t o = 0;
 #pragma unroll
   for (int k = 0; k < WPT; k++) {
-    const uint64_t m = xa[k] & xb[k];
-    for (uint64_t r = m; r; r &= r - 1) {
-      const uint64_t below = (r & (~r + 1)) - 1;  // the bits below the lowest set bit
-      const uint32_t ia = ra[k] + (uint32_t)__popcll(xa[k] & below);
-      const uint32_t ib = rb[k] + (uint32_t)__popcll(xb[k] & below);
-      pairs[src + o] = make_uint2(ia, ib);
-      pair_uid[src + o] = (uint32_t)((w0 + k) * 64 + __popcll(below));
-      o++;
+    const uint32_t id0 = (uint32_t)((w0 + k) * BM_UNIT_IDS);
+    uint32_t pa = xa[k].w, pb = xb[k].w;  // the units' ranks
+#pragma unroll
+    for (int h = 0; h < 3; h++) {
+      const uint32_t a32 = h == 0 ? xa[k].x : h == 1 ? xa[k].y : xa[k].z;
+      const uint32_t b32 = h == 0 ? xb[k].x : h == 1 ? xb[k].y : xb[k].z;
+      for (uint32_t r = a32 & b32; r; r &= r - 1) {
+        const uint32_t below = (r & (~r + 1)) - 1;  // the bits below the lowest set bit
+        pairs[src + o] = make_uint2(pa + (uint32_t)__popc(a32 & below), pb + (uint32_t)__popc(b32 & below));
+        pair_uid[src + o] = id0 + 32u * h + (uint32_t)__popc(below);
+        o++;
+      }
+      pa += (uint32_t)__popc(a32);
+      pb += (uint32_t)__popc(b32);
     }
   }
 }
@@ -1131,13 +1126,21 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   if (!MARK && J.algo == JA_BMAND) {  // workgroup-uniform: |A x B| from the bits of both bitmaps
     const int64_t w0 = (b - tile_base[D.job]) * (int64_t)J.ptile;
     const int64_t w1 = w0 + J.ptile < J.bm_words ? w0 + J.ptile : J.bm_words;
+    const uint4* A = reinterpret_cast<const uint4*>(J.A.bm);
+    const uint4* B = reinterpret_cast<const uint4*>(J.B.bm);
     int32_t c = 0;
-    if (J.bm3)
-      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
-        c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w) & ldg(J.bm3 + 2 * w));
-    else
-      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE)
-        c += __popcll(ldg(J.A.bm + 2 * w) & ldg(J.B.bm + 2 * w));
+    if (J.bm3) {
+      const uint4* C = reinterpret_cast<const uint4*>(J.bm3);
+      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE) {
+        const uint4 x = ldg(A + w), y = ldg(B + w), z = ldg(C + w);  // (w: the units' ranks)
+        c += __popc(x.x & y.x & z.x) + __popc(x.y & y.y & z.y) + __popc(x.z & y.z & z.z);
+      }
+    } else {
+      for (int64_t w = w0 + threadIdx.x; w < w1; w += PROBE_TILE) {
+        const uint4 x = ldg(A + w), y = ldg(B + w);
+        c += __popc(x.x & y.x) + __popc(x.y & y.y) + __popc(x.z & y.z);
+      }
+    }
     int32_t tot;
     block_excl_sum256(c, sScan, &tot);
     if (threadIdx.x == 0) {
@@ -1220,13 +1223,11 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   const bool hit0 = hit;
   int32_t tp = 0;
   if (pre && hit) {
-    const __amdgpu_buffer_rsrc_t r2 =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(J.chain_bm), 0, 0x7FFFFFFF, 0x00020000);
-    const uint4 E2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r2, (int)(key >> 6) * 16, 0, 0));
-    const uint64_t ex2 = (uint64_t)E2.y << 32 | E2.x;
-    const uint64_t bit = 1ull << (key & 63u);
-    tp = (int32_t)(E2.z + __popcll(ex2 & (bit - 1ull)));
-    if (!(ex2 & bit)) hit = false;
+    const __amdgpu_buffer_rsrc_t r2 = bm_rsrc(J.chain_bm);
+    const BmAt a = bm_at(key);
+    const uint4 E2 = bm_unit(r2, a);
+    tp = bm_pos(a, E2);
+    if (!bm_test(a, E2)) hit = false;
   }
   int32_t tot;
   const int32_t off = block_excl_sum256(hit ? 1 : 0, sScan, &tot);
@@ -1533,21 +1534,18 @@ __device__ __forceinline__ uint32_t chain_tests(const ChainList* cl, int ninc, i
     if (L.bm) {
       CPROF(2, __popc(alive));
       if (threadIdx.x == 0) CPROF(3, 1);
-      const __amdgpu_buffer_rsrc_t rbm =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(L.bm), 0, 0x7FFFFFFF, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rbm = bm_rsrc(L.bm);
       uint4 E[KPT];
 #pragma unroll
       for (int k = 0; k < KPT; k++) {
         E[k] = make_uint4(0, 0, 0, 0);
-        if ((alive >> k) & 1u)
-          E[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbm, (int)(key[k] >> 6) * 16, 0, 0));
+        if ((alive >> k) & 1u) E[k] = bm_unit(rbm, bm_at(key[k]));
       }
 #pragma unroll
       for (int k = 0; k < KPT; k++) {
-        const uint64_t ex = (uint64_t)E[k].y << 32 | E[k].x;
-        const uint64_t bit = 1ull << (key[k] & 63u);
-        p[k] = (int32_t)(E[k].z + __popcll(ex & (bit - 1ull)));  // list positions < 2^31
-        if (((alive >> k) & 1u) && (ex & bit)) hit |= 1u << k;
+        const BmAt a = bm_at(key[k]);
+        p[k] = bm_pos(a, E[k]);  // list positions < 2^31
+        if (((alive >> k) & 1u) && bm_test(a, E[k])) hit |= 1u << k;
       }
     } else {
       const ProbeDesc D = cr[l];  // workgroup-uniform
@@ -1814,10 +1812,10 @@ __global__ void k_sel_lookup(const uint64_t* __restrict__ hi, const uint8_t* __r
 __device__ __forceinline__ bool list_has(const ChainList& L, uint32_t u, int64_t* pos) {
   if (L.n <= 0) return false;
   if (L.bm) {
-    const ulonglong2 w = ldg(reinterpret_cast<const ulonglong2*>(L.bm) + (u >> 6));
-    const uint64_t bit = 1ull << (u & 63u);
-    *pos = (int64_t)w.y + __popcll(w.x & (bit - 1ull));
-    return (w.x & bit) != 0;
+    const BmAt a = bm_at(u);
+    const uint4 U = ldg(reinterpret_cast<const uint4*>(L.bm) + a.unit);
+    *pos = bm_pos(a, U);
+    return bm_test(a, U);
   }
   const int64_t q = lower_bound_cl(L, u);
   *pos = q;
