@@ -400,6 +400,40 @@ def test_merge_tile_boundaries(nab, monkeypatch):
         ix.close()
 
 
+@pytest.mark.parametrize("mode", ["probe", "enum", "count_first"])
+def test_bitmap_unit_boundaries(mode, monkeypatch):
+    """Url-id bitmaps in 16-B units of 96 ids (yrwi_bitmap.h): lists whose ids sit
+    on both sides of every unit's word boundaries (ids 96v + 0/31/32/63/64/95),
+    the first and the last url id, a url space that is not a multiple of 96.  A
+    (every id) and C (every third) and B (the boundary ids) have bitmaps, D (ids
+    96v + 95 and 96v + 96, below the bitmap minimum) has none: 2-4 term joins,
+    an exclusion, through the bitmap probe, the bitmap-AND enumeration
+    (YRWI_BMENUM=2) and the count-first popcounts (YRWI_CHAIN_CF=2) -- rows and
+    top-k equal to the oracle's."""
+    monkeypatch.setenv("YRWI_BMENUM", "2" if mode == "enum" else "0")
+    monkeypatch.setenv("YRWI_CHAIN_CF", "2" if mode == "count_first" else "1")
+    m = 96 * 1000 + 37
+    keys = np.arange(m)
+    r = keys % 96
+    sel_b = np.isin(r, (0, 31, 32, 63, 64, 95)) | (keys == 0) | (keys == m - 1)
+    d = {b"TERMunitA___": _keyed_rows(keys, 11), b"TERMunitB___": _keyed_rows(keys[sel_b], 12),
+         b"TERMunitC___": _keyed_rows(keys[keys % 3 == 0], 13),
+         b"TERMunitD___": _keyed_rows(keys[(r == 95) | ((r == 0) & (keys > 0))][:3000], 14)}
+    A, B, C, D = d
+    ix = RWIIndex(0)
+    try:
+        for h, rows in d.items():
+            ix.add(h, rows)
+        for inc, exc in (([A, B], []), ([B, C], []), ([A, B, C], []), ([A, C, B, D], []), ([B, C], [D]),
+                         ([A, B, C], [D]), ([C, A], [B])):
+            assert np.array_equal(ix.term_search(inc, exc, 2147483647, NOW),
+                                  orc.term_search(d, inc, exc, 2147483647, NOW)), (inc, exc)
+            got = [(h.urlhash, h.score) for h in ix.search(inc, exc, now_ms=NOW, k=200)]
+            assert got == [(h, s) for h, s, _ in orc.search(d, inc, exc, now_ms=NOW, k=200)], (inc, exc)
+    finally:
+        ix.close()
+
+
 @pytest.mark.parametrize("gb", ["0.000001", "0.002"])
 def test_batch_split_by_scratch_budget(corpus, gb, monkeypatch):
     """A batch larger than the scratch budget runs as consecutive passes over

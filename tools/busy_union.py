@@ -10,7 +10,8 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].split("::")[-1]) for r in rows)
 gap_ns = float(sys.argv[2]) * 1e6 * 0.8 if len(sys.argv) > 2 else 40e6
-# the region: kernels between the first two idle gaps longer than gap_ns (after the warm-up)
+# the region: the stretch between two consecutive idle gaps longer than gap_ns
+# that holds the most k_compact dispatches (the index build has gaps of its own)
 ends, cuts = 0, []
 for s, e, n in iv:
     if ends and s - ends > gap_ns:
@@ -18,7 +19,9 @@ for s, e, n in iv:
     ends = max(ends, e)
 if len(cuts) < 2:
     sys.exit("no bracketing gaps found: %d" % len(cuts))
-r0, r1 = cuts[0][1], cuts[1][0]
+best = max(range(len(cuts) - 1),
+           key=lambda i: sum(1 for s, e, n in iv if s >= cuts[i][1] and e <= cuts[i + 1][0] and n.startswith("k_compact")))
+r0, r1 = cuts[best][1], cuts[best + 1][0]
 sel = [(s, e, n) for s, e, n in iv if s >= r0 and e <= r1]
 span = r1 - r0
 # union and concurrency
