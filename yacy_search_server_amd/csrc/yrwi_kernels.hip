@@ -2263,12 +2263,7 @@ __device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int3
 // from the url keys, C2 k_score 94 -> 115 us -- the headline pays for it; and a
 // separate per-chunk kernel counting in LDS first, k_hostcount: 107 + 18 us, its
 // distinct (chunk, host) pairs still cost a device atomic each.)
-#ifdef YRWI_RED_WPE  // A/B builds: the waves per SIMD k_reduce's register allocation must allow
-#define RED_WPE __attribute__((amdgpu_waves_per_eu(YRWI_RED_WPE, 8)))
-#else
-#define RED_WPE
-#endif
-__global__ __launch_bounds__(CHUNK_THREADS) RED_WPE void k_reduce(const RankQ* __restrict__ qs,
+__global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
   __shared__ int32_t sI[4 * (2 * NF + 8)];
@@ -3593,12 +3588,7 @@ __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t 
 #endif
 // Chunks run in `order` (every query's first chunks before anybody's later ones),
 // so a big query's later chunks find its threshold (Tq, see PruneP) established.
-#ifdef YRWI_SCORE_WPE  // A/B builds: the waves per SIMD k_score's register allocation must allow
-#define SCORE_WPE __attribute__((amdgpu_waves_per_eu(YRWI_SCORE_WPE, 8)))
-#else
-#define SCORE_WPE
-#endif
-__global__ __launch_bounds__(CHUNK_THREADS) SCORE_WPE void k_score(const RankQ* __restrict__ qs,
+__global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
                                                         const int32_t* __restrict__ chunk_q,
                                                         const int32_t* __restrict__ order,
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
