@@ -1793,6 +1793,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       RankQ& R = rq[(size_t)qi];
       if (!R.hp_nb) continue;
       R.ecnt = d_ecnt + eb;
+      R.hp_hist = d_hist;
       eb += R.n;
     }
     if (upload(ctx, d_bq, bq)) return YRWI_E_HIP;

@@ -309,6 +309,7 @@ struct RankQ {
   int32_t hp_nb;           // authority by partition (ecnt): the query's host buckets
   int32_t* ecnt;           // ... and every element's host count (nullptr: the host tables serve)
   int64_t hp_hoff;         // ... its first histogram entry (bucket-major: hp_hoff + bucket * nchunks + chunk)
+  int32_t* hp_hist;        // ... the histogram (k_reduce counts every chunk's buckets into it)
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)

@@ -2250,6 +2250,16 @@ constexpr int NP2 = (NF + 1) / 2;  // packed field pairs
 __device__ __forceinline__ bool frac_lt(int32_t c1, int32_t d1, int32_t c2, int32_t d2) { return c1 * d2 < c2 * d1; }
 
 
+constexpr int HB_SLOTS = 4096;   // LDS table slots of a bucket
+__device__ __forceinline__ uint32_t hp_bucket(uint32_t hid, int32_t nb) {
+  uint32_t x = hid * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  return (uint32_t)(((uint64_t)x * (uint64_t)nb) >> 32);
+}
+
+
 // One workgroup per CHUNK container elements.  Rows are read coalesced
 // (element s*256 + tid of the chunk), which is all the order-independent parts
 // need (min/max, tf, host counts); the order-dependent fold of posintext /
@@ -2276,12 +2286,16 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ uint32_t sSegM[SEGC];
   __shared__ uint32_t sSegL[SEGC];
   __shared__ int32_t sFirstInfo[3];
+  __shared__ int32_t sHB[HPART_MAXS];  // authority by partition: the chunk's elements per host bucket
 
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   const int64_t c = b - Q.chunk_base;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int hnb = Q.ecnt ? Q.hp_nb : 0;  // block-uniform
+  for (int i = threadIdx.x; i < hnb; i += CHUNK_THREADS) sHB[i] = 0;
+  if (hnb) __syncthreads();
 
   // ---- coalesced pass: order-independent summaries
   uint32_t pmn[NP2], pmx[NP2];  // fields 2j | 2j+1 << 16
@@ -2335,6 +2349,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       myfirst = min(myfirst, eo);
       av[s] = F.a;
       po = 0x80000000u | ((uint32_t)F.od << 16) | (uint32_t)F.p;
+      if (hnb) atomicAdd(&sHB[hp_bucket((uint32_t)(rg[s % RED_GROUP].w[3] >> 34), hnb)], 1);
       if (Q.want_authority && !Q.ecnt) {  // (a partitioned query: k_hbucket counts)
         const uint64_t key = elem_host(Q, rg[s % RED_GROUP].w[3], e) + 1;
         uint64_t slot = mix64(key) & Q.hmask;
@@ -2357,6 +2372,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   if (Q.want_authority && !Q.ecnt) {  // block-uniform: one atomicMax per wave instead of one per posting
     const int32_t wm = wave_max_i(hmax);
     if (lane == 0 && wm > 0) atomicMax(&shard[qi].maxdom, wm);
+  }
+  if (hnb) {  // the chunk's bucket counts (bucket-major), for k_hpart_scatter's scan
+    __syncthreads();
+    for (int i = threadIdx.x; i < hnb; i += CHUNK_THREADS) Q.hp_hist[Q.hp_hoff + (int64_t)i * Q.nchunks + c] = sHB[i];
   }
   // first valid element of the chunk (element order)
   int32_t firstIdx;
@@ -2671,7 +2690,8 @@ __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t 
 // :176-216) for queries whose records carry dense host ids, on one context
 // (RankQ::ecnt; sharded contexts keep the host tables the owner exchange reads).
 // A query's valid elements are spread over hp_nb buckets by a hash of their host
-// id (k_hpart_hist counts per chunk and bucket, a scan gives every (bucket, chunk)
+// id (k_reduce counts per chunk and bucket as it streams the records -- round 5
+// ran a separate k_hpart_hist pass over them, 6.5 us on C5 --, a scan gives every (bucket, chunk)
 // its place, k_hpart_scatter writes (host id, element) there); every host lands in
 // exactly one bucket, so one workgroup per bucket (k_hbucket) counts its hosts in
 // LDS, writes every element's host count (ecnt, what cardinal reads) and folds
@@ -2679,36 +2699,6 @@ __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t 
 // table probe per scored posting.  A bucket whose hosts overflow its LDS table
 // counts the rest in the query's global host table (only its workgroup touches
 // those hosts, so their counts are final when it reads them back).
-constexpr int HB_SLOTS = 4096;   // LDS table slots of a bucket
-__device__ __forceinline__ uint32_t hp_bucket(uint32_t hid, int32_t nb) {
-  uint32_t x = hid * 0x9E3779B1u;
-  x ^= x >> 15;
-  x *= 0x85EBCA77u;
-  x ^= x >> 13;
-  return (uint32_t)(((uint64_t)x * (uint64_t)nb) >> 32);
-}
-
-__global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_hist(const RankQ* __restrict__ qs,
-                                                              const int32_t* __restrict__ chunk_q,
-                                                              int32_t* __restrict__ hist) {
-  __shared__ int32_t sH[HPART_MAXS];
-  const int64_t b = blockIdx.x;
-  const RankQ& Q = qs[chunk_q[b]];
-  if (!Q.ecnt) return;  // block-uniform
-  const int64_t c = b - Q.chunk_base;
-  const int nb = Q.hp_nb;
-  for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) sH[i] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < CHUNK_IPT; s++) {
-    const int64_t e = c * CHUNK + s * CHUNK_THREADS + threadIdx.x;
-    if (e < Q.n && !(Q.removed && ldg(Q.removed + e)))
-      atomicAdd(&sH[hp_bucket((uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34), nb)], 1);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) hist[Q.hp_hoff + (int64_t)i * Q.nchunks + c] = sH[i];
-}
-
 __global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_scatter(const RankQ* __restrict__ qs,
                                                                  const int32_t* __restrict__ chunk_q,
                                                                  const int32_t* __restrict__ hoffs,
@@ -4459,7 +4449,7 @@ int launch_host_part(const RankQ* d_q, const int32_t* d_chunk_q, int64_t total_c
                      int32_t* d_hoffs, int64_t nhist, void* d_tmp, size_t tmp_bytes, uint2* d_part, const int2* d_bq,
                      int32_t nbuckets, ShardSum* d_shard, void* st) {
   if (total_chunks <= 0 || nbuckets <= 0) return 0;
-  hipLaunchKernelGGL(k_hpart_hist, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_hist);
+  // (the histogram: k_reduce, launched before on this stream)
   size_t t = tmp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(d_tmp, t, d_hist, d_hoffs, (int)(nhist + 1), S(st)) != hipSuccess) return -1;
   hipLaunchKernelGGL(k_hpart_scatter, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
