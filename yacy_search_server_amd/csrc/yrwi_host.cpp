@@ -1878,7 +1878,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
   hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid))
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid, hp_buckets > 0))
     return ctx->fail(YRWI_E_HIP, "reduce launch");
   if (hp_buckets > 0 &&
       launch_host_part(d_q, d_cq, chunks, d_hist, d_hoffs, hp_hist, d_hptmp, hp_tmp, d_part, d_bq,

@@ -404,9 +404,11 @@ int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njob
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
+// hp_any: some query of the launch counts host buckets (RankQ::ecnt): k_reduce
+// then takes HPART_MAXS ints of dynamic LDS for them (the others launch without)
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr, bool hp_any = false);
 // authority host counts by partition (RankQ::ecnt): histogram per (query bucket, chunk) -> scan ->
 // scatter (host id, element) -> per-bucket LDS counts, every element's count, maxdomcount
 int launch_host_part(const RankQ* d_q, const int32_t* d_chunk_q, int64_t total_chunks, int32_t* d_hist,

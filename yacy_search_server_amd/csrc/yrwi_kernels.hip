@@ -2286,7 +2286,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ uint32_t sSegM[SEGC];
   __shared__ uint32_t sSegL[SEGC];
   __shared__ int32_t sFirstInfo[3];
-  __shared__ int32_t sHB[HPART_MAXS];  // authority by partition: the chunk's elements per host bucket
+  extern __shared__ int32_t sHB[];  // authority by partition: the chunk's elements per host bucket (dynamic)
 
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
@@ -4436,10 +4436,11 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid, bool hp_any) {
+  // (static, the 4 KB cost every batch's k_reduce LDS whether it counted hosts or not)
   if (total_chunks > 0)
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                       d_chunks, d_shard);
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS),
+                       hp_any ? HPART_MAXS * sizeof(int32_t) : 0, S(st), d_q, d_chunk_q, d_chunks, d_shard);
   if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // k_reduce alone (statistics)
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
