@@ -8,7 +8,7 @@ ARGS=${@:---steps 3 --warmup 1 --no-cpu --latency 0 --inflight 1 --legs none}
 R=$(pwd)
 mkdir -p $R/gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d /tmp/pmc_$TAG -o run -- python3 $R/bench.py $ARGS > /tmp/pmc_$TAG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc $CTRS --kernel-include-regex "${PMC_KERNELS:-k_reduce|k_score|k_compact|k_probe}" --output-format csv -d /tmp/pmc_$TAG -o run -- python3 $R/bench.py $ARGS > /tmp/pmc_$TAG.log 2>&1
 python3 - "$R/gpurun_out/pmc/$TAG.csv" /tmp/pmc_$TAG <<'PY'
 import csv, glob, sys
 from collections import defaultdict
