@@ -1,6 +1,6 @@
 #!/bin/bash
 # One rocprofv3 --pmc pass (own run, kernel trace only) over a short isolated bench;
-# per-kernel counter sums into gpurun_out/pmc/<tag>.csv (summarise with tools/pmc_table.py).
+# per-kernel counter sums into gpurun_out/pmc/<tag>.csv (kernel, counter, total, dispatches, per dispatch).
 #   bash tools/pmc_pass.sh <tag> "<COUNTER ...>" [bench args]
 set -e
 TAG=$1; CTRS=$2; shift 2
