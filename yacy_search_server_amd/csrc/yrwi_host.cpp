@@ -1952,7 +1952,8 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   }
   int32_t* d_order = arena_alloc<int32_t>(ctx, 2 * chunks);
   unsigned long long* d_tq = arena_alloc<unsigned long long>(ctx, nq);
-  if (!d_order || !d_tq) return ctx->fail(YRWI_E_NOMEM, "arena");
+  uint8_t* d_qtab = arena_alloc<uint8_t>(ctx, (int64_t)nq * (int64_t)score_qtab_bytes());
+  if (!d_order || !d_tq || !d_qtab) return ctx->fail(YRWI_E_NOMEM, "arena");
   if (upload(ctx, d_order, order)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_tq, 0, sizeof(unsigned long long) * (size_t)nq, ctx->stream));
   // (a separate launch of every query's first chunk, so that all later chunks
@@ -1964,7 +1965,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   hipEvent_t s0 = span_open(ctx, tm);
   hipEvent_t smid = tm ? ctx->event() : nullptr;
   if (launch_score(d_q, d_cq, d_order, nq, chunks, seed, d_norm, d_cand, d_ccnt, kc, d_redo, d_zero + 1, d_tq,
-                   ctx->stream, smid))
+                   d_qtab, ctx->stream, smid))
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kscore.push_back({s0, smid});

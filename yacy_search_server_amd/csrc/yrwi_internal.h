@@ -421,8 +421,9 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 // chunks in d_order ((chunk, query) int pairs); d_tq: per-query score threshold (zeroed), see PruneP in yrwi_kernels.hip
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
-                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* stream,
+                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* d_qtab, void* stream,
                  void* ev_mid = nullptr);
+size_t score_qtab_bytes();  // per query: d_qtab of launch_score (its pruning parameters and term tables)
 // candidates one k_topq group may hold (lists per group = min(64, capacity / list stride))
 int topq_capacity(int32_t keff);
 // top-k of candidate-list groups: group g = lists [gbase[g], gbase[g]+gn[g]) of d_in (stride

@@ -3420,6 +3420,34 @@ __device__ __forceinline__ PruneP prune_params(const NormState& N, const RankQ& 
   return P;
 }
 
+// A query's pruning parameters and term tables, built once per query (k_qtabs,
+// right before k_score) instead of in every chunk's workgroup: k_score's
+// prologue took 5.2 of a C2 workgroup's 24.5 us (YRWI_PHASE_CLOCK), the dependent
+// reads of the query's constants, thread 0's prune_params and the 2304-entry
+// table build between two barriers; now one coalesced copy of 9.9 KB (L2-resident:
+// every chunk of the query reads the same) beside the threshold's read.
+struct QTab {
+  PruneP P;
+  CardTab T;
+};
+#ifndef YRWI_CARD_TAB_MIN
+#define YRWI_CARD_TAB_MIN 512  // a chunk of at most this many postings computes its cardinals without the tables
+#endif
+__global__ __launch_bounds__(256) void k_qtabs(const RankQ* __restrict__ qs, const NormState* __restrict__ norm,
+                                              QTab* __restrict__ out) {
+  const int qi = blockIdx.x;
+  const RankQ& Q = qs[qi];
+  const NormState& N = norm[qi];
+  if (Q.n > YRWI_CARD_TAB_MIN) build_card_tab(&out[qi].T, N, Q);  // (only chunks above it read the tables)
+  if (threadIdx.x == 0) out[qi].P = prune_params(N, Q);
+}
+__device__ __forceinline__ void copy_card_tab(CardTab* dst, const CardTab* __restrict__ src) {
+  static_assert(sizeof(CardTab) % 16 == 0, "16-B copies");
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  for (int i = threadIdx.x; i < (int)(sizeof(CardTab) / 16); i += blockDim.x) d4[i] = ldg(s4 + i);
+}
+
 // Upper bound of cardinal for a posting's record: domlength and date exactly
 // (a posting's own date may lie above the clone-clamped maximum), the other
 // int terms at their maxima, tf / authority maxima, flags and language exactly.
@@ -3580,9 +3608,6 @@ __device__ __forceinline__ uint64_t score_threshold(const uint64_t* a, uint32_t 
 }
 
 
-#ifndef YRWI_CARD_TAB_MIN
-#define YRWI_CARD_TAB_MIN 512
-#endif
 // Chunks run in `order` (every query's first chunks before anybody's later ones),
 // so a big query's later chunks find its threshold (Tq, see PruneP) established.
 __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict__ qs,
@@ -3591,7 +3616,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
                                                         const NormState* __restrict__ norm, Cand* __restrict__ cand,
                                                         int32_t* __restrict__ cand_cnt, int32_t kc,
                                                         int32_t* __restrict__ redo, int32_t* __restrict__ nredo,
-                                                        unsigned long long* __restrict__ Tq) {
+                                                        unsigned long long* __restrict__ Tq,
+                                                        const QTab* __restrict__ qtab) {
   __shared__ uint64_t s1[SCORE_SMALL];
   __shared__ uint64_t s2[SCORE_SMALL];
   __shared__ int32_t sScan[4];
@@ -3612,20 +3638,25 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const int qi = ob.y;
   const RankQ& Q = qs[qi];
   const NormState& N = norm[qi];  // per-query constants: scalar loads
+  const int64_t c = b - Q.chunk_base;
+  const int32_t kq = Q.k < kc ? Q.k : kc;
+  // the one-byte fields' term tables pay off only for a chunk with many postings
+  // (2304 entries per workgroup); a short chunk computes its few cardinals directly
+  const int64_t nel = Q.n - c * CHUNK < CHUNK ? Q.n - c * CHUNK : CHUNK;
+  const CardTab* tab = kq <= SCORE_SMALL && nel > YRWI_CARD_TAB_MIN ? &sCard : nullptr;  // workgroup-uniform
   if (tid == 0) {
     sT = __hip_atomic_load(Tq + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sP = prune_params(N, Q);
+    sP = qtab[qi].P;
   }
   if (tid < 32) sFlag[tid] = 0;
+  if (tab) copy_card_tab(&sCard, &qtab[qi].T);
   __syncthreads();
   const FilterQ* F = Q.filt;
   int32_t* flagc = (F && F->flagcount) ? sFlag : nullptr;
-  const int64_t c = b - Q.chunk_base;
   // strided element map (neighbouring lanes read neighbouring rows); the
   // candidate key carries the container index.  The hashCode (tie-break) is only
   // computed for the selected prefix.
   uint64_t a[CHUNK_IPT];
-  const int32_t kq = Q.k < kc ? Q.k : kc;
   if (kq > SCORE_SMALL) {  // large k (doubledom stacks): only the flag counts here
     if (flagc) {
       (void)score_elems<false>(Q, N, c, flagc, a, nullptr);
@@ -3635,12 +3666,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     if (tid == 0) redo[atomicAdd(nredo, 1)] = (int32_t)b;
     return;
   }
-  // the one-byte fields' term tables pay off only for a chunk with many postings
-  // (2304 entries per workgroup); a short chunk computes its few cardinals directly
-  const int64_t nel = Q.n - c * CHUNK < CHUNK ? Q.n - c * CHUNK : CHUNK;
-  const CardTab* tab = nel > YRWI_CARD_TAB_MIN ? &sCard : nullptr;  // workgroup-uniform
-  if (tab) build_card_tab(&sCard, N, Q);
-  __syncthreads();
   const PruneP P = sP;
   const uint64_t T0 = sT;
   PHASE(5)
@@ -4481,19 +4506,22 @@ int launch_combine(const RankQ* d_q, int32_t nq, const ShardSum* d_shards, int32
 
 int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_order, int32_t nq, int64_t total_chunks,
                  int64_t seed_chunks, const NormState* d_norm, Cand* d_cand, int32_t* d_cand_cnt, int32_t kc,
-                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* st, void* ev_mid) {
+                 int32_t* d_redo, int32_t* d_nredo, unsigned long long* d_tq, void* d_qtab, void* st,
+                 void* ev_mid) {
   if (total_chunks <= 0) {  // (the statistics' event is recorded all the same: its elapsed time is read)
     if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));
     return 0;
   }
+  QTab* qt = reinterpret_cast<QTab*>(d_qtab);
+  hipLaunchKernelGGL(k_qtabs, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, d_norm, qt);
   // seed_chunks (0 < seed < total): the first chunks of `order` run as a launch of
   // their own, so every later chunk starts with its query's threshold set
   const int64_t s0 = (seed_chunks > 0 && seed_chunks < total_chunks) ? seed_chunks : total_chunks;
   hipLaunchKernelGGL(k_score, dim3((unsigned)s0), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_order, d_norm,
-                     d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+                     d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq, (const QTab*)qt);
   if (s0 < total_chunks)
     hipLaunchKernelGGL(k_score, dim3((unsigned)(total_chunks - s0)), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q,
-                       d_order + 2 * s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq);
+                       d_order + 2 * s0, d_norm, d_cand, d_cand_cnt, kc, d_redo, d_nredo, d_tq, (const QTab*)qt);
   if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // the k_score launches alone (statistics)
   const unsigned g = (unsigned)std::min<int64_t>(total_chunks, 512);
   hipLaunchKernelGGL(k_score_full, dim3(g), dim3(CHUNK_THREADS), 0, S(st), d_q, d_chunk_q, d_norm, d_cand,
@@ -4541,6 +4569,7 @@ int launch_score(const RankQ* d_q, const int32_t* d_chunk_q, const int32_t* d_or
 }
 
 int topq_capacity(int32_t keff) { return keff <= 2048 ? 4096 : 8192; }
+size_t score_qtab_bytes() { return sizeof(QTab); }
 
 int launch_topq(const int64_t* d_gbase, const int32_t* d_gn, const int32_t* d_gk, int64_t ngroups, const Cand* d_in,
                 const int32_t* d_in_cnt, int32_t in_stride, int32_t keff, Cand* d_out, int32_t* d_out_cnt, void* st) {
