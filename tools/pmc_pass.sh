@@ -22,5 +22,5 @@ with open(sys.argv[1], "w") as o:
     o.write("kernel,counter,total,dispatches,per_dispatch\n")
     for (k, c), v in sorted(tot.items()):
         n = len(disp[k]) or 1
-        o.write(f"{k},{c},{v:.0f},{n},{v / n:.1f}\n")
+        o.write(f"\"{k}\",{c},{v:.0f},{n},{v / n:.1f}\n")
 PY
