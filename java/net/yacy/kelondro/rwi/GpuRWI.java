@@ -12,7 +12,19 @@
 //   search/query/SearchEvent.java:612-631      -> GpuRWI.query(...) (whole local RWI path)
 //   search/query/SearchEvent.java:736-806,1297 -> GpuRWI.queryFiltered(...) (constraints, doubledom)
 //   kelondro/rwi/IndexCell.java:353-386        -> GpuRWI.loadHeaps(...) (BLOB heaps into HBM)
+//
+// Java level: 1.8, YaCy's own (build.properties javacSource/javacTarget, pom.xml
+// maven.compiler.source/target).  No API newer than Java 8 is used here or in the
+// other drop-ins (tests/test_java_sequence.py scans java/ for them).
 package net.yacy.kelondro.rwi;
+
+import java.lang.ref.PhantomReference;
+import java.lang.ref.Reference;
+import java.lang.ref.ReferenceQueue;
+import java.util.ArrayList;
+import java.util.Collections;
+import java.util.Set;
+import java.util.concurrent.ConcurrentHashMap;
 
 public final class GpuRWI implements AutoCloseable {
 
@@ -24,9 +36,61 @@ public final class GpuRWI implements AutoCloseable {
 
     private long ctx;  // yrwi_ctx*
 
+    /**
+     * The release of one search event (GpuReferenceOrder, GpuRWIStack), Java 8 style:
+     * a phantom reference to the object that owns the event.  The owner's close()
+     * calls release(); an owner dropped without close() is released by this
+     * context's reaper thread once the collector has enqueued the reference
+     * (java.lang.ref.Cleaner does the same from Java 9 on, which YaCy's 1.8 build
+     * does not have).  release() runs at most once.
+     */
+    public static final class EventHandle extends PhantomReference<Object> {
+        private final GpuRWI gpu;
+        private long event;
+
+        EventHandle(final Object owner, final GpuRWI gpu, final long event, final ReferenceQueue<Object> q) {
+            super(owner, q);
+            this.gpu = gpu;
+            this.event = event;
+        }
+
+        public void release() {
+            final long e;
+            synchronized (this) { e = this.event; this.event = 0; }
+            if (e == 0) return;
+            this.gpu.handles.remove(this);
+            this.gpu.eventClose(e);
+        }
+    }
+
+    private final ReferenceQueue<Object> unreachable = new ReferenceQueue<Object>();
+    // the handles must stay strongly reachable until released, or they are collected themselves
+    private final Set<EventHandle> handles = Collections.newSetFromMap(new ConcurrentHashMap<EventHandle, Boolean>());
+    private final Thread reaper;
+
     public GpuRWI(final int device) {
         this.ctx = open(device);
         if (this.ctx == 0) throw new IllegalStateException("yrwi_open failed");
+        final ReferenceQueue<Object> q = this.unreachable;
+        this.reaper = new Thread(new Runnable() {
+            @Override
+            public void run() {
+                while (true) {
+                    final Reference<?> r;
+                    try { r = q.remove(); } catch (final InterruptedException e) { return; }
+                    if (r instanceof EventHandle) ((EventHandle) r).release();
+                }
+            }
+        }, "GpuRWI event reaper");
+        this.reaper.setDaemon(true);
+        this.reaper.start();
+    }
+
+    /** Registers `event` for release when `owner` becomes unreachable (or at close()). */
+    public EventHandle track(final Object owner, final long event) {
+        final EventHandle h = new EventHandle(owner, this, event, this.unreachable);
+        this.handles.add(h);
+        return h;
     }
 
     /** IndexCell.add for a whole container: the RowSet chunkcache bytes (n * 40, sorted). */
@@ -213,7 +277,7 @@ public final class GpuRWI implements AutoCloseable {
     }
 
     public synchronized void eventClose(final long event) {
-        eventClose(this.ctx, event);
+        if (this.ctx != 0) eventClose(this.ctx, event);  // after close() the context freed it
     }
 
     /** WordReferenceFactory.compressIndex of each include word's list (search.java:264-281):
@@ -230,7 +294,11 @@ public final class GpuRWI implements AutoCloseable {
 
     @Override
     public synchronized void close() {
-        if (this.ctx != 0) { close(this.ctx); this.ctx = 0; }
+        if (this.ctx == 0) return;
+        this.reaper.interrupt();
+        for (final EventHandle h : new ArrayList<EventHandle>(this.handles)) h.release();  // events before the context
+        close(this.ctx);
+        this.ctx = 0;
     }
 
     /** RankingProfile public coefficients in declaration order (RankingProfile.java:81-88). */

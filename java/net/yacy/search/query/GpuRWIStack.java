@@ -19,10 +19,10 @@
 //
 // Wiring (INTEGRATION.md): SearchEvent.<init> opens one per event when a GpuRWI is
 // configured; addRWIs and pullOneRWI delegate to it; cleanup() closes it (a dropped
-// event returns its device memory through the Cleaner).
+// event returns its device memory through GpuRWI's reaper, GpuRWI.EventHandle: a
+// phantom reference, Java 8 like YaCy's build).
 package net.yacy.search.query;
 
-import java.lang.ref.Cleaner;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
@@ -42,23 +42,11 @@ import net.yacy.search.ranking.RankingProfile;
 
 public final class GpuRWIStack implements AutoCloseable {
 
-    private static final Cleaner CLEANER = Cleaner.create();
     private static final int ROW = 40;  // WordReferenceRow.urlEntryRow.objectsize
-
-    private static final class Release implements Runnable {
-        private final GpuRWI gpu;
-        private long event;
-        Release(final GpuRWI gpu, final long event) { this.gpu = gpu; this.event = event; }
-        @Override
-        public synchronized void run() {
-            if (this.event != 0) { this.gpu.eventClose(this.event); this.event = 0; }
-        }
-    }
 
     private final GpuRWI gpu;
     private final long event;
-    private final Release release;
-    private final Cleaner.Cleanable cleanable;
+    private final GpuRWI.EventHandle release;
     // every arrival's rows (the bytes given to the GPU, in arrival order) and whether it was local
     private final ArrayList<byte[]> rows = new ArrayList<byte[]>();
     private final ArrayList<Boolean> local = new ArrayList<Boolean>();
@@ -77,8 +65,7 @@ public final class GpuRWIStack implements AutoCloseable {
         this.event = gpu.eventOpenFiltered(GpuRWI.profile32(profile), targetLanguage, System.currentTimeMillis(), k,
                                            maxPostings, filter);
         if (this.event == 0) throw new IllegalStateException("yrwi_event_open failed");
-        this.release = new Release(gpu, this.event);
-        this.cleanable = CLEANER.register(this, this.release);
+        this.release = gpu.track(this, this.event);
     }
 
     /** The addRWIs constraints of a query (SearchEvent.java:736-806) as the event takes
@@ -159,7 +146,7 @@ public final class GpuRWIStack implements AutoCloseable {
     public synchronized void close() {
         if (!this.closed) {
             this.closed = true;
-            this.cleanable.clean();
+            this.release.release();
         }
     }
 }

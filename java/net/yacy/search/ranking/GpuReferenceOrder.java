@@ -23,8 +23,9 @@
 // reference races the workers' min/max updates against cardinal()).  The queue is
 // returned complete and ends with WordReferenceVars.poison, as addRWIs expects.
 //
-// Per container this class makes no copy of the rows (the RowSet's own byte[]
-// goes to JNI, GpuRows), keeps the scores in one long[] in container order, and
+// Per container this class hands the RowSet's own byte[] to JNI (GpuRows: no
+// exportCollection copy on the Java side; the JNI copies it once into native
+// memory, yrwi_jni.c copy_in), keeps the scores in one long[] in container order, and
 // each queued entry carries its position in it (Entry), so cardinal(e) is an
 // array read: no per-posting key String and no map.  authority() asks the GPU's
 // accumulated host counts (they exist when coeff_authority > 12, the only case in
@@ -35,12 +36,12 @@
 // Resources: the event is order-only (yrwi_event_open_order: the state and a host
 // table sized by expected hosts, no url set or stack), its device block reused
 // from closed orders (no device-wide allocation per SearchEvent).  close() returns
-// it; a SearchEvent that is dropped without cleanup() still returns it through the
-// Cleaner.  Every native call goes through GpuRWI, which serialises them on the
-// shared context (a context is not thread-safe).
+// it; a SearchEvent that is dropped without cleanup() still returns it through
+// GpuRWI's reaper (a phantom reference, GpuRWI.EventHandle: Java 8, YaCy's level).
+// Every native call goes through GpuRWI, which serialises them on the shared
+// context (a context is not thread-safe).
 package net.yacy.search.ranking;
 
-import java.lang.ref.Cleaner;
 import java.util.HashMap;
 import java.util.Iterator;
 import java.util.concurrent.BlockingQueue;
@@ -58,19 +59,6 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
     /** Distinct hosts one SearchEvent's order may see (sizes the event's host table,
      *  12 B per slot, two slots per host: 3 MB). */
     public static final long DEFAULT_MAX_HOSTS = 1L << 17;
-
-    private static final Cleaner CLEANER = Cleaner.create();
-
-    /** Returns the event to the context if the order was dropped unclosed. */
-    private static final class Release implements Runnable {
-        private final GpuRWI gpu;
-        private long event;
-        Release(final GpuRWI gpu, final long event) { this.gpu = gpu; this.event = event; }
-        @Override
-        public synchronized void run() {
-            if (this.event != 0) { this.gpu.eventClose(this.event); this.event = 0; }
-        }
-    }
 
     /** A queued posting with its position in the container's score array. */
     public static final class Entry extends WordReferenceVars {
@@ -90,8 +78,7 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
     private final GpuRWI gpu;
     private long event;  // yrwi_event*: this order's ReferenceOrder state on the GPU
-    private final Release release;
-    private final Cleaner.Cleanable cleanable;
+    private final GpuRWI.EventHandle release;  // returns the event, also if the order is dropped unclosed
     private final boolean authorityProfile;
     private final HashMap<String, Integer> authorityCache = new HashMap<String, Integer>();
 
@@ -107,8 +94,7 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
         // "now" is fixed for the event's lifetime (the clone's virtualAge clamp, J6)
         this.event = gpu.eventOpenOrder(GpuRWI.profile32(profile), language, System.currentTimeMillis(), maxHosts);
         if (this.event == 0) throw new IllegalStateException("yrwi_event_open_order failed");
-        this.release = new Release(gpu, this.event);
-        this.cleanable = CLEANER.register(this, this.release);
+        this.release = gpu.track(this, this.event);
     }
 
     @Override
@@ -152,7 +138,7 @@ public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
     public synchronized void close() {
         if (this.event != 0) {
             this.event = 0;
-            this.cleanable.clean();  // Release.run once: the event back to the context
+            this.release.release();  // once: the event back to the context
         }
     }
 }
