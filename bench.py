@@ -258,6 +258,14 @@ class Runner:
         self.args, self.rank, self.world, self.local, self.dist = args, rank, world, local, dist
         self.ix = None
 
+    def transports(self):
+        """Every rank's yrwi_shard_info (rank order), gathered over the job's process group."""
+        if self.dist is None:
+            return None
+        infos = [None] * self.world
+        self.dist.all_gather_object(infos, getattr(self, "transport", None))
+        return infos
+
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
@@ -274,6 +282,8 @@ class Runner:
                 uid.copy_(torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8))
             self.dist.broadcast(uid, 0)
             ix = RWIIndex(self.local, shard=(self.rank, self.world, bytes(uid.cpu().numpy())))
+            self.transport = ix.shard_info()
+            log(f"rank {self.rank}: shard transport {self.transport}")
         else:
             ix = RWIIndex(self.local)
         t0 = time.time()
@@ -671,6 +681,7 @@ def run(args, rank, world, local):
         prof.coeff_date, prof.coeff_domlength, prof.coeff_authority, prof.coeff_termfrequency = 15, 15, 13, 10
     elif args.profile == "date":
         prof = RankingProfile.date()
+    shard_transport = transport_summary(R.transports()) if world > 1 else None
     M = R.measure(bats, idx.hashes, prof, args.k, args.steps, args.warmup, args.inflight)
     value = M["total_post"] / M["dt"]
     ms_per_step = M["dt"] / args.steps * 1e3
@@ -757,6 +768,8 @@ def run(args, rank, world, local):
             "phase_ms": phase_ms(iso),
             "url_dictionary_build_s": round(t_dict, 3),
             "legs": legs or None,
+            # world > 1: how the shards' collectives travelled (yrwi_shard_info of every rank)
+            "shard_transport": shard_transport,
         }
         ident = source_identity()
         out["build"] = ident
@@ -835,9 +848,49 @@ def compact_line(out, detail):
     line["inflight"] = out.get("inflight")
     if out.get("legs"):
         line["legs"] = {name: _short_leg(leg) for name, leg in out["legs"].items()}
+    if out.get("shard_transport"):
+        t = out["shard_transport"]
+        line["transport"] = t["transport"]
+        line["rccl_ranks"] = t["rccl_ranks"]
+    line["roofline_kernels"] = _short_kernels(out.get("roofline_kernels"))
+    line["phase_ms"] = out.get("phase_ms")
     line["build"] = out.get("build")
+    # the full record, written on the box that ran this (the driver's copy stays there;
+    # everything the line's figures rest on is in the line itself)
     line["detail"] = detail
     return line
+
+
+def transport_summary(infos):
+    """One record for the line from every rank's yrwi_shard_info: the transport
+    (one name when all ranks agree, else the per-rank list), RCCL communicator rank
+    counts (min / max over the ranks), lanes with their own communicator, and the
+    ranks that shared a device with another."""
+    infos = [i for i in (infos or []) if i]
+    if not infos:
+        return None
+    names = sorted({i["transport"] for i in infos})
+    rr = [int(i["rccl_ranks"]) for i in infos]
+    oc = [int(i["lanes_own_comm"]) for i in infos]
+    return {"transport": names[0] if len(names) == 1 else [i["transport"] for i in infos],
+            "rccl_ranks": {"min": min(rr), "max": max(rr)},
+            "lanes_own_comm": {"min": min(oc), "max": max(oc)},
+            "ranks": len(infos),
+            "ranks_sharing_a_device": sum(1 for i in infos if int(i["device_peers"]) > 0),
+            "pci_bus_ids": [i["pci_bus_id"] for i in infos]}
+
+
+def _short_kernels(kern):
+    """The per-kernel roofline block, a few fields per kernel (it is what the headline's
+    roofline is chosen from)."""
+    if not kern:
+        return None
+    keep = ("mean_launch_us", "achieved", "frac", "traffic", "hbm_frac", "rocprof_mean_launch_us")
+    out = {}
+    for name, r in kern.items():
+        if isinstance(r, dict):
+            out[name] = {k: (round(r[k], 4) if isinstance(r[k], float) else r[k]) for k in keep if r.get(k) is not None}
+    return out
 
 
 LEG_DESC = {

@@ -180,14 +180,38 @@ int yrwi_open(int device, yrwi_ctx** out);
  * c satisfies c >> (6 - log2(world)) == r.  `nccl_id` is the 128-byte
  * ncclUniqueId from yrwi_get_unique_id() on rank 0, broadcast by the caller.
  * The shards merge their partial results over RCCL (Protocol.java:802 merges
- * peers' results); when RCCL cannot form the group -- ranks sharing one device --
- * and the ranks share a node, the device collectives run host-staged through
- * shared memory instead (an id starting with "YRWI-HOSTSTAGE " selects that
- * without trying RCCL). */
+ * peers' results).  The ranks of a node first post their devices' PCI bus ids
+ * in the node's host mailbox: ranks that share one device (RCCL refuses a
+ * duplicate GPU) run the device collectives host-staged through shared memory
+ * instead, as does an id starting with "YRWI-HOSTSTAGE".  Ranks on distinct
+ * devices use RCCL only: if ncclCommInitRank fails the call returns YRWI_E_RCCL
+ * and yrwi_last_error(NULL) gives RCCL's error string.  yrwi_shard_info says
+ * which transport a context runs on. */
 int yrwi_open_shard(int device, int rank, int world, const uint8_t nccl_id[128], yrwi_ctx** out);
 int yrwi_get_unique_id(uint8_t nccl_id[128]);
 void yrwi_close(yrwi_ctx* ctx);
+/* ctx's last error; NULL: why the calling thread's last yrwi_open / yrwi_open_shard failed */
 const char* yrwi_last_error(yrwi_ctx* ctx);
+
+enum {
+  YRWI_TRANSPORT_NONE = 0,        /* not sharded (yrwi_open) */
+  YRWI_TRANSPORT_RCCL = 1,        /* RCCL communicators (xGMI between the node's GPUs) */
+  YRWI_TRANSPORT_HOSTSTAGED = 2,  /* ranks share one device: host shared memory (/dev/shm) */
+  YRWI_TRANSPORT_LOOPBACK = 3     /* in-process test group */
+};
+typedef struct yrwi_transport_info {
+  int32_t transport;       /* YRWI_TRANSPORT_* */
+  int32_t rank, world;
+  int32_t rccl_ranks;      /* ncclCommCount of lane 0's communicator (0: no communicator) */
+  int32_t lanes;           /* lanes (batches in flight) */
+  int32_t lanes_own_comm;  /* lanes with a communicator of their own (ncclCommSplit) */
+  int32_t device_peers;    /* other ranks of the group on this rank's device (-1: not exchanged) */
+  int32_t mailbox;         /* 1: list sizes summed through the node's host mailbox */
+  char pci_bus_id[16];     /* this rank's device */
+} yrwi_transport_info;
+/* The transport of a (shard) context and its communicator's rank count:
+ * Distribution.java:153-158 partitions, Protocol.java:802 merges over it. */
+int yrwi_shard_info(yrwi_ctx* ctx, yrwi_transport_info* out);
 
 /* ---- index (IndexCell.add / RowSet import; the lists are what
  *      Index.get(termHash) returns, IndexCell.java:353-386) ---- */

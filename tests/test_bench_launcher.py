@@ -52,3 +52,28 @@ def test_compact_line_fits_the_driver_tail():
         assert k in line["cpu_baseline"], k
     assert set(line["legs"]) == {"C3", "C4", "C5_custom", "C5_date"}
     assert all("ms_per_step" in v and "frac" in v for v in line["legs"].values())
+
+
+def test_line_reports_the_shard_transport():
+    """world > 1: the line names how the shards' collectives travelled and the RCCL
+    communicators' rank counts (min / max over the ranks, from yrwi_shard_info), so
+    an 8-GPU record shows that RCCL saw 8 ranks -- or that it did not."""
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+        full = json.load(f)
+    info = lambda r, t, n, peers: {"transport": t, "rank": r, "world": 8, "rccl_ranks": n, "lanes": 8,
+                                   "lanes_own_comm": 8 if n else 0, "device_peers": peers, "mailbox": 1,
+                                   "pci_bus_id": f"0000:{r:02x}:00.0"}
+    full["shard_transport"] = bench.transport_summary([info(r, "rccl", 8, 0) for r in range(8)])
+    line = bench.compact_line(full, "profiles/bench_detail_x.json")
+    assert len(json.dumps(line)) <= 6000
+    assert line["transport"] == "rccl" and line["rccl_ranks"] == {"min": 8, "max": 8}
+    assert "k_compact" in line["roofline_kernels"] and "frac" in line["roofline_kernels"]["k_compact"]
+    mixed = bench.transport_summary([info(0, "rccl", 2, 0), info(1, "host-staged", 0, 1)])
+    assert mixed["transport"] == ["rccl", "host-staged"] and mixed["rccl_ranks"] == {"min": 0, "max": 2}
+    assert mixed["ranks_sharing_a_device"] == 1
+    assert bench.transport_summary([None, None]) is None
+    # one GPU: no transport keys
+    full.pop("shard_transport")
+    assert "transport" not in bench.compact_line(full, "x")

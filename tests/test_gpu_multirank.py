@@ -2,8 +2,10 @@
 that owns one URL-hash shard on device 0.  RCCL refuses several ranks on one
 device, so the ranks' device collectives (ShardSum all-gather, authority
 host-count exchange, top-k all-gather) run host-staged through the node's
-shared memory (yrwi_coll.cpp) -- after RCCL's init fails ("auto", the
-production fallback) or straight away (a YRWI-HOSTSTAGE group id).  The list-size
+shared memory (yrwi_coll.cpp): "auto" (an RCCL unique id) finds through the
+mailbox that the ranks' PCI bus ids are equal and never tries RCCL; "staged"
+names the transport in the group id (YRWI-HOSTSTAGE).  Each rank's
+yrwi_shard_info must say host-staged.  The list-size
 planning goes through the host mailbox as on the 8-GPU node.  This runs
 yrwi_open_shard, global-size planning, the ordered combine, the host-count
 exchange and the top-k merge of libyrwi across processes; the result must be
@@ -30,6 +32,7 @@ def _rank_main(rank, world, uid, out_q):
         full = synth.preset("small")
         part = synth.build_index(full.shard(rank, world))
         ix = RWIIndex(0, shard=(rank, world, uid))
+        info = ix.shard_info()
         for t in range(full.n_terms):
             if part.sizes[t]:
                 ix.add(part.hashes[t], part.list_rows(t))
@@ -50,7 +53,7 @@ def _rank_main(rank, world, uid, out_q):
             if [(h.urlhash, h.score, h.tiebreak) for h in g] != exp:
                 bad.append(qi)
         ix.close()
-        out_q.put((rank, "ok", bad))
+        out_q.put((rank, "ok", (bad, info)))
     except Exception as e:  # report, never hang the parent
         out_q.put((rank, "error", repr(e)))
 
@@ -83,7 +86,11 @@ def test_sharded_query_on_one_gpu(world, transport, monkeypatch):
     assert len(res) == world, ("ranks that never reported", res)
     for rank, status, info in res:
         assert status == "ok", (rank, info)
-        assert info == [], (rank, info)
+        bad, tinfo = info
+        assert bad == [], (rank, bad)
+        assert tinfo["transport"] == "host-staged", tinfo
+        assert tinfo["rank"] == rank and tinfo["world"] == world and tinfo["rccl_ranks"] == 0, tinfo
+        assert tinfo["device_peers"] == world - 1 and tinfo["mailbox"] == 1, tinfo
 
 
 def test_rccl_self_world1(monkeypatch):
@@ -103,6 +110,9 @@ def test_rccl_self_world1(monkeypatch):
     idx = synth.build_index(full)
     ix = RWIIndex(0, shard=(0, 1, unique_id()))
     try:
+        info = ix.shard_info()
+        assert info["transport"] == "rccl" and info["rccl_ranks"] == 1 and info["world"] == 1, info
+        assert info["lanes_own_comm"] == info["lanes"] >= 1, info
         for t in range(full.n_terms):
             if idx.sizes[t]:
                 ix.add(idx.hashes[t], idx.list_rows(t))

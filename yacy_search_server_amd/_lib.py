@@ -107,6 +107,14 @@ class CIndexInfo(ctypes.Structure):
                                               "index_bytes_used", "bitmap_lists")]
 
 
+class CTransportInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("transport", "rank", "world", "rccl_ranks", "lanes", "lanes_own_comm",
+                                              "device_peers", "mailbox")] + [("pci_bus_id", ctypes.c_char * 16)]
+
+
+TRANSPORTS = {0: "none", 1: "rccl", 2: "host-staged", 3: "loopback"}
+
+
 class CLoadStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("files", "records", "free_records", "bad_keys", "terms", "postings",
                                               "dropped_terms")]
@@ -124,6 +132,7 @@ SIGNATURES = {
     "yrwi_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "yrwi_close": (None, [_VP]),
     "yrwi_last_error": (ctypes.c_char_p, [_VP]),
+    "yrwi_shard_info": (ctypes.c_int, [_VP, ctypes.POINTER(CTransportInfo)]),
     "yrwi_put_list": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP, ctypes.c_int64, ctypes.c_int]),
     "yrwi_build_url_ids": (ctypes.c_int, [_VP]),
     "yrwi_list_size": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),

@@ -15,6 +15,7 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/statvfs.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -179,6 +180,8 @@ struct HxHead {
   std::atomic<int32_t> attached;
   int32_t pad0;
   std::atomic<int64_t> aborted[HX_ABORTS];
+  // device identity of every rank (hostx_device_peers): PCI domain / bus / device + 1, 0 = not yet posted
+  std::atomic<int64_t> devid[HX_MAXW];
   char pad[56];
 };
 
@@ -241,6 +244,28 @@ bool hostx_wait_attached(const HostX* x, double limit_s) {
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
   }
   return true;
+}
+
+// Posts this rank's device identity and waits (up to limit_s) for every rank's.
+// Returns how many other ranks of the group run on the same device (PCI domain,
+// bus and device equal), or -1 when some rank never posted.  Every rank reads the
+// same table, so all of them reach the same answer.
+int hostx_device_peers(const HostX* x, int64_t my_devid, double limit_s) {
+  if (!x) return -1;
+  HxHead* h = x->head();
+  h->devid[x->rank].store(my_devid, std::memory_order_release);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    int posted = 0, same = 0;
+    for (int r = 0; r < x->world; r++) {
+      const int64_t d = h->devid[r].load(std::memory_order_acquire);
+      posted += d != 0;
+      same += r != x->rank && d == my_devid;
+    }
+    if (posted == x->world) return same;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) return -1;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
 }
 
 void hostx_abort(HostX* x, int64_t seq) {
@@ -415,7 +440,8 @@ struct DxRank {
 struct DxHead {
   std::atomic<int32_t> attached;
   int32_t pad;
-  char pad2[56];
+  std::atomic<uint64_t> cap;  // payload bytes per rank, set by the first rank to attach
+  char pad2[48];
   DxRank r[DX_MAXW];
 };
 }  // namespace
@@ -447,6 +473,15 @@ DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx) {
   const size_t bytes = ((sizeof(DxHead) + 4095) & ~(size_t)4095) + (size_t)world * cap;
   const int fd = shm_open(nm, O_CREAT | O_RDWR, 0600);
   if (fd < 0) return nullptr;
+  // the segment is sparse: a tmpfs smaller than it would raise SIGBUS on a later
+  // write instead of an error here, so its free space must cover every region
+  struct statvfs fs;
+  if (fstatvfs(fd, &fs) != 0 || (uint64_t)fs.f_bavail * fs.f_frsize < (uint64_t)bytes) {
+    fprintf(stderr, "yrwi: host-staged collectives need %zu MB of /dev/shm (YRWI_DEVX_MB x ranks)\n",
+            bytes >> 20);
+    close(fd);
+    return nullptr;
+  }
   if (ftruncate(fd, (off_t)bytes) != 0) {
     close(fd);
     return nullptr;
@@ -454,6 +489,17 @@ DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx) {
   void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) return nullptr;
+  // every rank must place the regions alike: the first to attach records its
+  // payload size, the others must have the same (YRWI_DEVX_MB differs otherwise)
+  uint64_t want = 0;
+  DxHead* hd = static_cast<DxHead*>(p);
+  if (!hd->cap.compare_exchange_strong(want, (uint64_t)cap, std::memory_order_acq_rel) && want != (uint64_t)cap) {
+    fprintf(stderr, "yrwi: host-staged collectives: YRWI_DEVX_MB differs between ranks (%llu vs %zu bytes)\n",
+            (unsigned long long)want, cap);
+    hd->attached.fetch_add(1, std::memory_order_acq_rel);
+    munmap(p, bytes);
+    return nullptr;
+  }
   DevX* x = new DevX();
   x->base = p;
   x->bytes = bytes;

@@ -174,9 +174,18 @@ static int warm_lane(Lane* L) {
   return 0;
 }
 
+// why the calling thread's last yrwi_open / yrwi_open_shard failed (no context to
+// hold it): yrwi_last_error(NULL)
+static thread_local std::string t_open_error;
+static void set_open_error(const std::string& m) { t_open_error = m; }
+
 static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   *out = nullptr;
-  if (hipSetDevice(device) != hipSuccess) return YRWI_E_HIP;
+  t_open_error.clear();
+  if (hipSetDevice(device) != hipSuccess) {
+    set_open_error("hipSetDevice(" + std::to_string(device) + ") failed");
+    return YRWI_E_HIP;
+  }
   yrwi_ctx* ctx = new yrwi_ctx();
   ctx->device = device;
   ctx->rank = rank;
@@ -202,6 +211,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
     } else if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
       close_lanes(ctx);
       delete ctx;
+      set_open_error("hipStreamCreateWithFlags failed");
       return YRWI_E_HIP;
     }
     L->hostreg = &ctx->hostreg;
@@ -215,7 +225,10 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
   int wrc = 0;
   for (Lane* L : ctx->lanes) {
     L->wait();
-    if (L->rc && !wrc) wrc = L->rc;
+    if (L->rc && !wrc) {
+      wrc = L->rc;
+      set_open_error("lane set-up: " + L->err);
+    }
   }
   if (wrc) {
     close_lanes(ctx);
@@ -254,38 +267,69 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
       ctx->lanes[l]->loop = loop_join(id, world, rank);
       ok = ctx->lanes[l]->loop != nullptr;
     }
+    ctx->transport = YRWI_TRANSPORT_LOOPBACK;
     if (!ok) {
       yrwi_close(ctx);
       *out = nullptr;
       return YRWI_E_ARG;
     }
   } else if (ctx->sharded) {
+    ctx->transport = YRWI_TRANSPORT_RCCL;
+    // The transport is decided from facts every rank sees alike, before any
+    // collective: ranks on ONE device (RCCL refuses a duplicate GPU) or an id
+    // tagged YRWI-HOSTSTAGE exchange through host shared memory; ranks on
+    // distinct devices use RCCL, and an RCCL failure there is an error, never a
+    // silent switch to the host path.
+    const bool staged = world > 1 && std::memcmp(nccl_id, STAGE_TAG, sizeof(STAGE_TAG)) == 0;
+    int peers = -1;
+    if (world > 1 && ctx->hostx) {
+      char bus[32] = {0};
+      int64_t devid = 0;
+      if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device) == hipSuccess) {
+        uint64_t h = 1469598103934665603ull;  // FNV-1a of "dddd:bb:dd.f"
+        for (const char* c = bus; *c; c++) h = (h ^ (uint8_t)*c) * 1099511628211ull;
+        devid = (int64_t)(h >> 1) | 1;
+      } else {
+        devid = -(int64_t)rank - 1;  // unknown: distinct from every other rank's
+      }
+      peers = hostx_device_peers(ctx->hostx, devid, 120.0);
+    }
+    ctx->device_peers = peers;
+    if (staged || peers > 0) {
+      const char* why = staged ? "host-staged group id" : "ranks share a device";
+      ctx->devx = (ctx->hostx && (staged ? hostx_wait_attached(ctx->hostx, 120.0) : true))
+                      ? devx_open(nccl_id, world, rank, ctx->hostx) : nullptr;
+      if (!ctx->devx) {
+        set_open_error(std::string("host-staged collectives (") + why + ") unavailable: " +
+                       (ctx->hostx ? "shared-memory segment" : "no host mailbox"));
+        yrwi_close(ctx);
+        *out = nullptr;
+        return YRWI_E_RCCL;
+      }
+      for (Lane* L : ctx->lanes) L->devx = ctx->devx;
+      ctx->transport = YRWI_TRANSPORT_HOSTSTAGED;
+      if (!staged) fprintf(stderr, "yrwi: rank %d of %d: %s -- collectives host-staged through /dev/shm\n", rank,
+                           world, why);
+      return 0;
+    }
     ncclUniqueId u;
     std::memcpy(&u, nccl_id, 128);
     ncclComm_t c0 = nullptr;
-    // YRWI-HOSTSTAGE group ids (tests) skip RCCL for the host-staged transport
-    const bool staged = world > 1 && std::memcmp(nccl_id, STAGE_TAG, sizeof(STAGE_TAG)) == 0;
-    bool ok = !staged && ncclCommInitRank(&c0, world, u, rank) == ncclSuccess;
-    // (a staged group has had no rendezvous yet: wait for the peers to map the
-    // mailbox; after a failed RCCL init they have, the init met them)
-    if (!ok && world > 1 && ctx->hostx && hostx_wait_attached(ctx->hostx, staged ? 120.0 : 10.0)) {
-      // RCCL could not form the group (several ranks on one device: it refuses a
-      // duplicate GPU; the init fails on every rank alike) but every rank mapped
-      // the node's mailbox: the rank phase's device collectives go through host
-      // shared memory (yrwi_coll.cpp, host-staged collectives)
-      if (c0) ncclCommDestroy(c0);
-      ctx->devx = devx_open(nccl_id, world, rank, ctx->hostx);
-      if (ctx->devx) {
-        for (Lane* L : ctx->lanes) L->devx = ctx->devx;
-        return 0;
-      }
+    const ncclResult_t irc = ncclCommInitRank(&c0, world, u, rank);
+    if (irc != ncclSuccess) {
+      set_open_error(std::string("ncclCommInitRank (rank ") + std::to_string(rank) + " of " + std::to_string(world) +
+                     "): " + ncclGetErrorString(irc));
+      yrwi_close(ctx);
+      *out = nullptr;
+      return YRWI_E_RCCL;
     }
-    if (ok) ctx->lanes[0]->comm = c0;
+    bool ok = true;
+    ctx->lanes[0]->comm = c0;
     // the mailbox only works if every rank mapped the same segment (one node, one
     // /dev/shm): every rank opened it before the init above, so after it each
     // rank sees world attachments or not; all ranks agree (min over the ranks)
     // and drop the mailbox together if any one saw fewer (device all-gather then)
-    if (ok && world > 1) {
+    if (world > 1) {
       int32_t* d_flag = nullptr;
       int32_t flag = hostx_attached(ctx->hostx) == world ? 1 : 0;
       ok = hipMalloc(&d_flag, 4) == hipSuccess;
@@ -313,11 +357,32 @@ extern "C" int yrwi_open_shard(int device, int rank, int world, const uint8_t nc
         ctx->lanes[l]->comm = c0;
       }
     if (!ok) {
+      set_open_error("RCCL group set-up after ncclCommInitRank failed (mailbox agreement all-reduce)");
       yrwi_close(ctx);
       *out = nullptr;
       return YRWI_E_RCCL;
     }
   }
+  return 0;
+}
+
+extern "C" int yrwi_shard_info(yrwi_ctx* ctx, yrwi_transport_info* out) {
+  if (!ctx || !out) return YRWI_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  out->transport = ctx->transport;
+  out->rank = ctx->rank;
+  out->world = ctx->world;
+  out->lanes = (int32_t)ctx->lanes.size();
+  out->device_peers = ctx->device_peers;
+  out->mailbox = ctx->hostx ? 1 : 0;
+  ncclComm_t c0 = ctx->lanes.empty() ? nullptr : ctx->lanes[0]->comm;
+  if (c0) {
+    int n = 0;
+    if (ncclCommCount(c0, &n) == ncclSuccess) out->rccl_ranks = n;
+    for (size_t l = 0; l < ctx->lanes.size(); l++)
+      out->lanes_own_comm += ctx->lanes[l]->comm && (l == 0 || ctx->lanes[l]->comm != c0);
+  }
+  hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id), ctx->device);
   return 0;
 }
 
@@ -343,7 +408,10 @@ extern "C" void yrwi_close(yrwi_ctx* ctx) {
   delete ctx;
 }
 
-extern "C" const char* yrwi_last_error(yrwi_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+extern "C" const char* yrwi_last_error(yrwi_ctx* ctx) {
+  if (ctx) return ctx->err.c_str();
+  return t_open_error.empty() ? "null context" : t_open_error.c_str();
+}
 
 // ======================================================================= index
 extern "C" int yrwi_put_list(yrwi_ctx* ctx, const uint8_t term[12], const uint8_t* rows40, int64_t n, int sorted) {

@@ -401,6 +401,8 @@ struct CtxBase {
   int64_t coll_seq = 0;
   HostX* hostx = nullptr;
   DevX* devx = nullptr;
+  int transport = 0;  // YRWI_TRANSPORT_* (yrwi_shard_info): how the shards' collectives travel
+  int device_peers = -1;  // other ranks of the group on this device (-1: unknown / not exchanged)
   std::atomic<size_t> scratch_hint{0};  // Lane::scratch_hint
   std::atomic<int64_t> scratch_total{0};  // Lane::scratch_total
   std::mutex st_mu;
@@ -633,6 +635,8 @@ void hostx_close(HostX* x, bool unlink_name);
 void hostx_abort(HostX* x, int64_t seq);  // batch part `seq` failed: every rank's exchanges of that part fail at once
 int hostx_attached(const HostX* x);  // ranks that mapped the segment so far (0: no mailbox)
 bool hostx_wait_attached(const HostX* x, double limit_s);  // every rank mapped it (false: timeout)
+// other ranks of the group on this rank's device (-1: some rank never posted its identity)
+int hostx_device_peers(const HostX* x, int64_t my_devid, double limit_s);
 int hostx_allsum(Lane* L, std::vector<int64_t>& v);  // 0 done, 1 not handled, < 0 error
 // host-staged device collectives (ranks that share a device: RCCL refuses them)
 DevX* devx_open(const uint8_t id[128], int world, int rank, HostX* hx);

@@ -243,7 +243,8 @@ class Query:
 
 def _check(ctx, rc: int):
     if rc != 0:
-        msg = _lib.lib().yrwi_last_error(ctx) if ctx else b""
+        # ctx None: an open failed, and yrwi_last_error(NULL) holds this thread's reason
+        msg = _lib.lib().yrwi_last_error(ctx)
         raise YrwiError(rc, (msg or b"").decode(errors="replace"))
 
 
@@ -270,6 +271,17 @@ class RWIIndex:
             _check(None, L.yrwi_open_shard(device, rank, world, uid, ctypes.byref(h)))
         self._h = h
         self.device = device
+
+    def shard_info(self) -> dict:
+        """How this context's collectives travel (yrwi_shard_info): transport ("rccl",
+        "host-staged", "loopback", "none"), RCCL communicator rank count, lanes, lanes
+        with their own communicator, other ranks on this device, mailbox, PCI bus id."""
+        info = _lib.CTransportInfo()
+        _check(self._h, _lib.lib().yrwi_shard_info(self._h, ctypes.byref(info)))
+        d = {f: getattr(info, f) for f, _ in _lib.CTransportInfo._fields_}
+        d["transport"] = _lib.TRANSPORTS.get(d["transport"], str(d["transport"]))
+        d["pci_bus_id"] = d["pci_bus_id"].decode(errors="replace")
+        return d
 
     def close(self):
         if self._h:
