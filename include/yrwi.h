@@ -360,8 +360,10 @@ int yrwi_event_open(yrwi_ctx* ctx, const yrwi_profile* prof, const char* languag
                     const yrwi_filter* filter, int64_t max_postings, yrwi_event** out);
 /* An event for yrwi_event_order / yrwi_event_authority only (GpuReferenceOrder: the
  * ReferenceOrder of a SearchEvent whose addRWIs stays in Java): no url set and no
- * stack, the host table sized for max_hosts distinct hosts (authority profiles;
- * more: YRWI_E_CAPACITY), device memory reused from closed order-only events.
+ * stack, the host table first sized for max_hosts distinct hosts (authority
+ * profiles) and grown by yrwi_event_order before a container could fill it
+ * (ReferenceOrder.doms is unbounded, ReferenceOrder.java:176-198), device memory
+ * reused from closed order-only events.
  * The event entry points serialise on the context (callers on several threads). */
 int yrwi_event_open_order(yrwi_ctx* ctx, const yrwi_profile* prof, const char* language, int64_t now_ms,
                           int64_t max_hosts, yrwi_event** out);

@@ -56,8 +56,9 @@ import net.yacy.kelondro.rwi.ReferenceContainer;
 
 public class GpuReferenceOrder extends ReferenceOrder implements AutoCloseable {
 
-    /** Distinct hosts one SearchEvent's order may see (sizes the event's host table,
-     *  12 B per slot, two slots per host: 3 MB). */
+    /** Distinct hosts one SearchEvent's order is expected to see (the event's first
+     *  host table, 12 B per slot, two slots per host: 3 MB); more hosts grow the
+     *  table (yrwi_event_order), as ReferenceOrder.doms is unbounded. */
     public static final long DEFAULT_MAX_HOSTS = 1L << 17;
 
     /** A queued posting with its position in the container's score array. */

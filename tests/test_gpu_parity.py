@@ -315,15 +315,12 @@ def test_j5_side_arrays(long_lists, j5, monkeypatch):
         ix.close()
 
 
-@pytest.mark.parametrize("bmenum,chain", [("2", "1"), ("2", "0"), ("0", "0")],
-                         ids=["enum_chained", "enum_stepwise", "probe_stepwise"])
-def test_bitmap_enumeration(long_lists, bmenum, chain, monkeypatch):
-    """JA_BMENUM (YRWI_BMENUM=2: every unchained, undistanced join of two dense
-    bitmap lists enumerates the AND of both bitmaps; 0: never): the pairs and their
-    order equal the probe's -- term_search rows, top-k with tie-breaks, with and
-    without excluded terms, stepwise (YRWI_NO_CHAIN=1: every fold step a join job)
-    and chained (only the unchained steps enumerate)."""
-    monkeypatch.setenv("YRWI_BMENUM", bmenum)
+@pytest.mark.parametrize("chain", ["1", "0"], ids=["chained", "stepwise"])
+def test_dense_bitmap_joins(long_lists, chain, monkeypatch):
+    """Joins of dense bitmap lists (the bitmap probe; round 5 also enumerated the
+    AND of both bitmaps here, removed in round 6): term_search rows, top-k with
+    tie-breaks, with and without excluded terms and a distance filter, stepwise
+    (YRWI_NO_CHAIN=1: every fold step a join job) and chained."""
     monkeypatch.setenv("YRWI_NO_CHAIN", "1" if chain == "0" else "0")
     cfg, df, big, idx, ix = long_lists
     d = idx.as_dict()
@@ -400,17 +397,15 @@ def test_merge_tile_boundaries(nab, monkeypatch):
         ix.close()
 
 
-@pytest.mark.parametrize("mode", ["probe", "enum", "count_first"])
+@pytest.mark.parametrize("mode", ["probe", "count_first"])
 def test_bitmap_unit_boundaries(mode, monkeypatch):
     """Url-id bitmaps in 16-B units of 96 ids (yrwi_bitmap.h): lists whose ids sit
     on both sides of every unit's word boundaries (ids 96v + 0/31/32/63/64/95),
     the first and the last url id, a url space that is not a multiple of 96.  A
     (every id) and C (every third) and B (the boundary ids) have bitmaps, D (ids
     96v + 95 and 96v + 96, below the bitmap minimum) has none: 2-4 term joins,
-    an exclusion, through the bitmap probe, the bitmap-AND enumeration
-    (YRWI_BMENUM=2) and the count-first popcounts (YRWI_CHAIN_CF=2) -- rows and
-    top-k equal to the oracle's."""
-    monkeypatch.setenv("YRWI_BMENUM", "2" if mode == "enum" else "0")
+    an exclusion, through the bitmap probe and the count-first popcounts
+    (YRWI_CHAIN_CF=2) -- rows and top-k equal to the oracle's."""
     monkeypatch.setenv("YRWI_CHAIN_CF", "2" if mode == "count_first" else "1")
     m = 96 * 1000 + 37
     keys = np.arange(m)

@@ -204,7 +204,9 @@ def test_reference_order_events_reuse_memory_and_bound_hosts(corpus):
     """Order-only events (GpuReferenceOrder, one per SearchEvent) reuse closed
     events' device blocks: a second order after a first was closed starts from a
     clean state (the same scores as the first); an authority profile whose
-    containers bring more hosts than max_hosts fails with YRWI_E_CAPACITY."""
+    containers bring more hosts than max_hosts grows the event's host table
+    (ReferenceOrder.doms is unbounded, ReferenceOrder.java:176-198): its scores
+    and authority answers equal those of an event sized for all hosts."""
     cfg, idx, ix = corpus
     c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
     rows = np.asarray(idx.rows, dtype=np.uint8)[:3000]
@@ -216,9 +218,16 @@ def test_reference_order_events_reuse_memory_and_bound_hosts(corpus):
     assert firsts[0] == firsts[1] == firsts[2]
     nhosts = len({bytes(r[6:12]) for r in rows})
     assert nhosts > 64
-    with ix.reference_order(c5, "en", NOW, max_hosts=8) as ev:
-        with pytest.raises(Exception):
-            ev.order(rows, True)
+    hosts = sorted({bytes(r[6:12]) for r in rows})
+    with ix.reference_order(c5, "en", NOW, max_hosts=4096) as big:
+        want = [big.order(rows[a:b], a == 0).tolist() for a, b in ((0, 40), (40, 1000), (1000, 3000))]
+        want_auth = big.authority(hosts)
+    # max_hosts 8: 16 slots; the table grows at the second and third container
+    for _ in range(2):  # the second round starts from a pooled (grown) block
+        with ix.reference_order(c5, "en", NOW, max_hosts=8) as ev:
+            got = [ev.order(rows[a:b], a == 0).tolist() for a, b in ((0, 40), (40, 1000), (1000, 3000))]
+            assert got == want
+            assert ev.authority(hosts) == want_auth
 
 
 @pytest.mark.parametrize("kw", [dict(constraint=b"\0\0\x10\x01"), dict(language="de"), None])

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Marginal cost of a kernel in throughput mode, measured by duplication.
+
+Builds variants of libyrwi (never the product: a patched copy of csrc/ in /tmp,
+output gpurun_var/libyrwi_dup_<name>.so) in which ONE idempotent launch is issued
+twice in a row -- the second launch rewrites what the first wrote, so results stay
+right, and the bench's step-time delta against the product build is what that
+kernel costs among the other lanes' kernels.  Run the variants on the GPU box with
+tools/ab.sh (YRWI_LIB).  Only kernels that are idempotent on the C2 workload
+(default profile, 2-term, no authority) are listed.
+  python3 tools/whatif_dup.py [names...]"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "yacy_search_server_amd", "csrc")
+
+K = "yrwi_kernels.hip"
+VARIANTS = {
+    "compact": [(K, "  hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),\n"
+                    "                     d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,\n"
+                    "                     perm, (const int32_t*)bo.tile_job);\n", 2)],
+    "probe": [(K, "    hipLaunchKernelGGL(kp, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,\n"
+                  "                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm, d_tile_lvl,\n"
+                  "                       (const ProbeDesc*)d_prange);\n", 2)],
+    "reduce": [(K, "    hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS),\n"
+                   "                       hp_any ? HPART_MAXS * sizeof(int32_t) : 0, S(st), d_q, d_chunk_q, d_chunks, d_shard);\n", 2)],
+    "shardfin": [(K, "  hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);\n", 2)],
+    "combine": [(K, "  hipLaunchKernelGGL(k_combine, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, S(st), d_q, nq, d_shards, world, d_norm);\n", 2)],
+    "emit": [(K, "  hipLaunchKernelGGL(k_emit, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, nq, d_final, d_final_cnt, kmax,\n"
+                 "                     d_hits, d_nout, mode);\n", 2)],
+    "copyin": [(K, "  hipLaunchKernelGGL(k_copy_in, dim3(blocks), dim3(256), 0, (hipStream_t)stream, c);\n", 2)],
+    "qtabs": [(K, "  hipLaunchKernelGGL(k_qtabs, dim3((unsigned)nq), dim3(256), 0, S(st), d_q, d_norm, qt);\n", 2)],
+}
+TOPQ = ("    hipLaunchKernelGGL(k_topq<4096>, dim3((unsigned)ngroups), dim3(TOPQ_THREADS), 2 * 4096 * sizeof(uint64_t), S(st),\n"
+        "                       d_gbase, d_gn, d_gk, d_in, d_in_cnt, in_stride, keff, d_out, d_out_cnt);\n")
+VARIANTS["topq"] = [(K, TOPQ, 2)]
+
+
+def build(name):
+    tmp = f"/tmp/whatif_{name}"
+    shutil.rmtree(tmp, ignore_errors=True)
+    src = os.path.join(tmp, "pkg", "csrc")  # the tree's shape: csrc/../../include/yrwi.h
+    shutil.copytree(CSRC, src)
+    os.makedirs(os.path.join(tmp, "include"), exist_ok=True)
+    shutil.copy(os.path.join(ROOT, "include", "yrwi.h"), os.path.join(tmp, "include"))
+    for f, text, times in VARIANTS[name]:
+        p = os.path.join(src, f)
+        s = open(p).read()
+        assert s.count(text) == 1, (name, f, s.count(text))
+        s = s.replace(text, "{\n" + text * times + "}\n")  # (a braced block: some sit under an if)
+        open(p, "w").write(s)
+    out = os.path.join(ROOT, "gpurun_var", f"libyrwi_dup_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.check_call(["make", "-s", "-j8", "-C", src, f"OUT={out}",
+                           f"OBJ={tmp}/obj", out])
+    print("built", out)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(VARIANTS):
+        build(n)

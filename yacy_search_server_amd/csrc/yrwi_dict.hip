@@ -868,8 +868,7 @@ void index_changed(CtxBase* ctx, const KeyT& term, int64_t old_n, bool added) {
 
 int ensure_url_ids(CtxBase* ctx) {
   if (!ctx->uid_dirty) return 0;
-  const bool force_repack = getenv("YRWI_REPACK_ALWAYS") && atoi(getenv("YRWI_REPACK_ALWAYS"));
-  if (int rc = repack_index(ctx, force_repack)) return rc;
+  if (int rc = repack_index(ctx, false)) return rc;
   hipStream_t st = ctx->stream;
   std::vector<ListRec*> lists, changed, others;
   int64_t n = 0, nchanged = 0;

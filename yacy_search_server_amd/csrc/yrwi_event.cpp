@@ -29,6 +29,10 @@ struct yrwi_event {
   // one entry returned and none queued since
   std::map<uint64_t, std::vector<DDEntry>> dd;
   uint64_t dd_next = 0;
+  // order-only authority events: an upper bound of the distinct hosts in the host
+  // table (postings given since the last exact count); the table grows before a
+  // container could fill it (grow_host_table)
+  int64_t hosts_bound = 0;
 };
 
 namespace {
@@ -40,6 +44,23 @@ int ceil_log2(int64_t x) {
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// the kernels' host-table hash (yrwi_kernels.hip mix64), for rehashing on the host
+uint64_t mix64_host(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// order-only event block: state, host keys, host counts
+struct OrderLayout {
+  size_t o_hk, o_hc, need;
+  explicit OrderLayout(int64_t hslots) {
+    o_hk = align256(sizeof(EvState));
+    o_hc = o_hk + align256((size_t)hslots * 8);
+    need = o_hc + align256((size_t)hslots * 4);
+  }
+};
 
 }  // namespace
 
@@ -74,8 +95,8 @@ extern "C" int yrwi_event_open_order(yrwi_ctx* ctx, const yrwi_profile* prof, co
   // authority profile, the host table (2 slots per expected host)
   const int64_t hslots = q.want_authority ? (int64_t)1 << ceil_log2(std::max<int64_t>(2 * max_hosts, 64)) : 1;
   q.hmask = (uint64_t)(hslots - 1);
-  const size_t o_st = 0, o_hk = align256(sizeof(EvState)), o_hc = o_hk + align256((size_t)hslots * 8);
-  const size_t need = o_hc + align256((size_t)hslots * 4);
+  const OrderLayout lay(hslots);
+  const size_t o_st = 0, o_hk = lay.o_hk, o_hc = lay.o_hc, need = lay.need;
   // device memory from the context's pool of closed order-only events (a hipMalloc
   // would synchronise the whole device once per SearchEvent)
   void* mem = nullptr;
@@ -273,6 +294,68 @@ extern "C" int yrwi_event_add(yrwi_ctx* ctx, yrwi_arrival* arr, int32_t narr) {
   return first;
 }
 
+// ReferenceOrder.doms is an unbounded map (ReferenceOrder.java:176-198): an
+// order-only event's host table (sized by the caller's expected hosts) grows
+// before a container of `incoming` postings could fill it past 3/4 -- the live
+// hosts are counted exactly when the running bound says it might, and rehashed
+// into a table twice their (count + incoming) on the host (rare: the table at
+// least doubles each time).  The state moves to the new block as it is.
+static int grow_host_table(yrwi_ctx* ctx, yrwi_event* ev, int64_t incoming) {
+  RankQ& q = ev->h.q;
+  if (!q.want_authority || !ev->pooled) return 0;
+  const int64_t slots = (int64_t)q.hmask + 1;
+  if (ev->hosts_bound + incoming <= slots / 4 * 3) return 0;
+  Lane* L = ctx->lanes[0];
+  std::vector<uint64_t> keys((size_t)slots);
+  std::vector<uint32_t> cnt((size_t)slots);
+  HIPCHK(ctx, hipMemcpyAsync(keys.data(), q.hkeys, (size_t)slots * 8, hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, hipMemcpyAsync(cnt.data(), q.hcnt, (size_t)slots * 4, hipMemcpyDeviceToHost, L->stream));
+  HIPCHK(ctx, lane_sync(L));
+  int64_t used = 0;
+  for (uint64_t k : keys) used += k != 0;
+  ev->hosts_bound = used;
+  if (used + incoming <= slots / 4 * 3) return 0;
+  const int64_t ns = (int64_t)1 << ceil_log2(std::max<int64_t>(2 * (used + incoming), 2 * slots));
+  const OrderLayout lay(ns);
+  std::vector<uint64_t> nk((size_t)ns, 0);
+  std::vector<uint32_t> nc((size_t)ns, 0);
+  for (int64_t i = 0; i < slots; i++) {
+    if (!keys[(size_t)i]) continue;
+    uint64_t t = mix64_host(keys[(size_t)i]) & (uint64_t)(ns - 1);
+    while (nk[(size_t)t]) t = (t + 1) & (uint64_t)(ns - 1);
+    nk[(size_t)t] = keys[(size_t)i];
+    nc[(size_t)t] = cnt[(size_t)i];
+  }
+  void* mem = nullptr;
+  if (hipMalloc(&mem, lay.need) != hipSuccess) return ctx->fail(YRWI_E_NOMEM, "event host table growth");
+  uint8_t* base = static_cast<uint8_t*>(mem);
+  auto* nst = reinterpret_cast<EvState*>(base);
+  auto* nhk = reinterpret_cast<uint64_t*>(base + lay.o_hk);
+  auto* nhc = reinterpret_cast<uint32_t*>(base + lay.o_hc);
+  if (hipMemcpyAsync(nst, ev->h.st, sizeof(EvState), hipMemcpyDeviceToDevice, L->stream) != hipSuccess ||
+      hipMemcpyAsync(nhk, nk.data(), (size_t)ns * 8, hipMemcpyHostToDevice, L->stream) != hipSuccess ||
+      hipMemcpyAsync(nhc, nc.data(), (size_t)ns * 4, hipMemcpyHostToDevice, L->stream) != hipSuccess ||
+      lane_sync(L) != hipSuccess) {
+    hipFree(mem);
+    return ctx->fail(YRWI_E_HIP, "event host table growth copy");
+  }
+  {
+    std::lock_guard<std::mutex> lk(ctx->ev_pool_mu);
+    if (ctx->ev_pool.size() < 64) {
+      ctx->ev_pool.emplace_back(ev->bytes, ev->mem);
+      ev->mem = nullptr;
+    }
+  }
+  if (ev->mem) hipFree(ev->mem);
+  ev->mem = mem;
+  ev->bytes = lay.need;
+  ev->h.st = nst;
+  q.hkeys = nhk;
+  q.hcnt = nhc;
+  q.hmask = (uint64_t)(ns - 1);
+  return 0;
+}
+
 extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* rows40, int64_t n, int32_t local,
                                 int64_t* scores) {
   if (!ctx || !ev || n < 0 || n >= ((int64_t)1 << 31) || (n > 0 && (!rows40 || !scores))) return YRWI_E_ARG;
@@ -282,6 +365,7 @@ extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* ro
   drain(ctx);
   Lane* L = ctx->lanes[0];
   if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
+  if (int rc = grow_host_table(ctx, ev, n)) return rc;
   uint8_t* d_rows = arena_alloc<uint8_t>(L, n * YRWI_ROW_BYTES);
   int64_t* d_sc = arena_alloc<int64_t>(L, n);
   EvDev* d_ev = arena_alloc<EvDev>(L, 1);
@@ -309,6 +393,7 @@ extern "C" int yrwi_event_order(yrwi_ctx* ctx, yrwi_event* ev, const uint8_t* ro
   HIPCHK(ctx, hipMemcpyAsync(&st, d_status, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(ctx, hipMemcpyAsync(scores, d_sc, (size_t)n * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(ctx, lane_sync(L));
+  ev->hosts_bound += n;
   if (st == YRWI_E_HASH) return ctx->fail(st, "container: url hash is not well-formed Base64");
   if (st == YRWI_E_NULL_LANGUAGE) return ctx->fail(st, "container: row with empty language cell (reference NPE)");
   if (st == YRWI_E_CAPACITY) return ctx->fail(st, "event tables full: max_postings too small");

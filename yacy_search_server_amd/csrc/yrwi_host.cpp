@@ -204,11 +204,7 @@ static int open_common(int device, int rank, int world, yrwi_ctx** out) {
     L->rank = rank;
     L->world = world;
     ctx->lanes.push_back(L);
-    const char* sh = getenv("YRWI_SHARED_STREAM");
-    if (l > 0 && sh && atoi(sh)) {
-      L->stream = ctx->lanes[0]->stream;  // lanes overlap host work only; the device runs one queue
-      L->own_stream = false;
-    } else if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
       close_lanes(ctx);
       delete ctx;
       set_open_error("hipStreamCreateWithFlags failed");
@@ -887,7 +883,6 @@ static int64_t loaded_bytes(const JoinQ& J) {
   const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
   if (J.algo == JA_MERGE) return 4 * (ns + nl);
   if (J.algo == JA_BMAND) return (J.bm3 ? 48 : 32) * J.bm_words;  // every bitmap's 16-B units
-  if (J.algo == JA_BMENUM) return 32 * J.bm_words;  // both bitmaps' 16-B units
   const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
   return bm ? 20 * ns : 4 * ns + std::min(4 * nl, 128 * ns);
 }
@@ -921,19 +916,9 @@ static void span_close(Lane* L, Timing* tm, hipEvent_t b) {
 
 // Give every job its algorithm and tile count, put merge jobs first and lay out
 // the global tile index space: merge tiles [0, merge_tiles), probe tiles after.
-// YRWI_CHAIN_FUSED=1: a chained job's probe tiles keep their matches in LDS and
-// test them in the same workgroup (k_probe<.., CHAIN>, BM_TILE tiles) instead of
-// writing them for k_chain.  Measured slower on C3 (3.62 against 3.22-3.30 ms per
-// step: the probe workgroups lose occupancy and the long tiles), kept as the
-// experiment's switch.
-static bool chain_fused() {
-  static const bool on = getenv("YRWI_CHAIN_FUSED") && atoi(getenv("YRWI_CHAIN_FUSED"));
-  return on;
-}
-
 static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& jobs, std::vector<int>& owner,
                         std::vector<int64_t>& tile_base, int* nmerge, int64_t* merge_tiles, int64_t* tiles,
-                        bool* long_tiles, int bm_enum) {
+                        bool* long_tiles) {
   *long_tiles = false;
   std::vector<size_t> order(jobs.size());
   for (size_t i = 0; i < jobs.size(); i++) {
@@ -956,24 +941,6 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     if (J.B.bm && J.B.n * 64 < nurls) J.B.bm = nullptr;
     const int64_t ns = std::min(J.A.n, J.B.n), nl = std::max(J.A.n, J.B.n);
     J.small_is_A = J.A.n <= J.B.n;
-    // both lists with dense bitmaps, the smaller one above 1/12 of the url ids:
-    // their AND streams 2 x 16 B per 96 url ids, less than its 4-B ids
-    // (JA_BMENUM, YRWI_BMENUM=1; a job whose pairs go to the chain tests, an
-    // exclusion or a distance filter keeps the probe).  Off by default: on C2 it
-    // took k_probe 116 -> 124 us and k_compact 228 -> 276 us (a tile's matches
-    // are one compaction workgroup's: far more than a probe tile's)
-    if (bm_enum && J.A.bm && J.B.bm && !J.chained && J.mode != JM_MARK && J.maxd >= 65535 && nurls > 0) {
-      const int64_t words = bm_units(nurls);
-      if (bm_enum == 2 || 8 * words < ns) {
-        J.algo = JA_BMENUM;
-        J.ptile = BMENUM_WORDS;
-        J.bm_words = words;
-        J.ntiles = ceil_div(words, BMENUM_WORDS);
-        J.chain_bm = nullptr;
-        order[i] = i;
-        continue;
-      }
-    }
     // skewed sizes: probe the large list; a large list with a url-id bitmap is
     // probed at any ratio (the small side's ids stream, the bitmap stays in L2)
     const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
@@ -981,15 +948,12 @@ static void layout_jobs(int64_t probe_ratio, int64_t nurls, std::vector<JoinQ>& 
     // long bitmap tiles only where no record is gathered per match (a deferred
     // step writes sources, an exclusion marks): a final step's compaction keeps
     // its band order per 1024-id tile (C2 k_compact 220 -> 236 us with 2048)
-    // (a fused chained job's tiles keep their matches in LDS for the chain tests:
-    // BM_TILE, whose registers leave room for them)
     // A chained probe job whose first later include list has a bitmap (J.chain_bm,
     // set by the caller) tests it inside k_probe -- a bitmap probe on BM_TILE
     // tiles (the long tiles' registers leave no room for it), a range probe on its
     // usual tiles; merge jobs leave it to k_chain.
     if (J.algo == JA_MERGE) J.chain_bm = nullptr;
-    const bool light = chain_fused() ? (J.out_tup != nullptr || J.mode == JM_MARK) && !J.chained
-                                     : J.out_tup != nullptr || J.mode == JM_MARK || (J.chained && !J.chain_bm);
+    const bool light = J.out_tup != nullptr || J.mode == JM_MARK || (J.chained && !J.chain_bm);
     J.ptile = bm ? (light && ns >= BM_LARGE_MIN ? KPT_LARGE * PROBE_TILE : BM_TILE) : PROBE_TILE;
     if (J.ptile == KPT_LARGE * PROBE_TILE) *long_tiles = true;
     J.ntiles = J.algo == JA_MERGE ? ceil_div(J.A.n + J.B.n, JOIN_TILE) : ceil_div(ns, J.ptile);
@@ -1071,7 +1035,6 @@ struct PendingCompact {
   int64_t* d_off = nullptr;
   BandOrder bo;
   std::vector<std::array<int64_t, CHAIN_LVL>> level;  // per job (layout order): k_chain's level counts
-  std::vector<char> probed;  // per job: a probe job, whose chain tests ran inside k_probe (else k_chain)
 };
 
 // One fold step's join jobs: layout, launch, joined sizes back to the plans.
@@ -1083,18 +1046,14 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   std::vector<int64_t> tile_base;
   int nmerge;
   int64_t merge_tiles, tiles;
-  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
-  const int64_t h0 = hprof ? now_ns() : 0;
   bool long_tiles;
-  if (chq && !chain_fused())  // candidates for the probe's own test of the first later include (layout_jobs)
+  if (chq)  // candidates for the probe's own test of the first later include (layout_jobs)
     for (size_t j = 0; j < jobs.size(); j++) {
       const ChainQ& Cq = (*chq)[(size_t)owner[j]];
       jobs[j].chain_bm = jobs[j].chained && Cq.pos0 == 0 && Cq.ninc >= 1 ? Cq.l[0].bm : nullptr;
     }
-  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles,
-              ctx->bm_enum);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
-  const int64_t h1 = hprof ? now_ns() : 0;
   if (st)
     for (const JoinQ& J : jobs) {  // §8(d) K of the step as the reference dispatches it
       const int64_t K = step_bytes(J.mode, J.A.n, J.B.n), loaded = loaded_bytes(J);
@@ -1125,14 +1084,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   }
   JoinQ* d_jobs = arena_alloc<JoinQ>(ctx, nj);
   int64_t* d_tb = arena_alloc<int64_t>(ctx, nj);
-  unsigned long long* d_cursor = nullptr;  // JA_BMENUM jobs' pair-slot cursors
-  for (int j = 0; j < nj && !d_cursor; j++)
-    if (jobs[(size_t)j].algo == JA_BMENUM) {
-      if (!(d_cursor = arena_alloc<unsigned long long>(ctx, nj))) return ctx->fail(YRWI_E_NOMEM, "arena");
-      HIPCHK(ctx, hipMemsetAsync(d_cursor, 0, (size_t)nj * 8, ctx->stream));
-    }
-  if (d_cursor)
-    for (int j = 0; j < nj; j++) jobs[(size_t)j].cursor = d_cursor + j;
   TileDesc* d_split = arena_alloc<TileDesc>(ctx, merge_tiles);
   ProbeDesc* d_pdesc = arena_alloc<ProbeDesc>(ctx, tiles - merge_tiles);
   uint2* d_pairs = arena_alloc<uint2>(ctx, npairs);
@@ -1151,13 +1102,12 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   ChainQ* d_cq = nullptr;
   std::vector<int2> cgrp;  // chain groups: runs of up to CHAIN_GMAX merge tiles of one chained job (k_chain)
   int2* d_cgrp = nullptr;
-  ProbeDesc* d_prange = nullptr;  // later-list ranges of every probe tile (k_probe<.., CHAIN>)
   if (chain) {
     // a group holds about 640 expected matches (independent lists: nA nB / nurls
     // per job), so a workgroup tests close to one round of 768
-    for (int j = 0; j < nj; j++) {  // (fused: a probe job's tiles test their matches inside k_probe)
+    for (int j = 0; j < nj; j++) {
       const JoinQ& J = jobs[(size_t)j];
-      if (!J.chained || J.ntiles <= 0 || (chain_fused() && J.algo != JA_MERGE)) continue;
+      if (!J.chained || J.ntiles <= 0) continue;
       double per_tile = (double)J.A.n * (double)J.B.n / (double)std::max<int64_t>(1, ctx->nurls) /
                         (double)J.ntiles;
       const ChainQ& Cq = (*chq)[(size_t)owner[(size_t)j]];
@@ -1169,8 +1119,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
     d_lvl = arena_alloc<int32_t>(ctx, tiles * CHAIN_LVL);
     d_crange = arena_alloc<ProbeDesc>(ctx, (int64_t)cgrp.size() * CHAIN_MAXL);
-    if (chain_fused() && !(d_prange = arena_alloc<ProbeDesc>(ctx, (tiles - merge_tiles) * CHAIN_MAXL)))
-      return ctx->fail(YRWI_E_NOMEM, "arena");
     d_cgrp = arena_alloc<int2>(ctx, (int64_t)cgrp.size());
     d_cq = arena_alloc<ChainQ>(ctx, nj);
     if (!d_lvl || !d_crange || !d_cgrp || !d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
@@ -1196,18 +1144,16 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       cq.push_back(C);
     }
   }
-  const int64_t h2 = hprof ? now_ns() : 0;
   if (chain ? upload(ctx, d_jobs, jobs, d_tb, tile_base, d_cq, cq, d_cgrp, cgrp)
             : upload(ctx, d_jobs, jobs, d_tb, tile_base))
     return YRWI_E_HIP;
-  const int64_t h3 = hprof ? now_ns() : 0;
   hipEvent_t e0 = tm ? ctx->event() : nullptr, em = tm ? ctx->event() : nullptr, e1 = tm ? ctx->event() : nullptr;
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
                        false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange, d_cgrp,
-                       (int64_t)cgrp.size(), d_prange))
+                       (int64_t)cgrp.size()))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
@@ -1227,15 +1173,9 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     st->n_probe_dispatches += tiles > merge_tiles;
     st->n_chain_launches += chain && !cgrp.empty() ? 1 : 0;  // k_chain launches (timed in t_chain_ns)
   }
-  const int64_t h4 = hprof ? now_ns() : 0;
   std::vector<int64_t> mh((size_t)nj, 0);
-  const int64_t h5 = hprof ? now_ns() : 0;
   HIPCHK(ctx, lane_sync(ctx));
   std::memcpy(mh.data(), land, (size_t)nj * sizeof(int64_t));
-  if (hprof)
-    fprintf(stderr, "[yrwi join] jobs %d layout %.3f alloc %.3f upload %.3f launch %.3f d2h %.3f sync %.3f ms\n", nj,
-            (h1 - h0) / 1e6, (h2 - h1) / 1e6, (h3 - h2) / 1e6, (h4 - h3) / 1e6, (h5 - h4) / 1e6,
-            (now_ns() - h5) / 1e6);
   if (st)  // k_compact per joined row: pair + id read, the records it gathers (32 B, + 16 B of the joined
            // side for enumeration steps, + the deferred rows' sources and records), record + id written;
            // deferred output: A's sources read, sources + id written; chained: the rows of every list of
@@ -1286,8 +1226,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     pend->d_off = d_off;
     pend->bo = bo;
     pend->level.assign((size_t)nj, {0, 0, 0, 0, 0});
-    pend->probed.assign((size_t)nj, 0);
-    for (int j = 0; j < nj; j++) pend->probed[(size_t)j] = chain_fused() && jobs[(size_t)j].algo != JA_MERGE;
     const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
     for (int j = 0; j < nj; j++)
       if (jobs[(size_t)j].chain)
@@ -1322,8 +1260,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
   int nmerge;
   int64_t merge_tiles, tiles;
   bool long_tiles;
-  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles,
-              ctx->bm_enum);
+  layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
   if (st)
     for (const JoinQ& J : jobs) st->bytes_alg_capped += std::min<int64_t>(12 * J.B.n, loaded_bytes(J));
@@ -1360,7 +1297,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
     P.cont = P.seq[0]->dl();  // (a single list under a url selection: restricted below)
     acc_g[qi] = P.seq_ng[0];
   }
-  static const bool defer = !(getenv("YRWI_NO_DEFER") && atoi(getenv("YRWI_NO_DEFER")));
+  constexpr bool defer = true;  // deferred multi-term folds (round 2): a step before the last writes sources only
   // Chained folds (ChainQ): every query with lists after its first join step --
   // later includes (t <= 4) and / or exclusions -- and no maxDistance filter.  The
   // decision rests on global facts only (fold length, exclusion terms in effect),
@@ -1598,9 +1535,6 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         const int t = (int)P.seq.size();
         if (t >= 3) P.step_mode[1] = dispatch_mode(v[2 * k], P.seq_ng[2]);
         if (t >= 4) P.step_mode[2] = dispatch_mode(v[2 * k + 1], P.seq_ng[3]);
-        // the chain tests of a probe job ran inside k_probe: their bytes are k_probe's
-        const int jk = job_of[(size_t)cqs[k]];
-        const bool in_probe = jk >= 0 && pend.active && pend.probed[(size_t)jk];
         if (st) {  // the later steps' K (local sizes), charged min(K, the bytes the chain tests load for them)
           for (int l = 2; l < t; l++) {
             const int64_t acc = loc[2 * k + (size_t)(l - 2)], n = P.seq[(size_t)l]->n;
@@ -1608,13 +1542,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
             const int64_t K = step_bytes(m, acc, n);
             const int64_t loaded = P.seq[(size_t)l]->bm ? 20 * acc : 4 * acc + std::min(4 * n, 128 * acc);
             st->bytes_alg += K;
-            if (in_probe) {
-              st->bytes_probe += K;
-              st->bytes_probe_capped += std::min(K, loaded);
-              st->bytes_probe_loaded += loaded;
-            } else {
-              st->bytes_chain += std::min(K, loaded);
-            }
+            st->bytes_chain += std::min(K, loaded);
             st->bytes_alg_capped += std::min(K, loaded);
             if (m == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
           }
@@ -1646,17 +1574,11 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
           const int j = job_of[(size_t)cqs[k]];
           const ChainQ& C = chq[(size_t)cqs[k]];
           const int64_t pre = (j >= 0 && pend.active) ? pend.level[(size_t)j][(size_t)C.ninc] : 0;
-          const bool in_probe = j >= 0 && pend.active && pend.probed[(size_t)j];
           for (int l = C.ninc; l < C.nl; l++) {
             const int64_t b = std::min<int64_t>(12 * C.l[l].n, C.l[l].bm ? 20 * pre
                                                                          : 4 * pre + std::min(4 * C.l[l].n, 128 * pre));
             st->bytes_alg_capped += b;
-            if (in_probe) {
-              st->bytes_probe_capped += b;
-              st->bytes_probe_loaded += b;
-            } else {
-              st->bytes_chain += b;
-            }
+            st->bytes_chain += b;
           }
         }
       }
@@ -1754,10 +1676,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   const int nq = (int)plans.size();
   const int W = exchange ? ctx->world : 1;
   const bool shx = exchange && ctx->sharded;  // the url-hash-shard protocol
-  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;
-  int64_t hq[8] = {0};
-  auto mark = [&](int i) { if (hprof) hq[i] = now_ns(); };
-  mark(0);
   std::vector<RankQ> rq((size_t)nq);
   std::vector<int64_t> chunk_base((size_t)nq), slot_base((size_t)nq + 1);
   int64_t chunks = 0, nslots = 0;
@@ -1940,9 +1858,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++) chunk_q[(size_t)(chunk_base[(size_t)qi] + c)] = qi;
   int32_t* d_cq = arena_alloc<int32_t>(ctx, chunks);
   if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
-  mark(1);
   if (upload(ctx, d_q, rq, d_cb, chunk_base, d_cq, chunk_q)) return YRWI_E_HIP;
-  mark(2);
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
   hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
@@ -1986,7 +1902,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     return 0;
   }
 
-  mark(3);
   // ---- score + per-chunk top-k
   int32_t keff = 1;
   for (auto& R : rq) keff = std::max(keff, R.k);
@@ -2037,7 +1952,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     return ctx->fail(YRWI_E_HIP, "score launch");
   span_close(ctx, tm, sp);
   if (tm) tm->kscore.push_back({s0, smid});
-  mark(4);
   // ---- top-k passes over groups of candidate lists until one list per query;
   // a query with a single list (one chunk) is final as it stands
   std::vector<const Cand*> fptr((size_t)nq);
@@ -2121,7 +2035,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));
   }
   if (!d_fptr || !d_fcnt) return ctx->fail(YRWI_E_NOMEM, "arena");
-  mark(5);
   if (upload(ctx, d_fptr, fptr, d_fcnt, fcnt)) return YRWI_E_HIP;
   std::vector<int32_t> hD;  // max-distance fold state per query (overflow check)
   const uint8_t* hD_land = nullptr;
@@ -2168,13 +2081,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     if (!hD_land) return YRWI_E_HIP;
   }
   if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }
-  mark(6);
   HIPCHK(ctx, lane_sync(ctx));
-  mark(7);
-  if (hprof)
-    fprintf(stderr, "[yrwi rank] setup %.3f upload %.3f norm %.3f score %.3f topq %.3f emit %.3f sync %.3f ms\n",
-            (hq[1] - hq[0]) / 1e6, (hq[2] - hq[1]) / 1e6, (hq[3] - hq[2]) / 1e6, (hq[4] - hq[3]) / 1e6,
-            (hq[5] - hq[4]) / 1e6, (hq[6] - hq[5]) / 1e6, (hq[7] - hq[6]) / 1e6);
   if (hD_land) {
     hD.resize((size_t)nq);
     std::memcpy(hD.data(), hD_land, (size_t)nq * 4);
@@ -2271,7 +2178,6 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
                            yrwi_hit* out, int32_t* nout, yrwi_stats* st) {
   const int64_t t0 = now_ns();
   const int64_t r0 = t_realloc;
-  static const bool hprof = getenv("YRWI_HOST_PROF") != nullptr;  // per-batch host breakdown to stderr
   int64_t tp = 0, tj = 0, tr = 0, w0 = L->wait_ns, wj = 0;
   std::vector<Plan> all((size_t)nq);
   for (int i = 0; i < nq; i++) {
@@ -2370,12 +2276,6 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
   if (st) {
     st->t_total_ns = now_ns() - t0;
     st->n_realloc = (int32_t)(t_realloc - r0);
-  }
-  if (hprof) {
-    const int64_t wall = now_ns() - t0, wait = L->wait_ns - w0;
-    fprintf(stderr, "[yrwi host] nq %d passes %d wall %.3f plan %.3f join %.3f (wait %.3f) rank %.3f (wait %.3f) ms, "
-            "scratch %.1f MB\n", nq, npass, wall / 1e6, tp / 1e6, tj / 1e6, wj / 1e6, tr / 1e6, (wait - wj) / 1e6,
-            L->arena.capacity() / 1e6);
   }
   return 0;
 }

@@ -89,15 +89,12 @@ struct ListRec {
 // overlapping while it runs); reported per batch in yrwi_stats.n_realloc
 inline std::atomic<int64_t> g_realloc{0};
 inline thread_local int64_t t_realloc = 0;  // the calling thread's events (per-batch statistics)
-// one device-wide allocation event; YRWI_REALLOC_LOG=1 prints each (kind, bytes, time)
+// one device-wide allocation event (what and how much: the statistics count them)
 inline void note_realloc(const char* what, size_t bytes) {
+  (void)what;
+  (void)bytes;
   g_realloc++;
   t_realloc++;
-  static const bool log = getenv("YRWI_REALLOC_LOG") != nullptr;
-  if (log)
-    fprintf(stderr, "[yrwi realloc] %s %.1f MB at %.3f ms\n", what, bytes / 1e6,
-            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
-                    .count() / 1e3);
 }
 
 // bump allocator over device chunks
@@ -274,7 +271,6 @@ struct Lane {
   Stage out_stage;           // pinned landing buffer for results
   Stage down_stage;          // pinned landing buffer for small per-step readbacks (joined sizes)
   int64_t probe_ratio = 8;   // YRWI_PROBE_RATIO, read once per call
-  int bm_enum = 0;           // JA_BMENUM: 0 never (default), 1 where it reads fewer bytes, 2 whenever both bitmaps are dense (YRWI_BMENUM)
   bool band_order = true;    // band-major compaction schedule (BandOrder); YRWI_BAND_ORDER
   int64_t nurls = 0;         // url ids of the context's dictionary (set with dkhi)
   const uint64_t* dkhi = nullptr;  // the context's url dictionary keys (set when it is built)
@@ -476,22 +472,14 @@ inline T* arena_alloc(Lane* ctx, int64_t count) {
 // Wait for this lane's work so far: an event, not a stream sync, so lanes that
 // share one stream do not wait for work the other lane enqueues later.
 inline hipError_t lane_sync(Lane* L) {
-  // YRWI_BLOCKING_SYNC=1: the lane thread sleeps in the wait instead of spinning
-  static const bool blocking = getenv("YRWI_BLOCKING_SYNC") && atoi(getenv("YRWI_BLOCKING_SYNC"));
-  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming |
-                                                              (blocking ? hipEventBlockingSync : 0)) != hipSuccess)
+  // (a blocking-sync event or a polled wait, measured in round 2: no better,
+  // profiles/r02f_sync_poll_sweep.txt)
+  if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
     return hipErrorOutOfMemory;
   hipError_t e = hipEventRecord(L->sync_ev, L->stream);
   if (e != hipSuccess) return e;
   const auto t0 = std::chrono::steady_clock::now();
-  // YRWI_SYNC_POLL_US > 0: poll the event, sleeping that long between polls (the
-  // lanes' waits would otherwise spin one host core each against the job's quota)
-  static const int poll_us = getenv("YRWI_SYNC_POLL_US") ? atoi(getenv("YRWI_SYNC_POLL_US")) : 0;
-  if (poll_us > 0 && !blocking) {
-    while ((e = hipEventQuery(L->sync_ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
-  } else {
-    e = hipEventSynchronize(L->sync_ev);
-  }
+  e = hipEventSynchronize(L->sync_ev);
   L->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   return e;
 }
@@ -605,8 +593,6 @@ inline int begin_pass(Lane* ctx) {
   ctx->evnext = 0;
   const char* e = getenv("YRWI_PROBE_RATIO");  // tests force either join algorithm with it
   ctx->probe_ratio = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)8;
-  const char* be = getenv("YRWI_BMENUM");  // tests force or forbid the bitmap-AND enumeration
-  ctx->bm_enum = be ? atoi(be) : 0;
   const char* b = getenv("YRWI_BAND_ORDER");  // 0: job-order tile schedule (A/B measurements; same results)
   ctx->band_order = !(b && b[0] == '0');
   return 0;

@@ -93,20 +93,12 @@ enum JoinMode : int32_t {
 // JA_BMAND: a counted-only join of two lists that both have url-id bitmaps:
 // popcount(bits A & bits B) over ranges of bitmap units (tiles of BMAND_WORDS
 // 16-B units), in place of probing one list's ids into the other (k_probe)
-// JA_BMENUM: the matched pairs of two lists that both have dense url-id bitmaps,
-// from the AND of the bitmaps (tiles of BMENUM_WORDS units): each set bit is a
-// match, its rows are each unit's rank + the bits below it -- no id of either
-// list is read.  Taken where streaming both bitmaps (32 B per 96 url ids) costs
-// less than the smaller list's ids alone (4 B per id: the probe's bitmap words
-// mostly hit L2, since a batch's jobs over one large list run back to back --
-// at 20 B per probed id C2 took it for lists above 1/40 density and k_probe went
-// 119 -> 165 us, k_compact 225 -> 337 us with four-word-per-thread tiles, whose
-// match runs left few compaction workgroups).  A
-// tile claims its run of the job's pair slots with one atomic add on the job's
-// cursor (the compaction reads every tile at tile_src, in tile order).
-enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2, JA_BMENUM = 3 };
+// (An AND-of-bitmaps enumeration of two dense lists' matches, JA_BMENUM, was
+// built and measured in round 5 -- C2 k_probe 116 -> 164 us, k_compact 228 -> 276:
+// its tiles' long match runs left few compaction workgroups -- and removed in
+// round 6)
+enum JoinAlgo : int32_t { JA_MERGE = 0, JA_PROBE = 1, JA_BMAND = 2 };
 constexpr int BMAND_WORDS = 4096;  // 16-B bitmap units per JA_BMAND tile
-constexpr int BMENUM_WORDS = 256;  // 16-B bitmap units per JA_BMENUM tile: one per thread (24576 url ids)
 // url-id bitmap units (DList::bm, yrwi_bitmap.h): 96 ids per 16 B
 constexpr int64_t BM_UNIT_IDS = 96;
 inline int64_t bm_units(int64_t nurls) { return (nurls + BM_UNIT_IDS - 1) / BM_UNIT_IDS; }
@@ -194,9 +186,8 @@ struct JoinQ {
   int32_t* chain_tup0;
   int32_t chain_fill;
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
-  int64_t bm_words;    // JA_BMAND / JA_BMENUM: 16-B bitmap units of the url-id space (bm_units)
+  int64_t bm_words;    // JA_BMAND: 16-B bitmap units of the url-id space (bm_units)
   const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
-  unsigned long long* cursor;  // JA_BMENUM: pair slots claimed so far (zeroed per step)
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
@@ -398,7 +389,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_begin,
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
                      bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
-                     const int2* d_cgrp = nullptr, int64_t ngroups = 0, ProbeDesc* d_prange = nullptr);
+                     const int2* d_cgrp = nullptr, int64_t ngroups = 0);
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);

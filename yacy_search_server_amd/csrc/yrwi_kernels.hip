@@ -666,25 +666,15 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(const JoinQ* __restrict__
 // thread, all tiles in parallel); k_probe binary-searches each key inside its
 // tile's range.  Output and mark semantics are k_join's.
 
-// XCD-aware block order (cdna_hip_programming.md T1): blocks are dealt round-robin
-// over the 8 XCDs, so logical block k of an XCD's share is placed on one XCD and
-// consecutive tiles (the same job's lists, a popular list's bitmap) share its L2.
-// A bijection of [0, n) for any n.
-#ifndef YRWI_XCD_SWZ
-#define YRWI_XCD_SWZ 0  // measured: k_compact 274 -> 465 us, k_probe 201 -> 214 us with the remap (profiles/r02h_xcd_swizzle.txt)
-#endif
+// XCD slices (cdna_hip_programming.md T1): blocks are dealt round-robin over the
+// 8 XCDs, so logical block k of XCD x's share maps to slice x of an order; a
+// bijection of [0, n) for any n.  (Applied to job order -- consecutive tiles on
+// one XCD -- it was measured slower: k_compact 274 -> 465 us, k_probe 201 -> 214 us,
+// profiles/r02h_xcd_swizzle.txt; the band orders below use it.)
 __device__ __forceinline__ int64_t xcd_slice(int64_t bid, int64_t n) {
   const int64_t q = n >> 3, r = n & 7;  // XCD group x holds q + (x < r) blocks
   const int64_t x = bid & 7, k = bid >> 3;
   return x * q + (x < r ? x : r) + k;
-}
-__device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t n) {
-#if YRWI_XCD_SWZ
-  return xcd_slice(bid, n);
-#else
-  (void)n;
-  return bid;
-#endif
 }
 
 // ======================================================= join: band order
@@ -849,7 +839,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   if (t >= ntiles) return;
   const int j = find_job(tile_base, njobs, tile0 + t);
   const JoinQ& J = jobs[j];
-  if (J.algo == JA_BMAND || J.algo == JA_BMENUM) {  // a range of bitmap units: no ids to read, no range
+  if (J.algo == JA_BMAND) {  // a range of bitmap units: no ids to read, no range
     const uint32_t id0 =
         (uint32_t)min((tile0 + t - tile_base[j]) * (int64_t)J.ptile * BM_UNIT_IDS, (int64_t)0xFFFFFFFF);
     if (tile_key) tile_key[tile0 + t] = id0;
@@ -913,8 +903,7 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
                                                 int64_t tile_base0, uint2* __restrict__ pairs,
                                                 uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
                                                 int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64,
-                                                uint16_t* sLoc = nullptr, uint32_t* sPos = nullptr,
-                                                int64_t* src_out = nullptr, int32_t* tile_lvl = nullptr) {
+                                                int32_t* tile_lvl = nullptr) {
   // url-id bitmap of the large list: one 16-B load per key (yrwi_bitmap.h) gives
   // membership and, for a hit, its list position (rank + bits below).  BM_TILE
   // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
@@ -1013,18 +1002,13 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
       for (int x = 0; x < J.chain_fill; x++) lv[2 + x] = lv[1];
     }
   }
-  if (src_out) *src_out = src;
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
     if (!((hm >> k) & 1u)) continue;
     const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
     const int64_t ia = J.small_is_A ? ik : (int64_t)jls[k], ib = J.small_is_A ? (int64_t)jls[k] : ik;
     const int32_t lo = base[k] + (int32_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-    if (J.count_only) {  // counted only
-    } else if (sLoc) {  // a chained job's tile: its matches stay in LDS for the chain tests
-      sLoc[lo] = (uint16_t)(k * PROBE_TILE + (int)threadIdx.x);
-      sPos[lo] = (uint32_t)jls[k];
-    } else {
+    if (!J.count_only) {
       pairs[src + lo] = make_uint2((uint32_t)ia, (uint32_t)ib);
       pair_uid[src + lo] = keys[k];
       if (pre) stg(J.chain_tup0 + src + lo, tp[k]);
@@ -1034,92 +1018,27 @@ __device__ __forceinline__ int32_t probe_bitmap(const JoinQ& J, const DList& Sm,
 }
 
 
-// One JA_BMENUM tile: BMENUM_WORDS 16-B bitmap units, WPT consecutive units per
-// thread (both lists' units stream coalesced).  A match is a bit set in both;
-// its rows are each unit's rank + the bits below it.  Matches leave in url-id
-// order (thread-consecutive units, block scan of the counts) into the run the
-// tile claims from the job's cursor.
-__device__ __forceinline__ void probe_bmenum(const JoinQ& J, int64_t tj, int64_t b, uint2* __restrict__ pairs,
-                                             uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
-                                             int32_t* __restrict__ tile_cnt, int32_t* sScan) {
-  constexpr int WPT = BMENUM_WORDS / PROBE_TILE;
-  static_assert(WPT * PROBE_TILE == BMENUM_WORDS, "whole units per thread");
-  __shared__ int64_t sBase;
-  const int64_t w0 = tj * BMENUM_WORDS + (int64_t)threadIdx.x * WPT;
-  uint4 xa[WPT], xb[WPT];
-  int32_t cnt = 0;
-#pragma unroll
-  for (int k = 0; k < WPT; k++) {
-    const int64_t w = w0 + k;
-    xa[k] = xb[k] = make_uint4(0, 0, 0, 0);
-    if (w < J.bm_words) {
-      xa[k] = ldg(reinterpret_cast<const uint4*>(J.A.bm) + w);
-      xb[k] = ldg(reinterpret_cast<const uint4*>(J.B.bm) + w);
-      cnt += __popc(xa[k].x & xb[k].x) + __popc(xa[k].y & xb[k].y) + __popc(xa[k].z & xb[k].z);
-    }
-  }
-  int32_t tot;
-  int32_t off = block_excl_sum256(cnt, sScan, &tot);
-  if (threadIdx.x == 0) {
-    const int64_t base = tot ? (int64_t)atomicAdd(J.cursor, (unsigned long long)tot) : 0;
-    sBase = base;
-    tile_src[b] = J.pair_base + base;
-    tile_cnt[b] = tot;
-  }
-  __syncthreads();
-  const int64_t src = J.pair_base + sBase + off;
-  int32_t o = 0;
-#pragma unroll
-  for (int k = 0; k < WPT; k++) {
-    const uint32_t id0 = (uint32_t)((w0 + k) * BM_UNIT_IDS);
-    uint32_t pa = xa[k].w, pb = xb[k].w;  // the units' ranks
-#pragma unroll
-    for (int h = 0; h < 3; h++) {
-      const uint32_t a32 = h == 0 ? xa[k].x : h == 1 ? xa[k].y : xa[k].z;
-      const uint32_t b32 = h == 0 ? xb[k].x : h == 1 ? xb[k].y : xb[k].z;
-      for (uint32_t r = a32 & b32; r; r &= r - 1) {
-        const uint32_t below = (r & (~r + 1)) - 1;  // the bits below the lowest set bit
-        pairs[src + o] = make_uint2(pa + (uint32_t)__popc(a32 & below), pb + (uint32_t)__popc(b32 & below));
-        pair_uid[src + o] = id0 + 32u * h + (uint32_t)__popc(below);
-        o++;
-      }
-      pa += (uint32_t)__popc(a32);
-      pb += (uint32_t)__popc(b32);
-    }
-  }
-}
 
-__device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t src, int32_t cnt,
-                               const uint16_t* sLoc, const uint32_t* sPos, const uint32_t* __restrict__ small_uid,
-                               int64_t s0, bool small_is_A, uint2* __restrict__ pairs,
-                               uint32_t* __restrict__ pair_uid, int32_t* __restrict__ tile_cnt,
-                               int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ cr, uint32_t* sL,
-                               uint64_t* sScan64);
 
 // MARK: an exclusion step (its own instantiation, so kernel traces tell the
-// include steps' dispatches from the exclusion steps').  CHAIN: the first step of
-// chained folds: a chained job's tile keeps its matches in LDS and tests them
-// against the fold's later lists in the same workgroup (chain_lds_tile, with the
-// ranges k_chain_part<true> found for the tile): only survivors reach HBM.
-template <bool LONG, bool MARK, bool CHAIN>
+// include steps' dispatches from the exclusion steps').  (Round 4 also built a
+// CHAIN instantiation that kept a chained tile's matches in LDS and ran the chain
+// tests in the same workgroup: C3 3.62 against 3.22-3.30 ms/step, DESIGN.md §3;
+// removed in round 6.)
+template <bool LONG, bool MARK>
 __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ jobs,
                                                      const int64_t* __restrict__ tile_base,
                                                      const ProbeDesc* __restrict__ pdesc, int64_t tile0,
                                                      uint2* __restrict__ pairs, uint32_t* __restrict__ pair_uid,
                                                      int64_t* __restrict__ tile_src, int32_t* __restrict__ tile_cnt,
-                                                     const int2* __restrict__ perm, int32_t* __restrict__ tile_lvl,
-                                                     const ProbeDesc* __restrict__ prange) {
-  static_assert(!(MARK && CHAIN), "an exclusion step chains nothing");
+                                                     const int2* __restrict__ perm, int32_t* __restrict__ tile_lvl) {
   constexpr int mark = MARK ? 1 : 0;
-  constexpr int CAP = CHAIN ? BM_TILE : 1;  // a chained tile's matches at most (BM_TILE >= PROBE_TILE)
-  __shared__ uint16_t sLoc[CAP];  // a chained tile's matches: small-list index in the tile,
-  __shared__ uint32_t sPos[CAP];  // and the large list's position
   __shared__ int32_t sScan[4];
   __shared__ uint64_t sScan64[4];
 #if PROBE_LDS > 0
   __shared__ uint32_t sL[PROBE_LDS];
 #endif
-  const int64_t t = perm ? (int64_t)perm[xcd_slice(blockIdx.x, gridDim.x)].x : xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t t = perm ? (int64_t)perm[xcd_slice(blockIdx.x, gridDim.x)].x : (int64_t)blockIdx.x;
   const int64_t b = tile0 + t;
   const ProbeDesc D = pdesc[t];
   const JoinQ& J = jobs[D.job];
@@ -1149,31 +1068,18 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
     }
     return;
   }
-  if (!MARK && J.algo == JA_BMENUM) {  // workgroup-uniform: the matches from the AND of both bitmaps
-    probe_bmenum(J, b - tile_base[D.job], b, pairs, pair_uid, tile_src, tile_cnt, sScan);
-    return;
-  }
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
-  const bool chained = CHAIN && J.chain != nullptr;  // workgroup-uniform
   if (Lg.bm) {
     // a launch without long tiles does not carry the KPT_LARGE code (its registers
     // cost C2 a wave per SIMD: k_probe 111 -> 119 us)
-    // (a chained job's tiles are BM_TILE: layout_jobs)
-    if (LONG && !chained && J.ptile == KPT_LARGE * PROBE_TILE) {
+    if (LONG && J.ptile == KPT_LARGE * PROBE_TILE) {
       // (a job whose probe tests a chain list itself has BM_TILE tiles: layout_jobs)
       probe_bitmap<KPT_LARGE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark, sScan64);
       return;
     }
-    int64_t src = 0;
-    const int32_t cnt = probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src,
-                                                           tile_cnt, mark, sScan64, chained ? sLoc : nullptr, sPos,
-                                                           &src, chained ? nullptr : tile_lvl);
-    if (CHAIN && chained) {
-      __syncthreads();  // the tile's matches in LDS
-      chain_lds_tile(J.chain, b, src, cnt, sLoc, sPos, Sm.uid, (b - tile_base[D.job]) * J.ptile, J.small_is_A, pairs,
-                     pair_uid, tile_cnt, tile_lvl, prange + t * CHAIN_MAXL, sL, sScan64);
-    }
+    probe_bitmap<BM_TILE / PROBE_TILE>(J, Sm, Lg, b, tile_base[D.job], pairs, pair_uid, tile_src, tile_cnt, mark,
+                                       sScan64, tile_lvl);
     return;
   }
   const int64_t s0 = (b - tile_base[D.job]) * PROBE_TILE;
@@ -1219,7 +1125,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   }
   // a chained job's first later include list with a bitmap: tested here (as in
   // probe_bitmap), only its survivors written, the tile's first two level counts
-  const bool pre = !CHAIN && J.chain_bm != nullptr && tile_lvl != nullptr;  // workgroup-uniform
+  const bool pre = J.chain_bm != nullptr && tile_lvl != nullptr;  // workgroup-uniform
   const bool hit0 = hit;
   int32_t tp = 0;
   if (pre && hit) {
@@ -1246,16 +1152,6 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
       for (int x = 0; x < J.chain_fill; x++) lv[2 + x] = tot;
     }
     if (hit) stg(J.chain_tup0 + src + off, tp);
-  }
-  if (CHAIN && chained) {  // the matches in LDS, then the chain tests
-    if (hit) {
-      sLoc[off] = (uint16_t)threadIdx.x;
-      sPos[off] = (uint32_t)jl;
-    }
-    __syncthreads();
-    chain_lds_tile(J.chain, b, src, tot, sLoc, sPos, Sm.uid, s0, J.small_is_A, pairs, pair_uid, tile_cnt, tile_lvl,
-                   prange + t * CHAIN_MAXL, sL, sScan64);
-    return;
   }
   if (hit && !J.count_only) {
     pairs[src + off] = make_uint2((uint32_t)ia, (uint32_t)ib);
@@ -1344,48 +1240,34 @@ __device__ __forceinline__ int64_t lower_bound_cl(const ChainList& L, uint32_t k
   return lower_bound_list(d, key);
 }
 
-// the range [lo, hi) of a list without a bitmap that holds the ids of a unit's
-// matches: one thread per (unit, list), all units in parallel (as k_probe_part).
-// PRE: the units are the probe tiles [tile0, tile0 + n) of the step (k_probe<..,
-// CHAIN> tests their matches), the range spans the tile's small-list ids, which
-// hold its matches.  Otherwise the units are chain groups of merge tiles (grp),
-// after k_join: the range spans the group's matches.
-template <bool PRE>
+// the range [lo, hi) of a list without a bitmap that holds the ids of a chain
+// group's matches: one thread per (group, list), all groups in parallel (as
+// k_probe_part), after the step's joins: the range spans the group's matches.
 __global__ void k_chain_part(const JoinQ* __restrict__ jobs, const int64_t* __restrict__ tile_base, int njobs,
-                             const int2* __restrict__ grp, int64_t tile0, int64_t n,
+                             const int2* __restrict__ grp, int64_t n,
                              const uint32_t* __restrict__ pair_uid, const int64_t* __restrict__ tile_src,
                              const int32_t* __restrict__ tile_cnt, ProbeDesc* __restrict__ crange) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * CHAIN_MAXL) return;
   const int64_t u = i / CHAIN_MAXL;
   const int l = (int)(i % CHAIN_MAXL);
-  const int2 G = PRE ? make_int2(0, 0) : grp[u];
-  const int64_t t = PRE ? tile0 + u : G.x;
+  const int2 G = grp[u];
+  const int64_t t = G.x;
   const int j = find_job(tile_base, njobs, t);
   const JoinQ& J = jobs[j];
   const ChainQ* C = J.chain;
   if (!C || l >= ldg(&C->nl)) return;
   const ChainList L = load_cl(&C->l[l]);
   if (L.bm) return;
-  uint32_t k0, k1;
-  if (PRE) {
-    const DList& Sm = J.small_is_A ? J.A : J.B;
-    const int64_t s0 = (t - tile_base[j]) * J.ptile;
-    const int64_t s1 = s0 + J.ptile < Sm.n ? s0 + J.ptile : Sm.n;
-    if (s0 >= s1) return;
-    k0 = ldg(Sm.uid + s0);
-    k1 = ldg(Sm.uid + s1 - 1);
-  } else {
-    int f = -1, e = -1;
-    for (int k = 0; k < G.y; k++)
-      if (tile_cnt[G.x + k] > 0) {
-        if (f < 0) f = k;
-        e = k;
-      }
-    if (f < 0) return;
-    k0 = ldg(pair_uid + tile_src[G.x + f]);
-    k1 = ldg(pair_uid + tile_src[G.x + e] + tile_cnt[G.x + e] - 1);
-  }
+  int f = -1, e = -1;
+  for (int k = 0; k < G.y; k++)
+    if (tile_cnt[G.x + k] > 0) {
+      if (f < 0) f = k;
+      e = k;
+    }
+  if (f < 0) return;
+  const uint32_t k0 = ldg(pair_uid + tile_src[G.x + f]);
+  const uint32_t k1 = ldg(pair_uid + tile_src[G.x + e] + tile_cnt[G.x + e] - 1);
   ProbeDesc D;
   D.lo = lower_bound_cl(L, k0);
   D.hi = lower_bound_cl(L, k1 + 1u);  // ids < 2^32 - 1: no wrap
@@ -1730,63 +1612,6 @@ __global__ __launch_bounds__(256) void k_chain(const JoinQ* __restrict__ jobs, c
   }
 }
 
-// k_probe<.., CHAIN>: the chain tests of one probe tile of a chained job, on the
-// cnt matches the probe left in LDS (sLoc / sPos, in url-id order) instead of in
-// the tile's slots: rounds of 256 (one per thread); only the survivors are
-// written, at the front of the tile's slots, with their rows in the later include
-// lists; the tile's survivor count and its level counts.  The matches that do
-// not survive are never written to HBM nor read back.
-__device__ void chain_lds_tile(const ChainQ* __restrict__ C, int64_t b, int64_t src, int32_t cnt,
-                               const uint16_t* sLoc, const uint32_t* sPos, const uint32_t* __restrict__ small_uid,
-                               int64_t s0, bool small_is_A, uint2* __restrict__ pairs,
-                               uint32_t* __restrict__ pair_uid, int32_t* __restrict__ tile_cnt,
-                               int32_t* __restrict__ tile_lvl, const ProbeDesc* __restrict__ cr, uint32_t* sL,
-                               uint64_t* sScan64) {
-  const int tid = (int)threadIdx.x;
-  const int ninc = ldg(&C->ninc), nl = ldg(&C->nl), pos0 = ldg(&C->pos0), npos = ldg(&C->npos);
-  int32_t* tup0 = npos > 0 ? ldg(&C->tup[0]) : nullptr;
-  int32_t* tup1 = npos > 1 ? ldg(&C->tup[1]) : nullptr;
-  int32_t n1 = 0, n2 = 0, n3 = 0, run = 0;
-  for (int r0 = 0; r0 < cnt; r0 += 256) {  // workgroup-uniform
-    const int i = r0 + tid;
-    uint32_t key[1] = {0};
-    uint2 pr = make_uint2(0, 0);
-    int32_t pos[CHAIN_MAXI][1] = {{0}, {0}};
-    uint32_t alive = 0;
-    if (i < cnt) {  // the small list's id (the tile just read it: a cache hit) and the pair
-      const int64_t ik = s0 + sLoc[i];
-      const uint32_t jl = sPos[i];
-      key[0] = ldg(small_uid + ik);
-      pr = small_is_A ? make_uint2((uint32_t)ik, jl) : make_uint2(jl, (uint32_t)ik);
-      alive = 1;
-    }
-    uint32_t after1, after2, after3;
-    alive = chain_tests<1>(C->l, ninc, nl, pos0, cr, key, alive, pos, after1, after2, after3, sL);
-    const uint64_t c = (uint64_t)alive | (uint64_t)after1 << 16 | (uint64_t)after2 << 32 | (uint64_t)after3 << 48;
-    uint64_t tot;
-    const uint64_t ex = block_excl_sum256_u64(c, sScan64, &tot);
-    if (alive) {
-      const int64_t o = src + run + (int64_t)(ex & 0xFFFFu);
-      stg(reinterpret_cast<uint2*>(pairs) + o, pr);
-      stg(pair_uid + o, key[0]);
-      if (tup0) stg(tup0 + o, pos[0][0]);
-      if (tup1) stg(tup1 + o, pos[1][0]);
-    }
-    run += (int32_t)(tot & 0xFFFFu);
-    n1 += (int32_t)((tot >> 16) & 0xFFFFu);
-    n2 += (int32_t)((tot >> 32) & 0xFFFFu);
-    n3 += (int32_t)((tot >> 48) & 0xFFFFu);
-  }
-  if (tid == 0) {
-    tile_cnt[b] = run;
-    int32_t* lv = tile_lvl + b * CHAIN_LVL;
-    lv[0] = cnt;
-    lv[1] = n1;
-    lv[2] = n2;
-    lv[3] = n3;
-    lv[4] = run;
-  }
-}
 
 // ============================================================ url selection
 // TermSearch's urlselection (yrwi_query_desc.urlselection): the selection's url
@@ -1914,13 +1739,6 @@ __device__ __forceinline__ Rec joined_rec(Rec o, uint64_t b0, uint64_t b1, int m
 #endif
 constexpr int COMPACT_TILES = YRWI_COMPACT_TILES;
 constexpr int COMPACT_UNROLL = YRWI_COMPACT_UNROLL;
-// Cost-attribution builds only (their records are wrong; never the product):
-// bit 0 skips the accumulated side's record gather, bit 1 the joined side's J5
-// gather -- what each part of k_compact's time costs.  (The url ids are always
-// written: the rank phase gathers dictionary keys by them.)
-#ifndef YRWI_COMPACT_WHATIF
-#define YRWI_COMPACT_WHATIF 0
-#endif
 
 struct CompactJob {
   const uint64_t* af;
@@ -1997,7 +1815,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
   // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
-  const int64_t p0 = (perm ? xcd_slice(blockIdx.x, gridDim.x) : xcd_swizzle(blockIdx.x, gridDim.x)) * COMPACT_TILES;
+  const int64_t p0 = (perm ? xcd_slice(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x) * COMPACT_TILES;
   if (threadIdx.x < 64) {
     const int64_t p = p0 + threadIdx.x;
     int32_t c = 0;
@@ -2111,12 +1929,10 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                     X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
         continue;
       }
-      if (YRWI_COMPACT_WHATIF & 1) {
-        A[u].w[0] = pr[u].x; A[u].w[1] = pr[u].y; A[u].w[2] = A[u].w[3] = 0;
-      } else if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
       else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
       else A[u] = load_rec(X.af, pr[u].x);
-      if (X.mode == JM_ENUM && !(YRWI_COMPACT_WHATIF & 2)) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
+      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
@@ -4287,24 +4103,13 @@ int launch_feat_rows(const uint64_t* feat, const uint32_t* uid, const uint64_t* 
   return rc(hipGetLastError());
 }
 
-// YRWI_SYNC_DEBUG=1: synchronise after every launch of a join step and name it on
-// stderr (a kernel that never finishes is the last one named)
-static void dbg_sync(const char* what, void* st) {
-  static const bool on = getenv("YRWI_SYNC_DEBUG") && atoi(getenv("YRWI_SYNC_DEBUG"));
-  if (!on) return;
-  fprintf(stderr, "[yrwi sync] %s ...", what);
-  fflush(stderr);
-  const hipError_t e = hipStreamSynchronize(reinterpret_cast<hipStream_t>(st));
-  fprintf(stderr, " done (%s)\n", hipGetErrorString(e));
-}
-
 int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int32_t nmerge,
                      int64_t merge_tiles, int64_t total_tiles, TileDesc* d_desc, ProbeDesc* d_pdesc,
                      uint2* d_pairs, uint32_t* d_pair_uid, int64_t* d_tile_src, int32_t* d_tile_cnt,
                      int64_t* d_tile_off, bool mark, bool long_tiles, const BandOrder& bo,
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
-                     ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups, ProbeDesc* d_prange) {
+                     ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -4326,13 +4131,11 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
   if (merge_tiles > 0) {
     hipLaunchKernelGGL(k_partition, dim3((unsigned)((merge_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, nmerge, merge_tiles, d_desc, d_tile_src, tkey, tjob);
-    dbg_sync("k_partition", st);
     if (!mark) hipLaunchKernelGGL(k_scan_bounds, dim3((unsigned)nmerge), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_src);
   }
   if (probe_tiles > 0)
     hipLaunchKernelGGL(k_probe_part, dim3((unsigned)((probe_tiles + 255) / 256)), dim3(256), 0, S(st), d_jobs,
                        d_tile_base, njobs, merge_tiles, probe_tiles, d_pdesc, tkey, tjob, pkey, bo.pshift);
-  if (probe_tiles > 0) dbg_sync("k_probe_part", st);
   if (perm || pperm) {
     OrderArgs oa{};
     int nb = 0;
@@ -4352,51 +4155,33 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     if (pperm) prob(perm ? 1 : 0, pkey, probe_tiles, 0, tjob + merge_tiles, pperm);
     hipLaunchKernelGGL(k_order_hist, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
     hipLaunchKernelGGL(k_order_scatter, dim3((unsigned)nb), dim3(ORDER_THREADS), 0, S(st), oa);
-    dbg_sync("k_order", st);
   }
   if (ev0) hipEventRecord(reinterpret_cast<hipEvent_t>(ev0), S(st));
   if (merge_tiles > 0)
     hipLaunchKernelGGL(k_join, dim3((unsigned)std::min<int64_t>(merge_tiles, join_grid)), dim3(JOIN_THREADS), 0,
                        S(st), d_jobs, d_desc, merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, mark ? 1 : 0);
-  if (merge_tiles > 0) dbg_sync("k_join", st);
   if (evm) hipEventRecord(reinterpret_cast<hipEvent_t>(evm), S(st));
-  const bool fused = chain && d_prange != nullptr;  // YRWI_CHAIN_FUSED (yrwi_host.cpp chain_fused)
   if (probe_tiles > 0) {
-    if (fused) {  // the chained jobs' later-list ranges of every probe tile, for k_probe<.., true>
-      const int64_t nr = probe_tiles * CHAIN_MAXL;
-      hipLaunchKernelGGL(k_chain_part<true>, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                         d_tile_base, njobs, (const int2*)nullptr, merge_tiles, probe_tiles,
-                         (const uint32_t*)d_pair_uid, (const int64_t*)d_tile_src, (const int32_t*)d_tile_cnt,
-                         d_prange);
-      dbg_sync("k_chain_part<probe tiles>", st);
-    }
-    auto kp = long_tiles ? (mark ? k_probe<true, true, false>
-                                 : fused ? k_probe<true, false, true> : k_probe<true, false, false>)
-                         : (mark ? k_probe<false, true, false>
-                                 : fused ? k_probe<false, false, true> : k_probe<false, false, false>);
+    auto kp = long_tiles ? (mark ? k_probe<true, true> : k_probe<true, false>)
+                         : (mark ? k_probe<false, true> : k_probe<false, false>);
     hipLaunchKernelGGL(kp, dim3((unsigned)probe_tiles), dim3(PROBE_TILE), 0, S(st), d_jobs, d_tile_base, d_pdesc,
-                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm, d_tile_lvl,
-                       (const ProbeDesc*)d_prange);
-    dbg_sync(mark ? "k_probe (exclusion)" : "k_probe", st);
+                       merge_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, (const int2*)pperm, d_tile_lvl);
   }
   if (ev1) hipEventRecord(reinterpret_cast<hipEvent_t>(ev1), S(st));
   if (!mark) {
-    if (chain && ngroups > 0) {  // chain groups (fused: of merge tiles only)
+    if (chain && ngroups > 0) {  // chain groups
       const int64_t nr = ngroups * CHAIN_MAXL;
-      hipLaunchKernelGGL(k_chain_part<false>, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs,
-                         d_tile_base, njobs, d_cgrp, (int64_t)0, ngroups, (const uint32_t*)d_pair_uid,
+      hipLaunchKernelGGL(k_chain_part, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, S(st), d_jobs,
+                         d_tile_base, njobs, d_cgrp, ngroups, (const uint32_t*)d_pair_uid,
                          (const int64_t*)d_tile_src, (const int32_t*)d_tile_cnt, d_crange);
-      dbg_sync("k_chain_part", st);
       // chained steps: evc0 / evc1 bracket k_chain alone (the population rocprofv3 averages)
       if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       hipLaunchKernelGGL(k_chain, dim3((unsigned)ngroups), dim3(256), 0, S(st), d_jobs, d_tile_base, njobs, d_cgrp,
                          d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_lvl, (const ProbeDesc*)d_crange);
       if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
-      dbg_sync("k_chain", st);
     }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off, (const int32_t*)(chain ? d_tile_lvl : nullptr));
-    dbg_sync("k_scan_tiles", st);
     if (!chain) {  // chained steps compact once the fold's dispatch modes are known (launch_compact)
       if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       if (int r = launch_compact(d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
@@ -4417,7 +4202,6 @@ int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njob
   hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
                      d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
                      perm, (const int32_t*)bo.tile_job);
-  dbg_sync(chain ? "k_compact<chain>" : "k_compact", st);
   return rc(hipGetLastError());
 }
 
