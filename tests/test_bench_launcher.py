@@ -37,7 +37,7 @@ def test_compact_line_fits_the_driver_tail():
     roofline, the CPU baseline, parity, latency and one summary per leg."""
     sys.path.insert(0, ROOT)
     import bench
-    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "archive", "r04_bench.json")) as f:
         full = json.load(f)
     full["build"] = bench.source_identity()
     line = bench.compact_line(full, "profiles/bench_detail_x.json")
@@ -60,7 +60,7 @@ def test_line_reports_the_shard_transport():
     an 8-GPU record shows that RCCL saw 8 ranks -- or that it did not."""
     sys.path.insert(0, ROOT)
     import bench
-    with open(os.path.join(ROOT, "profiles", "r04_bench.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "archive", "r04_bench.json")) as f:
         full = json.load(f)
     info = lambda r, t, n, peers: {"transport": t, "rank": r, "world": 8, "rccl_ranks": n, "lanes": 8,
                                    "lanes_own_comm": 8 if n else 0, "device_peers": peers, "mailbox": 1,

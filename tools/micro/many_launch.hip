@@ -1,6 +1,6 @@
 // many_launch.hip -- does rocprofv3 --pmc survive ~200k dispatches of a small
 // kernel?  (The round-4 C5 counter pass died with SIGSEGV inside the HIP launch
-// path during the index build's 200k per-list launches: profiles/r04_c5_pmc_crash.log.)
+// path during the index build's 200k per-list launches: profiles/archive/r04_c5_pmc_crash.log.)
 // Same shape as that build: one small kernel launch per "list", each over its own
 // slice of one large device buffer.  No library code of yrwi is involved.
 #include <hip/hip_runtime.h>

@@ -1,6 +1,6 @@
 # Does rocprofv3 --pmc survive ~200k small kernel dispatches without any yrwi code?
 # (round 4's C5 counter pass died with SIGSEGV inside the HIP launch path during the
-# index build's 200k per-list launches: profiles/r04_c5_pmc_crash.log.)  Then the same
+# index build's 200k per-list launches: profiles/archive/r04_c5_pmc_crash.log.)  Then the same
 # pass over libyrwi's C5 index build, untouched (no --kernel-exclude-regex), once.
 set -o pipefail
 R=$(pwd)

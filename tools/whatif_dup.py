@@ -39,6 +39,25 @@ TOPQ = ("    hipLaunchKernelGGL(k_topq<4096>, dim3((unsigned)ngroups), dim3(TOPQ
 VARIANTS["topq"] = [(K, TOPQ, 2)]
 
 
+# variants that change code rather than duplicate a launch: (file, old, new) edits
+H = "yrwi_host.cpp"
+EDITS = {
+    # k_emit into a device buffer, then DMA copies to the pinned destination
+    "emitdma": [
+        (H, "  uint8_t* land = nullptr;\n  {\n    void* hp = h_hits;",
+            "  uint8_t* land = nullptr;\n  void* hp_dst = nullptr;\n  void* np_dst = nullptr;\n  {\n    void* hp = h_hits;"),
+        (H, "    HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hits), hp, 0));\n"
+            "    HIPCHK(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&d_nout), np, 0));\n  }",
+            "    hp_dst = hp;\n    np_dst = np;\n    d_hits = arena_alloc<yrwi_hit>(ctx, (int64_t)nq * kmax);\n"
+            "    d_nout = arena_alloc<int32_t>(ctx, nq);\n    if (!d_hits || !d_nout) return ctx->fail(YRWI_E_NOMEM, \"arena\");\n  }"),
+        (H, "  if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }\n  HIPCHK(ctx, lane_sync(ctx));\n  if (hD_land) {",
+            "  HIPCHK(ctx, hipMemcpyAsync(hp_dst, d_hits, hb, hipMemcpyDeviceToHost, ctx->stream));\n"
+            "  HIPCHK(ctx, hipMemcpyAsync(np_dst, d_nout, nb, hipMemcpyDeviceToHost, ctx->stream));\n"
+            "  if (tm) { tm->ts = ctx->event(); hipEventRecord(tm->ts, ctx->stream); }\n  HIPCHK(ctx, lane_sync(ctx));\n  if (hD_land) {"),
+    ],
+}
+
+
 def build(name):
     tmp = f"/tmp/whatif_{name}"
     shutil.rmtree(tmp, ignore_errors=True)
@@ -46,12 +65,17 @@ def build(name):
     shutil.copytree(CSRC, src)
     os.makedirs(os.path.join(tmp, "include"), exist_ok=True)
     shutil.copy(os.path.join(ROOT, "include", "yrwi.h"), os.path.join(tmp, "include"))
-    for f, text, times in VARIANTS[name]:
+    for f, text, times in VARIANTS.get(name, []):
         p = os.path.join(src, f)
         s = open(p).read()
         assert s.count(text) == 1, (name, f, s.count(text))
         s = s.replace(text, "{\n" + text * times + "}\n")  # (a braced block: some sit under an if)
         open(p, "w").write(s)
+    for f, old, new in EDITS.get(name, []):
+        p = os.path.join(src, f)
+        s = open(p).read()
+        assert s.count(old) == 1, (name, f, old[:60], s.count(old))
+        open(p, "w").write(s.replace(old, new))
     out = os.path.join(ROOT, "gpurun_var", f"libyrwi_dup_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     subprocess.check_call(["make", "-s", "-j8", "-C", src, f"OUT={out}",
@@ -60,5 +84,5 @@ def build(name):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(VARIANTS):
+    for n in sys.argv[1:] or list(VARIANTS) + list(EDITS):
         build(n)

@@ -159,6 +159,15 @@ struct Arena {
   }
 };
 
+// a gapped joined container's tile table (JoinQ::fused, RankQ::toff)
+struct Gap {
+  const int64_t* toff = nullptr;
+  const int32_t* tcnt = nullptr;
+  const int32_t* ctile = nullptr;
+  int64_t ntiles = 0;
+  int32_t ptile = 0;
+};
+
 struct Plan {
   bool empty = true;                 // no result anywhere (J1 on global sizes)
   std::vector<const ListRec*> seq;   // fold order; a list absent from this shard is an empty ListRec
@@ -181,6 +190,7 @@ struct Plan {
   const yrwi_filter* filter = nullptr;  // addRWIs constraints (nullptr: none)
   // runtime container (a deferred one between the steps of a multi-term fold)
   DList cont{nullptr, nullptr, nullptr, 0};
+  Gap gap;  // cont is gapped (a fused probe's last step; RankQ::toff) when gap.toff != nullptr
   int32_t step_mode[YRWI_MAX_TERMS] = {0};  // JoinMode of every fold step taken
   // count-first chained fold (t = 3, list 2 the smallest): list 0 x list 1 only
   // counted (its size decides step 1's dispatch), the survivors chained from list 2
@@ -473,7 +483,7 @@ inline T* arena_alloc(Lane* ctx, int64_t count) {
 // share one stream do not wait for work the other lane enqueues later.
 inline hipError_t lane_sync(Lane* L) {
   // (a blocking-sync event or a polled wait, measured in round 2: no better,
-  // profiles/r02f_sync_poll_sweep.txt)
+  // profiles/archive/r02f_sync_poll_sweep.txt)
   if (!L->sync_ev && hipEventCreateWithFlags(&L->sync_ev, hipEventDisableTiming) != hipSuccess)
     return hipErrorOutOfMemory;
   hipError_t e = hipEventRecord(L->sync_ev, L->stream);
@@ -506,7 +516,7 @@ inline uint8_t* stage_reserve(Lane* ctx, Stage* S, size_t bytes, bool drain) {
 // the pinned pages through their device address) on the lane's stream: no DMA
 // engine on the query path.  SDMA copies measured 1.3-1.5 ms per C2 batch over
 // the driver's 20-step run against 0.8 with HSA_ENABLE_SDMA=0 (the copy engines'
-// queues stall the lanes' first batches: profiles/r03a_sdma.txt).
+// queues stall the lanes' first batches: profiles/archive/r03a_sdma.txt).
 struct UpEnt {
   void* dst;
   const void* src;
