@@ -533,9 +533,8 @@ def kernel_lines(iso, pmc):
       k_join    SURVEY.md §8(d): sum of min(K, 4-B ids of both sides) over the merge-executed steps;
       k_probe   §8(d): sum of min(K, bytes the probe loads) over the probe-executed include steps
                 (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id); K as the reference
-                dispatches the step (J3); plus 23 t m_out of the joined containers whose records the
-                probe wrote itself (a query's last step fused into k_probe: bytes_features_fused);
-      k_compact §8(d): 23 B per include term and joined posting (23 t m_out) of the containers it wrote;
+                dispatches the step (J3);
+      k_compact §8(d): 23 B per include term and joined posting (23 t m_out);
       k_reduce  the 32-B ranking record of every joined posting (+ 1-B exclusion mark), k_shard_fin included;
       k_score   the same records (an upper bound: chunks the threshold prunes read 16 of the 32 B);
       k_chain   §8(d): the chained folds' later steps' K and the exclusions' 12 n_e, each charged
@@ -549,7 +548,7 @@ def kernel_lines(iso, pmc):
     for name, t_ns, alg, nl, extra in (
             ("k_join", iso["t_join_ns"], iso["bytes_join_capped"], n,
              {"alg_bytes_model_K": int(iso["bytes_join"] / n)}),
-            ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"] + iso.get("bytes_features_fused", 0), n,
+            ("k_probe", iso["t_probe_ns"], iso["bytes_probe_capped"], n,
              {"alg_bytes_model_K": int(iso["bytes_probe"] / n), "loaded_bytes": int(iso["bytes_probe_loaded"] / n)}),
             ("k_compact", iso["t_compact_ns"], iso["bytes_features"], n, {}),
             ("k_reduce", iso.get("t_reduce_ns", 0), iso.get("bytes_reduce", 0), nr, {}),

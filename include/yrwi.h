@@ -166,9 +166,6 @@ typedef struct yrwi_stats {
   int64_t n_chain_launches;
   int64_t t_chain_ns;
   int64_t bytes_chain;
-  /* 23 t m_out of the joined containers whose records the bitmap probe wrote itself (a query's last
-     step, fused into k_probe: no k_compact for it); bytes_features holds the rest */
-  int64_t bytes_features_fused;
 } yrwi_stats;
 
 /* ---- profile helpers (RankingProfile.java) ---- */

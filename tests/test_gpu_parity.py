@@ -565,9 +565,7 @@ def test_async_batches_pinned_and_pageable(corpus):
 
 
 def test_stats_compact_accounting(corpus):
-    """yrwi_stats: a two-term query joins in one step.  Through a bitmap probe its
-    records come from k_probe itself (fused): no k_compact bytes or time, and its
-    23 t m_out go to bytes_features_fused.  Otherwise k_compact's algorithmic
+    """yrwi_stats: a two-term query joins in one step, so k_compact's algorithmic
     bytes are the joined rows times 96 (enumeration: 12 B pair + url id, 32 B
     record of the accumulated side, 16 B of the joined side, 36 B written) or 80
     (by test: one 32-B record gathered), and its HIP-event time is positive
@@ -583,10 +581,6 @@ def test_stats_compact_accounting(corpus):
         if st.joined == 0:
             continue
         seen += 1
-        if st.bytes_features_fused:
-            assert st.bytes_features_fused == 46 * st.joined and st.bytes_features == 0, st.bytes_features_fused
-            assert st.bytes_compact == 0 and st.t_compact_ns == 0
-            continue
         assert st.bytes_compact in (96 * st.joined, 80 * st.joined), (st.bytes_compact, st.joined)
         assert st.t_compact_ns > 0
     assert seen > 0
@@ -752,49 +746,3 @@ def test_authority_host_partition(corpus, maxb, monkeypatch):
         for qi, (q, g) in enumerate(zip(batch, got)):
             exp = orc.search(d, q.include, q.exclude, orc.profile_from(prof), "en", now_ms=NOW, k=100)
             assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, (maxb, qi)
-
-
-@pytest.mark.parametrize("maxb", [None, "1"])
-def test_fused_probe_gapped_containers(maxb, monkeypatch):
-    """A 2-term query's last step as a simple bitmap probe writes its records into
-    the tile slots itself (JoinQ::fused, no pairs, no k_compact): the rank phase
-    reads the gapped container through the chunk slot maps (gap_map) and every
-    per-element array by slot.  Dense and sparse pairs of bitmap lists, the default,
-    C5 custom (authority by partition: host counts indexed by slot; maxb 1 forces
-    the global-table fallback) and /date profiles, k from 1 to 3000, next to
-    non-fused queries (one term, a distance filter) in the same batch -- the
-    oracle's hits, and the statistics show the fused path ran."""
-    from yacy_search_server_amd._lib import CStats
-    if maxb:
-        monkeypatch.setenv("YRWI_HPART_MAXB", maxb)
-    cfg = synth.preset("small")
-    idx = synth.build_index(cfg)
-    ix = RWIIndex(0)
-    try:
-        for t in range(cfg.n_terms):
-            if idx.sizes[t]:
-                ix.add(idx.hashes[t], idx.list_rows(t))
-        d = idx.as_dict()
-        order = [int(t) for t in np.argsort(-idx.sizes, kind="stable")]
-        big, mid = order[:6], order[40:60]
-        rng = np.random.default_rng(77)
-        c5 = RankingProfile("", "date=15,domlength=15,authority=13,tf=10")
-        batch = []
-        for i in range(36):
-            a = big[i % len(big)]
-            b = big[(i + 1 + i // 6) % len(big)] if i % 3 else mid[int(rng.integers(len(mid)))]
-            prof = [None, c5, RankingProfile.date()][i % 3]
-            k = [100, 1, 3000, 37][i % 4]
-            batch.append(Query([idx.hashes[a], idx.hashes[b]], [], now_ms=NOW, k=k, profile=prof))
-        batch.append(Query([idx.hashes[big[0]]], [], now_ms=NOW, k=100))                     # one list
-        batch.append(Query([idx.hashes[big[0]], idx.hashes[big[1]]], [], now_ms=NOW, k=100, max_distance=3))
-        st = CStats()
-        got = ix.search_batch(batch, stats=st)
-        assert st.bytes_features_fused > 0, "no query took the fused probe"
-        assert st.bytes_features >= 0
-        for qi, (q, g) in enumerate(zip(batch, got)):
-            prof = orc.profile_from(q.profile) if q.profile is not None else None
-            exp = orc.search(d, q.include, q.exclude, profile=prof, now_ms=NOW, k=q.k, max_distance=q.max_distance)
-            assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, qi
-    finally:
-        ix.close()

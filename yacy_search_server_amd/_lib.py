@@ -71,8 +71,7 @@ class CStats(ctypes.Structure):
                 ("n_probe_dispatches", ctypes.c_int64), ("t_probe_all_ns", ctypes.c_int64),
                 ("n_rank_passes", ctypes.c_int64), ("t_reduce_ns", ctypes.c_int64), ("t_scorek_ns", ctypes.c_int64),
                 ("bytes_reduce", ctypes.c_int64), ("bytes_score", ctypes.c_int64),
-                ("n_chain_launches", ctypes.c_int64), ("t_chain_ns", ctypes.c_int64), ("bytes_chain", ctypes.c_int64),
-                ("bytes_features_fused", ctypes.c_int64)]
+                ("n_chain_launches", ctypes.c_int64), ("t_chain_ns", ctypes.c_int64), ("bytes_chain", ctypes.c_int64)]
 
 
 class CNode(ctypes.Structure):

@@ -1054,16 +1054,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
   layout_jobs(ctx->probe_ratio, ctx->nurls, jobs, owner, tile_base, &nmerge, &merge_tiles, &tiles, &long_tiles);
   const int nj = (int)jobs.size();
-  // fused jobs (JoinQ::fused, requested by run_join_phase): exactly the tiles of
-  // k_probe's short path (bm_tile: BMF_SIMPLE), whose records k_probe then writes
-  for (JoinQ& J : jobs) {
-    if (!J.fused) continue;
-    const bool bm = (J.small_is_A ? J.B.bm : J.A.bm) != nullptr;
-    J.fused = J.algo == JA_PROBE && bm && J.ptile == BM_TILE && J.mode != JM_MARK && J.maxd >= 65535 &&
-                      !J.chain_bm && !J.count_only && J.out_feat && !J.out_tup && !J.chained && !J.A.tup ? 1 : 0;
-    if (J.fused && !(J.ctile = arena_alloc<int32_t>(ctx, ceil_div(std::min(J.A.n, J.B.n), CHUNK) + 1)))
-      return ctx->fail(YRWI_E_NOMEM, "arena");
-  }
   if (st)
     for (const JoinQ& J : jobs) {  // §8(d) K of the step as the reference dispatches it
       const int64_t K = step_bytes(J.mode, J.A.n, J.B.n), loaded = loaded_bytes(J);
@@ -1165,12 +1155,9 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
   hipEvent_t sp = span_open(ctx, tm);
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
-  // a step whose every job is fused (or only counted) launches no k_compact
-  const bool need_compact =
-      std::any_of(jobs.begin(), jobs.end(), [](const JoinQ& J) { return !J.fused && !J.count_only; });
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
                        false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange, d_cgrp,
-                       (int64_t)cgrp.size(), d_fast, d_fast_perm, need_compact))
+                       (int64_t)cgrp.size(), d_fast, d_fast_perm))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
@@ -1180,7 +1167,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     if (chain) {
       // c0 / c1 bracket k_chain alone; a step without chain groups launched none
       if (!cgrp.empty()) tm->kchain.push_back({c0, c1});
-    } else if (need_compact) {
+    } else {
       tm->kcompact.push_back({c0, c1});
     }
     tm->spans.push_back({sp, se});
@@ -1200,7 +1187,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     for (int j = 0; j < nj; j++) {
       const JoinQ& J = jobs[(size_t)j];
       const int64_t atw = J.A.tup ? J.A.tw : 0;
-      if (J.count_only || J.fused) continue;  // (a fused job's records: k_probe)
+      if (J.count_only) continue;
       if (J.chain) {
         const int64_t t = 2 + (*chq)[(size_t)owner[(size_t)j]].npos;
         st->bytes_compact += mh[(size_t)j] * (12 + 4 * (t - 2) + 32 + 24 * (t - 1) + 36);
@@ -1229,9 +1216,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
     P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
                    J.out_tup ? J.out_tw : 0};
-    P.gap = Gap{};
-    if (J.fused)  // gapped: tile t's records at slots [t * ptile, ...) (RankQ::toff)
-      P.gap = Gap{d_off + tile_base[(size_t)j], d_cnt + tile_base[(size_t)j], J.ctile, J.ntiles, J.ptile};
   }
   if (chain && pend) {
     pend->active = true;
@@ -1308,10 +1292,7 @@ static int run_exclusion(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Ti
 // containers: the next list's (Plan.seq_ng) and the accumulated container's,
 // which after the first step is the sum over the shards of their joined rows
 // (one exchange per step that some query continues past; none on one context).
-// fuse: the joined containers go to the rank phase (yrwi_query*): a query's last
-// step may write its records from the probe into tile slots (JoinQ::fused, a
-// gapped container); the callers that read a joined container as rows pass false.
-static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm, bool fuse) {
+static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, Timing* tm) {
   const size_t nq = plans.size();
   std::vector<int64_t> acc_g(nq, 0);  // global size of each query's accumulated container
   for (size_t qi = 0; qi < nq; qi++) {
@@ -1499,9 +1480,6 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         }
       }
       if (!J.out_uid && !P.chain) return ctx->fail(YRWI_E_NOMEM, "arena");
-      // the query's records straight from the probe (run_join_jobs keeps this only
-      // for a simple bitmap probe): its last step, no exclusion or selection after
-      J.fused = fuse && last && !P.chain && !J.A.tup && J.out_feat && P.nexcl_g == 0 && !P.has_sel ? 1 : 0;
       if (st) {
         st->bytes_alg += step_bytes(J.mode, J.A.n, J.B.n);
         if (J.mode == JM_ENUM) st->n_enum_steps++; else st->n_test_steps++;
@@ -1717,11 +1695,6 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.dkhi = ctx->dkhi;
     R.dklo = ctx->dklo;
     R.removed = P.removed;
-    R.toff = P.gap.toff;
-    R.tcnt = P.gap.tcnt;
-    R.ctile = P.gap.ctile;
-    R.ntiles = P.gap.ntiles;
-    R.ptile = P.gap.ptile;
     R.n = P.empty ? 0 : P.cont.n;
     R.nchunks = ceil_div(R.n, CHUNK);
     R.chunk_base = chunks;
@@ -1753,7 +1726,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     if (st) {
       st->joined += R.n;
       st->bytes_alg += 23 * (int64_t)P.seq.size() * R.n;  // ranking feature bytes per surviving posting and term
-      (R.toff ? st->bytes_features_fused : st->bytes_features) += 23 * (int64_t)P.seq.size() * R.n;
+      st->bytes_features += 23 * (int64_t)P.seq.size() * R.n;
       st->bytes_alg_capped += 23 * (int64_t)P.seq.size() * R.n;
     }
   }
@@ -1795,9 +1768,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
   void* d_hptmp = nullptr;
   size_t hp_tmp = 0;
   if (hp_buckets > 0) {
-    // (a gapped container's host counts are indexed by slot)
-    auto span = [&](const RankQ& R) { return R.toff ? R.ntiles * (int64_t)R.ptile : R.n; };
-    for (int qi = 0; qi < nq; qi++) if (rq[(size_t)qi].hp_nb) hp_elems += span(rq[(size_t)qi]);
+    for (int qi = 0; qi < nq; qi++) if (rq[(size_t)qi].hp_nb) hp_elems += rq[(size_t)qi].n;
     hp_tmp = host_part_tmp_bytes(hp_hist);
     d_hist = arena_alloc<int32_t>(ctx, hp_hist + 1);
     d_hoffs = arena_alloc<int32_t>(ctx, hp_hist + 1);
@@ -1813,7 +1784,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
       if (!R.hp_nb) continue;
       R.ecnt = d_ecnt + eb;
       R.hp_hist = d_hist;
-      eb += span(R);
+      eb += R.n;
     }
     if (upload(ctx, d_bq, bq)) return YRWI_E_HIP;
   }
@@ -2248,7 +2219,7 @@ static int run_batch_part_(const yrwi_ctx* ix, Lane* L, const yrwi_query_desc* q
       hipEventRecord(tm.t0, L->stream);
     }
     const int64_t tj0 = now_ns(), wj0 = L->wait_ns;
-    int rc = run_join_phase(L, plans, st, tmp, true);
+    int rc = run_join_phase(L, plans, st, tmp);
     if (rc) return rc;
     tj += now_ns() - tj0;
     wj += L->wait_ns - wj0;
@@ -2427,7 +2398,6 @@ extern "C" int yrwi_query_batch(yrwi_ctx* ctx, const yrwi_query_desc* q, int32_t
       st->n_chain_launches += p.n_chain_launches;
       st->t_chain_ns += p.t_chain_ns;
       st->bytes_chain += p.bytes_chain;
-      st->bytes_features_fused += p.bytes_features_fused;
     }
     st->t_total_ns = now_ns() - t0;
   }
@@ -2569,7 +2539,7 @@ extern "C" int yrwi_term_search(yrwi_ctx* ctx, const yrwi_query_desc* q, uint8_t
   if ((rc = ctx->take(L, resolve_selections(L, plans)))) return rc;
   if (begin_pass(L)) return ctx->take(L, YRWI_E_HIP);
   if ((rc = ctx->take(L, plan_batch(L, plans)))) return rc;
-  rc = ctx->take(L, run_join_phase(L, plans, nullptr, nullptr, false));
+  rc = ctx->take(L, run_join_phase(L, plans, nullptr, nullptr));
   if (rc) return rc;
   const Plan& P = plans[0];
   if (P.empty || P.cont.n == 0) {

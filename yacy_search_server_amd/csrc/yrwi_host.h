@@ -159,15 +159,6 @@ struct Arena {
   }
 };
 
-// a gapped joined container's tile table (JoinQ::fused, RankQ::toff)
-struct Gap {
-  const int64_t* toff = nullptr;
-  const int32_t* tcnt = nullptr;
-  const int32_t* ctile = nullptr;
-  int64_t ntiles = 0;
-  int32_t ptile = 0;
-};
-
 struct Plan {
   bool empty = true;                 // no result anywhere (J1 on global sizes)
   std::vector<const ListRec*> seq;   // fold order; a list absent from this shard is an empty ListRec
@@ -190,7 +181,6 @@ struct Plan {
   const yrwi_filter* filter = nullptr;  // addRWIs constraints (nullptr: none)
   // runtime container (a deferred one between the steps of a multi-term fold)
   DList cont{nullptr, nullptr, nullptr, 0};
-  Gap gap;  // cont is gapped (a fused probe's last step; RankQ::toff) when gap.toff != nullptr
   int32_t step_mode[YRWI_MAX_TERMS] = {0};  // JoinMode of every fold step taken
   // count-first chained fold (t = 3, list 2 the smallest): list 0 x list 1 only
   // counted (its size decides step 1's dispatch), the survivors chained from list 2

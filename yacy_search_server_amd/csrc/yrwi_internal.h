@@ -188,15 +188,6 @@ struct JoinQ {
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
   int64_t bm_words;    // JA_BMAND: 16-B bitmap units of the url-id space (bm_units)
   const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
-  // fused (set by the host after layout_jobs): the query's last step, a bitmap
-  // probe of BM_TILE tiles with no exclusion mark, distance filter or chain test,
-  // whose records go straight to the rank phase.  Each tile writes every match's
-  // finished record and url id into its own slots of out_feat / out_uid (k_probe,
-  // BMF_FUSED): tile j's matches at [j * ptile, j * ptile + tile_cnt) -- no pairs,
-  // no k_compact.  ctile (k_scan_tiles): the tile holding element c * CHUNK of the
-  // gapped container, per chunk c (RankQ::ctile).
-  int32_t fused;
-  int32_t* ctile;
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
@@ -223,15 +214,14 @@ struct ProbeDesc {
 // k_order_scatter): the smaller list's ids, the larger list's url-id bitmap, the
 // tile's first small index and pair slot, its tile index.  BMF_SIMPLE: no
 // exclusion mark, distance filter or chain test -- nothing of the job is read.
-constexpr int32_t BMF_SIMPLE = 1, BMF_SMALL_A = 2, BMF_FUSED = 4;
+constexpr int32_t BMF_SIMPLE = 1, BMF_SMALL_A = 2;
 struct BmFast {
   const uint32_t* sm_uid;
   const uint64_t* lg_bm;
   int64_t sm_n, s0, src;
   int64_t t;       // the tile (index among the step's probe tiles)
   int32_t flags;   // BMF_*
-  int32_t job;
-  int32_t pad[2];
+  int32_t pad[3];
 };
 static_assert(sizeof(BmFast) == 64, "one 64-B scalar load");
 
@@ -327,17 +317,6 @@ struct RankQ {
   int32_t* ecnt;           // ... and every element's host count (nullptr: the host tables serve)
   int64_t hp_hoff;         // ... its first histogram entry (bucket-major: hp_hoff + bucket * nchunks + chunk)
   int32_t* hp_hist;        // ... the histogram (k_reduce counts every chunk's buckets into it)
-  // gapped container (toff != nullptr; JoinQ::fused): element e lives at a slot,
-  // not at index e -- tile j's elements at slots [j * ptile, j * ptile + tcnt[j]),
-  // element e is tile j's (e - toff[j])-th; ctile[c] = the tile holding element
-  // c * CHUNK.  Every per-element array (feat, uid, ecnt) and every candidate's
-  // index are in slots (slot order is container order, so the index tie-break is
-  // unchanged); chunks still cut the container's n elements.
-  const int64_t* toff;
-  const int32_t* tcnt;
-  const int32_t* ctile;
-  int64_t ntiles;
-  int32_t ptile;
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -429,7 +408,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
                      bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
                      const int2* d_cgrp = nullptr, int64_t ngroups = 0, BmFast* d_fast = nullptr,
-                     BmFast* d_fast_perm = nullptr, bool compact = true);
+                     BmFast* d_fast_perm = nullptr);
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);

@@ -838,8 +838,7 @@ __device__ __forceinline__ bool probe_heads(const DList& Lg, int64_t lo, int64_t
 // path of k_probe serves the tile -- a bitmap probe of BM_TILE ids whose pairs
 // are written with no exclusion mark, distance filter or chain test (the job's
 // tiles, in whatever order k_probe takes them, read this and nothing else).
-__device__ __forceinline__ BmFast bm_tile(const JoinQ* jobs0, const JoinQ& J, int64_t b, int64_t tile_base0,
-                                          int64_t t) {
+__device__ __forceinline__ BmFast bm_tile(const JoinQ& J, int64_t b, int64_t tile_base0, int64_t t) {
   BmFast F{};
   const DList& Sm = J.small_is_A ? J.A : J.B;
   const DList& Lg = J.small_is_A ? J.B : J.A;
@@ -849,13 +848,10 @@ __device__ __forceinline__ BmFast bm_tile(const JoinQ* jobs0, const JoinQ& J, in
   F.s0 = (b - tile_base0) * (int64_t)J.ptile;
   F.src = J.pair_base + F.s0;
   F.t = t;
-  F.job = (int32_t)(&J - jobs0);
   F.flags = J.small_is_A ? BMF_SMALL_A : 0;
   if (t >= 0 && J.algo == JA_PROBE && Lg.bm && J.ptile == BM_TILE && J.mode != JM_MARK && J.maxd >= 65535 &&
-      !J.chain_bm && !J.count_only) {
+      !J.chain_bm && !J.count_only)
     F.flags |= BMF_SIMPLE;
-    if (J.fused) F.flags |= BMF_FUSED;  // (the host's decision: fused implies every condition above)
-  }
   return F;
 }
 
@@ -878,7 +874,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
     D.pad = 0;
     D.lo = D.hi = 0;
     pdesc[t] = D;
-    if (fast) fast[t] = bm_tile(jobs, J, tile0 + t, tile_base[j], t);
+    if (fast) fast[t] = bm_tile(J, tile0 + t, tile_base[j], t);
     return;
   }
   const DList& Sm = J.small_is_A ? J.A : J.B;
@@ -892,7 +888,7 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
   ProbeDesc D;
   D.job = j;
   D.pad = 0;
-  if (fast) fast[t] = bm_tile(jobs, J, tile0 + t, tile_base[j], t);
+  if (fast) fast[t] = bm_tile(J, tile0 + t, tile_base[j], t);
   if (Lg.bm) {  // bitmap probe: no range needed
     D.lo = D.hi = 0;
     pdesc[t] = D;
@@ -932,14 +928,12 @@ __global__ void k_probe_part(const JoinQ* __restrict__ jobs, const int64_t* __re
 // index and pair slot).  SIMPLE (a BmFast tile, built by k_probe_part: no
 // exclusion mark, no distance filter, no chain test, pairs written) reads nothing
 // of the job; otherwise J supplies those.
-__device__ __forceinline__ Rec joined_rec(Rec o, uint64_t b0, uint64_t b1, int mode, int64_t now_ms);
-
 template <int KPT, bool SIMPLE>
 __device__ __forceinline__ int32_t probe_bitmap(const BmFast& T, const JoinQ* Jp, int64_t b,
                                                 uint2* __restrict__ pairs,
                                                 uint32_t* __restrict__ pair_uid, int64_t* __restrict__ tile_src,
                                                 int32_t* __restrict__ tile_cnt, int mark, uint64_t* sScan64,
-                                                int32_t* tile_lvl = nullptr, uint32_t* sF = nullptr) {
+                                                int32_t* tile_lvl = nullptr) {
   // url-id bitmap of the large list: one 16-B load per key (yrwi_bitmap.h) gives
   // membership and, for a hit, its list position (rank + bits below).  BM_TILE
   // small-list ids per tile, KPT per thread, lane-consecutive: key k*256 + tid, so
@@ -1042,40 +1036,6 @@ __device__ __forceinline__ int32_t probe_bitmap(const BmFast& T, const JoinQ* Jp
       for (int x = 0; x < Jp->chain_fill; x++) lv[2 + x] = lv[1];
     }
   }
-  if (SIMPLE && (T.flags & BMF_FUSED)) {  // workgroup-uniform: the finished records, into the tile's slots
-    // The tile's matches go to LDS in key order first (sF: rows in A and B, url
-    // id), then the workgroup gathers and folds them densely, one match per thread
-    // -- each thread's own hits are a few percent of its keys, and a gather
-    // instruction of a few live lanes costs what a full one does.  What k_compact<false>
-    // computes from a pair: the accumulated side's record (a by-test step's larger
-    // side's) and an enumeration's J5 words of B, joined_rec.
-#pragma unroll
-    for (int k = 0; k < KPT; k++) {
-      if (!((hm >> k) & 1u)) continue;
-      const int64_t ik = s0 + k * PROBE_TILE + (int64_t)threadIdx.x;
-      const int32_t lo = base[k] + (int32_t)((ex[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-      sF[lo] = (uint32_t)(small_is_A ? ik : (int64_t)jls[k]);
-      sF[KPT * PROBE_TILE + lo] = (uint32_t)(small_is_A ? (int64_t)jls[k] : ik);
-      sF[2 * KPT * PROBE_TILE + lo] = keys[k];
-    }
-    __syncthreads();
-    const JoinQ& J = *Jp;
-    const int mode = J.mode;
-    const int64_t now_ms = J.now_ms;
-    const uint64_t* rf = mode == JM_TEST_LARGE_B ? J.B.feat : J.A.feat;  // the record side
-    const uint64_t* bf = J.B.j5 ? J.B.j5 : J.B.feat;                     // an enumeration's J5 side
-    const int64_t bw = J.B.j5 ? 2 : FEAT_WORDS;
-    uint64_t* of = J.out_feat;
-    uint32_t* ou = J.out_uid;
-    for (int m = threadIdx.x; m < run; m += PROBE_TILE) {
-      const int64_t ia = sF[m], ib = sF[KPT * PROBE_TILE + m];
-      const Rec A = load_rec(rf, mode == JM_TEST_LARGE_B ? ib : ia);
-      const ulonglong2 Bw = mode == JM_ENUM ? ldg_j5(bf + ib * bw) : make_ulonglong2(0, 0);
-      store_rec(of, s0 + m, joined_rec(A, Bw.x, Bw.y, mode, now_ms));
-      stg(ou + s0 + m, sF[2 * KPT * PROBE_TILE + m]);
-    }
-    return run;
-  }
   const bool write = SIMPLE || !Jp->count_only;  // workgroup-uniform
 #pragma unroll
   for (int k = 0; k < KPT; k++) {
@@ -1122,10 +1082,8 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   if (!MARK && fast) {
     const BmFast F = fast[p];
     if (F.flags & BMF_SIMPLE) {
-      // (a fused tile's matches are staged in sL, the range probe's LDS: 3 x BM_TILE words)
-      static_assert(PROBE_LDS >= 3 * BM_TILE, "fused tile staging");
-      probe_bitmap<BM_TILE / PROBE_TILE, true>(F, jobs + F.job, tile0 + F.t, pairs, pair_uid, tile_src, tile_cnt, 0,
-                                               sScan64, nullptr, reinterpret_cast<uint32_t*>(sL));
+      probe_bitmap<BM_TILE / PROBE_TILE, true>(F, nullptr, tile0 + F.t, pairs, pair_uid, tile_src, tile_cnt, 0,
+                                               sScan64);
       return;
     }
     t = F.t;
@@ -1166,7 +1124,7 @@ __global__ __launch_bounds__(PROBE_TILE) void k_probe(const JoinQ* __restrict__ 
   if (Lg.bm) {
     // a launch without long tiles does not carry the KPT_LARGE code (its registers
     // cost C2 a wave per SIMD: k_probe 111 -> 119 us)
-    const BmFast T = bm_tile(jobs, J, b, tile_base[D.job], -1);
+    const BmFast T = bm_tile(J, b, tile_base[D.job], -1);
     if (LONG && J.ptile == KPT_LARGE * PROBE_TILE) {
       // (a job whose probe tests a chain list itself has BM_TILE tiles: layout_jobs)
       probe_bitmap<KPT_LARGE, false>(T, &J, b, pairs, pair_uid, tile_src, tile_cnt, mark, sScan64);
@@ -1276,10 +1234,6 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const JoinQ* __restrict__ jo
     int32_t tot;
     int32_t ex = block_excl_sum256(c, sScan, &tot);
     if (t < J.ntiles) tile_off[base + t] = running + ex;
-    if (J.ctile && c > 0) {  // a fused job's chunks: the tile holding each chunk's first element
-      const int64_t off = running + ex;
-      for (int64_t k = (off + CHUNK - 1) / CHUNK; k * CHUNK < off + c; k++) J.ctile[k] = (int32_t)t;
-    }
     running += tot;
   }
   if (threadIdx.x == 0 && J.m_out) *J.m_out = running;
@@ -1928,9 +1882,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
         j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
       }
       c = tile_cnt[t];
-      // a count-first fold's counted join: nothing to compact; a fused job's probe
-      // wrote its records itself
-      if (c && (jobs[j].count_only || jobs[j].fused)) c = 0;
+      if (c && jobs[j].count_only) c = 0;  // a count-first fold's counted join: nothing to compact
       if (c) {
         const JoinQ& J = jobs[j];
         CompactJob& X = sJ[threadIdx.x];
@@ -2195,78 +2147,6 @@ __device__ __forceinline__ uint32_t hp_bucket(uint32_t hid, int32_t nb) {
 // from the url keys, C2 k_score 94 -> 115 us -- the headline pays for it; and a
 // separate per-chunk kernel counting in LDS first, k_hostcount: 107 + 18 us, its
 // distinct (chunk, host) pairs still cost a device atomic each.)
-// ---- gapped containers (RankQ::toff: a fused probe's last step, JoinQ::fused)
-// the slot of element e: the first tile whose end passes e (a binary search over
-// the tile table -- the rare sequential paths; chunks take gap_map)
-__device__ int64_t gap_slot(const RankQ& Q, int64_t e) {
-  int64_t lo = 0, hi = Q.ntiles - 1;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (ldg(Q.toff + mid) + ldg(Q.tcnt + mid) > e) hi = mid; else lo = mid + 1;
-  }
-  return lo * Q.ptile + (e - ldg(Q.toff + lo));
-}
-
-// sMap[i] = the slot of element c * CHUNK + i, for the chunk's elements (i <
-// min(CHUNK, n - c * CHUNK)).  The tiles overlapping the chunk (from ctile[c], in
-// order, CHUNK_THREADS at a time) mark their first element in it with slot - i;
-// every element then takes the mark at or before it: a block-wide "last mark"
-// scan, each thread over its CHUNK_IPT consecutive elements.  The whole block
-// calls it; it ends with a barrier.  sW: 4 ints.
-__device__ void gap_map(const RankQ& Q, int64_t c, int32_t* sMap, int32_t* sW) {
-  constexpr int32_t NONE = INT32_MIN;  // (a mark is slot - i >= -CHUNK)
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t e0 = c * CHUNK, e1 = min(e0 + (int64_t)CHUNK, Q.n);
-  for (int i = tid; i < CHUNK; i += CHUNK_THREADS) sMap[i] = NONE;
-  __syncthreads();
-  for (int64_t tb = max(ldg(Q.ctile + c), 0);; tb += CHUNK_THREADS) {
-    const int64_t t = tb + tid;
-    int more = 0;
-    if (t < Q.ntiles) {
-      const int64_t off = ldg(Q.toff + t);
-      if (off < e1) {
-        more = 1;
-        const int32_t cnt = ldg(Q.tcnt + t);
-        if (cnt > 0 && off + cnt > e0) {
-          const int64_t st = off > e0 ? off : e0;
-          sMap[st - e0] = (int32_t)(t * Q.ptile + (st - off) - (st - e0));
-        }
-      }
-    }
-    if (!__syncthreads_or(more)) break;  // (tiles are in container order: the rest start past the chunk)
-  }
-  int32_t v[CHUNK_IPT];
-  int32_t last = NONE;
-#pragma unroll
-  for (int j = 0; j < CHUNK_IPT; j++) {
-    const int32_t m = sMap[tid * CHUNK_IPT + j];
-    if (m != NONE) last = m;
-    v[j] = last;
-  }
-  // the latest mark of the threads before this one (a wave scan, then the waves)
-  int32_t inc = last;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t u = __shfl_up(inc, o, 64);
-    if (lane >= o && inc == NONE) inc = u;
-  }
-  int32_t carry = __shfl_up(inc, 1, 64);
-  if (lane == 0) carry = NONE;
-  if (lane == 63) sW[wv] = inc;
-  __syncthreads();
-  if (carry == NONE)
-    for (int w = wv - 1; w >= 0 && carry == NONE; w--) carry = sW[w];
-  const int64_t span = Q.ntiles * (int64_t)Q.ptile;
-#pragma unroll
-  for (int j = 0; j < CHUNK_IPT; j++) {
-    const int32_t d = v[j] != NONE ? v[j] : carry;
-    // (past the chunk's end: never read; every slot kept inside the container)
-    const int64_t sl = (int64_t)(d == NONE ? 0 : d) + tid * CHUNK_IPT + j;
-    sMap[tid * CHUNK_IPT + j] = (int32_t)(sl < 0 ? 0 : sl < span ? sl : span - 1);
-  }
-  __syncthreads();
-}
-
 __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restrict__ qs,
                                                          const int32_t* __restrict__ chunk_q,
                                                          ChunkSum* __restrict__ out, ShardSum* __restrict__ shard) {
@@ -2280,15 +2160,12 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   __shared__ uint32_t sSegM[SEGC];
   __shared__ uint32_t sSegL[SEGC];
   __shared__ int32_t sFirstInfo[3];
-  __shared__ int32_t sMap[CHUNK];  // a gapped container's slots of this chunk (gap_map)
   extern __shared__ int32_t sHB[];  // authority by partition: the chunk's elements per host bucket (dynamic)
 
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
   const int64_t c = b - Q.chunk_base;
-  const bool gap = Q.toff != nullptr;  // block-uniform
-  if (gap) gap_map(Q, c, sMap, sScan);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int hnb = Q.ecnt ? Q.hp_nb : 0;  // block-uniform
   for (int i = threadIdx.x; i < hnb; i += CHUNK_THREADS) sHB[i] = 0;
@@ -2320,7 +2197,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       for (int u = 0; u < RED_GROUP; u++) {
         const int64_t eu = min(e + (int64_t)u * CHUNK_THREADS, Q.n - 1);
         mk[u] = Q.removed ? ldg(Q.removed + eu) : (uint8_t)0;
-        rg[u] = load_rec(Q.feat, gap ? (int64_t)sMap[eu - c * CHUNK] : eu);
+        rg[u] = load_rec(Q.feat, eu);
       }
 #pragma unroll
       for (int u = 0; u < RED_GROUP; u++) vg[u] = vg[u] & (mk[u] == 0);
@@ -2643,9 +2520,8 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
     bool ok = e < e1 && e > first && !(Q.removed && ldg(Q.removed + e));
     int32_t p = -1, od = 0;
     if (ok) {
-      const int64_t s = Q.toff ? gap_slot(Q, e) : e;
-      p = (int32_t)(ldg(Q.feat + s * FEAT_WORDS) & 0xFFFF);
-      od = (int32_t)((ldg(Q.feat + s * FEAT_WORDS + 1) >> 16) & 0xFF);
+      p = (int32_t)(ldg(Q.feat + e * FEAT_WORDS) & 0xFFFF);
+      od = (int32_t)((ldg(Q.feat + e * FEAT_WORDS + 1) >> 16) & 0xFF);
     }
     if (__all(!ok || p <= L.prun)) {
       const int32_t m = wave_max_i(ok ? od : 0);
@@ -2702,14 +2578,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_scatter(const RankQ* __
                                                                  const int32_t* __restrict__ hoffs,
                                                                  uint2* __restrict__ part) {
   __shared__ int32_t sC[HPART_MAXS];
-  __shared__ int32_t sMap[CHUNK];
-  __shared__ int32_t sW[4];
   const int64_t b = blockIdx.x;
   const RankQ& Q = qs[chunk_q[b]];
   if (!Q.ecnt) return;
   const int64_t c = b - Q.chunk_base;
-  const bool gap = Q.toff != nullptr;  // block-uniform
-  if (gap) gap_map(Q, c, sMap, sW);
   const int nb = Q.hp_nb;
   for (int i = threadIdx.x; i < nb; i += CHUNK_THREADS) sC[i] = hoffs[Q.hp_hoff + (int64_t)i * Q.nchunks + c];
   __syncthreads();
@@ -2717,10 +2589,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hpart_scatter(const RankQ* __
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int64_t e = c * CHUNK + s * CHUNK_THREADS + threadIdx.x;
     if (e < Q.n && !(Q.removed && ldg(Q.removed + e))) {
-      const int64_t sl = gap ? (int64_t)sMap[s * CHUNK_THREADS + threadIdx.x] : e;  // (ecnt is indexed by slot)
-      const uint32_t h = (uint32_t)(ldg(Q.feat + sl * FEAT_WORDS + 3) >> 34);
+      const uint32_t h = (uint32_t)(ldg(Q.feat + e * FEAT_WORDS + 3) >> 34);
       const int32_t pos = atomicAdd(&sC[hp_bucket(h, nb)], 1);
-      part[pos] = make_uint2(h, (uint32_t)sl);
+      part[pos] = make_uint2(h, (uint32_t)e);
     }
   }
 }
@@ -2976,9 +2847,8 @@ __global__ void k_combine(const RankQ* __restrict__ qs, int nq, const ShardSum* 
       bool first = true;
       for (int64_t e = 0; e < Q.n; e++) {
         if (Q.removed && ldg(Q.removed + e)) continue;
-        const int64_t s = Q.toff ? gap_slot(Q, e) : e;
-        int32_t p = (int32_t)(ldg(Q.feat + s * FEAT_WORDS) & 0xFFFF);
-        int32_t od = (int32_t)((ldg(Q.feat + s * FEAT_WORDS + 1) >> 16) & 0xFF);
+        int32_t p = (int32_t)(ldg(Q.feat + e * FEAT_WORDS) & 0xFFFF);
+        int32_t od = (int32_t)((ldg(Q.feat + e * FEAT_WORDS + 1) >> 16) & 0xFF);
         if (first) { fd.P = p; first = false; }
         else fd.piece(p, od, od);
       }
@@ -3480,14 +3350,11 @@ __device__ unsigned long long g_phase[16];
 // s*CHUNK_THREADS + tid (with idx: of element idx[s*CHUNK_THREADS + tid], the
 // first cnt entries of a compacted list), bit s of the result set when that
 // element is live and admitted (and, with a threshold T, its key >= T)
-// smap: a gapped container's slots of the chunk (gap_map), nullptr when compact;
-// every per-element access and the candidate index take the slot.
 template <bool SCORE = true>
 __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState& N, int64_t c, int32_t* flagc,
                                                 uint64_t* a, uint64_t* z, uint64_t T = 0,
                                                 const PruneP* P = nullptr, const CardTab* tab = nullptr,
-                                                const int16_t* idx = nullptr, int32_t cnt = 0,
-                                                const int32_t* smap = nullptr) {
+                                                const int16_t* idx = nullptr, int32_t cnt = 0) {
   const FilterQ* F = Q.filt;
   uint32_t vm = 0;
 #pragma unroll
@@ -3499,11 +3366,9 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
     if (idx) {
       if (i >= cnt) continue;
       e = c * CHUNK + idx[i];
-      if (smap) e = smap[idx[i]];
     } else {
       e = c * CHUNK + i;
       if (e >= Q.n || (Q.removed && ldg(Q.removed + e))) continue;
-      if (smap) e = smap[i];
     }
     const Rec q = load_rec(Q.feat, e);
     uint64_t khi = 0;
@@ -3540,16 +3405,14 @@ __device__ __forceinline__ uint32_t score_elems(const RankQ& Q, const NormState&
 // compacted into idx (chunk-local indices); returns their count.  cardinal
 // then runs on dense waves of survivors instead of on every wave for a few lanes.
 __device__ __forceinline__ int32_t prune_chunk(const RankQ& Q, const NormState& N, int64_t c, uint64_t T,
-                                               const PruneP& P, const CardTab* tab, int16_t* idx, int32_t* sScan,
-                                               const int32_t* smap) {
+                                               const PruneP& P, const CardTab* tab, int16_t* idx, int32_t* sScan) {
   uint32_t keep = 0;
 #pragma unroll
   for (int s = 0; s < CHUNK_IPT; s++) {
     const int i = s * CHUNK_THREADS + (int)threadIdx.x;  // coalesced; the order of idx does not matter
     const int64_t e = c * CHUNK + i;
     if (e >= Q.n || (Q.removed && ldg(Q.removed + e))) continue;
-    const int64_t sl = smap ? (int64_t)smap[i] : e;
-    const ulonglong2 w23 = ldg(reinterpret_cast<const ulonglong2*>(Q.feat + sl * FEAT_WORDS) + 1);
+    const ulonglong2 w23 = ldg(reinterpret_cast<const ulonglong2*>(Q.feat + e * FEAT_WORDS) + 1);
     Rec q;
     q.w[0] = q.w[1] = 0;
     q.w[2] = w23.x;
@@ -3633,7 +3496,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   __shared__ uint64_t sT;
   __shared__ CardTab sCard;
   __shared__ int16_t sIdx[CHUNK];  // prune_chunk's survivors (chunk-local)
-  __shared__ int32_t sMap[CHUNK];  // a gapped container's slots of this chunk (gap_map)
   const int tid = threadIdx.x;
 #ifdef YRWI_PHASE_CLOCK
   if (threadIdx.x == 0 && blockIdx.x < PH_MAXB) g_ts[blockIdx.x * 8] = wall_clock64();
@@ -3656,11 +3518,6 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   if (tid < 32) sFlag[tid] = 0;
   if (tab) copy_card_tab(&sCard, &qtab[qi].T);
   __syncthreads();
-  const int32_t* smap = nullptr;  // block-uniform
-  if (Q.toff) {
-    gap_map(Q, c, sMap, sScan);
-    smap = sMap;
-  }
   const FilterQ* F = Q.filt;
   int32_t* flagc = (F && F->flagcount) ? sFlag : nullptr;
   // strided element map (neighbouring lanes read neighbouring rows); the
@@ -3669,7 +3526,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   uint64_t a[CHUNK_IPT];
   if (kq > SCORE_SMALL) {  // large k (doubledom stacks): only the flag counts here
     if (flagc) {
-      (void)score_elems<false>(Q, N, c, flagc, a, nullptr, 0, nullptr, nullptr, nullptr, 0, smap);
+      (void)score_elems<false>(Q, N, c, flagc, a, nullptr);
       __syncthreads();
       if (tid < 32 && sFlag[tid]) atomicAdd(&F->flagcount[tid], sFlag[tid]);
     }
@@ -3680,9 +3537,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   const uint64_t T0 = sT;
   PHASE(5)
   const bool comp = T0 && P.ok && !F;
-  const int32_t nc = comp ? prune_chunk(Q, N, c, T0, P, tab, sIdx, sScan, smap) : 0;
-  const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, tab, sIdx, nc, smap)
-                           : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, tab, nullptr, 0, smap);
+  const int32_t nc = comp ? prune_chunk(Q, N, c, T0, P, tab, sIdx, sScan) : 0;
+  const uint32_t vm = comp ? score_elems(Q, N, c, flagc, a, nullptr, T0, nullptr, tab, sIdx, nc)
+                           : score_elems(Q, N, c, flagc, a, nullptr, T0, &P, tab);
   int32_t nv;
   int32_t voff = block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);  // (its barriers also order the sFlag atomics)
   PHASE(0)
@@ -3700,8 +3557,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
     for (int s = 0; s < CHUNK_IPT; s++)
       if ((vm >> s) & 1u) {
         const int i = s * CHUNK_THREADS + tid;
-        const int li = comp ? sIdx[i] : i;
-        const int64_t e = smap ? (int64_t)smap[li] : c * CHUNK + li;
+        const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
         const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
         out[voff].k1 = a[s];
         out[voff].k2 = ((uint64_t)(h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
@@ -3725,8 +3581,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score(const RankQ* __restrict
   for (int s = 0; s < CHUNK_IPT; s++)
     if (((vm >> s) & 1u) && a[s] >= T) {
       const int i = s * CHUNK_THREADS + tid;
-      const int li = comp ? sIdx[i] : i;
-      const int64_t e = smap ? (int64_t)smap[li] : c * CHUNK + li;
+      const int64_t e = c * CHUNK + (comp ? sIdx[i] : i);
       const uint32_t h = (uint32_t)ldg(Q.feat + e * FEAT_WORDS + 3);  // ByteArray.hashCode (ByteArray.java:80-84)
       s1[off] = a[s];
       s2[off] = ((uint64_t)((uint32_t)h ^ 0x80000000u) << 32) | (uint64_t)(~((uint32_t)e | Q.idx_tag));
@@ -3774,13 +3629,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_score_full(const RankQ* __res
     build_card_tab(&sCard, N, Q);
     __syncthreads();
     const int64_t c = b - Q.chunk_base;
-    const int32_t* smap = nullptr;  // block-uniform
-    if (Q.toff) {  // (s1 is free until the selection below: its first 8 KB hold the chunk's slots)
-      gap_map(Q, c, reinterpret_cast<int32_t*>(s1), sScan);
-      smap = reinterpret_cast<const int32_t*>(s1);
-    }
     uint64_t a[CHUNK_IPT], z[CHUNK_IPT];
-    const uint32_t vm = score_elems(Q, N, c, nullptr, a, z, 0, nullptr, &sCard, nullptr, 0, smap);  // flags: k_score
+    const uint32_t vm = score_elems(Q, N, c, nullptr, a, z, 0, nullptr, &sCard);  // flags were counted by k_score
     const int32_t kq = Q.k < kc ? Q.k : kc;
     int32_t nv;
     (void)block_excl_sum<CHUNK_THREADS>(__popc(vm), sScan, &nv);
@@ -4311,12 +4161,11 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
                      ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups, BmFast* d_fast,
-                     BmFast* d_fast_perm, bool compact) {
+                     BmFast* d_fast_perm) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
-  // (no compaction: no compaction order -- a chained step compacts later, in it)
-  int2* perm = bo.key && bo.tile_job && !mark && (compact || chain) ? bo.perm : nullptr;
+  int2* perm = bo.key && bo.tile_job && !mark ? bo.perm : nullptr;
   int2* pperm = bo.pkey && bo.tile_job && probe_tiles > 1 ? bo.pperm : nullptr;
   uint32_t* tkey = perm ? bo.key : nullptr;
   uint32_t* pkey = pperm ? bo.pkey : nullptr;
@@ -4392,8 +4241,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     }
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)njobs), dim3(256), 0, S(st), d_jobs, d_tile_base, d_tile_cnt,
                        d_tile_off, (const int32_t*)(chain ? d_tile_lvl : nullptr));
-    if (!chain && compact) {  // chained steps compact once the fold's dispatch modes are known (launch_compact);
-                              // a step whose every job is fused or counted has nothing to compact
+    if (!chain) {  // chained steps compact once the fold's dispatch modes are known (launch_compact)
       if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       if (int r = launch_compact(d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
                                  d_tile_off, bo, false, st))
