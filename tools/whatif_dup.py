@@ -41,7 +41,15 @@ VARIANTS["topq"] = [(K, TOPQ, 2)]
 
 # variants that change code rather than duplicate a launch: (file, old, new) edits
 H = "yrwi_host.cpp"
+def _compact_lds(kb):  # k_compact with kb KiB of unused dynamic LDS: fewer resident workgroups per CU
+    return [(K, "hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),",
+             "hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), %d, S(st)," % (kb * 1024))]
+
+
 EDITS = {
+    "clds26": _compact_lds(26),
+    "clds32": _compact_lds(32),
+    "clds40": _compact_lds(40),
     # k_emit into a device buffer, then DMA copies to the pinned destination
     "emitdma": [
         (H, "  uint8_t* land = nullptr;\n  {\n    void* hp = h_hits;",
