@@ -66,6 +66,13 @@ EDITS = {
 }
 
 
+# variants that only change a compile-time constant (make EXTRA=...)
+FLAGS = {
+    "bm512": "-DYRWI_BM_TILE=512",
+    "bm256": "-DYRWI_BM_TILE=256",
+}
+
+
 def build(name):
     tmp = f"/tmp/whatif_{name}"
     shutil.rmtree(tmp, ignore_errors=True)
@@ -86,11 +93,11 @@ def build(name):
         open(p, "w").write(s.replace(old, new))
     out = os.path.join(ROOT, "gpurun_var", f"libyrwi_dup_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    subprocess.check_call(["make", "-s", "-j8", "-C", src, f"OUT={out}",
-                           f"OBJ={tmp}/obj", out])
+    subprocess.check_call(["make", "-s", "-j8", "-C", src, f"OUT={out}", f"OBJ={tmp}/obj",
+                           "EXTRA=" + FLAGS.get(name, ""), out])
     print("built", out)
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(VARIANTS) + list(EDITS):
+    for n in sys.argv[1:] or list(VARIANTS) + list(EDITS) + list(FLAGS):
         build(n)
