@@ -373,6 +373,59 @@ def _keyed_rows(keys, seed):
     return rows
 
 
+@pytest.mark.parametrize("chain", ["1", "0"], ids=["chained", "stepwise"])
+@pytest.mark.parametrize("algo", ["probe", "merge"])
+def test_compaction_pieces(algo, chain, monkeypatch):
+    """The normalisation pieces the compaction writes (k_compact_sum, one per tile)
+    in place of k_reduce's chunk summaries: 2- and 3-term joins whose posintext
+    rises along the url order (a tile's records overflow its SEGC segments and
+    k_shard_fin rewalks the tile's run), runs of posintext 0, empty tiles; probe
+    and merge tiles, chained and stepwise folds; profiles without authority beside
+    queries with exclusions or authority (k_reduce's path) in one batch."""
+    monkeypatch.setenv("YRWI_PROBE_RATIO", "1" if algo == "probe" else "1000000000")
+    monkeypatch.setenv("YRWI_NO_CHAIN", "1" if chain == "0" else "0")
+    rng = np.random.default_rng(17)
+    n = 20000
+    keys = np.arange(n)
+
+    def rows_for(sel, seed, mode):
+        r = _keyed_rows(keys[sel], seed)
+        m = len(r)
+        if mode == "rise":
+            p = np.minimum(65535, np.arange(1, m + 1) * 3)
+        elif mode == "noisy":
+            p = np.minimum(65535, np.arange(m) // 8 + rng.integers(0, 200, m))
+            p[(np.arange(m) // 300) % 5 == 2] = 0
+        else:
+            p = rng.integers(0, 3000, m)
+        r[:, 34] = (p >> 8) & 0xFF
+        r[:, 35] = p & 0xFF
+        r[:, 38] = rng.integers(0, 256, m) * (rng.random(m) < 0.5)
+        return r
+
+    d = {
+        b"TERMpcA_____": rows_for(np.ones(n, bool), 1, "rise"),
+        b"TERMpcB_____": rows_for(rng.random(n) < 0.6, 2, "noisy"),
+        b"TERMpcC_____": rows_for(rng.random(n) < 0.3, 3, "rand"),
+        b"TERMpcD_____": rows_for(rng.random(n) < 0.05, 4, "rise"),
+        b"TERMpcE_____": rows_for(rng.random(n) < 0.5, 5, "rand"),
+    }
+    A, B, C, D, E = list(d)
+    ix = RWIIndex(0)
+    try:
+        for h, r in d.items():
+            ix.add(h, r)
+        qs = [([A, B], []), ([B, A], []), ([A, C], []), ([B, D], []), ([A, B, C], []), ([A, C, D], []),
+              ([A, B], [E]), ([A, B, C], [E]), ([D, E], [])]
+        for pname, prof in _profiles():
+            batch = [Query(inc, exc, k=100, profile=_rp(prof), now_ms=NOW) for inc, exc in qs]
+            for qi, (q, g) in enumerate(zip(batch, ix.search_batch(batch))):
+                exp = orc.search(d, q.include, q.exclude, orc.profile_from(prof), "en", now_ms=NOW, k=100)
+                assert [(h.urlhash, h.score, h.tiebreak) for h in g] == exp, (pname, qi)
+    finally:
+        ix.close()
+
+
 @pytest.mark.parametrize("nab", [(2048, 2048), (2047, 2050), (4095, 4097), (6000, 6289), (12288, 1)])
 def test_merge_tile_boundaries(nab, monkeypatch):
     """Merge-path tiles (forced) over lists whose combined length sits on and

@@ -66,6 +66,47 @@ EDITS = {
 }
 
 
+# k_compact also accumulating k_reduce's order-independent summary of the records
+# it writes (packed min / max, tf fractions, pmax, count) plus a wave prefix max of
+# posintext per pass, reduced per wave into a sink: what fusing the normalisation
+# summary into the compaction would add to k_compact (results unchanged)
+_CS_HELP = (K, "template <bool CHAIN>\n__global__ __launch_bounds__(256) void k_compact(",
+            "typedef unsigned short wi_u16x2 __attribute__((ext_vector_type(2)));\n"
+            "__device__ __forceinline__ uint32_t wi_min16(uint32_t a, uint32_t b) { return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(wi_u16x2, a), __builtin_bit_cast(wi_u16x2, b))); }\n"
+            "__device__ __forceinline__ uint32_t wi_max16(uint32_t a, uint32_t b) { return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(wi_u16x2, a), __builtin_bit_cast(wi_u16x2, b))); }\n"
+            "__device__ uint32_t g_wi_sink[1024];\n"
+            "template <bool CHAIN>\n__global__ __launch_bounds__(256) void k_compact(")
+_CS_INIT = (K, "  const int32_t total = sPre[COMPACT_TILES];\n  for (int m0 = threadIdx.x; m0 < total; m0 += COMPACT_UNROLL * 256) {",
+            "  const int32_t total = sPre[COMPACT_TILES];\n"
+            "  constexpr int WNP = (NF + 1) / 2;\n  uint32_t wmn[WNP], wmx[WNP];\n"
+            "  for (int j = 0; j < WNP; j++) { wmn[j] = 0xFFFFFFFFu; wmx[j] = 0u; }\n"
+            "  int32_t wpmax = -1, wnval = 0, wtcn = -1, wtdn = 1, wtcx = -1, wtdx = 1, wlastp = -1;\n  uint32_t wacc = 0;\n"
+            "  for (int m0 = threadIdx.x; m0 < total; m0 += COMPACT_UNROLL * 256) {")
+_CS_ACC = (K, "      store_rec(X.ofeat, o, (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms));\n"
+              "      stg(X.ouid + o, uid[u]);\n    }\n  }\n}\n",
+              "      const Rec R = (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms);\n"
+              "      store_rec(X.ofeat, o, R);\n      stg(X.ouid + o, uid[u]);\n"
+              "      const Feat F = decode_rec(R);\n"
+              "      for (int j = 0; j < WNP; j++) {\n"
+              "        const uint32_t w = (uint32_t)F.f[2 * j] | (2 * j + 1 < NF ? (uint32_t)F.f[2 * j + 1] << 16 : 0u);\n"
+              "        wmn[j] = wi_min16(wmn[j], w); wmx[j] = wi_max16(wmx[j], w);\n      }\n"
+              "      const int32_t tc = F.f[F_HITCOUNT], td = F.f[F_WORDSINTEXT] + F.f[F_WORDSINTITLE] + 1;\n"
+              "      if (wtcn < 0 || tc * wtdn < wtcn * td) { wtcn = tc; wtdn = td; }\n"
+              "      if (wtcx < 0 || wtcx * td < tc * wtdx) { wtcx = tc; wtdx = td; }\n"
+              "      wpmax = max(wpmax, F.p); wnval++; wlastp = F.p;\n"
+              "    }\n"
+              "    int32_t pm = wlastp;\n"
+              "    for (int o2 = 1; o2 < 64; o2 <<= 1) { const int32_t y = __shfl_up(pm, o2, 64); if ((threadIdx.x & 63) >= o2) pm = max(pm, y); }\n"
+              "    wacc += (uint32_t)(pm > wlastp);\n"
+              "  }\n"
+              "  uint32_t h = wacc ^ (uint32_t)wpmax ^ (uint32_t)wnval ^ (uint32_t)(wtcn * 7 + wtdn * 3 + wtcx * 5 + wtdx);\n"
+              "  for (int j = 0; j < WNP; j++) h ^= wmn[j] * 31u + wmx[j];\n"
+              "  for (int o2 = 32; o2 > 0; o2 >>= 1) h ^= (uint32_t)__shfl_xor((int)h, o2, 64);\n"
+              "  if ((threadIdx.x & 63) == 0 && h == 0x12345678u) g_wi_sink[blockIdx.x & 1023] = h;\n"
+              "}\n")
+EDITS["csum"] = [_CS_HELP, _CS_INIT, _CS_ACC]
+
+
 # variants that only change a compile-time constant (make EXTRA=...)
 FLAGS = {
     "bm512": "-DYRWI_BM_TILE=512",

@@ -1034,6 +1034,7 @@ struct PendingCompact {
   int32_t* d_cnt = nullptr;
   int64_t* d_off = nullptr;
   BandOrder bo;
+  bool sum = false;  // some job writes normalisation pieces (k_compact_sum)
   std::vector<std::array<int64_t, CHAIN_LVL>> level;  // per job (layout order): k_chain's level counts
 };
 
@@ -1097,6 +1098,16 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   if (!d_jobs || !d_tb || !d_split || !d_pdesc || !d_fast || !d_fast_perm || !d_pairs || !d_puid || !d_src ||
       !d_cnt || !d_off)
     return ctx->fail(YRWI_E_NOMEM, "arena");
+  // the queries' last steps that summarise their containers as they compact them:
+  // one ChunkSum per tile of the step, the job's run from its first tile
+  bool sum = false;
+  for (const JoinQ& J : jobs) sum |= J.want_sum != 0;
+  if (sum) {
+    ChunkSum* d_psum = arena_alloc<ChunkSum>(ctx, tiles);
+    if (!d_psum) return ctx->fail(YRWI_E_NOMEM, "arena");
+    for (int j = 0; j < nj; j++)
+      if (jobs[(size_t)j].want_sum) jobs[(size_t)j].psum = d_psum + tile_base[(size_t)j];
+  }
   // chained jobs: their ChainQ (level counts into the landing buffer, the later
   // include lists' rows in slot-indexed arrays beside the pairs), per-tile level
   // counts and the list ranges of k_chain_part
@@ -1157,7 +1168,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
   const BandOrder bo = band_order(ctx, tiles, merge_tiles, true);
   if (launch_join_step(d_jobs, d_tb, nj, nmerge, merge_tiles, tiles, d_split, d_pdesc, d_pairs, d_puid, d_src, d_cnt, d_off,
                        false, long_tiles, bo, ctx->stream, e0, em, e1, c0, c1, chain, d_lvl, d_crange, d_cgrp,
-                       (int64_t)cgrp.size(), d_fast, d_fast_perm))
+                       (int64_t)cgrp.size(), d_fast, d_fast_perm, sum))
     return ctx->fail(YRWI_E_HIP, "join launch");
   if (tm) {
     tm->kjoin.push_back({e0, em, e1});
@@ -1216,6 +1227,8 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
     P.cont = DList{nullptr, nullptr, nullptr, mh[(size_t)j], J.out_uid, J.out_feat, nullptr, J.out_tup,
                    J.out_tup ? J.out_tw : 0};
+    P.pieces = J.psum;
+    P.npieces = J.psum ? J.ntiles : 0;
   }
   if (chain && pend) {
     pend->active = true;
@@ -1229,6 +1242,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     pend->d_cnt = d_cnt;
     pend->d_off = d_off;
     pend->bo = bo;
+    pend->sum = sum;
     pend->level.assign((size_t)nj, {0, 0, 0, 0, 0});
     const int64_t* hl = reinterpret_cast<const int64_t*>(land) + nj;
     for (int j = 0; j < nj; j++)
@@ -1466,6 +1480,9 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
       } else {
         J.out_feat = P.chain ? nullptr : arena_alloc<uint64_t>(ctx, cap * FEAT_WORDS);
         if (!J.out_feat && !P.chain) return ctx->fail(YRWI_E_NOMEM, "arena");
+        // the container the rank phase reads: summarised by the compaction unless
+        // exclusion marks (run_exclusion, after this) or host counts need a pass over it
+        J.want_sum = last && P.excl.empty() && P.prof.coeff_authority <= 12 ? 1 : 0;
         if (P.chain) {
           chain_q.push_back((int)qi);
         } else if (J.A.tup) {
@@ -1565,7 +1582,7 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         hipEvent_t c0 = tm ? ctx->event() : nullptr, c1 = tm ? ctx->event() : nullptr;
         if (c0) hipEventRecord(c0, ctx->stream);
         if (launch_compact(pend.d_jobs, pend.d_tb, pend.nj, pend.tiles, pend.d_pairs, pend.d_puid, pend.d_src,
-                           pend.d_cnt, pend.d_off, pend.bo, true, ctx->stream))
+                           pend.d_cnt, pend.d_off, pend.bo, true, ctx->stream, pend.sum))
           return ctx->fail(YRWI_E_HIP, "compact launch");
         if (c1) {
           hipEventRecord(c1, ctx->stream);
@@ -1696,6 +1713,9 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     R.dklo = ctx->dklo;
     R.removed = P.removed;
     R.n = P.empty ? 0 : P.cont.n;
+    R.pieces = P.empty || P.removed ? nullptr : P.pieces;
+    R.npieces = R.pieces ? P.npieces : 0;
+    R.ngroups = ceil_div(R.npieces, 64);
     R.nchunks = ceil_div(R.n, CHUNK);
     R.chunk_base = chunks;
     chunk_base[(size_t)qi] = chunks;
@@ -1862,11 +1882,31 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     for (int64_t c = 0; c < rq[(size_t)qi].nchunks; c++) chunk_q[(size_t)(chunk_base[(size_t)qi] + c)] = qi;
   int32_t* d_cq = arena_alloc<int32_t>(ctx, chunks);
   if (!d_cq) return ctx->fail(YRWI_E_NOMEM, "arena");
+  // groups of the compaction's pieces (k_piece_merge): (query, group) of each
+  std::vector<int2> group_q;
+  for (int qi = 0; qi < nq; qi++)
+    for (int64_t g = 0; g < rq[(size_t)qi].ngroups; g++) group_q.push_back(make_int2(qi, (int32_t)g));
+  int2* d_gq = nullptr;
+  if (!group_q.empty()) {
+    ChunkSum* d_groups = arena_alloc<ChunkSum>(ctx, (int64_t)group_q.size());
+    d_gq = arena_alloc<int2>(ctx, (int64_t)group_q.size());
+    if (!d_groups || !d_gq) return ctx->fail(YRWI_E_NOMEM, "arena");
+    int64_t gb = 0;
+    for (int qi = 0; qi < nq; qi++) {
+      RankQ& R = rq[(size_t)qi];
+      R.groups = R.ngroups ? d_groups + gb : nullptr;
+      gb += R.ngroups;
+    }
+    if (upload(ctx, d_gq, group_q)) return YRWI_E_HIP;
+  }
   if (upload(ctx, d_q, rq, d_cb, chunk_base, d_cq, chunk_q)) return YRWI_E_HIP;
   HIPCHK(ctx, hipMemsetAsync(d_ss, 0, sizeof(ShardSum) * nq, ctx->stream));
   hipEvent_t sp = span_open(ctx, tm);
   hipEvent_t rmid = tm ? ctx->event() : nullptr;  // after k_reduce, before k_shard_fin
-  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid, hp_buckets > 0))
+  bool reduce = false;  // a query without the compaction's pieces
+  for (int qi = 0; qi < nq; qi++) reduce |= !rq[(size_t)qi].pieces && rq[(size_t)qi].nchunks > 0;
+  if (launch_reduce(d_q, d_cb, d_cq, nq, chunks, d_cs, d_ss, ctx->stream, rmid, hp_buckets > 0, reduce, d_gq,
+                    (int64_t)group_q.size()))
     return ctx->fail(YRWI_E_HIP, "reduce launch");
   if (hp_buckets > 0 &&
       launch_host_part(d_q, d_cq, chunks, d_hist, d_hoffs, hp_hist, d_hptmp, hp_tmp, d_part, d_bq,
@@ -1878,7 +1918,7 @@ static int run_rank_phase(Lane* ctx, std::vector<Plan>& plans, int32_t kmax, yrw
     st->n_rank_passes++;
     for (int qi = 0; qi < nq; qi++) {
       const int64_t n = rq[(size_t)qi].n;
-      st->bytes_reduce += (int64_t)FEAT_BYTES * n + (rq[(size_t)qi].removed ? n : 0);
+      if (!rq[(size_t)qi].pieces) st->bytes_reduce += (int64_t)FEAT_BYTES * n + (rq[(size_t)qi].removed ? n : 0);
       st->bytes_score += (int64_t)FEAT_BYTES * n + (rq[(size_t)qi].removed ? n : 0);
     }
   }

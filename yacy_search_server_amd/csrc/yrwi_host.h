@@ -192,6 +192,10 @@ struct Plan {
   bool cf3 = false;
   int64_t cf_count2 = 0;
   uint8_t* removed = nullptr;
+  // normalisation pieces the last step's compaction wrote (JoinQ::psum): the rank
+  // phase folds them instead of reading the container back (k_reduce), or nullptr
+  const ChunkSum* pieces = nullptr;
+  int64_t npieces = 0;
   int nexcl_g = 0;      // exclusion terms in effect (J1 on global sizes; excl holds this shard's lists of them)
   bool chain = false;   // chained fold (ChainQ, yrwi_internal.h): one join step, k_chain does the rest
   int seq_term[YRWI_MAX_TERMS] = {0};  // include term (linc index) of every seq list

@@ -153,6 +153,7 @@ struct ChainQ {
                              // 2 (from list 3): pairs (row in list 3, row in list 0), tup[0] list 1, tup[1] list 2
 };
 
+struct ChunkSum;
 struct JoinQ {
   DList A, B;
   int64_t tile_base;   // first global tile of this job
@@ -188,6 +189,12 @@ struct JoinQ {
   int32_t count_only;  // count the matches (tile_cnt, m_out) and write nothing: a count-first fold's list 0 x 1
   int64_t bm_words;    // JA_BMAND: 16-B bitmap units of the url-id space (bm_units)
   const uint64_t* bm3; // JA_BMAND: a third list's bitmap in the AND (count-first from list 3), or nullptr
+  // the query's last step, when the rank phase can take its normalisation pieces
+  // from the compaction (no exclusion marks, no authority counts): one ChunkSum per
+  // tile of the job (index tile - tile_base), written by k_compact_sum
+  ChunkSum* psum;
+  int32_t want_sum;    // host: allocate psum (run_join_jobs)
+  int32_t pad_sum;
 };
 
 // One merge-path tile of a JA_MERGE job (written by k_partition): the tile's A
@@ -230,6 +237,7 @@ static_assert(sizeof(BmFast) == 64, "one 64-B scalar load");
 struct ChunkSum {
   int32_t nvalid;
   int32_t first;        // container index of the first valid element, -1 if none
+  int32_t end;          // container index past the summary's last element
   int32_t p_first, od_first, a_first;
   int32_t pmax;         // max posintext over valid elements
   int32_t M_rest, L_rest;  // max / last positive stored distance over the rest
@@ -317,6 +325,13 @@ struct RankQ {
   int32_t* ecnt;           // ... and every element's host count (nullptr: the host tables serve)
   int64_t hp_hoff;         // ... its first histogram entry (bucket-major: hp_hoff + bucket * nchunks + chunk)
   int32_t* hp_hist;        // ... the histogram (k_reduce counts every chunk's buckets into it)
+  // normalisation pieces written by the compaction (JoinQ::psum), in container
+  // order, or nullptr: k_reduce skips the query; k_piece_merge merges them 64 at a
+  // time into groups, which k_shard_fin folds instead of chunk summaries
+  const ChunkSum* pieces;
+  int64_t npieces;
+  ChunkSum* groups;
+  int64_t ngroups;
 };
 
 struct Cand {  // top-k candidate: sort descending on (k1, k2)
@@ -408,17 +423,24 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
                      bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
                      const int2* d_cgrp = nullptr, int64_t ngroups = 0, BmFast* d_fast = nullptr,
-                     BmFast* d_fast_perm = nullptr);
+                     BmFast* d_fast_perm = nullptr, bool sum = false);
+// sum: some job of the step has normalisation pieces (JoinQ::psum): k_compact_sum
+// (one wave per tile) compacts the whole step instead of k_compact
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
-                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream);
+                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream,
+                   bool sum = false);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 // hp_any: some query of the launch counts host buckets (RankQ::ecnt): k_reduce
 // then takes HPART_MAXS ints of dynamic LDS for them (the others launch without)
+// reduce: some query of the launch has no normalisation pieces (RankQ::pieces) --
+// without one k_reduce is not launched
+// group_q / ngroups: (query, group) of every group of merged pieces (k_piece_merge)
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr, bool hp_any = false);
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* stream, void* ev_mid = nullptr, bool hp_any = false,
+                  bool reduce = true, const int2* d_group_q = nullptr, int64_t ngroups = 0);
 // authority host counts by partition (RankQ::ecnt): histogram per (query bucket, chunk) -> scan ->
 // scatter (host id, element) -> per-bucket LDS counts, every element's count, maxdomcount
 int launch_host_part(const RankQ* d_q, const int32_t* d_chunk_q, int64_t total_chunks, int32_t* d_hist,

@@ -2165,6 +2165,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
   const int64_t b = blockIdx.x;
   const int qi = chunk_q[b];
   const RankQ& Q = qs[qi];
+  if (Q.pieces) return;  // the compaction summarised this query (k_compact_sum)
   const int64_t c = b - Q.chunk_base;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int hnb = Q.ecnt ? Q.hp_nb : 0;  // block-uniform
@@ -2454,6 +2455,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       SS.tf_mx = S.tf_mx;
     }
   } else if (t == 2 * NP2 + 2) {
+    S.end = (int32_t)min((int64_t)(c + 1) * CHUNK, Q.n);
     if (firstIdx != BIG) {
       S.first = (int32_t)(c * CHUNK + firstIdx);
       S.p_first = sFirstInfo[0];
@@ -2475,6 +2477,277 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
       S.seg[i] = (sSegP[i] << 16) | ((sSegM[i] & 0xFFu) << 8) | (sSegL[i] & 0xFFu);
       if (one && nvb) SS.seg[i] = S.seg[i];
     }
+  }
+}
+
+// ---------------------------------------------- compaction with summary pieces
+// k_compact for a step with normalisation pieces (JoinQ::psum): one wave per tile,
+// the tile's matches in container order, 64 x COMPACT_UNROLL at a time, the same
+// records and url ids as k_compact.  For a job with psum the wave also writes the
+// tile's ChunkSum -- what k_reduce computes for a chunk (ReferenceOrder
+// NormalizeWorker :163-210, see k_reduce), here over the tile's run of the container
+// [tile_off, tile_off + cnt), every element of it valid -- from the records it has
+// in registers, so the rank phase does not read the container back for it
+// (k_shard_fin folds the pieces in tile order).  The summary's arithmetic runs
+// while the wave waits for its next gathers.
+template <bool CHAIN>
+__global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jobs,
+                                                    const int64_t* __restrict__ tile_base, int njobs, int64_t ntiles,
+                                                    const uint2* __restrict__ pairs,
+                                                    const uint32_t* __restrict__ pair_uid,
+                                                    const int64_t* __restrict__ tile_src,
+                                                    const int32_t* __restrict__ tile_cnt,
+                                                    const int64_t* __restrict__ tile_off, const int2* __restrict__ perm,
+                                                    const int32_t* __restrict__ tile_job) {
+  const int lane = threadIdx.x;
+  // band order (k_order_hist / k_order_scatter): this wave's tile is position p of the sorted order
+  const int64_t p = perm ? xcd_slice(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (p >= ntiles) return;
+  int64_t t = p;
+  int j;
+  if (perm) {
+    const int2 tj = perm[p];
+    t = tj.x;
+    j = tj.y;
+  } else {
+    j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
+  }
+  const JoinQ& J = jobs[j];
+  if (J.count_only) return;  // a count-first fold's counted join: nothing to compact
+  const int32_t cnt = tile_cnt[t];
+  const int64_t off = tile_off[t];
+  ChunkSum* __restrict__ S = J.psum ? J.psum + (t - tile_base[j]) : nullptr;
+  if (cnt == 0) {
+    if (S && lane == 0) {
+      S->nvalid = 0;
+      S->first = -1;
+      S->end = (int32_t)off;
+      S->nseg = 0;
+      S->overflow = 0;
+    }
+    return;
+  }
+  CompactJob X;
+  X.af = J.A.feat;
+  X.bf = J.mode == JM_ENUM && J.B.j5 ? J.B.j5 : J.B.feat;
+  X.bw = J.mode == JM_ENUM && J.B.j5 ? 2 : FEAT_WORDS;
+  X.ofeat = J.out_feat;
+  X.ouid = J.out_uid;
+  X.now_ms = J.now_ms;
+  X.off = off;
+  X.src = tile_src[t];
+  X.mode = J.mode;
+  X.atw = J.A.tup ? J.A.tw : 0;
+  X.atup = J.A.tup;
+  X.otup = J.out_tup;
+  X.otw = J.out_tup ? J.out_tw : 0;
+  X.fold = J.fold;
+  X.ctw = 0;
+  X.cperm = 0;
+  X.ctup0 = X.ctup1 = nullptr;
+  if (CHAIN && J.chain) {
+    const int ni = ldg(&J.chain->npos);
+    X.ctw = 2 + ni;
+    X.cperm = ldg(&J.chain->perm);
+    X.ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
+    X.ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
+  }
+  // summary state: order-independent parts per lane, the ordered fold wave-uniform
+  uint32_t pmn[NP2], pmx[NP2];  // fields 2j | 2j+1 << 16
+#pragma unroll
+  for (int k = 0; k < NP2; k++) { pmn[k] = 0xFFFFFFFFu; pmx[k] = 0u; }
+  int32_t pmax = -1, tcn = -1, tdn = 1, tcx = -1, tdx = 1, vamn = BIG, vamx = -1;
+  int32_t mrest = 0, lkey = 0;  // over the rest: max stored distance, (position + 1) << 8 | last positive one
+  int32_t pf = 0, of = 0, af = 0;  // the tile's first element (lane 0)
+  int32_t prun = -1, nseg = 0, segP = 0, segM = 0, segK = 0;  // prefix max of the rest; the open segment
+  for (int32_t m0 = 0; m0 < cnt; m0 += COMPACT_UNROLL * 64) {
+    int64_t pi[COMPACT_UNROLL];
+    uint2 pr[COMPACT_UNROLL];
+    uint32_t uid[COMPACT_UNROLL];
+    bool ok[COMPACT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      const int32_t m = m0 + u * 64 + lane;
+      ok[u] = m < cnt;
+      if (ok[u]) {
+        pi[u] = X.src + m;
+        pr[u] = pairs[pi[u]];
+        uid[u] = pair_uid[pi[u]];
+      }
+    }
+    if (X.otw) {  // deferred rows: the joined row's sources (no summary: not a last step)
+#pragma unroll
+      for (int u = 0; u < COMPACT_UNROLL; u++) {
+        if (!ok[u]) continue;
+        const int64_t o = X.off + m0 + u * 64 + lane;
+        int32_t* dst = X.otup + o * X.otw;
+        if (X.atw) {
+          const int32_t* srcr = X.atup + (int64_t)pr[u].x * X.atw;
+          for (int k = 0; k < X.atw; k++) stg(dst + k, ldg(srcr + k));
+        } else {
+          stg(dst, (int32_t)pr[u].x);
+        }
+        stg(dst + X.otw - 1, (int32_t)pr[u].y);
+        stg(X.ouid + o, uid[u]);
+      }
+      continue;
+    }
+    Rec A[COMPACT_UNROLL];
+    ulonglong2 B[COMPACT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      B[u] = make_ulonglong2(0, 0);
+      if (!ok[u]) continue;
+      if (CHAIN && X.ctw) {
+        const int32_t t2 = X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0;
+        A[u] = X.cperm == 2 ? fold_chain(X.fold, (int32_t)pr[u].y, t2, ldg(X.ctup1 + pi[u]), (int32_t)pr[u].x,
+                                         X.ctw, X.now_ms)
+               : X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x,
+                                      X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms)
+                       : fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2,
+                                    X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
+        continue;
+      }
+      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
+      else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
+      else A[u] = load_rec(X.af, pr[u].x);
+      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
+    }
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      const int32_t m = m0 + u * 64 + lane;  // the element's place in the tile
+      Rec R;
+      if (ok[u]) {
+        R = (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms);
+        store_rec(X.ofeat, X.off + m, R);
+        stg(X.ouid + X.off + m, uid[u]);
+      }
+      if (!S) continue;  // (wave-uniform)
+      // ---- the summary over these 64 elements, in order
+      int32_t P = -1, OD = 0;
+      const bool rest = ok[u] && m > 0;
+      if (ok[u]) {
+        const Feat F = decode_rec(R);
+#pragma unroll
+        for (int k = 0; k < NP2; k++) {
+          const uint32_t w = (uint32_t)F.f[2 * k] | (2 * k + 1 < NF ? (uint32_t)F.f[2 * k + 1] << 16 : 0u);
+          pmn[k] = pk_min16(pmn[k], w);
+          pmx[k] = pk_max16(pmx[k], w);
+        }
+        const int32_t tc = F.f[F_HITCOUNT], td = F.f[F_WORDSINTEXT] + F.f[F_WORDSINTITLE] + 1;
+        if (tcn < 0 || frac_lt(tc, td, tcn, tdn)) { tcn = tc; tdn = td; }
+        if (tcx < 0 || frac_lt(tcx, tdx, tc, td)) { tcx = tc; tdx = td; }
+        pmax = max(pmax, F.p);
+        P = F.p;
+        OD = F.od;
+        if (m == 0) {
+          pf = F.p;
+          of = F.od;
+          af = F.a;
+        } else {
+          vamn = min(vamn, F.a);
+          vamx = max(vamx, F.a);
+          mrest = max(mrest, F.od);
+          if (F.od > 0) lkey = max(lkey, ((m + 1) << 8) | F.od);
+        }
+      }
+      // records: rest elements above the prefix max of the rest before them
+      const int32_t incl = wave_incl_max(rest ? P : -1);
+      const int32_t pex = max(lane == 0 ? -1 : __shfl_up(incl, 1, 64), prun);
+      const bool isrec = rest && P > pex;
+      const uint64_t heads = __ballot(isrec);
+      // per segment: max stored distance, (position + 1) << 8 | the last positive one
+      // (a segmented inclusive scan headed at the records)
+      int32_t sm = rest ? OD : 0;
+      int32_t sk = (rest && OD > 0) ? ((m + 1) << 8) | OD : 0;
+      bool hd = isrec;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t m2 = __shfl_up(sm, o, 64), k2 = __shfl_up(sk, o, 64);
+        const bool h2 = __shfl_up((int)hd, o, 64) != 0;
+        if (lane >= o && !hd) { sm = max(sm, m2); sk = max(sk, k2); hd = h2; }
+      }
+      // the lanes before the first record continue the open segment
+      const int pre_end = heads ? __ffsll((long long)heads) - 2 : 63;
+      if (pre_end >= 0 && nseg > 0) {
+        segM = max(segM, __shfl(sm, pre_end, 64));
+        segK = max(segK, __shfl(sk, pre_end, 64));
+      }
+      uint64_t hm = heads;
+      while (hm) {  // wave-uniform
+        const int r = __ffsll((long long)hm) - 1;
+        hm &= hm - 1;
+        const int end = hm ? __ffsll((long long)hm) - 2 : 63;
+        if (nseg > 0 && nseg <= SEGC && lane == 0)
+          S->seg[nseg - 1] = ((uint32_t)segP << 16) | (((uint32_t)segM & 0xFFu) << 8) | ((uint32_t)segK & 0xFFu);
+        nseg++;
+        segP = __shfl(P, r, 64);
+        segM = __shfl(sm, end, 64);
+        segK = __shfl(sk, end, 64);
+      }
+      prun = max(prun, __shfl(incl, 63, 64));
+    }
+  }
+  if (!S) return;
+  if (nseg > 0 && nseg <= SEGC && lane == 0)
+    S->seg[nseg - 1] = ((uint32_t)segP << 16) | (((uint32_t)segM & 0xFFu) << 8) | ((uint32_t)segK & 0xFFu);
+  // the wave's reductions; lane i writes field i
+#pragma unroll
+  for (int k = 0; k < NP2; k++) {
+    uint32_t x = pmn[k], y = pmx[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      x = pk_min16(x, (uint32_t)__shfl_xor((int)x, o, 64));
+      y = pk_max16(y, (uint32_t)__shfl_xor((int)y, o, 64));
+    }
+    pmn[k] = x;
+    pmx[k] = y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t c1 = __shfl_xor(tcn, o, 64), d1 = __shfl_xor(tdn, o, 64);
+    const int32_t c2 = __shfl_xor(tcx, o, 64), d2 = __shfl_xor(tdx, o, 64);
+    if (c1 >= 0 && (tcn < 0 || frac_lt(c1, d1, tcn, tdn))) { tcn = c1; tdn = d1; }
+    if (c2 >= 0 && (tcx < 0 || frac_lt(tcx, tdx, c2, d2))) { tcx = c2; tdx = d2; }
+  }
+  pmax = wave_max_i(pmax);
+  vamn = wave_min_i(vamn);
+  vamx = wave_max_i(vamx);
+  mrest = wave_max_i(mrest);
+  lkey = wave_max_i(lkey);
+  pf = __shfl(pf, 0, 64);
+  of = __shfl(of, 0, 64);
+  af = __shfl(af, 0, 64);
+#pragma unroll
+  for (int k = 0; k < NP2; k++) {
+    if (lane == k) {
+      S->mn[2 * k] = (int32_t)(pmn[k] & 0xFFFFu);
+      S->mx[2 * k] = (int32_t)(pmx[k] & 0xFFFFu);
+      if (2 * k + 1 < NF) {
+        S->mn[2 * k + 1] = (int32_t)(pmn[k] >> 16);
+        S->mx[2 * k + 1] = (int32_t)(pmx[k] >> 16);
+      }
+    }
+  }
+  if (lane == 16) {
+    S->nvalid = cnt;
+    S->first = (int32_t)off;
+    S->end = (int32_t)(off + cnt);
+    S->p_first = pf;
+    S->od_first = of;
+    S->a_first = af;
+    S->pmax = pmax;
+  } else if (lane == 17) {
+    S->M_rest = mrest;
+    S->L_rest = (int32_t)((uint32_t)lkey & 0xFFu);
+    S->va_mn_rest = vamn;
+    S->va_mx_rest = vamx;
+    S->nseg = nseg;
+    S->overflow = nseg > SEGC ? 1 : 0;
+  } else if (lane == 18) {
+    // the same double WordReferenceRow.termFrequency computes (decode_rec)
+    S->tf_mn = (double)tcn / (double)tdn;
+    S->tf_mx = (double)tcx / (double)tdx;
   }
 }
 
@@ -2507,17 +2780,16 @@ __device__ __forceinline__ void seg_bcast(SegList& L) {
   L.overflow = __shfl(L.overflow, 0, 64);
 }
 
-// Walk every valid element of chunk c after its first one as a single-element
-// piece (exact fallback for a chunk whose summary overflowed).  Whole wave: 64
-// elements per step are loaded in parallel; a step without a new prefix-max
-// record merges with two wave reductions, otherwise lane 0 walks it from LDS.
-// L must be wave-uniform on entry and is wave-uniform on exit.
-__device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& L, int32_t* sP, int32_t* sO) {
+// Walk every valid element of a summary's run after its first one (first, end)
+// as a single-element piece (exact fallback for a summary whose segments
+// overflowed).  Whole wave: 64 elements per step are loaded in parallel; a step
+// without a new prefix-max record merges with two wave reductions, otherwise
+// lane 0 walks it from LDS.  L must be wave-uniform on entry and is on exit.
+__device__ void rewalk_piece(const RankQ& Q, int32_t first, int32_t end, SegList& L, int32_t* sP, int32_t* sO) {
   const int lane = threadIdx.x;
-  const int64_t e0 = c * CHUNK, e1 = min((int64_t)(c + 1) * CHUNK, Q.n);
-  for (int64_t b = e0; b < e1; b += 64) {
+  for (int64_t b = (int64_t)first + 1; b < end; b += 64) {
     const int64_t e = b + lane;
-    bool ok = e < e1 && e > first && !(Q.removed && ldg(Q.removed + e));
+    bool ok = e < end && !(Q.removed && ldg(Q.removed + e));
     int32_t p = -1, od = 0;
     if (ok) {
       p = (int32_t)(ldg(Q.feat + e * FEAT_WORDS) & 0xFFFF);
@@ -2542,10 +2814,10 @@ __device__ void rewalk_chunk(const RankQ& Q, int64_t c, int32_t first, SegList& 
 
 // what the ordered fold reads of one chunk summary (nvc 0: empty or past the end)
 struct FoldIn {
-  int32_t nvc, pm, Mall, Lall, pf, of, ns, first;
+  int32_t nvc, pm, Mall, Lall, pf, of, ns, first, end;
 };
 __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t nc) {
-  FoldIn f{0, -1, 0, 0, 0, 0, 0, 0};
+  FoldIn f{0, -1, 0, 0, 0, 0, 0, 0, 0};
   if (c < nc) {
     const ChunkSum& X = C[c];
     f.nvc = X.nvalid;
@@ -2556,6 +2828,7 @@ __device__ __forceinline__ FoldIn fold_in(const ChunkSum* C, int64_t c, int64_t 
     f.of = X.od_first;
     f.ns = X.overflow ? -1 : X.nseg;
     f.first = X.first;
+    f.end = X.end;
   }
   return f;
 }
@@ -2658,19 +2931,19 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_hbucket(const RankQ* __restri
   if ((threadIdx.x & 63) == 0 && wm > 0) atomicMax(&shard[qb.x].maxdom, wm);
 }
 
-// one wave per query: ordered combination of the chunk summaries of this shard
-__global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, const int64_t* __restrict__ chunk_base,
-                                                  const ChunkSum* __restrict__ cs, ShardSum* __restrict__ out) {
-  __shared__ uint32_t sSeg[SSEG];
-  __shared__ int32_t sRw[128];
-  const int qi = blockIdx.x;
-  const RankQ& Q = qs[qi];
-  const int lane = threadIdx.x;
-  const ChunkSum* C = cs + chunk_base[qi];
-  const int64_t nc = Q.nchunks;
-  ShardSum& S = out[qi];
-  if (nc == 1 && !C[0].overflow) return;  // k_reduce wrote this one (one chunk, no overflow)
+// What an ordered combination of summaries yields besides its fold pieces.
+struct FoldRes {
+  int32_t nv, vamn, vamx;
+  int64_t firstc;  // the first summary with a valid element
+  int32_t mn[NF], mx[NF];
+  double tfmn, tfmx;
+};
 
+// Ordered combination (one wave) of the summaries C[0, nc), in container order:
+// the order-independent parts into R, the fold's pieces into L.
+__device__ void fold_run(const RankQ& Q, const ChunkSum* __restrict__ C, int64_t nc, SegList& L, int32_t* sRw,
+                         FoldRes& R) {
+  const int lane = threadIdx.x;
   // ---- min / max / counts / first chunk, one pass.  virtualAge over the shard's
   // rest = chunk rests + first elements of every chunk but the shard's first: each
   // lane keeps its own first chunk's first element aside until the shard's first
@@ -2707,10 +2980,9 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
   vamx = wave_max_i(vamx);
 
   // ---- ordered fold pieces
-  SegList L{sSeg, SSEG, 0, 0, -1};
   if (nv > 0) {
     const ChunkSum& X = C[firstc];
-    if (X.overflow) rewalk_chunk(Q, firstc, X.first, L, sRw, sRw + 64);
+    if (X.overflow) rewalk_piece(Q, X.first, X.end, L, sRw, sRw + 64);
     else if (lane == 0)
       for (int i = 0; i < X.nseg; i++) L.add((int32_t)(X.seg[i] >> 16), (int32_t)((X.seg[i] >> 8) & 0xFF), (int32_t)(X.seg[i] & 0xFF));
   }
@@ -2751,11 +3023,11 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
       hm &= hm - 1;
       const int end = hm ? __ffsll((long long)hm) - 2 : 63;
       const int32_t pf = __shfl(cur.pf, r, 64), of = __shfl(cur.of, r, 64);
-      const int32_t ns = __shfl(cur.ns, r, 64), fi = __shfl(cur.first, r, 64);
+      const int32_t ns = __shfl(cur.ns, r, 64), fi = __shfl(cur.first, r, 64), en = __shfl(cur.end, r, 64);
       if (lane == 0) L.add(pf, of, of);
       if (ns < 0) {
         seg_bcast(L);
-        rewalk_chunk(Q, c0 + r, fi, L, sRw, sRw + 64);
+        rewalk_piece(Q, fi, en, L, sRw, sRw + 64);
       } else {
         const uint32_t sg = lane < ns ? C[c0 + r].seg[lane] : 0u;
         for (int s = 0; s < ns; s++) {
@@ -2770,26 +3042,104 @@ __global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, 
     seg_bcast(L);
     cur = nxt;
   }
+  R.nv = nv;
+  R.vamn = vamn;
+  R.vamx = vamx;
+  R.firstc = firstc;
+  for (int f = 0; f < NF; f++) { R.mn[f] = mn[f]; R.mx[f] = mx[f]; }
+  R.tfmn = tfmn;
+  R.tfmx = tfmx;
+}
+
+// one wave per query: ordered combination of the summaries of this shard -- the
+// chunk summaries of k_reduce, or the merged compaction pieces (RankQ::groups)
+__global__ __launch_bounds__(64) void k_shard_fin(const RankQ* __restrict__ qs, const int64_t* __restrict__ chunk_base,
+                                                  const ChunkSum* __restrict__ cs, ShardSum* __restrict__ out) {
+  __shared__ uint32_t sSeg[SSEG];
+  __shared__ int32_t sRw[128];
+  const int qi = blockIdx.x;
+  const RankQ& Q = qs[qi];
+  const int lane = threadIdx.x;
+  const ChunkSum* C = Q.pieces ? Q.groups : cs + chunk_base[qi];
+  const int64_t nc = Q.pieces ? Q.ngroups : Q.nchunks;
+  ShardSum& S = out[qi];
+  if (!Q.pieces && nc == 1 && !C[0].overflow) return;  // k_reduce wrote this one (one chunk, no overflow)
+  SegList L{sSeg, SSEG, 0, 0, -1};
+  FoldRes R;
+  fold_run(Q, C, nc, L, sRw, R);
   __syncthreads();
   if (lane == 0) {
-    S.nvalid = nv;
-    S.has_first = nv > 0;
-    if (nv > 0) {
-      S.p_first = C[firstc].p_first;
-      S.od_first = C[firstc].od_first;
-      S.a_first = C[firstc].a_first;
+    S.nvalid = R.nv;
+    S.has_first = R.nv > 0;
+    if (R.nv > 0) {
+      S.p_first = C[R.firstc].p_first;
+      S.od_first = C[R.firstc].od_first;
+      S.a_first = C[R.firstc].a_first;
     } else {
       S.p_first = S.od_first = S.a_first = 0;
     }
-    for (int f = 0; f < NF; f++) { S.mn[f] = mn[f]; S.mx[f] = mx[f]; }
-    S.va_mn_rest = vamn;
-    S.va_mx_rest = vamx;
-    S.tf_mn = tfmn;
-    S.tf_mx = tfmx;
+    for (int f = 0; f < NF; f++) { S.mn[f] = R.mn[f]; S.mx[f] = R.mx[f]; }
+    S.va_mn_rest = R.vamn;
+    S.va_mx_rest = R.vamx;
+    S.tf_mn = R.tfmn;
+    S.tf_mx = R.tfmx;
     S.nseg = L.n > SSEG ? SSEG : L.n;
     S.overflow = L.overflow;
   }
   for (int i = lane; i < SSEG && i < L.n; i += 64) S.seg[i] = sSeg[i];
+}
+
+// The compaction's tile pieces of a query (RankQ::pieces) merged 64 at a time into
+// one ChunkSum each (RankQ::groups), one wave per group, all groups of the batch
+// at once: k_shard_fin then folds a few summaries per query, as many as k_reduce
+// would have written for its chunks, instead of every tile's in one wave.
+__global__ __launch_bounds__(64) void k_piece_merge(const RankQ* __restrict__ qs, const int2* __restrict__ group_q) {
+  __shared__ uint32_t sSeg[SEGC];
+  __shared__ int32_t sRw[128];
+  const int2 gq = group_q[blockIdx.x];  // (query, group)
+  const RankQ& Q = qs[gq.x];
+  const int lane = threadIdx.x;
+  const int64_t c0 = (int64_t)gq.y * 64;
+  const ChunkSum* C = Q.pieces + c0;
+  const int64_t nc = min((int64_t)64, Q.npieces - c0);
+  ChunkSum& S = Q.groups[gq.y];
+  SegList L{sSeg, SEGC, 0, 0, -1};
+  FoldRes R;
+  fold_run(Q, C, nc, L, sRw, R);
+  // pmax over every element; over the rest: max stored distance (the first
+  // summary's rest, every later summary whole) and the last positive one
+  const FoldIn f = fold_in(C, lane, nc);
+  const int32_t fc = (int32_t)R.firstc;
+  const int32_t pm = wave_max_i(f.nvc ? f.pm : -1);
+  const int32_t mr = wave_max_i(!f.nvc ? 0 : lane == fc ? C[lane].M_rest : lane > fc ? f.Mall : 0);
+  const int32_t lk = wave_max_i(f.nvc && lane > fc && f.Lall > 0 ? ((lane + 1) << 8) | f.Lall : 0);
+  __syncthreads();
+  if (lane == 0) {
+    S.nvalid = R.nv;
+    S.end = nc > 0 ? C[nc - 1].end : 0;
+    if (R.nv > 0) {
+      const ChunkSum& F = C[fc];
+      S.first = F.first;
+      S.p_first = F.p_first;
+      S.od_first = F.od_first;
+      S.a_first = F.a_first;
+      S.L_rest = lk ? (lk & 0xFF) : F.L_rest;
+    } else {
+      S.first = -1;
+      S.p_first = S.od_first = S.a_first = 0;
+      S.L_rest = 0;
+    }
+    S.pmax = pm;
+    S.M_rest = mr;
+    for (int k = 0; k < NF; k++) { S.mn[k] = R.mn[k]; S.mx[k] = R.mx[k]; }
+    S.va_mn_rest = R.vamn;
+    S.va_mx_rest = R.vamx;
+    S.tf_mn = R.tfmn;
+    S.tf_mx = R.tfmx;
+    S.nseg = L.n;
+    S.overflow = L.overflow;
+  }
+  if (lane < SEGC && lane < L.n) S.seg[lane] = sSeg[lane];
 }
 
 // fold state transition for one piece (WordReferenceVars.max :431-445)
@@ -4161,7 +4511,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
                      ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups, BmFast* d_fast,
-                     BmFast* d_fast_perm) {
+                     BmFast* d_fast_perm, bool sum) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -4244,7 +4594,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
     if (!chain) {  // chained steps compact once the fold's dispatch modes are known (launch_compact)
       if (evc0) hipEventRecord(reinterpret_cast<hipEvent_t>(evc0), S(st));
       if (int r = launch_compact(d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt,
-                                 d_tile_off, bo, false, st))
+                                 d_tile_off, bo, false, st, sum))
         return r;
       if (evc1) hipEventRecord(reinterpret_cast<hipEvent_t>(evc1), S(st));
     }
@@ -4254,9 +4604,16 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
 
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
-                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* st) {
+                   const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* st,
+                   bool sum) {
   if (total_tiles <= 0) return 0;
   const int2* perm = bo.key && bo.tile_job ? bo.perm : nullptr;
+  if (sum) {  // one wave per tile
+    auto ks = chain ? k_compact_sum<true> : k_compact_sum<false>;
+    hipLaunchKernelGGL(ks, dim3((unsigned)total_tiles), dim3(64), 0, S(st), d_jobs, d_tile_base, njobs, total_tiles,
+                       d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off, perm, (const int32_t*)bo.tile_job);
+    return rc(hipGetLastError());
+  }
   auto kc = chain ? k_compact<true> : k_compact<false>;
   hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
                      d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
@@ -4311,11 +4668,13 @@ extern "C" int yrwi_chain_prof(unsigned long long* out) {  // profiling build on
 
 int launch_reduce(const RankQ* d_q, const int64_t* d_chunk_base, const int32_t* d_chunk_q, int32_t nq,
                   int64_t total_chunks,
-                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid, bool hp_any) {
+                  ChunkSum* d_chunks, ShardSum* d_shard, void* st, void* ev_mid, bool hp_any, bool reduce,
+                  const int2* d_group_q, int64_t ngroups) {
   // (static, the 4 KB cost every batch's k_reduce LDS whether it counted hosts or not)
-  if (total_chunks > 0)
+  if (total_chunks > 0 && reduce)
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)total_chunks), dim3(CHUNK_THREADS),
                        hp_any ? HPART_MAXS * sizeof(int32_t) : 0, S(st), d_q, d_chunk_q, d_chunks, d_shard);
+  if (ngroups > 0) hipLaunchKernelGGL(k_piece_merge, dim3((unsigned)ngroups), dim3(64), 0, S(st), d_q, d_group_q);
   if (ev_mid) hipEventRecord(reinterpret_cast<hipEvent_t>(ev_mid), S(st));  // k_reduce alone (statistics)
   hipLaunchKernelGGL(k_shard_fin, dim3((unsigned)nq), dim3(64), 0, S(st), d_q, d_chunk_base, d_chunks, d_shard);
   return rc(hipGetLastError());
