@@ -5,7 +5,7 @@
 set -e
 mkdir -p gpurun_out/ab
 ARGS=${AB_ARGS:---steps 20 --warmup 5 --no-cpu --latency 0}
-for i in 1 2; do
+for i in $(seq 1 ${ROUNDS:-2}); do
   for nv in "$@"; do
     n=${nv%%=*}; p=${nv#*=}
     if [ "$p" = cur ]; then unset YRWI_LIB; else export YRWI_LIB=$(pwd)/$p; fi

@@ -7,4 +7,10 @@ if [ -n "$TESTS" ]; then
     > gpurun_out/abr/tests.log 2>&1 || exit $?
 fi
 AB_ARGS=${AB_ARGS:-"--steps 40 --warmup 8 --no-cpu --latency 0 --legs none"} bash tools/ab.sh $AB || exit $?
-if [ -n "$KSTATS" ]; then bash tools/kstats.sh abr_cur || exit $?; fi
+if [ -n "$KSTATS" ]; then  # every build's isolated kernel times, same box
+  for nv in $AB; do
+    n=${nv%%=*}; p=${nv#*=}
+    if [ "$p" = cur ]; then unset YRWI_LIB; else export YRWI_LIB=$(pwd)/$p; fi
+    bash tools/kstats.sh abr_$n || exit $?
+  done
+fi

@@ -106,6 +106,15 @@ _CS_ACC = (K, "      store_rec(X.ofeat, o, (CHAIN && X.ctw) ? A[u] : joined_rec(
               "}\n")
 EDITS["csum"] = [_CS_HELP, _CS_INIT, _CS_ACC]
 
+# k_compact_sum's layout without its summaries: every step through the one-wave-per-tile
+# kernel, no pieces (k_reduce reads the containers as before; results unchanged)
+EDITS["sumlayout"] = [
+    (H, "        J.want_sum = last && P.excl.empty() && P.prof.coeff_authority <= 12 ? 1 : 0;",
+        "        J.want_sum = 0;"),
+    (H, "  bool sum = false;\n  for (const JoinQ& J : jobs) sum |= J.want_sum != 0;",
+        "  bool sum = true;\n  for (const JoinQ& J : jobs) sum |= J.want_sum != 0;"),
+]
+
 
 # variants that only change a compile-time constant (make EXTRA=...)
 FLAGS = {
