@@ -21,6 +21,7 @@ constexpr int CHUNK = 2048;          // container elements per rank/score workgr
 constexpr int CHUNK_THREADS = 256;
 constexpr int CHUNK_IPT = CHUNK / CHUNK_THREADS;
 constexpr int SEGC = 32;             // fold segments kept per chunk summary
+constexpr int SUM_MIN_PER_TILE = 64; // a chained fold's survivors per tile for k_compact_sum's pieces
 constexpr int SSEG = 128;            // fold segments kept per shard summary
 constexpr int NF = 11;               // min/max int fields (virtualAge handled apart)
 
@@ -193,7 +194,7 @@ struct JoinQ {
   // from the compaction (no exclusion marks, no authority counts): one ChunkSum per
   // tile of the job (index tile - tile_base), written by k_compact_sum
   ChunkSum* psum;
-  int32_t want_sum;    // host: allocate psum (run_join_jobs)
+  int32_t want_sum;    // host: psum wanted (1), or if a chained fold's survivors fill its tiles (2)
   int32_t pad_sum;
 };
 
@@ -423,13 +424,13 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* ev_mid, void* ev_end, void* ev_compact0 = nullptr, void* ev_compact1 = nullptr,
                      bool chain = false, int32_t* d_tile_lvl = nullptr, ProbeDesc* d_crange = nullptr,
                      const int2* d_cgrp = nullptr, int64_t ngroups = 0, BmFast* d_fast = nullptr,
-                     BmFast* d_fast_perm = nullptr, bool sum = false);
-// sum: some job of the step has normalisation pieces (JoinQ::psum): k_compact_sum
-// (one wave per tile) compacts the whole step instead of k_compact
+                     BmFast* d_fast_perm = nullptr, int sum = 0);
+// sum: jobs of the step with normalisation pieces (JoinQ::psum), compacted by
+// k_compact_sum (one wave per tile): 0 none, 1 every job, 2 some (k_compact the rest)
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* stream,
-                   bool sum = false);
+                   int sum = 0);
 int launch_rank(const RankQ* d_q, const int64_t* d_chunk_base, int32_t nq, int64_t total_chunks,
                 ChunkSum* d_chunks, ShardSum* d_shard, NormState* d_norm, int32_t world, void* stream);
 // hp_any: some query of the launch counts host buckets (RankQ::ecnt): k_reduce

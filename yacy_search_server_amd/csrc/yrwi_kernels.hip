@@ -1862,7 +1862,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
                                                  const int32_t* __restrict__ tile_cnt,
                                                  const int64_t* __restrict__ tile_off,
                                                  const int2* __restrict__ perm,
-                                                 const int32_t* __restrict__ tile_job) {
+                                                 const int32_t* __restrict__ tile_job, int skip_sum) {
   __shared__ int32_t sPre[COMPACT_TILES + 1];
   __shared__ CompactJob sJ[COMPACT_TILES];
   // band order (k_order_hist / k_order_scatter): this block's tiles are positions p0.. of the sorted order
@@ -1883,6 +1883,7 @@ __global__ __launch_bounds__(256) void k_compact(const JoinQ* __restrict__ jobs,
       }
       c = tile_cnt[t];
       if (c && jobs[j].count_only) c = 0;  // a count-first fold's counted join: nothing to compact
+      if (c && skip_sum && jobs[j].psum) c = 0;  // compacted by k_compact_sum
       if (c) {
         const JoinQ& J = jobs[j];
         CompactJob& X = sJ[threadIdx.x];
@@ -2481,15 +2482,18 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 }
 
 // ---------------------------------------------- compaction with summary pieces
-// k_compact for a step with normalisation pieces (JoinQ::psum): one wave per tile,
-// the tile's matches in container order, 64 x COMPACT_UNROLL at a time, the same
-// records and url ids as k_compact.  For a job with psum the wave also writes the
-// tile's ChunkSum -- what k_reduce computes for a chunk (ReferenceOrder
-// NormalizeWorker :163-210, see k_reduce), here over the tile's run of the container
-// [tile_off, tile_off + cnt), every element of it valid -- from the records it has
-// in registers, so the rank phase does not read the container back for it
-// (k_shard_fin folds the pieces in tile order).  The summary's arithmetic runs
-// while the wave waits for its next gathers.
+// The last step of queries whose containers need no pass but the normalisation
+// (JoinQ::psum: no exclusion marks, no authority counts): one
+// wave per tile, the tile's matches in order, 64 x COMPACT_UNROLL at a time, the
+// same records and url ids as k_compact, and the tile's ChunkSum -- what k_reduce
+// computes for a chunk (ReferenceOrder NormalizeWorker :163-210, see k_reduce),
+// here over the tile's run of the container [tile_off, tile_off + cnt), every
+// element of it valid -- from the records it has in registers, so the rank phase
+// does not read the container back for it (k_piece_merge / k_shard_fin fold the
+// pieces in tile order).  The step's other jobs go through k_compact (skip_sum):
+// the one-wave-per-tile layout leaves lanes idle on sparse tiles -- a chained
+// fold's survivors (C3 1.23 -> 1.37 ms/step through this kernel) get pieces only
+// when they average SUM_MIN_PER_TILE per tile.  CHAIN: the step has chained jobs.
 template <bool CHAIN>
 __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jobs,
                                                     const int64_t* __restrict__ tile_base, int njobs, int64_t ntiles,
@@ -2513,12 +2517,12 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
     j = tile_job ? tile_job[t] : find_job(tile_base, njobs, t);
   }
   const JoinQ& J = jobs[j];
-  if (J.count_only) return;  // a count-first fold's counted join: nothing to compact
+  if (!J.psum) return;  // (k_compact's)
   const int32_t cnt = tile_cnt[t];
   const int64_t off = tile_off[t];
-  ChunkSum* __restrict__ S = J.psum ? J.psum + (t - tile_base[j]) : nullptr;
+  ChunkSum* __restrict__ S = J.psum + (t - tile_base[j]);
   if (cnt == 0) {
-    if (S && lane == 0) {
+    if (lane == 0) {
       S->nvalid = 0;
       S->first = -1;
       S->end = (int32_t)off;
@@ -2527,30 +2531,26 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
     }
     return;
   }
-  CompactJob X;
-  X.af = J.A.feat;
-  X.bf = J.mode == JM_ENUM && J.B.j5 ? J.B.j5 : J.B.feat;
-  X.bw = J.mode == JM_ENUM && J.B.j5 ? 2 : FEAT_WORDS;
-  X.ofeat = J.out_feat;
-  X.ouid = J.out_uid;
-  X.now_ms = J.now_ms;
-  X.off = off;
-  X.src = tile_src[t];
-  X.mode = J.mode;
-  X.atw = J.A.tup ? J.A.tw : 0;
-  X.atup = J.A.tup;
-  X.otup = J.out_tup;
-  X.otw = J.out_tup ? J.out_tw : 0;
-  X.fold = J.fold;
-  X.ctw = 0;
-  X.cperm = 0;
-  X.ctup0 = X.ctup1 = nullptr;
+  const uint64_t* afeat = J.A.feat;
+  const uint64_t* bfeat = J.mode == JM_ENUM && J.B.j5 ? J.B.j5 : J.B.feat;
+  const int32_t bw = J.mode == JM_ENUM && J.B.j5 ? 2 : FEAT_WORDS;
+  const int32_t mode = J.mode;
+  const int32_t atw = J.A.tup ? J.A.tw : 0;
+  const int32_t* atup = J.A.tup;
+  const FoldSrc* fold = J.fold;
+  uint64_t* ofeat = J.out_feat;
+  uint32_t* ouid = J.out_uid;
+  const int64_t now_ms = J.now_ms;
+  const int64_t src = tile_src[t];
+  // a chained fold's survivors (k_chain): the records of all the fold's lists (fold_chain)
+  int32_t ctw = 0, cperm = 0;
+  const int32_t *ctup0 = nullptr, *ctup1 = nullptr;
   if (CHAIN && J.chain) {
     const int ni = ldg(&J.chain->npos);
-    X.ctw = 2 + ni;
-    X.cperm = ldg(&J.chain->perm);
-    X.ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
-    X.ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
+    ctw = 2 + ni;
+    cperm = ldg(&J.chain->perm);
+    ctup0 = ni > 0 ? ldg(&J.chain->tup[0]) : nullptr;
+    ctup1 = ni > 1 ? ldg(&J.chain->tup[1]) : nullptr;
   }
   // summary state: order-independent parts per lane, the ordered fold wave-uniform
   uint32_t pmn[NP2], pmx[NP2];  // fields 2j | 2j+1 << 16
@@ -2561,7 +2561,6 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
   int32_t pf = 0, of = 0, af = 0;  // the tile's first element (lane 0)
   int32_t prun = -1, nseg = 0, segP = 0, segM = 0, segK = 0;  // prefix max of the rest; the open segment
   for (int32_t m0 = 0; m0 < cnt; m0 += COMPACT_UNROLL * 64) {
-    int64_t pi[COMPACT_UNROLL];
     uint2 pr[COMPACT_UNROLL];
     uint32_t uid[COMPACT_UNROLL];
     bool ok[COMPACT_UNROLL];
@@ -2570,27 +2569,9 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
       const int32_t m = m0 + u * 64 + lane;
       ok[u] = m < cnt;
       if (ok[u]) {
-        pi[u] = X.src + m;
-        pr[u] = pairs[pi[u]];
-        uid[u] = pair_uid[pi[u]];
+        pr[u] = pairs[src + m];
+        uid[u] = pair_uid[src + m];
       }
-    }
-    if (X.otw) {  // deferred rows: the joined row's sources (no summary: not a last step)
-#pragma unroll
-      for (int u = 0; u < COMPACT_UNROLL; u++) {
-        if (!ok[u]) continue;
-        const int64_t o = X.off + m0 + u * 64 + lane;
-        int32_t* dst = X.otup + o * X.otw;
-        if (X.atw) {
-          const int32_t* srcr = X.atup + (int64_t)pr[u].x * X.atw;
-          for (int k = 0; k < X.atw; k++) stg(dst + k, ldg(srcr + k));
-        } else {
-          stg(dst, (int32_t)pr[u].x);
-        }
-        stg(dst + X.otw - 1, (int32_t)pr[u].y);
-        stg(X.ouid + o, uid[u]);
-      }
-      continue;
     }
     Rec A[COMPACT_UNROLL];
     ulonglong2 B[COMPACT_UNROLL];
@@ -2598,31 +2579,30 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       B[u] = make_ulonglong2(0, 0);
       if (!ok[u]) continue;
-      if (CHAIN && X.ctw) {
-        const int32_t t2 = X.ctw > 2 ? ldg(X.ctup0 + pi[u]) : 0;
-        A[u] = X.cperm == 2 ? fold_chain(X.fold, (int32_t)pr[u].y, t2, ldg(X.ctup1 + pi[u]), (int32_t)pr[u].x,
-                                         X.ctw, X.now_ms)
-               : X.cperm ? fold_chain(X.fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x,
-                                      X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms)
-                       : fold_chain(X.fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2,
-                                    X.ctw > 3 ? ldg(X.ctup1 + pi[u]) : 0, X.ctw, X.now_ms);
+      if (CHAIN && ctw) {
+        const int64_t pi = src + m0 + u * 64 + lane;
+        const int32_t t2 = ctw > 2 ? ldg(ctup0 + pi) : 0;
+        A[u] = cperm == 2 ? fold_chain(fold, (int32_t)pr[u].y, t2, ldg(ctup1 + pi), (int32_t)pr[u].x, ctw, now_ms)
+               : cperm    ? fold_chain(fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x, ctw > 3 ? ldg(ctup1 + pi) : 0,
+                                       ctw, now_ms)
+                          : fold_chain(fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2, ctw > 3 ? ldg(ctup1 + pi) : 0,
+                                       ctw, now_ms);
         continue;
       }
-      if (X.mode == JM_TEST_LARGE_B) A[u] = load_rec(X.bf, pr[u].y);
-      else if (X.atw) A[u] = fold_deferred(*X.fold, X.atup + (int64_t)pr[u].x * X.atw, X.atw, X.now_ms);
-      else A[u] = load_rec(X.af, pr[u].x);
-      if (X.mode == JM_ENUM) B[u] = ldg_j5(X.bf + (int64_t)pr[u].y * X.bw);
+      if (mode == JM_TEST_LARGE_B) A[u] = load_rec(bfeat, pr[u].y);
+      else if (atw) A[u] = fold_deferred(*fold, atup + (int64_t)pr[u].x * atw, atw, now_ms);
+      else A[u] = load_rec(afeat, pr[u].x);
+      if (mode == JM_ENUM) B[u] = ldg_j5(bfeat + (int64_t)pr[u].y * bw);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       const int32_t m = m0 + u * 64 + lane;  // the element's place in the tile
       Rec R;
       if (ok[u]) {
-        R = (CHAIN && X.ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, X.mode, X.now_ms);
-        store_rec(X.ofeat, X.off + m, R);
-        stg(X.ouid + X.off + m, uid[u]);
+        R = (CHAIN && ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, mode, now_ms);
+        store_rec(ofeat, off + m, R);
+        stg(ouid + off + m, uid[u]);
       }
-      if (!S) continue;  // (wave-uniform)
       // ---- the summary over these 64 elements, in order
       int32_t P = -1, OD = 0;
       const bool rest = ok[u] && m > 0;
@@ -2688,7 +2668,6 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
       prun = max(prun, __shfl(incl, 63, 64));
     }
   }
-  if (!S) return;
   if (nseg > 0 && nseg <= SEGC && lane == 0)
     S->seg[nseg - 1] = ((uint32_t)segP << 16) | (((uint32_t)segM & 0xFFu) << 8) | ((uint32_t)segK & 0xFFu);
   // the wave's reductions; lane i writes field i
@@ -4511,7 +4490,7 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
                      void* st, void* ev0,
                      void* evm, void* ev1, void* evc0, void* evc1, bool chain, int32_t* d_tile_lvl,
                      ProbeDesc* d_crange, const int2* d_cgrp, int64_t ngroups, BmFast* d_fast,
-                     BmFast* d_fast_perm, bool sum) {
+                     BmFast* d_fast_perm, int sum) {
   if (total_tiles <= 0) return 0;
   const int64_t probe_tiles = total_tiles - merge_tiles;
   // band orders (k_order_hist / k_order_scatter): all tiles for k_compact, probe tiles for k_probe
@@ -4605,19 +4584,20 @@ int launch_join_step(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t nj
 int launch_compact(const JoinQ* d_jobs, const int64_t* d_tile_base, int32_t njobs, int64_t total_tiles,
                    const uint2* d_pairs, const uint32_t* d_pair_uid, const int64_t* d_tile_src,
                    const int32_t* d_tile_cnt, const int64_t* d_tile_off, const BandOrder& bo, bool chain, void* st,
-                   bool sum) {
+                   int sum) {
   if (total_tiles <= 0) return 0;
   const int2* perm = bo.key && bo.tile_job ? bo.perm : nullptr;
-  if (sum) {  // one wave per tile
+  if (sum != 1) {  // jobs without normalisation pieces (all of them when sum == 0)
+    auto kc = chain ? k_compact<true> : k_compact<false>;
+    hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
+                       d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
+                       perm, (const int32_t*)bo.tile_job, sum ? 1 : 0);
+  }
+  if (sum) {  // the jobs with pieces: one wave per tile
     auto ks = chain ? k_compact_sum<true> : k_compact_sum<false>;
     hipLaunchKernelGGL(ks, dim3((unsigned)total_tiles), dim3(64), 0, S(st), d_jobs, d_tile_base, njobs, total_tiles,
                        d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off, perm, (const int32_t*)bo.tile_job);
-    return rc(hipGetLastError());
   }
-  auto kc = chain ? k_compact<true> : k_compact<false>;
-  hipLaunchKernelGGL(kc, dim3((unsigned)((total_tiles + COMPACT_TILES - 1) / COMPACT_TILES)), dim3(256), 0, S(st),
-                     d_jobs, d_tile_base, njobs, total_tiles, d_pairs, d_pair_uid, d_tile_src, d_tile_cnt, d_tile_off,
-                     perm, (const int32_t*)bo.tile_job);
   return rc(hipGetLastError());
 }
 
