@@ -559,7 +559,8 @@ def kernel_lines(iso, pmc):
         if t <= 0:
             continue
         a = alg / nl
-        kd = pk.get(name, {})
+        # (the compaction: k_compact and / or k_compact_sum per step, pooled by tools/pmc_summary.py)
+        kd = pk.get("compaction", pk.get(name, {})) if name == "k_compact" else pk.get(name, {})
         traffic = kd.get("hbm_bytes_per_launch")
         # bytes credited: the SURVEY 8(d) model, capped at the bytes the counters saw
         # leave L2 (a model above them credits requests L2 / LDS served)

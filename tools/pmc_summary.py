@@ -29,8 +29,8 @@ def short(name):
         return "k_probe_excl" if len(args) > 1 and args[1] in ("true", "1") else "k_probe"
     if "k_probeILb" in name:
         return "k_probe_excl" if "ELb1E" in name.split("k_probeILb", 1)[1][:8] else "k_probe"
-    for k in ("k_chain_part", "k_chain", "k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds", "k_compact",
-              "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
+    for k in ("k_chain_part", "k_chain", "k_join", "k_probe_part", "k_probe", "k_partition", "k_topq", "k_scan_tiles", "k_scan_bounds",
+              "k_compact_sum", "k_compact", "k_piece_merge", "k_reduce", "k_shard_fin", "k_combine", "k_order_hist", "k_order_scatter", "k_copy_in",
               "k_score_all", "k_score_full", "k_score", "k_merge", "k_emit", "k_validate", "k_features", "k_feat_rows"):
         if k + "E" in name or name.endswith(k) or (k + "I") in name or k in name:
             return k
@@ -95,8 +95,23 @@ def main(tag, config):
     # one batch's HBM traffic: every kernel of the query path, per launch x launches per batch
     # (k_combine runs once per batch pass); index build, uploads and fills excluded
     path = ("k_partition", "k_probe_part", "k_scan_bounds", "k_order_hist", "k_order_scatter", "k_join", "k_probe",
-            "k_probe_excl", "k_chain_part", "k_chain", "k_scan_tiles", "k_compact", "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq",
-            "k_emit")
+            "k_probe_excl", "k_chain_part", "k_chain", "k_scan_tiles", "k_compact", "k_compact_sum", "k_piece_merge",
+            "k_reduce", "k_shard_fin", "k_combine", "k_score", "k_score_full", "k_topq", "k_emit")
+    # a join step's compaction (launch_compact) is k_compact, k_compact_sum (the jobs
+    # with normalisation pieces) or both: per step (k_scan_tiles runs once per step)
+    # they pool into "compaction", the figure bench.py holds against its HIP events
+    steps = out["kernels"].get("k_scan_tiles", {}).get("calls")
+    parts = [out["kernels"][k] for k in ("k_compact", "k_compact_sum") if k in out["kernels"]]
+    if steps and parts:
+        c = {"calls": steps, "total_ns": sum(p.get("total_ns", 0.0) for p in parts),
+             "pooled": [k for k in ("k_compact", "k_compact_sum") if k in out["kernels"]]}
+        c["avg_ns"] = c["total_ns"] / steps
+        if all("hbm_bytes_per_launch" in p and p.get("calls") for p in parts):
+            c["hbm_bytes_per_launch"] = sum(p["hbm_bytes_per_launch"] * p["calls"] for p in parts) / steps
+        if all("read_requests_dram_per_launch" in p and p.get("calls") for p in parts):
+            c["read_requests_dram_per_launch"] = sum(p["read_requests_dram_per_launch"] * p["calls"]
+                                                     for p in parts) / steps
+        out["kernels"]["compaction"] = c
     nb = out["kernels"].get("k_combine", {}).get("calls")
     if nb:
         tot = 0.0
@@ -113,7 +128,8 @@ def main(tag, config):
     ident = source_identity()
     out["head"] = os.environ.get("PROF_HEAD") or ident["head"]
     out["src"] = ident["src"]
-    for name in ("k_compact", "k_join", "k_probe", "k_probe_excl", "k_chain", "k_reduce", "k_score"):
+    for name in ("compaction", "k_compact", "k_compact_sum", "k_join", "k_probe", "k_probe_excl", "k_chain", "k_reduce",
+                 "k_piece_merge", "k_score"):
         kd = out["kernels"].get(name, {})
         out[name + "_hbm_bytes_per_launch"] = kd.get("hbm_bytes_per_launch")
         out[name + "_avg_ns"] = kd.get("avg_ns")
