@@ -2560,53 +2560,73 @@ __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jo
   int32_t mrest = 0, lkey = 0;  // over the rest: max stored distance, (position + 1) << 8 | last positive one
   int32_t pf = 0, of = 0, af = 0;  // the tile's first element (lane 0)
   int32_t prun = -1, nseg = 0, segP = 0, segM = 0, segK = 0;  // prefix max of the rest; the open segment
-  for (int32_t m0 = 0; m0 < cnt; m0 += COMPACT_UNROLL * 64) {
-    uint2 pr[COMPACT_UNROLL];
-    uint32_t uid[COMPACT_UNROLL];
-    bool ok[COMPACT_UNROLL];
+  // Software pipeline, one group = 64 x COMPACT_UNROLL matches: while group g's
+  // summary runs, group g+1's gathers are in flight and group g+2's pairs loaded
+  // (the summary's arithmetic would otherwise sit between the wave's gathers).
+  uint2 npr[COMPACT_UNROLL];
+  uint32_t nuid[COMPACT_UNROLL], uid[COMPACT_UNROLL];
+  Rec A[COMPACT_UNROLL];
+  ulonglong2 B[COMPACT_UNROLL];
+  auto load_pairs = [&](int32_t g0) {
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
-      const int32_t m = m0 + u * 64 + lane;
-      ok[u] = m < cnt;
-      if (ok[u]) {
-        pr[u] = pairs[src + m];
-        uid[u] = pair_uid[src + m];
+      const int32_t m = g0 + u * 64 + lane;
+      if (m < cnt) {
+        npr[u] = pairs[src + m];
+        nuid[u] = pair_uid[src + m];
       }
     }
-    Rec A[COMPACT_UNROLL];
-    ulonglong2 B[COMPACT_UNROLL];
+  };
+  auto gather = [&](int32_t g0) {  // from npr (group g0's pairs); uid takes nuid
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       B[u] = make_ulonglong2(0, 0);
-      if (!ok[u]) continue;
+      uid[u] = nuid[u];
+      if (g0 + u * 64 + lane >= cnt) continue;
+      const uint2 pr = npr[u];
       if (CHAIN && ctw) {
-        const int64_t pi = src + m0 + u * 64 + lane;
+        const int64_t pi = src + g0 + u * 64 + lane;
         const int32_t t2 = ctw > 2 ? ldg(ctup0 + pi) : 0;
-        A[u] = cperm == 2 ? fold_chain(fold, (int32_t)pr[u].y, t2, ldg(ctup1 + pi), (int32_t)pr[u].x, ctw, now_ms)
-               : cperm    ? fold_chain(fold, (int32_t)pr[u].y, t2, (int32_t)pr[u].x, ctw > 3 ? ldg(ctup1 + pi) : 0,
+        A[u] = cperm == 2 ? fold_chain(fold, (int32_t)pr.y, t2, ldg(ctup1 + pi), (int32_t)pr.x, ctw, now_ms)
+               : cperm    ? fold_chain(fold, (int32_t)pr.y, t2, (int32_t)pr.x, ctw > 3 ? ldg(ctup1 + pi) : 0,
                                        ctw, now_ms)
-                          : fold_chain(fold, (int32_t)pr[u].x, (int32_t)pr[u].y, t2, ctw > 3 ? ldg(ctup1 + pi) : 0,
+                          : fold_chain(fold, (int32_t)pr.x, (int32_t)pr.y, t2, ctw > 3 ? ldg(ctup1 + pi) : 0,
                                        ctw, now_ms);
         continue;
       }
-      if (mode == JM_TEST_LARGE_B) A[u] = load_rec(bfeat, pr[u].y);
-      else if (atw) A[u] = fold_deferred(*fold, atup + (int64_t)pr[u].x * atw, atw, now_ms);
-      else A[u] = load_rec(afeat, pr[u].x);
-      if (mode == JM_ENUM) B[u] = ldg_j5(bfeat + (int64_t)pr[u].y * bw);
+      if (mode == JM_TEST_LARGE_B) A[u] = load_rec(bfeat, pr.y);
+      else if (atw) A[u] = fold_deferred(*fold, atup + (int64_t)pr.x * atw, atw, now_ms);
+      else A[u] = load_rec(afeat, pr.x);
+      if (mode == JM_ENUM) B[u] = ldg_j5(bfeat + (int64_t)pr.y * bw);
+    }
+  };
+  load_pairs(0);
+  gather(0);
+  load_pairs(COMPACT_UNROLL * 64);
+  for (int32_t m0 = 0; m0 < cnt; m0 += COMPACT_UNROLL * 64) {
+    Rec Rg[COMPACT_UNROLL];
+#pragma unroll
+    for (int u = 0; u < COMPACT_UNROLL; u++) {
+      const int32_t m = m0 + u * 64 + lane;
+      if (m < cnt) {
+        Rg[u] = (CHAIN && ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, mode, now_ms);
+        store_rec(ofeat, off + m, Rg[u]);
+        stg(ouid + off + m, uid[u]);
+      }
+    }
+    if (m0 + COMPACT_UNROLL * 64 < cnt) {  // (wave-uniform) the next group's gathers, the one after's pairs
+      gather(m0 + COMPACT_UNROLL * 64);
+      load_pairs(m0 + 2 * COMPACT_UNROLL * 64);
     }
 #pragma unroll
     for (int u = 0; u < COMPACT_UNROLL; u++) {
       const int32_t m = m0 + u * 64 + lane;  // the element's place in the tile
-      Rec R;
-      if (ok[u]) {
-        R = (CHAIN && ctw) ? A[u] : joined_rec(A[u], B[u].x, B[u].y, mode, now_ms);
-        store_rec(ofeat, off + m, R);
-        stg(ouid + off + m, uid[u]);
-      }
+      const bool okm = m < cnt;
+      const Rec& R = Rg[u];
       // ---- the summary over these 64 elements, in order
       int32_t P = -1, OD = 0;
-      const bool rest = ok[u] && m > 0;
-      if (ok[u]) {
+      const bool rest = okm && m > 0;
+      if (okm) {
         const Feat F = decode_rec(R);
 #pragma unroll
         for (int k = 0; k < NP2; k++) {
