@@ -535,7 +535,9 @@ def kernel_lines(iso, pmc):
                 (url-id bitmap: 4-B id + one 16-B bitmap word per smaller-side id); K as the reference
                 dispatches the step (J3);
       k_compact §8(d): 23 B per include term and joined posting (23 t m_out);
-      k_reduce  the 32-B ranking record of every joined posting (+ 1-B exclusion mark), k_shard_fin included;
+      k_reduce  the 32-B ranking record of every joined posting the compaction did not summarise
+                (+ 1-B exclusion mark); its time includes k_piece_merge (the compaction's pieces,
+                no container read: 0 bytes when every query has them);
       k_score   the same records (an upper bound: chunks the threshold prunes read 16 of the 32 B);
       k_chain   §8(d): the chained folds' later steps' K and the exclusions' 12 n_e, each charged
                 min(K, the bytes k_chain loads for it) (k_chain_part and k_scan_tiles included).
@@ -569,6 +571,8 @@ def kernel_lines(iso, pmc):
         e = {"mean_launch_us": round(t * 1e6, 2), "alg_bytes": int(a), "credited_bytes": int(cred),
              "capped_at_traffic": bool(traffic and a > traffic), "achieved": round(gbps, 1), "frac": _frac(gbps)}
         e.update(extra)
+        if name == "k_reduce" and not alg:
+            e["note"] = "k_piece_merge only: every query's container was summarised by k_compact_sum"
         if name == "k_probe" and iso.get("n_probe_dispatches"):
             # every k_probe dispatch, the exclusion steps' too (profiles key those as k_probe_excl)
             e["mean_dispatch_us_all_steps"] = round(iso["t_probe_all_ns"] / iso["n_probe_dispatches"] / 1e3, 2)
