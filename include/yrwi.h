@@ -132,7 +132,8 @@ typedef struct yrwi_stats {
   int64_t bytes_compact; /* bytes k_compact moves: per joined row 12 B pair + url id read, the 32-B ranking
                             record of the accumulated side and 16 B of the joined side's (by-test steps: one
                             32-B record) read, 32-B record + url id written */
-  int64_t t_compact_ns;  /* device time of the k_compact launches */
+  int64_t t_compact_ns;  /* device time of the compaction launches (k_compact and / or k_compact_sum, which also
+                            writes the normalisation pieces of the queries that need no other pass) */
   int64_t t_kernels_ns;  /* device time of all the batch's kernel launches (HIP events around every group of
                             back-to-back launches; host waits and collectives excluded) */
   /* SURVEY.md §8(d) bytes with no step credited for reads its kernel never makes: every join step
@@ -151,10 +152,11 @@ typedef struct yrwi_stats {
      their number and device time (HIP events around each) */
   int64_t n_probe_dispatches;
   int64_t t_probe_all_ns;
-  /* rank phase, per pass: the k_reduce launch and the k_score launches (k_shard_fin / k_score_full
-     excluded: the populations rocprofv3 averages), HIP events around each; the bytes their kernels must read: k_reduce the 32-B ranking record of every
-     joined row (+ its 1-B exclusion mark), k_score the same records (an upper bound: chunks pruned by
-     the per-query threshold read only words 2-3) */
+  /* rank phase, per pass: the k_reduce launch (with k_piece_merge, which merges the compaction's pieces)
+     and the k_score launches (k_shard_fin / k_score_full excluded: the populations rocprofv3 averages),
+     HIP events around each; the bytes their kernels must read: k_reduce the 32-B ranking record of every
+     joined row of the queries without pieces (+ its 1-B exclusion mark), k_score the same records of
+     every query (an upper bound: chunks pruned by the per-query threshold read only words 2-3) */
   int64_t n_rank_passes;
   int64_t t_reduce_ns;
   int64_t t_scorek_ns;
