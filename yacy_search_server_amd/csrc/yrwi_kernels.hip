@@ -2483,9 +2483,9 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 
 // ---------------------------------------------- compaction with summary pieces
 // The last step of queries whose containers need no pass but the normalisation
-// (JoinQ::psum: no exclusion marks, no authority counts): one
-// wave per tile, the tile's matches in order, 64 x COMPACT_UNROLL at a time, the
-// same records and url ids as k_compact, and the tile's ChunkSum -- what k_reduce
+// (JoinQ::psum: no exclusion marks, no authority counts): one wave per tile, the
+// tile's matches in order, 64 x COMPACT_UNROLL at a time, the same records and
+// url ids as k_compact, and the tile's ChunkSum -- what k_reduce
 // computes for a chunk (ReferenceOrder NormalizeWorker :163-210, see k_reduce),
 // here over the tile's run of the container [tile_off, tile_off + cnt), every
 // element of it valid -- from the records it has in registers, so the rank phase
