@@ -115,6 +115,14 @@ EDITS["sumlayout"] = [
         "  bool sum = true;\n  for (const JoinQ& J : jobs) sum |= J.want_sum != 0;"),
 ]
 
+# a chained fold's pieces at a lower survivor density per tile (SUM_MIN_PER_TILE)
+def _sum_min(v):
+    return [("yrwi_internal.h", "constexpr int SUM_MIN_PER_TILE = 64;", "constexpr int SUM_MIN_PER_TILE = %d;" % v)]
+
+
+EDITS["summin0"] = _sum_min(0)
+EDITS["summin16"] = _sum_min(16)
+
 
 # variants that only change a compile-time constant (make EXTRA=...)
 FLAGS = {

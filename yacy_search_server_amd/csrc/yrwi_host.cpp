@@ -1100,7 +1100,6 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     return ctx->fail(YRWI_E_NOMEM, "arena");
   // the queries' last steps that summarise their containers as they compact them:
   // one ChunkSum per tile of the step, the job's run from its first tile
-  // (want_sum 2, a chained fold's: decided once k_chain has counted its survivors)
   auto sum_mode = [&]() {
     bool any = false, all = true;
     for (const JoinQ& J : jobs) {
@@ -1110,16 +1109,15 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
     }
     return any ? (all ? 1 : 2) : 0;
   };
-  ChunkSum* d_psum = nullptr;
   bool any_want = false;
   for (const JoinQ& J : jobs) any_want |= J.want_sum != 0;
   if (any_want) {
-    d_psum = arena_alloc<ChunkSum>(ctx, tiles);
+    ChunkSum* d_psum = arena_alloc<ChunkSum>(ctx, tiles);
     if (!d_psum) return ctx->fail(YRWI_E_NOMEM, "arena");
     for (int j = 0; j < nj; j++)
-      if (jobs[(size_t)j].want_sum == 1) jobs[(size_t)j].psum = d_psum + tile_base[(size_t)j];
+      if (jobs[(size_t)j].want_sum) jobs[(size_t)j].psum = d_psum + tile_base[(size_t)j];
   }
-  int sum = sum_mode();
+  const int sum = sum_mode();
   // chained jobs: their ChainQ (level counts into the landing buffer, the later
   // include lists' rows in slot-indexed arrays beside the pairs), per-tile level
   // counts and the list ranges of k_chain_part
@@ -1227,12 +1225,7 @@ static int run_join_jobs(Lane* ctx, std::vector<Plan>& plans, std::vector<JoinQ>
       J.out_uid = arena_alloc<uint32_t>(ctx, mh[(size_t)j]);
       J.out_feat = arena_alloc<uint64_t>(ctx, mh[(size_t)j] * FEAT_WORDS);
       if (!J.out_uid || !J.out_feat) return ctx->fail(YRWI_E_NOMEM, "arena");
-      // pieces from the compaction when the survivors fill a wave per tile on average
-      // (sparser tiles leave k_compact_sum's lanes idle: k_compact packs four per block)
-      if (J.want_sum == 2 && mh[(size_t)j] >= (int64_t)SUM_MIN_PER_TILE * J.ntiles)
-        J.psum = d_psum + tile_base[(size_t)j];
     }
-    sum = sum_mode();
     if (upload(ctx, d_jobs, jobs)) return YRWI_E_HIP;
   }
   for (int j = 0; j < nj; j++) {
@@ -1499,10 +1492,13 @@ static int run_join_phase(Lane* ctx, std::vector<Plan>& plans, yrwi_stats* st, T
         if (!J.out_feat && !P.chain) return ctx->fail(YRWI_E_NOMEM, "arena");
         // the container the rank phase reads: summarised by the compaction unless
         // exclusion marks (run_exclusion, after this) or host counts need a pass over
-        // it; a chained fold's (no exclusions inside the chain) once its survivors
-        // are known to fill the one-wave tiles (run_join_jobs: 2)
+        // it.  Not a chained fold with exclusions inside the chain: its survivors are
+        // sparse in their tiles, and k_compact, four tiles per workgroup, packs them
+        // (C3 1.23 -> 1.37 ms/step through k_compact_sum); the chained folds without
+        // take the pieces (C4 9.59-9.69 -> 9.24-9.26 ms/step against pieces only for
+        // those averaging 64 survivors per tile, 9.47-9.52 at 16)
         const bool chain_excl = P.chain && chq[qi].nl > chq[qi].ninc;
-        J.want_sum = last && P.excl.empty() && !chain_excl && P.prof.coeff_authority <= 12 ? (P.chain ? 2 : 1) : 0;
+        J.want_sum = last && P.excl.empty() && !chain_excl && P.prof.coeff_authority <= 12 ? 1 : 0;
         if (P.chain) {
           chain_q.push_back((int)qi);
         } else if (J.A.tup) {

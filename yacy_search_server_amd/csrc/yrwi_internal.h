@@ -21,7 +21,6 @@ constexpr int CHUNK = 2048;          // container elements per rank/score workgr
 constexpr int CHUNK_THREADS = 256;
 constexpr int CHUNK_IPT = CHUNK / CHUNK_THREADS;
 constexpr int SEGC = 32;             // fold segments kept per chunk summary
-constexpr int SUM_MIN_PER_TILE = 64; // a chained fold's survivors per tile for k_compact_sum's pieces
 constexpr int SSEG = 128;            // fold segments kept per shard summary
 constexpr int NF = 11;               // min/max int fields (virtualAge handled apart)
 
@@ -194,7 +193,7 @@ struct JoinQ {
   // from the compaction (no exclusion marks, no authority counts): one ChunkSum per
   // tile of the job (index tile - tile_base), written by k_compact_sum
   ChunkSum* psum;
-  int32_t want_sum;    // host: psum wanted (1), or if a chained fold's survivors fill its tiles (2)
+  int32_t want_sum;    // host: psum wanted (run_join_jobs allocates it)
   int32_t pad_sum;
 };
 

@@ -2490,10 +2490,10 @@ __global__ __launch_bounds__(CHUNK_THREADS) void k_reduce(const RankQ* __restric
 // here over the tile's run of the container [tile_off, tile_off + cnt), every
 // element of it valid -- from the records it has in registers, so the rank phase
 // does not read the container back for it (k_piece_merge / k_shard_fin fold the
-// pieces in tile order).  The step's other jobs go through k_compact (skip_sum):
-// the one-wave-per-tile layout leaves lanes idle on sparse tiles -- a chained
-// fold's survivors (C3 1.23 -> 1.37 ms/step through this kernel) get pieces only
-// when they average SUM_MIN_PER_TILE per tile.  CHAIN: the step has chained jobs.
+// pieces in tile order).  The step's other jobs go through k_compact (skip_sum),
+// among them the chained folds with exclusions inside the chain: their survivors
+// are sparse in their tiles (C3 1.23 -> 1.37 ms/step through this kernel), and
+// k_compact packs four tiles per workgroup.  CHAIN: the step has chained jobs.
 template <bool CHAIN>
 __global__ __launch_bounds__(64) void k_compact_sum(const JoinQ* __restrict__ jobs,
                                                     const int64_t* __restrict__ tile_base, int njobs, int64_t ntiles,
