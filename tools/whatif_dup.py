@@ -123,6 +123,11 @@ def _sum_min(v):
 EDITS["summin0"] = _sum_min(0)
 EDITS["summin16"] = _sum_min(16)
 
+# chained folds with exclusions inside the chain through k_compact_sum too
+EDITS["chainexcl"] = [("yrwi_host.cpp",
+                       "J.want_sum = last && P.excl.empty() && !chain_excl && P.prof.coeff_authority <= 12 ? 1 : 0;",
+                       "J.want_sum = last && P.excl.empty() && (chain_excl || !chain_excl) && P.prof.coeff_authority <= 12 ? 1 : 0;")]
+
 
 # variants that only change a compile-time constant (make EXTRA=...)
 FLAGS = {
