@@ -133,6 +133,9 @@ EDITS["chainexcl"] = [("yrwi_host.cpp",
 FLAGS = {
     "bm512": "-DYRWI_BM_TILE=512",
     "bm256": "-DYRWI_BM_TILE=256",
+    "cu1": "-DYRWI_COMPACT_UNROLL=1",
+    "cu3": "-DYRWI_COMPACT_UNROLL=3",
+    "cu4": "-DYRWI_COMPACT_UNROLL=4",
 }
 
 
